@@ -1,0 +1,161 @@
+"""Deterministic builders for the BASELINE.json configurations c1..c5.
+
+All inputs are synthetic or come from the small data tables under ``data/`` (extracted
+from the reference's shipped xlsx/CSV files by tools/make_package_data.py):
+
+* c1  CE plumbing: PLM1, gases Ne/Ar/Kr/Xe, 100 walkers (sampler: 500 steps, seed 12345).
+* c2  CE log-prob: 2048 walkers x 3 wells (PLM1, PLM6, PLM7) x 5 gases.
+* c3  RTD log-prob: 2048 walkers x 1 well x 4 tracers (CFC12, SF6, H3, He4_ter), N=1200,
+      exponential model, sampled log10 J (savenum-1 style), obs = MAP PLM1, sd = 0.10 obs.
+* c4  joint CE + RTD: 2048 walkers x 64 wells x (5 gases + 5 tracers), N=1200, synthetic
+      non-constant series, per-well obs perturbed lognormally.
+* c5  c4 sharded as walker blocks over ranks.
+"""
+import json
+import os
+
+import numpy as np
+
+from .spec import CEBlock, ModelSpec, RTDBlock, Series, Tracer, LOG10_J_HE4_DEFAULT
+
+_DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
+
+
+def field_data():
+    with open(os.path.join(_DATA, "plm_field_data.json")) as f:
+        return json.load(f)
+
+
+def atmos_series(name, n=None):
+    """Reference-shaped yearly input series for a tracer, age-first, length n (default
+    the full 25256).  'He3' uses the H3 history (run_age_mcmc.py:217-220)."""
+    z = np.load(os.path.join(_DATA, "atmos_series.npz"), allow_pickle=False)
+    key = "H3" if name == "He3" else name
+    N = int(z["N_full"]) if n is None else int(n)
+    fill = float(z[key + "_fill"])
+    tail = np.asarray(z[key + "_tail"], dtype=np.float64)
+    c = np.full(N, fill)
+    m = min(N, len(tail))
+    c[:m] = tail[:m]
+    return Series(c, np.arange(N, dtype=np.float64), 0.0)
+
+
+def tracer(name, n=None, series=None, log10_J=None):
+    """Per-tracer convolution kwargs of run_age_mcmc.py:205-224."""
+    s = series if series is not None else atmos_series(name, n)
+    if name in ("CFC11", "CFC12", "CFC113", "SF6"):
+        return Tracer(name, s)
+    if name == "He4_ter":
+        return Tracer(name, Series(s.c_by_age * 0.0, s.idx_by_age, s.dtp), rad_accum="4He",
+                      log10_J=log10_J)
+    if name == "He3":
+        return Tracer(name, s, t_half=12.34, rad_accum="3He")
+    if name == "H3":
+        return Tracer(name, s, t_half=12.34)
+    raise ValueError(name)
+
+
+def ce_block(wells, gases, E_min=None, obs=None, sd=None):
+    fd = field_data()
+    if obs is None:
+        obs = np.array([[fd["obs"][w][g] for g in gases] for w in wells])
+    if sd is None:
+        sd = obs * np.array([fd["err_percent"][g] / 100 for g in gases])
+    if E_min is None:
+        E_min = np.array([fd["well_elev"][w] - 10.0 for w in wells])
+    return CEBlock(obs=obs, sd=sd, E_min=E_min, gases=tuple(gases))
+
+
+def sample_prior(spec, W, rng):
+    """Draw theta SoA [P][L][W] from the natural-space priors of ``spec``."""
+    L = spec.n_wells
+    th = np.zeros((spec.n_params, L, W))
+    for i, role in enumerate(spec.roles):
+        sh = (L, W)
+        c, r = spec.ce, spec.rtd
+        if role == "Ae_beta":
+            v = rng.beta(*c.beta_Ae, size=sh)
+        elif role == "F_beta":
+            v = rng.beta(*c.beta_F, size=sh)
+        elif role == "E_beta":
+            v = rng.beta(*c.beta_E, size=sh)
+        elif role == "m":
+            v = rng.normal(c.m_mu, c.m_sd, size=sh)
+        elif role == "b_beta":
+            v = rng.beta(*c.beta_b, size=sh)
+        elif role == "nu_ce_beta":
+            v = rng.beta(*c.beta_nu, size=sh)
+        elif role == "nu_rtd_beta":
+            v = rng.beta(*r.beta_nu, size=sh)
+        elif role in ("tau1", "tau2", "f1", "eta1", "eta2", "D1", "D2"):
+            lo, hi = getattr(r, role)
+            v = rng.uniform(lo, hi, size=sh)
+        elif role == "J":
+            v = rng.normal(r.J_mu, r.J_sd, size=sh)
+        elif role == "thalf_cfc_beta":
+            v = rng.beta(*r.beta_thalf, size=sh)
+        elif role == "lamsf6":
+            v = np.abs(rng.normal(0.0, r.lamsf6_sd, size=sh))
+        else:
+            raise ValueError(role)
+        if role.endswith("_beta"):
+            # rng.beta(2, 0.1) returns exactly 1.0 often; PyMC3 samples these in logodds
+            # space and never sits on the boundary, so keep draws strictly inside (0, 1).
+            v = np.clip(v, 1e-9, 1.0 - 1e-9)
+        th[i] = v
+    return th
+
+
+def c1(W=100):
+    spec = ModelSpec(n_wells=1, ce=ce_block(["PLM1"], ("Ne", "Ar", "Kr", "Xe")))
+    return spec, sample_prior(spec, W, np.random.default_rng(12345))
+
+
+def c2(W=2048):
+    spec = ModelSpec(n_wells=3, ce=ce_block(["PLM1", "PLM6", "PLM7"], ("He", "Ne", "Ar", "Kr", "Xe")))
+    return spec, sample_prior(spec, W, np.random.default_rng(12345))
+
+
+def c3(W=2048, N=1200):
+    fd = field_data()
+    names = ("CFC12", "SF6", "H3", "He4_ter")
+    mu = np.array([[fd["map_obs_PLM1"][t] for t in names]])
+    rtd = RTDBlock(tracers=[tracer(t, N) for t in names], obs=mu, sd=0.10 * mu,
+                   mod_type1="exponential", par_names=("tau1", "J"))
+    spec = ModelSpec(n_wells=1, rtd=rtd)
+    return spec, sample_prior(spec, W, np.random.default_rng(23456))
+
+
+def c4_spec(L=64, N=1200, seed=34567, mod_type1="exponential", mod_type2=None, par_names=("tau1",)):
+    rng = np.random.default_rng(seed)
+    fd = field_data()
+    base_wells = ["PLM1", "PLM6", "PLM7"]
+    wells = [base_wells[l % 3] for l in range(L)]
+    gases = ("He", "Ne", "Ar", "Kr", "Xe")
+    ce_obs = np.array([[fd["obs"][w][g] for g in gases] for w in wells]) * rng.lognormal(0, 0.1, (L, 5))
+    ce = ce_block(wells, gases, obs=ce_obs)
+    names = ("CFC12", "SF6", "H3", "He3", "He4_ter")
+    trs = []
+    for t in names:
+        s = atmos_series(t, N)
+        c = s.c_by_age * rng.lognormal(0.0, 0.05, N)   # non-constant everywhere
+        trs.append(tracer(t, series=Series(c, s.idx_by_age, 0.0),
+                          log10_J=LOG10_J_HE4_DEFAULT if t == "He4_ter" else None))
+    base = dict(fd["map_obs_PLM1"])
+    base["He3"] = 8.0
+    rtd_obs = np.array([[base[t] for t in names]] * L) * rng.lognormal(0, 0.1, (L, len(names)))
+    rtd = RTDBlock(tracers=trs, obs=rtd_obs, sd=0.10 * rtd_obs, mod_type1=mod_type1,
+                   mod_type2=mod_type2, par_names=par_names)
+    return ModelSpec(n_wells=L, ce=ce, rtd=rtd)
+
+
+def c4(W=2048, L=64, N=1200):
+    spec = c4_spec(L=L, N=N)
+    return spec, sample_prior(spec, W, np.random.default_rng(34568))
+
+
+def shard_walkers(W_total, rank, world):
+    """Contiguous walker block of ``rank`` (c5: W/G walkers per GPU)."""
+    per = (W_total + world - 1) // world
+    lo = min(W_total, rank * per)
+    return lo, min(W_total, lo + per)

@@ -1,0 +1,194 @@
+"""Per-walker log-probability of the reference models, restated on the CPU.
+
+TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).  A literal per-(walker, well) loop:
+
+* CE:  priors + T=(E-b)/m mapping of ng_interp/noble_gas_mcmc.py:216-250, the forward
+       model through ``oracle.ce.ce_exc_wrapper`` (:205-213), StudentT over the gases (:266).
+* RTD: priors of run_age_mcmc_utils.py:286-344, one ``oracle.rtd.forward_mod`` per tracer
+       (:376-383), StudentT over the tracers (:388-396).
+
+``spec`` is a ``noblegas_rtd_mcmc_amd.spec.ModelSpec`` read as plain data.
+"""
+import numpy as np
+
+from . import ce as _ce
+from . import rtd as _rtd
+from . import stats as _st
+
+
+def _beta_lp(x, ab, jac):
+    lp = _st.beta_logp(x, ab[0], ab[1])
+    return lp + (_st.jac_logodds(x) if jac else 0.0)
+
+
+def _unif_lp(x, lohi, jac):
+    lp = _st.uniform_logp(x, lohi[0], lohi[1])
+    return lp + (_st.jac_interval(x, lohi[0], lohi[1]) if jac else 0.0)
+
+
+def ce_unit(spec, l, p, want_prior=True, want_like=True, jac=False):
+    """CE contribution of one (walker, well); ``p`` maps role -> value."""
+    c = spec.ce
+    lp = 0.0
+    if want_prior:
+        lp += _beta_lp(p["Ae_beta"], c.beta_Ae, jac)
+        lp += _beta_lp(p["F_beta"], c.beta_F, jac)
+        lp += _beta_lp(p["E_beta"], c.beta_E, jac)
+        lp += _st.normal_logp(p["m"], c.m_mu, c.m_sd)
+        lp += _beta_lp(p["b_beta"], c.beta_b, jac)
+        lp += _beta_lp(p["nu_ce_beta"], c.beta_nu, jac)
+    if want_like:
+        Ae = p["Ae_beta"] * (c.logA_max - c.logA_min) + c.logA_min
+        F = p["F_beta"] * (c.logF_max - c.logF_min) + c.logF_min
+        E = p["E_beta"] * (c.E_max - c.E_min[l]) + c.E_min[l]
+        b = p["b_beta"] * (c.b_max - c.b_min) + c.b_min
+        with np.errstate(all="ignore"):
+            T = (E - b) / p["m"]
+        nu = p["nu_ce_beta"] * (c.nu_max - c.nu_min) + c.nu_min
+        mod = _ce.ce_exc_wrapper([Ae, F, E, T], gases=c.gases)
+        lp += float(np.sum(_st.studentt_logp(c.obs[l], mod, c.sd[l], nu)))
+    return float(lp)
+
+
+def rtd_par_values(spec, p):
+    """Reference par_names order values for ForwardMod (f2 = 1 - f1 inserted after f1)."""
+    r = spec.rtd
+    names, vals = [], []
+    for name in r.par_names:
+        if name == "thalf_cfc":
+            v = p["thalf_cfc_beta"] * (r.thalf[1] - r.thalf[0]) + r.thalf[0]
+        else:
+            v = p[name]
+        names.append(name)
+        vals.append(v)
+        if name == "f1":
+            names.append("f2")
+            vals.append(1 - p["f1"])
+    return names, vals
+
+
+def rtd_conc_unit(spec, p):
+    """Per-tracer model concentrations (ForwardMod.perform) of one (walker, well)."""
+    r = spec.rtd
+    names, vals = rtd_par_values(spec, p)
+    out = []
+    for t in r.tracers:
+        cv, ci, t_samp = t.series.reference_frame()
+        kw = {"C_values": cv, "C_index": ci, "mod_type1": r.mod_type1, "mod_type2": r.mod_type2 or False,
+              "t_half": t.t_half or False, "rad_accum": t.rad_accum or False}
+        names_t, vals_t = list(names), list(vals)
+        if t.rad_accum in ("4He",) and "J" not in names_t and t.log10_J is not None:
+            names_t.append("J")
+            vals_t.append(t.log10_J)
+        out.append(_forward_mod_tsamp(t.name, kw, names_t, vals_t, t_samp, t))
+    return np.array(out)
+
+
+def _forward_mod_tsamp(tracer, kw, names, vals, t_samp, t):
+    # forward_mod uses t_samp = index[-1] (run_age_mcmc_utils.py:94); a Series with dtp != 0
+    # is evaluated through convolve() directly with the same composition.
+    if t_samp == kw["C_index"][-1] and t.rad_accum != "SF6":
+        return _rtd.forward_mod(tracer, kw, names, vals)
+    p = {"tau1": False, "tau2": 0.0, "f1": 1.0, "f2": 0.0, "eta1": False, "eta2": False,
+         "D1": False, "D2": False, "J": False, "thalf_cfc": False, "lamsf6": False}
+    p.update(dict(zip(names, vals)))
+    if tracer == "He4_ter" and p["J"] == False:  # noqa: E712
+        p["J"] = _rtd.J_he4_default()
+    lam = _rtd.thalf_2_lambda(kw["t_half"]) if kw["t_half"] else 0.0
+    if "thalf_cfc" in names and tracer == "CFC12":
+        lam = _rtd.thalf_2_lambda(p["thalf_cfc"])
+
+    def one(tau, mod, eta, D):
+        return _rtd.convolve(kw["C_values"], kw["C_index"], t_samp, tau, mod, lamba=lam,
+                             rad_accum=kw["rad_accum"], J=10 ** p["J"], eta=eta, D=D, J_sf6=t.J_sf6)
+    c = p["f1"] * one(p["tau1"], kw["mod_type1"], p["eta1"], p["D1"])
+    if kw["mod_type2"]:
+        c = c + p["f2"] * one(p["tau2"], kw["mod_type2"], p["eta2"], p["D2"])
+    else:
+        c = c + p["f2"] * 0.0
+    if tracer == "SF6":
+        c *= (1 + p["lamsf6"])
+    return float(c)
+
+
+def rtd_unit(spec, l, p, want_prior=True, want_like=True, jac=False):
+    r = spec.rtd
+    lp = 0.0
+    if want_prior:
+        lp += _unif_lp(p["tau1"], r.tau1, jac)
+        lp += _beta_lp(p["nu_rtd_beta"], r.beta_nu, jac)
+        names = r.par_names
+        if "tau2" in names:
+            lp += _unif_lp(p["tau2"], r.tau2, jac)
+        if "f1" in names:
+            lp += _unif_lp(p["f1"], r.f1, jac)
+        if "eta1" in names:
+            lp += _unif_lp(p["eta1"], r.eta1, jac)
+        if "eta2" in names:
+            lp += _unif_lp(p["eta2"], r.eta2, jac)
+        if "D1" in names:
+            lp += _unif_lp(p["D1"], r.D1, jac)
+        if "D2" in names:
+            lp += _unif_lp(p["D2"], r.D2, jac)
+        if "J" in names:
+            lp += _st.normal_logp(p["J"], r.J_mu, r.J_sd)
+        if "thalf_cfc" in names:
+            lp += _beta_lp(p["thalf_cfc_beta"], r.beta_thalf, jac)
+        if "lamsf6" in names:
+            lp += _st.halfnormal_logp(p["lamsf6"], r.lamsf6_sd) + (_st.jac_log(p["lamsf6"]) if jac else 0.0)
+    if want_like:
+        nu = p["nu_rtd_beta"] * (r.nu_max - r.nu_min) + r.nu_min
+        mod = rtd_conc_unit(spec, p)
+        lp += float(np.sum(_st.studentt_logp(r.obs[l], mod, r.sd[l], nu)))
+    return float(lp)
+
+
+def unit_logp(spec, theta_soa, w, l):
+    p = {role: float(theta_soa[i, l, w]) for i, role in enumerate(spec.roles)}
+    lp = 0.0
+    if spec.ce is not None:
+        lp += ce_unit(spec, l, p, spec.include_prior, spec.include_like, spec.jacobian)
+    if spec.rtd is not None:
+        lp += rtd_unit(spec, l, p, spec.include_prior, spec.include_like, spec.jacobian)
+    return lp
+
+
+def log_prob(spec, theta_soa, walkers=None):
+    """Per-walker log-prob for theta SoA [P][L][W] (optionally a subset of walkers)."""
+    theta_soa = np.asarray(theta_soa, dtype=np.float64)
+    W = theta_soa.shape[2]
+    walkers = range(W) if walkers is None else walkers
+    out = []
+    for w in walkers:
+        s = 0.0
+        for l in range(spec.n_wells):
+            s += unit_logp(spec, theta_soa, w, l)
+        out.append(s)
+    return np.array(out)
+
+
+def forward(spec, theta_soa, walkers=None):
+    """Model outputs: CE conc [L][G][W'] and RTD conc [L][K][W'] (None where absent)."""
+    theta_soa = np.asarray(theta_soa, dtype=np.float64)
+    W = theta_soa.shape[2]
+    walkers = list(range(W) if walkers is None else walkers)
+    ce_out = rtd_out = None
+    if spec.ce is not None:
+        ce_out = np.zeros((spec.n_wells, len(spec.ce.gases), len(walkers)))
+    if spec.rtd is not None:
+        rtd_out = np.zeros((spec.n_wells, len(spec.rtd.tracers), len(walkers)))
+    for j, w in enumerate(walkers):
+        for l in range(spec.n_wells):
+            p = {role: float(theta_soa[i, l, w]) for i, role in enumerate(spec.roles)}
+            if ce_out is not None:
+                c = spec.ce
+                Ae = p["Ae_beta"] * (c.logA_max - c.logA_min) + c.logA_min
+                F = p["F_beta"] * (c.logF_max - c.logF_min) + c.logF_min
+                E = p["E_beta"] * (c.E_max - c.E_min[l]) + c.E_min[l]
+                b = p["b_beta"] * (c.b_max - c.b_min) + c.b_min
+                with np.errstate(all="ignore"):
+                    T = (E - b) / p["m"]
+                ce_out[l, :, j] = _ce.ce_exc_wrapper([Ae, F, E, T], gases=c.gases)
+            if rtd_out is not None:
+                rtd_out[l, :, j] = rtd_conc_unit(spec, p)
+    return ce_out, rtd_out

@@ -1,0 +1,147 @@
+"""Pin the CPU oracle (oracle/) against the golden vectors produced by the reference's
+own code (tests/golden/make_golden.py).  CPU only."""
+import numpy as np
+import pytest
+from scipy import stats
+
+from oracle import ce as oce
+from oracle import models as omod
+from oracle import rtd as ortd
+from oracle import stats as ost
+from noblegas_rtd_mcmc_amd.spec import Series
+from noblegas_rtd_mcmc_amd.workloads import atmos_series
+
+from golden_specs import spec_from_golden
+
+GASES = ["He", "Ne", "Ar", "Kr", "Xe"]
+RTOL = 1e-13
+
+
+def close(a, b, rtol=RTOL, atol=0.0):
+    a, b = np.asarray(a), np.asarray(b)
+    same_nan = np.isnan(a) & np.isnan(b)
+    same_inf = np.isinf(a) & np.isinf(b) & (np.sign(a) == np.sign(b))
+    ok = same_nan | same_inf | (np.abs(a - b) <= atol + rtol * np.abs(b))
+    return ok
+
+
+def test_ce_forward_matches_reference(golden):
+    z = golden("ce_golden.npz")
+    E, T, Ae, F, S = z["E"], z["T"], z["Ae"], z["F"], z["S"]
+    pm, Pin = z["pmode"], z["P_in"]
+    P = np.where(pm == 0, oce.lapse_rate(E), np.where(pm == 1, 0.000101325, Pin))
+    assert close(P, z["P"]).all()
+    assert close(oce.vapor_pressure(T), z["vapor"]).all()
+    sol = np.stack([oce.solubility(g, T, S) for g in GASES], 1)
+    assert close(sol, z["solubility"]).all()
+    dry = oce.equil_conc_dry(GASES, T, P, S)
+    assert close(np.stack([dry[g] for g in GASES], 1), z["equil_dry"]).all()
+    wet = oce.equil_conc(GASES, T, P, S)
+    assert close(np.stack([wet[g] for g in GASES], 1), z["equil"]).all()
+    for key, add in (("ce_total", True), ("ce_excess", False)):
+        r = oce.ce_exc(GASES, E, T, Ae, F, P=P, S=S, add_eq_conc=add)
+        assert close(np.stack([r[g] for g in GASES], 1), z[key]).all(), key
+    # the -9999 sentinel path (T<0) is exercised
+    assert (z["equil_dry"][T < 0] == -9999.0).all() and (T < 0).sum() > 10
+
+
+def test_ce_exc_wrapper_and_J(golden):
+    z = golden("ce_golden.npz")
+    th = z["wrap_theta"]
+    out = np.stack([oce.ce_exc_wrapper(th[:, i]) for i in range(th.shape[1])])
+    assert close(out, z["wrap_out"]).all()
+    assert oce.J_flux(1., 2700, 1000, 3.0, 10.0, 0.05) == z["J_U3Th10"]
+    assert oce.J_flux(1., 2700, 1000, 3.7, 10.2, 0.05) == z["J_U37Th102"]
+
+
+TRACERS = {"CFC12": ("CFC12", False, False, False), "SF6": ("SF6", False, False, False),
+           "H3": ("H3", 12.34, False, False), "He3": ("H3", 12.34, "3He", False),
+           "He4_ter": ("He4_ter", False, "4He", 3.30885e-11)}
+MODS = ["piston", "exponential", "exp_pist_flow", "dispersion"]
+
+
+@pytest.mark.parametrize("n", [1200, 25256])
+@pytest.mark.parametrize("tname", list(TRACERS))
+def test_convolve_matches_reference(golden, n, tname):
+    z = golden("conv_golden.npz")
+    sname, t_half, accum, J = TRACERS[tname]
+    s = atmos_series(sname, n)
+    c = s.c_by_age * (0.0 if tname == "He4_ter" else 1.0)
+    cv, ci = np.flip(c), np.arange(n - 1, -1, -1)
+    lam = ortd.thalf_2_lambda(t_half) if t_half else 0.0
+    for mod in MODS:
+        key = "%s_%s_%d" % (tname, mod, n)
+        tau, eta, D, ref = z[key + "_tau"], z[key + "_eta"], z[key + "_D"], z[key + "_out"]
+        got = np.array([ortd.convolve(cv, ci, ci[-1], tau[i], mod, lamba=lam, rad_accum=accum, J=J,
+                                      eta=eta[i], D=D[i]) for i in range(len(tau))])
+        ok = close(got, ref, rtol=1e-12)
+        assert ok.all(), (key, np.nonzero(~ok)[0], got[~ok], ref[~ok])
+
+
+def test_convolve_shift_and_gtp(golden):
+    z = golden("conv_golden.npz")
+    s = atmos_series("CFC12", 1200)
+    cv, ci = np.flip(s.c_by_age), np.arange(1199, -1, -1)
+    for mod in MODS:
+        key = "shift_%s" % mod
+        got = [ortd.convolve(cv, ci, ci[-1] + 3.7, t, mod, eta=e, D=d)
+               for t, e, d in zip(z[key + "_tau"], z[key + "_eta"], z[key + "_D"])]
+        assert close(got, z[key + "_out"], rtol=1e-12).all(), mod
+    for (mi, tau, eta, D), g in zip(z["gtp_params"], z["gtp"]):
+        got = ortd.gen_g_tp(1200, 0, 0, tau, MODS[int(mi)], eta, D)
+        assert close(got, g, rtol=1e-12, atol=1e-300).all()
+    got = ortd.convolve(cv, ci, ci[-1], 10.0, "exponential", lamba=ortd.thalf_2_lambda(12.34), g_tau=z["gext"])
+    assert close(got, z["gext_out"], rtol=1e-12)
+
+
+FWD_CASES = [("exp_J_thalf_lamsf6", "exponential", False, ["tau1", "J", "thalf_cfc", "lamsf6"]),
+             ("epm", "exp_pist_flow", False, ["tau1", "eta1"]),
+             ("disp", "dispersion", False, ["tau1", "D1"]),
+             ("bmm_exp_piston", "exponential", "piston", ["tau1", "tau2", "f1", "f2"]),
+             ("bmm_epm_piston", "exp_pist_flow", "piston", ["tau1", "tau2", "f1", "f2", "eta1"]),
+             ("bmm_disp_exp", "dispersion", "exponential", ["tau1", "tau2", "f1", "f2", "D1"]),
+             ("bmm_exp_epm", "exponential", "exp_pist_flow", ["tau1", "tau2", "f1", "f2", "eta2"])]
+
+
+@pytest.mark.parametrize("case", FWD_CASES, ids=[c[0] for c in FWD_CASES])
+def test_forward_mod_matches_reference(golden, case):
+    z = golden("fwd_golden.npz")
+    name, m1, m2, pn = case
+    th = z[name + "_theta"]
+    for tname, (sname, t_half, accum, _) in TRACERS.items():
+        s = atmos_series(sname, 1200)
+        c = s.c_by_age * (0.0 if tname == "He4_ter" else 1.0)
+        kw = {"C_values": np.flip(c), "C_index": np.arange(1199, -1, -1), "mod_type1": m1, "mod_type2": m2,
+              "t_half": t_half, "rad_accum": accum}
+        got = [ortd.forward_mod(tname, kw, pn, th[i]) for i in range(len(th))]
+        assert close(got, z["%s_%s" % (name, tname)], rtol=1e-12).all(), (name, tname)
+
+
+@pytest.mark.parametrize("prefix", ["c2", "c3", "c4", "bmm"])
+def test_model_logp_matches_reference(golden, prefix):
+    z = golden("logp_golden.npz")
+    spec, th = spec_from_golden(z, prefix)
+    got = omod.log_prob(spec, th)
+    ref = z[prefix + "_logp"]
+    assert close(got, ref, rtol=1e-12, atol=1e-9).all(), (got - ref)
+
+
+def test_stats_pinned_to_scipy():
+    rng = np.random.default_rng(5)
+    x, mu, sd, nu = rng.normal(size=64), rng.normal(size=64), rng.uniform(0.1, 3, 64), rng.uniform(1, 30, 64)
+    assert np.allclose(ost.studentt_logp(x, mu, sd, nu), stats.t.logpdf(x, nu, loc=mu, scale=sd), rtol=1e-13)
+    u = rng.uniform(0, 1, 64)
+    for a, b in ((2, 2), (2, 4), (2, 2.5), (2, 0.1)):
+        assert np.allclose(ost.beta_logp(u, a, b), stats.beta.logpdf(u, a, b), rtol=1e-12)
+    assert np.allclose(ost.normal_logp(x, -146.0, 17.0), stats.norm.logpdf(x, -146.0, 17.0), rtol=1e-13)
+    assert np.allclose(ost.halfnormal_logp(np.abs(x), 1 / 6), stats.halfnorm.logpdf(np.abs(x), scale=1 / 6), rtol=1e-13)
+    assert np.all(ost.uniform_logp(np.array([0.5, 1001.0]), 1.0, 1000.0) == [-np.inf, -np.inf])
+    assert np.all(ost.beta_logp(np.array([-0.1, 1.1]), 2, 2) == -np.inf)
+    assert np.isinf(ost.studentt_logp(0.0, 0.0, -1.0, 3.0))
+
+
+def test_series_reference_frame_roundtrip():
+    s = Series(np.arange(5.0), np.arange(5.0), 3.0)
+    v, i, t = s.reference_frame()
+    s2 = Series.from_reference_frame(v, i, t)
+    assert np.array_equal(s2.c_by_age, s.c_by_age) and s2.dtp == 3.0
