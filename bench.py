@@ -1,0 +1,181 @@
+#!/usr/bin/env python3
+"""Headline benchmark: joint CE + RTD-convolution log-likelihood evaluations per second.
+
+Workload (BASELINE.json configs[3]), per GPU: 2048 walkers x 64 wells x
+(CE over 5 gases + RTD convolution of 5 tracers over a 1200-year input series,
+exponential RTD) in float64.  One step = one full log-prob of the rank's walker block
+(theta resident in HBM) + an RCCL all-gather of the per-block log-prob vector (N > 1).
+Scaling is weak: every rank owns its own 2048-walker block (c5).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line; see DESIGN.md 'Measurement' for the roofline accounting.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "log-likelihood evals/sec (CE + RTD-conv), 2048 walkers, 1/2/4/8 MI355X"
+FP64_VALU_PEAK = 78.6e12     # 256 CU x 4 SIMD x 16 lanes x 2 FLOP (FMA) x 2.4 GHz
+HBM_PEAK = 8.0e12            # MI355X_MICROARCH.md chip table
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--walkers", type=int, default=2048)
+    ap.add_argument("--wells", type=int, default=64)
+    ap.add_argument("--ages", type=int, default=1200)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(spec, theta, budget_s, workers):
+    """The oracle (reference-faithful NumPy per-walker loop) on the host cores, on a
+    bounded sample of walkers of the same workload."""
+    import multiprocessing as mp
+    from oracle import models as om
+    t0 = time.perf_counter()
+    om.log_prob(spec, theta, walkers=[0])                   # one walker: size the sample
+    per = time.perf_counter() - t0
+    n = max(workers, int(budget_s / max(per, 1e-6)) * workers)
+    idx = [i % theta.shape[2] for i in range(n)]
+    chunks = [idx[i::workers] for i in range(workers)]
+    ctx = mp.get_context("fork")
+    t0 = time.perf_counter()
+    with ctx.Pool(workers) as pool:
+        pool.starmap(_cpu_chunk, [(spec, theta, c) for c in chunks])
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "evals/s", "cores": workers, "kind": "port",
+            "sample": "%d walker log-probs of the same workload (oracle/models.py per-walker loop: "
+                      "reference-faithful NumPy CE + convolve per (well, tracer)), %d processes, %.1f s"
+                      % (n, workers, dt)}
+
+
+def _cpu_chunk(spec, theta, walkers):
+    from oracle import models as om
+    return om.log_prob(spec, theta, walkers=walkers)
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    from noblegas_rtd_mcmc_amd import workloads
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    W = args.walkers
+    spec = workloads.c4_spec(L=args.wells, N=args.ages)
+    # this rank's walker block of the global ensemble (weak scaling: W per GPU)
+    theta_h = workloads.sample_prior(spec, W, np.random.default_rng(34568 + rank))
+    theta = torch.from_numpy(theta_h).to(dev)
+    lp = LogProb(spec, max_walkers=W, device=local)
+    out = torch.empty(W, dtype=torch.float64, device=dev)
+    gathered = torch.empty(W * world, dtype=torch.float64, device=dev)
+
+    def step():
+        lp(theta, out=out)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, out)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    # timed region: kernels bracketed by HIP events on the launch stream (no host syncs)
+    lp.ctx.set_profiling(True)
+    lp.kernel_stats(reset=True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    lp.ctx.set_profiling(False)
+    ks = lp.kernel_stats(reset=True)
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    assert torch.isfinite(out).any()
+
+    if rank == 0:
+        info = lp.info(W)
+        U = spec.n_wells * W
+        C = info["channels"]
+        N = spec.rtd.n_ages
+        rtd_ms = ks["rtd"][0] / max(ks["rtd"][1], 1)
+        # algorithmic work of the RTD kernel per launch: one FMA (2 FLOP) per
+        # (unit, channel, age >= 1) -- the Horner evaluation (DESIGN.md 'Roofline')
+        flops = 2.0 * U * C * (N - 1)
+        achieved = flops / (rtd_ms * 1e-3)
+        # algorithmic HBM bytes of the same launch: theta rows read + concentrations written
+        n_rows = 1 + (1 if "J" in spec.roles else 0)
+        hbm_bytes = U * 8.0 * n_rows + U * 8.0 * len(spec.rtd.tracers) + N * ((C + 1) // 2 * 2) * 8.0
+        traffic = None
+        pmc = os.path.join(REPO, "profiles", "pmc_rtd_summary.json")
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                traffic = json.load(f).get("hbm_bytes_per_launch")
+        evals = W * world * args.steps
+        line = {
+            "metric": METRIC,
+            "value": evals / dt,
+            "unit": "evals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {"workload": "c4 joint CE+RTD log-prob: %d walkers/GPU x %d wells x (5 gases CE + 5 tracers "
+                                   "RTD exponential, N=%d ages)" % (W, args.wells, N),
+                       "walkers_per_gpu": W, "wells": args.wells, "gases": 5, "tracers": 5, "ages": N,
+                       "parallelism": "walker blocks per GPU + RCCL all-gather of logp" if world > 1 else "single GPU"},
+            "roofline": {"bound": "valu_fp64", "achieved": achieved / 1e12, "peak": FP64_VALU_PEAK / 1e12,
+                         "unit": "TFLOP/s", "frac": achieved / FP64_VALU_PEAK, "traffic": traffic,
+                         "kernel": "rtd_conc_kernel", "kernel_ms": rtd_ms, "flop_per_launch": flops,
+                         "hbm": {"algorithmic_bytes": hbm_bytes, "achieved_GBps": hbm_bytes / (rtd_ms * 1e-3) / 1e9,
+                                 "peak_GBps": HBM_PEAK / 1e9,
+                                 "frac": hbm_bytes / (rtd_ms * 1e-3) / HBM_PEAK}},
+            "kernels_ms": {k: v[0] / max(v[1], 1) for k, v in ks.items()},
+            "geometry": info,
+        }
+        if not args.no_cpu_baseline and world == 1:
+            workers = min(16, os.cpu_count() or 1)
+            line["cpu_baseline"] = cpu_baseline(spec, theta_h, args.cpu_seconds, workers)
+        else:
+            line["cpu_baseline"] = None
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,222 @@
+/*
+ * ngrtd.h -- C ABI of libngrtd.so, the MI355X (gfx950) engine for the two
+ * log-likelihood hot paths of uz226/NobleGas_RTD_MCMC:
+ *
+ *   CE  : closed-equilibrium noble-gas forward model  (utils/noble_gas_utils.py)
+ *   RTD : residence-time-distribution convolution     (utils/convolution_integral_utils.py)
+ *
+ * and the per-walker log-probabilities built on them by the reference's PyMC3 models
+ * (ng_interp/noble_gas_mcmc.py:184-267, age_ens_runs_mcmc/run_age_mcmc_utils.py:275-397).
+ *
+ * Plain C: pointers + sizes, no framework types.  Every entry returns an int status
+ * (NGRTD_OK == 0, < 0 on API/device error; the message is ngrtd_last_error(ctx)).
+ * Invalid parameter VALUES are not errors: like the reference they propagate as
+ * NaN / -9999 sentinels / -inf log densities with status 0.
+ *
+ * Memory: every compute entry takes `mem` = NGRTD_MEM_HOST (pointers are host memory;
+ * the call stages through ctx-owned device buffers and returns after the results are
+ * back) or NGRTD_MEM_DEVICE (pointers are device memory; the call is enqueued on the
+ * ctx stream and returns immediately).  Float data is IEEE float64 throughout.
+ *
+ * Threading: a ctx is bound to one device and one stream; it is not re-entrant.  Create
+ * it after any fork() (the reference forks PyMC3 chains, run_age_mcmc_utils.py:416).
+ */
+#ifndef NGRTD_H
+#define NGRTD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NGRTD_ABI_VERSION 1
+
+enum ngrtd_status {
+    NGRTD_OK = 0,
+    NGRTD_EINVAL = -1,   /* bad argument / unsupported configuration */
+    NGRTD_EDEVICE = -2,  /* HIP runtime error */
+    NGRTD_ENOMEM = -3,   /* allocation failed */
+    NGRTD_ESTATE = -4    /* unknown handle / destroyed object */
+};
+
+enum ngrtd_mem { NGRTD_MEM_HOST = 0, NGRTD_MEM_DEVICE = 1 };
+
+/* noble gases, utils/noble_gas_utils.py:38-73,138-149 */
+enum ngrtd_gas { NGRTD_HE = 0, NGRTD_NE = 1, NGRTD_AR = 2, NGRTD_KR = 3, NGRTD_XE = 4 };
+
+/* lumped-parameter RTD models, utils/convolution_integral_utils.py:178-196 */
+enum ngrtd_rtd_model {
+    NGRTD_MOD_NONE = -1,
+    NGRTD_MOD_PISTON = 0,
+    NGRTD_MOD_EXPONENTIAL = 1,
+    NGRTD_MOD_EXP_PIST_FLOW = 2,
+    NGRTD_MOD_DISPERSION = 3
+};
+
+/* rad_accum, convolution_integral_utils.py:313-333 */
+enum ngrtd_accum { NGRTD_ACC_NONE = 0, NGRTD_ACC_HE3 = 1, NGRTD_ACC_HE4 = 2, NGRTD_ACC_SF6 = 3 };
+
+typedef struct ngrtd_ctx ngrtd_ctx;
+typedef struct ngrtd_plan ngrtd_plan;
+
+/* ------------------------------------------------------------------ context */
+int ngrtd_abi_version(void);
+int ngrtd_create(ngrtd_ctx** out, int device);
+int ngrtd_destroy(ngrtd_ctx* ctx);
+const char* ngrtd_last_error(const ngrtd_ctx* ctx);
+/* Enqueue on an external hipStream_t from now on (e.g. torch.cuda.current_stream()
+ * .cuda_stream); NULL selects HIP's null (default) stream.  Until the first call the ctx
+ * uses a non-blocking stream of its own. */
+int ngrtd_set_stream(ngrtd_ctx* ctx, void* hip_stream);
+int ngrtd_synchronize(ngrtd_ctx* ctx);
+/* When on, every plan launch brackets each kernel with hipEvents on the ctx stream;
+ * ngrtd_plan_kernel_stats() then reports the accumulated device time per kernel. */
+int ngrtd_set_profiling(ngrtd_ctx* ctx, int on);
+
+/* ------------------------------------------------------- CE forward model
+ * Replaces noble_gas_fun(gases, E, T, Ae, F, P, S).<method>() of
+ * utils/noble_gas_utils.py:75-261, vectorised over n independent parameter sets.
+ *   what = NGRTD_CE_*:   out is [n][n_gases] (LAPSE_RATE / VAPOR_PRESSURE: [n])
+ *   p_mode:              pressure as parse_P (:91-100): lapse_rate(E), '1atm', or P[i]
+ *   S may be NULL (salinity 0.0, the reference default).                            */
+enum ngrtd_ce_what {
+    NGRTD_CE_EXC_TOTAL = 0,     /* ce_exc(add_eq_conc=True)       :235-253 */
+    NGRTD_CE_EXC_EXCESS = 1,    /* ce_exc(add_eq_conc=False)      :235-253 */
+    NGRTD_CE_EQUIL_DRY = 2,     /* equil_conc_dry()               :216-232 */
+    NGRTD_CE_EQUIL = 3,         /* equil_conc()                   :202-213 */
+    NGRTD_CE_SOLUBILITY = 4,    /* solubility(gas)                :117-180 */
+    NGRTD_CE_VAPOR_PRESSURE = 5,/* vapor_pressure()               :184-199 */
+    NGRTD_CE_PRESSURE = 6       /* self.P after parse_P           :91-113  */
+};
+enum ngrtd_p_mode { NGRTD_P_LAPSE_RATE = 0, NGRTD_P_1ATM = 1, NGRTD_P_GIVEN = 2 };
+
+int ngrtd_ce_forward(ngrtd_ctx* ctx, int32_t what, int32_t p_mode,
+                     const double* E, const double* T, const double* Ae, const double* F,
+                     const double* P, const double* S, int64_t n,
+                     const int32_t* gas_ids, int32_t n_gases, double* out, int32_t mem);
+
+/* ----------------------------------------------------------- RTD series
+ * The C_t input of tracer_conv_integral(C_t, t_samp) (convolution_integral_utils.py:106):
+ *   c_by_age[k]   = np.flip(C_t.to_numpy().ravel())[k]  (age k, :336)
+ *   idx_by_age[k] = np.flip(C_t.index)[k]  (4He/SF6 accumulation, :323/:331); NULL => k
+ *   dtp           = floor(t_samp - C_t.index[-1])  (:172)
+ * Host memory; copied.  Returns a handle >= 0 in *series_id.                        */
+int ngrtd_series_create(ngrtd_ctx* ctx, const double* c_by_age, const double* idx_by_age,
+                        int64_t n, double dtp, int32_t* series_id);
+int ngrtd_series_destroy(ngrtd_ctx* ctx, int32_t series_id);
+
+/* -------------------------------------------- single-tracer convolution
+ * tracer_conv_integral.update_pars(...) + .convolve() (:111-142, :284-340) for n
+ * independent parameter sets (one call = n convolutions of one series).  Per-set
+ * arrays may be NULL when the model does not read them (eta: exp_pist_flow only,
+ * D: dispersion only).  t_half: per-set half-life array, or NULL to use t_half_const
+ * (<= 0 or NaN => lamba = 0, :117-121).  J: per-set accumulation rate (the J / J_sf6
+ * kwarg, already 10**log10J), or NULL to use J_const.                                */
+int ngrtd_conv(ngrtd_ctx* ctx, int32_t series_id, int32_t mod_type, int32_t accum,
+               const double* tau, const double* eta, const double* D,
+               const double* t_half, double t_half_const,
+               const double* J, double J_const,
+               int64_t n, double* out, int32_t mem);
+
+/* gen_g_tp() (:155-281): the normalised weight vector g[N] of one parameter set. */
+int ngrtd_rtd_weights(ngrtd_ctx* ctx, int32_t series_id, int32_t mod_type,
+                      double tau, double eta, double D, double* g_out, int32_t mem);
+
+/* convolve(g_tau=g) (:298-302): dot product with an externally supplied weight vector. */
+int ngrtd_conv_dot(ngrtd_ctx* ctx, int32_t series_id, const double* g, double t_half,
+                   int32_t accum, double J, double* out, int32_t mem);
+
+/* ------------------------------------------------- batched log-probability
+ * Parameter roles of one (walker, well) -- the PyMC3 free RVs in natural space.   */
+enum ngrtd_role {
+    NGRTD_ROLE_AE_BETA = 0,      /* noble_gas_mcmc.py:224 */
+    NGRTD_ROLE_F_BETA = 1,       /* :225 */
+    NGRTD_ROLE_E_BETA = 2,       /* :226 */
+    NGRTD_ROLE_M = 3,            /* :234 */
+    NGRTD_ROLE_B_BETA = 4,       /* :237 */
+    NGRTD_ROLE_NU_CE_BETA = 5,   /* :249 */
+    NGRTD_ROLE_TAU1 = 6,         /* run_age_mcmc_utils.py:286 */
+    NGRTD_ROLE_TAU2 = 7,         /* :302 */
+    NGRTD_ROLE_F1 = 8,           /* :303 */
+    NGRTD_ROLE_ETA1 = 9,         /* :312 */
+    NGRTD_ROLE_ETA2 = 10,        /* :316 */
+    NGRTD_ROLE_D1 = 11,          /* :320 */
+    NGRTD_ROLE_D2 = 12,          /* :324 */
+    NGRTD_ROLE_J = 13,           /* log10 J, :298 */
+    NGRTD_ROLE_THALF_BETA = 14,  /* :334 */
+    NGRTD_ROLE_LAMSF6 = 15,      /* :343 */
+    NGRTD_ROLE_NU_RTD_BETA = 16, /* :291 */
+    NGRTD_ROLE_COUNT = 17
+};
+
+#define NGRTD_MAX_GASES 5
+#define NGRTD_MAX_TRACERS 8
+
+typedef struct {
+    int32_t series_id;
+    int32_t accum;          /* enum ngrtd_accum */
+    double t_half;          /* decay half-life (H3/He3: 12.34); <= 0 => none */
+    double J;               /* fixed accumulation rate (10**log10J or J_sf6) if not sampled */
+    int32_t is_cfc12;       /* per-walker decay from the thalf_cfc role (:107-109) */
+    int32_t is_sf6;         /* cout *= (1 + lamsf6) when the lamsf6 role is present (:160-161) */
+} ngrtd_tracer_desc;
+
+enum ngrtd_flags { NGRTD_WANT_LIKE = 1, NGRTD_WANT_PRIOR = 2, NGRTD_WANT_JACOBIAN = 4 };
+
+typedef struct {
+    int32_t n_wells;                        /* L */
+    int32_t n_params;                       /* P (rows of theta per well) */
+    int32_t role_index[NGRTD_ROLE_COUNT];   /* row of each role within P, -1 = absent */
+    int32_t flags;                          /* enum ngrtd_flags */
+    /* CE block (ng_interp/noble_gas_mcmc.py:184-267) */
+    int32_t ce_enabled;
+    int32_t ce_n_gases;
+    int32_t ce_gas_ids[NGRTD_MAX_GASES];
+    const double* ce_obs;                   /* [L][G] */
+    const double* ce_sd;                    /* [L][G] */
+    const double* ce_E_min;                 /* [L] */
+    double ce_E_max, ce_logA_min, ce_logA_max, ce_logF_min, ce_logF_max;
+    double ce_b_min, ce_b_max, ce_m_mu, ce_m_sd, ce_nu_min, ce_nu_max;
+    double ce_beta_a[5], ce_beta_b[5];      /* Beta priors: Ae, F, E, b, nu */
+    /* RTD block (run_age_mcmc_utils.py:275-397) */
+    int32_t rtd_enabled;
+    int32_t n_tracers;                      /* K */
+    int32_t mod_type1, mod_type2;           /* enum ngrtd_rtd_model; mod_type2 = NONE if single */
+    ngrtd_tracer_desc tracers[NGRTD_MAX_TRACERS];
+    const double* rtd_obs;                  /* [L][K] */
+    const double* rtd_sd;                   /* [L][K] */
+    double tau1_lo, tau1_hi, tau2_lo, tau2_hi, f1_lo, f1_hi;
+    double eta1_lo, eta1_hi, eta2_lo, eta2_hi, D1_lo, D1_hi, D2_lo, D2_hi;
+    double J_mu, J_sd, thalf_lo, thalf_hi, thalf_a, thalf_b, lamsf6_sd;
+    double rtd_nu_min, rtd_nu_max, rtd_nu_a, rtd_nu_b;
+} ngrtd_model_desc;
+
+int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* desc, int64_t max_walkers,
+                      ngrtd_plan** out);
+int ngrtd_plan_destroy(ngrtd_plan* plan);
+
+/* logp[w] = sum over wells of (log-likelihood + log-prior [+ log|Jacobian|]) for theta
+ * laid out structure-of-arrays [P][L][W] (float64).  W <= max_walkers.               */
+int ngrtd_logp(ngrtd_plan* plan, const double* theta, int64_t W, double* logp, int32_t mem);
+
+/* Forward model outputs of the plan (posterior predictive, run_age_mcmc.py:251-319,
+ * noble_gas_mcmc.py:645-653): ce_out [G][L][W] (may be NULL), rtd_out [K][L][W]
+ * (may be NULL).                                                                     */
+int ngrtd_forward(ngrtd_plan* plan, const double* theta, int64_t W, double* ce_out,
+                  double* rtd_out, int32_t mem);
+
+/* Accumulated device time (ms) and launch count of each kernel the plan launched while
+ * profiling was on: index 0 = RTD convolution kernel, 1 = per-unit CE/likelihood kernel,
+ * 2 = per-walker reduction.  times_ms/counts have room for n entries; resets if reset. */
+int ngrtd_plan_kernel_stats(ngrtd_plan* plan, double* times_ms, int64_t* counts, int32_t n,
+                            int32_t reset);
+
+/* Launch geometry the plan chose for its RTD kernel (units per lane, waves per block,
+ * blocks, ages per LDS slice, channels): for the roofline accounting in bench.py.    */
+int ngrtd_plan_info(ngrtd_plan* plan, int64_t W, int64_t* info, int32_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NGRTD_H */

@@ -1,0 +1,173 @@
+"""ctypes binding of libngrtd.so (include/ngrtd.h).
+
+This is the only way the package reaches the device: there is no CPU fallback.  If the
+library is missing (not built) or no GPU is visible, every compute entry raises.
+"""
+import ctypes as C
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libngrtd.so")
+
+NGRTD_OK, NGRTD_EINVAL, NGRTD_EDEVICE, NGRTD_ENOMEM, NGRTD_ESTATE = 0, -1, -2, -3, -4
+MEM_HOST, MEM_DEVICE = 0, 1
+MAX_GASES, MAX_TRACERS, ROLE_COUNT = 5, 8, 17
+MOD_NONE = -1
+CE_WHAT = {"ce_total": 0, "ce_excess": 1, "equil_dry": 2, "equil": 3, "solubility": 4,
+           "vapor_pressure": 5, "pressure": 6}
+P_MODE = {"lapse_rate": 0, "1atm": 1, "given": 2}
+WANT_LIKE, WANT_PRIOR, WANT_JACOBIAN = 1, 2, 4
+
+_dp = C.POINTER(C.c_double)
+_i32p = C.POINTER(C.c_int32)
+_i64p = C.POINTER(C.c_int64)
+
+
+class TracerDesc(C.Structure):
+    _fields_ = [("series_id", C.c_int32), ("accum", C.c_int32), ("t_half", C.c_double), ("J", C.c_double),
+                ("is_cfc12", C.c_int32), ("is_sf6", C.c_int32)]
+
+
+class ModelDesc(C.Structure):
+    _fields_ = [
+        ("n_wells", C.c_int32), ("n_params", C.c_int32), ("role_index", C.c_int32 * ROLE_COUNT),
+        ("flags", C.c_int32),
+        ("ce_enabled", C.c_int32), ("ce_n_gases", C.c_int32), ("ce_gas_ids", C.c_int32 * MAX_GASES),
+        ("ce_obs", _dp), ("ce_sd", _dp), ("ce_E_min", _dp),
+        ("ce_E_max", C.c_double), ("ce_logA_min", C.c_double), ("ce_logA_max", C.c_double),
+        ("ce_logF_min", C.c_double), ("ce_logF_max", C.c_double),
+        ("ce_b_min", C.c_double), ("ce_b_max", C.c_double), ("ce_m_mu", C.c_double), ("ce_m_sd", C.c_double),
+        ("ce_nu_min", C.c_double), ("ce_nu_max", C.c_double),
+        ("ce_beta_a", C.c_double * 5), ("ce_beta_b", C.c_double * 5),
+        ("rtd_enabled", C.c_int32), ("n_tracers", C.c_int32), ("mod_type1", C.c_int32), ("mod_type2", C.c_int32),
+        ("tracers", TracerDesc * MAX_TRACERS),
+        ("rtd_obs", _dp), ("rtd_sd", _dp),
+        ("tau1_lo", C.c_double), ("tau1_hi", C.c_double), ("tau2_lo", C.c_double), ("tau2_hi", C.c_double),
+        ("f1_lo", C.c_double), ("f1_hi", C.c_double),
+        ("eta1_lo", C.c_double), ("eta1_hi", C.c_double), ("eta2_lo", C.c_double), ("eta2_hi", C.c_double),
+        ("D1_lo", C.c_double), ("D1_hi", C.c_double), ("D2_lo", C.c_double), ("D2_hi", C.c_double),
+        ("J_mu", C.c_double), ("J_sd", C.c_double), ("thalf_lo", C.c_double), ("thalf_hi", C.c_double),
+        ("thalf_a", C.c_double), ("thalf_b", C.c_double), ("lamsf6_sd", C.c_double),
+        ("rtd_nu_min", C.c_double), ("rtd_nu_max", C.c_double), ("rtd_nu_a", C.c_double), ("rtd_nu_b", C.c_double),
+    ]
+
+
+# name -> (restype, argtypes): exactly the functions declared in include/ngrtd.h
+PROTOTYPES = {
+    "ngrtd_abi_version": (C.c_int, []),
+    "ngrtd_create": (C.c_int, [C.POINTER(C.c_void_p), C.c_int]),
+    "ngrtd_destroy": (C.c_int, [C.c_void_p]),
+    "ngrtd_last_error": (C.c_char_p, [C.c_void_p]),
+    "ngrtd_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "ngrtd_synchronize": (C.c_int, [C.c_void_p]),
+    "ngrtd_set_profiling": (C.c_int, [C.c_void_p, C.c_int]),
+    "ngrtd_ce_forward": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                   C.c_void_p, C.c_void_p, C.c_int64, _i32p, C.c_int32, C.c_void_p, C.c_int32]),
+    "ngrtd_series_create": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, C.c_double, _i32p]),
+    "ngrtd_series_destroy": (C.c_int, [C.c_void_p, C.c_int32]),
+    "ngrtd_conv": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
+                             C.c_void_p, C.c_double, C.c_void_p, C.c_double, C.c_int64, C.c_void_p, C.c_int32]),
+    "ngrtd_rtd_weights": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_double, C.c_double, C.c_double,
+                                    C.c_void_p, C.c_int32]),
+    "ngrtd_conv_dot": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_double, C.c_int32, C.c_double,
+                                 C.c_void_p, C.c_int32]),
+    "ngrtd_plan_create": (C.c_int, [C.c_void_p, C.POINTER(ModelDesc), C.c_int64, C.POINTER(C.c_void_p)]),
+    "ngrtd_plan_destroy": (C.c_int, [C.c_void_p]),
+    "ngrtd_logp": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int32]),
+    "ngrtd_forward": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int32]),
+    "ngrtd_plan_kernel_stats": (C.c_int, [C.c_void_p, _dp, _i64p, C.c_int32, C.c_int32]),
+    "ngrtd_plan_info": (C.c_int, [C.c_void_p, C.c_int64, _i64p, C.c_int32]),
+}
+
+
+class NgrtdError(RuntimeError):
+    pass
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def load():
+    """Load libngrtd.so (raises if it has not been built)."""
+    global _lib
+    with _lib_lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise NgrtdError("libngrtd.so not found at %s: build it with "
+                                 "`python -c 'import __graft_entry__ as g; g.build()'`" % LIB_PATH)
+            # One HIP runtime per process: torch bundles its own libamdhip64.so.7 (same
+            # soname as /opt/rocm's).  Import torch first so libngrtd binds to that copy;
+            # loading /opt/rocm's first leaves torch unable to see the GPU.
+            try:
+                import torch  # noqa: F401
+            except ImportError:
+                pass
+            lib = C.CDLL(LIB_PATH)
+            for name, (res, args) in PROTOTYPES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            if lib.ngrtd_abi_version() != 1:
+                raise NgrtdError("libngrtd ABI mismatch")
+            _lib = lib
+    return _lib
+
+
+def dptr(a):
+    """double* of a contiguous float64 numpy array (or None)."""
+    if a is None:
+        return None
+    return a.ctypes.data_as(_dp)
+
+
+class Context:
+    """One ngrtd_ctx per (process, device); created lazily, re-created after fork()."""
+    _instances = {}
+
+    def __init__(self, device=0):
+        self.lib = load()
+        self.device = device
+        h = C.c_void_p()
+        st = self.lib.ngrtd_create(C.byref(h), int(device))
+        if st != NGRTD_OK:
+            raise NgrtdError("ngrtd_create(device=%d) failed with status %d (no GPU visible?)" % (device, st))
+        self.h = h
+        self.pid = os.getpid()
+
+    @classmethod
+    def get(cls, device=0):
+        key = (os.getpid(), device)
+        ctx = cls._instances.get(key)
+        if ctx is None:
+            ctx = cls(device)
+            cls._instances[key] = ctx
+        return ctx
+
+    def check(self, status, what=""):
+        if status != NGRTD_OK:
+            msg = self.lib.ngrtd_last_error(self.h)
+            raise NgrtdError("%s failed (status %d): %s" % (what, status, msg.decode() if msg else ""))
+
+    def set_stream(self, stream_handle):
+        self.check(self.lib.ngrtd_set_stream(self.h, C.c_void_p(int(stream_handle))), "ngrtd_set_stream")
+
+    def synchronize(self):
+        self.check(self.lib.ngrtd_synchronize(self.h), "ngrtd_synchronize")
+
+    def set_profiling(self, on):
+        self.check(self.lib.ngrtd_set_profiling(self.h, int(bool(on))), "ngrtd_set_profiling")
+
+    def series_create(self, c_by_age, idx_by_age, dtp):
+        c = np.ascontiguousarray(c_by_age, dtype=np.float64)
+        i = np.ascontiguousarray(idx_by_age, dtype=np.float64)
+        sid = C.c_int32()
+        self.check(self.lib.ngrtd_series_create(self.h, dptr(c), dptr(i), c.shape[0], float(dtp), C.byref(sid)),
+                   "ngrtd_series_create")
+        return sid.value
+
+    def series_destroy(self, sid):
+        self.check(self.lib.ngrtd_series_destroy(self.h, int(sid)), "ngrtd_series_destroy")

@@ -1,0 +1,783 @@
+// ngrtd.hip -- host side of libngrtd.so: the C ABI of include/ngrtd.h.
+//
+// Owns device state (series, channel tables, plan workspaces), builds the RTD channel
+// tables (fixed-half-life decay and 4He/SF6 accumulation folded per tracer, as
+// convolution_integral_utils.py:305-333 applies them), chooses the launch geometry and
+// enqueues the kernels of ngrtd_kernels.hpp on the context stream.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "../../include/ngrtd.h"
+#include "ngrtd_kernels.hpp"
+
+using namespace ngrtd;
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    ~DevBuf() { if (p) (void)hipFree(p); }
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
+        hipError_t e = hipMalloc(&p, bytes ? bytes : 16);
+        if (e == hipSuccess) cap = bytes;
+        return e;
+    }
+    double* d() const { return static_cast<double*>(p); }
+};
+
+struct SeriesHost {
+    std::vector<double> c, idx;
+    double dtp = 0.0;
+    int64_t n = 0;
+};
+
+struct TableDev {
+    DevBuf buf;
+    int C = 0, CP = 0;
+    int chan_tracer[kMaxChan] = {}, chan_isB[kMaxChan] = {}, chan_lamw[kMaxChan] = {};
+};
+
+struct LaunchStats {
+    double ms[3] = {0, 0, 0};
+    int64_t n[3] = {0, 0, 0};
+};
+
+}  // namespace
+
+struct ngrtd_ctx {
+    int device = 0;
+    hipStream_t own = nullptr;
+    hipStream_t stream = nullptr;
+    std::string err;
+    bool profiling = false;
+    int next_series = 0;
+    std::map<int, SeriesHost> series;
+    // conv-API channel tables keyed by (series, lambda bits, accum, per-set decay)
+    std::map<std::tuple<int, uint64_t, int, int>, std::unique_ptr<TableDev>> tables;
+    DevBuf stage[8];
+    std::vector<hipEvent_t> event_pool;   // recycled profiling events
+    hipEvent_t take_event() {
+        if (!event_pool.empty()) { hipEvent_t e = event_pool.back(); event_pool.pop_back(); return e; }
+        hipEvent_t e = nullptr;
+        (void)hipEventCreate(&e);
+        return e;
+    }
+};
+
+namespace {
+struct PendingTiming { int kind; hipEvent_t a, b; };
+}
+
+struct ngrtd_plan {
+    ngrtd_ctx* ctx = nullptr;
+    ngrtd_model_desc desc{};
+    int64_t max_w = 0;
+    // device copies of the model data
+    DevBuf ce_obs, ce_sd, ce_emin, rtd_obs, rtd_sd;
+    TableDev table;
+    int N = 0;
+    double tp0 = 1e-5, dtp = 0.0;
+    // workspaces
+    DevBuf conc, ulogp, theta_stage, out_stage, ce_stage;
+    RtdArgs rtd{};
+    UnitArgs unit{};
+    LaunchStats stats;
+    std::vector<PendingTiming> pending;   // event pairs not yet read back (no host sync per launch)
+};
+
+static int drain_timings(ngrtd_plan* p);
+
+// ------------------------------------------------------------------ helpers
+static int set_err(ngrtd_ctx* ctx, int code, const char* fmt, ...) __attribute__((format(printf, 3, 4)));
+static int set_err(ngrtd_ctx* ctx, int code, const char* fmt, ...) {
+    if (ctx) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        ctx->err = buf;
+    }
+    return code;
+}
+
+#define HIP_TRY(ctx, expr)                                                                        \
+    do {                                                                                          \
+        hipError_t _e = (expr);                                                                   \
+        if (_e != hipSuccess)                                                                     \
+            return set_err((ctx), NGRTD_EDEVICE, "%s: %s (%s:%d)", #expr, hipGetErrorString(_e),   \
+                           __FILE__, __LINE__);                                                   \
+    } while (0)
+
+static int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+static double lam_of(double t_half) {
+    // update_pars / thalf_2_lambda (:117-121, :150): a falsy t_half means no decay
+    return (t_half != 0.0) ? -1 * std::log(0.5) / t_half : 0.0;
+}
+
+static double host_betaln(double a, double b) { return std::lgamma(a) + std::lgamma(b) - std::lgamma(a + b); }
+
+// Build the channel table [N][CP] of a set of tracers.  Per tracer: A_k = c_k d_k and,
+// for 4He/SF6 accumulation, B_k = idx_k d_k (conc = (sum A w + J sum B w) / sum w);
+// d_k = exp(-lam tp_k) (3He: 1 - exp(-lam tp_k)) unless the decay is per-unit (lamw).
+// An identically-zero A (He4_ter: C_t * 0.0, run_age_mcmc.py:212) is dropped.
+struct TracerBuild {
+    const SeriesHost* s;
+    int accum;
+    double lam;
+    bool lamw;
+};
+
+static int build_table(ngrtd_ctx* ctx, const std::vector<TracerBuild>& trs, TableDev& tab) {
+    const int64_t N = trs[0].s->n;
+    std::vector<std::vector<double>> cols;
+    int C = 0;
+    for (size_t t = 0; t < trs.size(); ++t) {
+        const TracerBuild& tb = trs[t];
+        if (tb.s->n != N) return set_err(ctx, NGRTD_EINVAL, "tracers must share the series length");
+        std::vector<double> d(N, 1.0);
+        if (!tb.lamw) {
+            for (int64_t k = 0; k < N; ++k) {
+                const double tp = (k == 0) ? (0.0 + 1e-5) + tb.s->dtp : (double)k + tb.s->dtp;
+                const double e = std::exp(-tb.lam * tp);
+                d[k] = (tb.accum == NGRTD_ACC_HE3) ? (1 - e) : e;
+            }
+        } else if (tb.accum == NGRTD_ACC_HE3) {
+            return set_err(ctx, NGRTD_EINVAL, "per-unit decay with 3He accumulation is not supported");
+        }
+        bool anyA = false;
+        std::vector<double> A(N), B;
+        for (int64_t k = 0; k < N; ++k) {
+            A[k] = tb.s->c[k] * d[k];
+            anyA |= (tb.s->c[k] != 0.0);
+        }
+        const bool hasB = (tb.accum == NGRTD_ACC_HE4 || tb.accum == NGRTD_ACC_SF6);
+        if (anyA || !hasB) {
+            if (C >= kMaxChan) return set_err(ctx, NGRTD_EINVAL, "more than %d RTD channels", kMaxChan);
+            tab.chan_tracer[C] = (int)t; tab.chan_isB[C] = 0; tab.chan_lamw[C] = tb.lamw;
+            cols.push_back(std::move(A));
+            ++C;
+        }
+        if (hasB) {
+            if (C >= kMaxChan) return set_err(ctx, NGRTD_EINVAL, "more than %d RTD channels", kMaxChan);
+            B.resize(N);
+            for (int64_t k = 0; k < N; ++k) B[k] = tb.s->idx[k] * d[k];
+            tab.chan_tracer[C] = (int)t; tab.chan_isB[C] = 1; tab.chan_lamw[C] = tb.lamw;
+            cols.push_back(std::move(B));
+            ++C;
+        }
+    }
+    tab.C = C;
+    tab.CP = (C + 1) & ~1;
+    std::vector<double> h((size_t)N * tab.CP, 0.0);
+    for (int c = 0; c < C; ++c)
+        for (int64_t k = 0; k < N; ++k) h[(size_t)k * tab.CP + c] = cols[c][k];
+    HIP_TRY(ctx, tab.buf.ensure(h.size() * sizeof(double) + 16));
+    HIP_TRY(ctx, hipMemcpy(tab.buf.p, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
+    return NGRTD_OK;
+}
+
+// ------------------------------------------------------- RTD kernel dispatch
+typedef void (*RtdKernel)(RtdArgs);
+
+template <int R, int C, bool L>
+static RtdKernel rtd_k() { return rtd_conc_kernel<R, C, L>; }
+
+static RtdKernel pick_rtd(int R, int C, bool lamw) {
+#define NGRTD_CASE_C(RR, LL)                                                                          \
+    switch (C) {                                                                                      \
+    case 1: return rtd_k<RR, 1, LL>(); case 2: return rtd_k<RR, 2, LL>(); case 3: return rtd_k<RR, 3, LL>(); \
+    case 4: return rtd_k<RR, 4, LL>(); case 5: return rtd_k<RR, 5, LL>(); case 6: return rtd_k<RR, 6, LL>(); \
+    case 7: return rtd_k<RR, 7, LL>(); case 8: return rtd_k<RR, 8, LL>(); default: return nullptr;      \
+    }
+    if (lamw) {
+        if (R == 1) { NGRTD_CASE_C(1, true) }
+        if (R == 2) { NGRTD_CASE_C(2, true) }
+        return nullptr;
+    }
+    if (R == 1) { NGRTD_CASE_C(1, false) }
+    if (R == 2) { NGRTD_CASE_C(2, false) }
+    if (R == 4) { NGRTD_CASE_C(4, false) }
+#undef NGRTD_CASE_C
+    return nullptr;
+}
+
+struct RtdGeom {
+    int R, NW, LW, blocks;
+    size_t lds;
+};
+
+static RtdGeom rtd_geometry(int64_t U, int N, int C, bool lamw) {
+    RtdGeom g{};
+    const int CP = (C + 1) & ~1;
+    int Rmax = (C <= 5) ? 4 : 2;
+    if (lamw) Rmax = std::min(Rmax, 2);
+    int R = Rmax;
+    while (R > 1 && cdiv(U, 64 * R) < 512) R /= 2;
+    g.R = R;
+    g.NW = 4;
+    const int max_rows = (64 * 1024) / (CP * 8);
+    g.LW = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(N, g.NW), max_rows / g.NW));
+    g.blocks = (int)cdiv(U, 64 * R);
+    const size_t tab_bytes = (size_t)g.NW * g.LW * CP * sizeof(double);
+    const size_t comb_bytes = (size_t)g.NW * R * (C + 1) * 64 * sizeof(double);
+    g.lds = std::max(tab_bytes, comb_bytes);
+    return g;
+}
+
+static int launch_rtd(ngrtd_ctx* ctx, RtdArgs a, bool lamw, hipStream_t st, RtdGeom* out_geom = nullptr) {
+    if (a.U <= 0) return NGRTD_OK;
+    const RtdGeom g = rtd_geometry(a.U, a.N, a.C, lamw);
+    if (out_geom) *out_geom = g;
+    RtdKernel k = pick_rtd(g.R, a.C, lamw);
+    if (!k) return set_err(ctx, NGRTD_EINVAL, "no RTD kernel for R=%d C=%d", g.R, a.C);
+    a.LW = g.LW;
+    hipLaunchKernelGGL(k, dim3(g.blocks), dim3(64 * g.NW), g.lds, st, a);
+    HIP_TRY(ctx, hipGetLastError());
+    return NGRTD_OK;
+}
+
+static hipStream_t S(ngrtd_ctx* c) { return c->stream; }
+
+// Staging: host pointers are copied into ctx buffers; device pointers pass through.
+static int stage_in(ngrtd_ctx* ctx, int slot, const double* src, int64_t n, int32_t mem, const double** out) {
+    if (!src) { *out = nullptr; return NGRTD_OK; }
+    if (mem == NGRTD_MEM_DEVICE) { *out = src; return NGRTD_OK; }
+    HIP_TRY(ctx, ctx->stage[slot].ensure((size_t)n * sizeof(double)));
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->stage[slot].p, src, (size_t)n * sizeof(double), hipMemcpyHostToDevice, S(ctx)));
+    *out = ctx->stage[slot].d();
+    return NGRTD_OK;
+}
+
+#define NG_CHECK(x)                 \
+    do {                            \
+        int _r = (x);               \
+        if (_r != NGRTD_OK) return _r; \
+    } while (0)
+
+extern "C" {
+
+int ngrtd_abi_version(void) { return NGRTD_ABI_VERSION; }
+
+int ngrtd_create(ngrtd_ctx** out, int device) {
+    if (!out) return NGRTD_EINVAL;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return NGRTD_EDEVICE;
+    if (device < 0 || device >= n) return NGRTD_EINVAL;
+    if (hipSetDevice(device) != hipSuccess) return NGRTD_EDEVICE;
+    auto* c = new (std::nothrow) ngrtd_ctx;
+    if (!c) return NGRTD_ENOMEM;
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) { delete c; return NGRTD_EDEVICE; }
+    c->stream = c->own;
+    *out = c;
+    return NGRTD_OK;
+}
+
+int ngrtd_destroy(ngrtd_ctx* ctx) {
+    if (!ctx) return NGRTD_ESTATE;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
+    ctx->event_pool.clear();
+    ctx->tables.clear();
+    for (auto& b : ctx->stage) { if (b.p) (void)hipFree(b.p); b.p = nullptr; b.cap = 0; }
+    if (ctx->own) (void)hipStreamDestroy(ctx->own);
+    delete ctx;
+    return NGRTD_OK;
+}
+
+const char* ngrtd_last_error(const ngrtd_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int ngrtd_set_stream(ngrtd_ctx* ctx, void* s) {
+    if (!ctx) return NGRTD_ESTATE;
+    ctx->stream = static_cast<hipStream_t>(s);   // NULL is HIP's null (default) stream
+    return NGRTD_OK;
+}
+
+int ngrtd_synchronize(ngrtd_ctx* ctx) {
+    if (!ctx) return NGRTD_ESTATE;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return NGRTD_OK;
+}
+
+int ngrtd_set_profiling(ngrtd_ctx* ctx, int on) {
+    if (!ctx) return NGRTD_ESTATE;
+    ctx->profiling = on != 0;
+    return NGRTD_OK;
+}
+
+// ----------------------------------------------------------------- CE forward
+int ngrtd_ce_forward(ngrtd_ctx* ctx, int32_t what, int32_t p_mode, const double* E, const double* T,
+                     const double* Ae, const double* F, const double* P, const double* Sal, int64_t n,
+                     const int32_t* gas_ids, int32_t n_gases, double* out, int32_t mem) {
+    if (!ctx) return NGRTD_ESTATE;
+    if (n < 0 || !out) return set_err(ctx, NGRTD_EINVAL, "bad n/out");
+    if (what < 0 || what > NGRTD_CE_PRESSURE) return set_err(ctx, NGRTD_EINVAL, "bad 'what' %d", what);
+    if (p_mode < 0 || p_mode > 2) return set_err(ctx, NGRTD_EINVAL, "bad p_mode %d", p_mode);
+    if (p_mode == NGRTD_P_GIVEN && !P) return set_err(ctx, NGRTD_EINVAL, "P required for NGRTD_P_GIVEN");
+    const bool scalar_out = (what == NGRTD_CE_VAPOR_PRESSURE || what == NGRTD_CE_PRESSURE);
+    if (!scalar_out && (n_gases < 1 || n_gases > kMaxGas || !gas_ids))
+        return set_err(ctx, NGRTD_EINVAL, "n_gases must be 1..5");
+    if (n == 0) return NGRTD_OK;
+    CeArgs a{};
+    a.what = what; a.p_mode = p_mode; a.G = scalar_out ? 1 : n_gases; a.n = n;
+    for (int j = 0; j < (scalar_out ? 0 : n_gases); ++j) {
+        if (gas_ids[j] < 0 || gas_ids[j] > 4) return set_err(ctx, NGRTD_EINVAL, "bad gas id %d", gas_ids[j]);
+        a.gas[j] = gas_ids[j];
+    }
+    NG_CHECK(stage_in(ctx, 0, E, n, mem, &a.E));
+    NG_CHECK(stage_in(ctx, 1, T, n, mem, &a.T));
+    NG_CHECK(stage_in(ctx, 2, Ae, n, mem, &a.Ae));
+    NG_CHECK(stage_in(ctx, 3, F, n, mem, &a.F));
+    NG_CHECK(stage_in(ctx, 4, (p_mode == NGRTD_P_GIVEN) ? P : nullptr, n, mem, &a.P));
+    NG_CHECK(stage_in(ctx, 5, Sal, n, mem, &a.S));
+    const int64_t nout = n * a.G;
+    if (mem == NGRTD_MEM_DEVICE) {
+        a.out = out;
+    } else {
+        HIP_TRY(ctx, ctx->stage[6].ensure((size_t)nout * sizeof(double)));
+        a.out = ctx->stage[6].d();
+    }
+    hipLaunchKernelGGL(ce_forward_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, S(ctx), a);
+    HIP_TRY(ctx, hipGetLastError());
+    if (mem != NGRTD_MEM_DEVICE) {
+        HIP_TRY(ctx, hipMemcpyAsync(out, a.out, (size_t)nout * sizeof(double), hipMemcpyDeviceToHost, S(ctx)));
+        HIP_TRY(ctx, hipStreamSynchronize(S(ctx)));
+    }
+    return NGRTD_OK;
+}
+
+// --------------------------------------------------------------------- series
+int ngrtd_series_create(ngrtd_ctx* ctx, const double* c_by_age, const double* idx_by_age, int64_t n,
+                        double dtp, int32_t* series_id) {
+    if (!ctx) return NGRTD_ESTATE;
+    if (!c_by_age || n <= 0 || n > (int64_t)1 << 30 || !series_id)
+        return set_err(ctx, NGRTD_EINVAL, "bad series arguments");
+    SeriesHost s;
+    s.n = n;
+    s.dtp = dtp;
+    s.c.assign(c_by_age, c_by_age + n);
+    s.idx.resize(n);
+    for (int64_t k = 0; k < n; ++k) s.idx[k] = idx_by_age ? idx_by_age[k] : (double)k;
+    const int id = ctx->next_series++;
+    ctx->series[id] = std::move(s);
+    *series_id = id;
+    return NGRTD_OK;
+}
+
+int ngrtd_series_destroy(ngrtd_ctx* ctx, int32_t id) {
+    if (!ctx) return NGRTD_ESTATE;
+    if (!ctx->series.erase(id)) return set_err(ctx, NGRTD_ESTATE, "unknown series %d", id);
+    for (auto it = ctx->tables.begin(); it != ctx->tables.end();)
+        it = (std::get<0>(it->first) == id) ? ctx->tables.erase(it) : std::next(it);
+    return NGRTD_OK;
+}
+
+static const SeriesHost* find_series(ngrtd_ctx* ctx, int id) {
+    auto it = ctx->series.find(id);
+    return it == ctx->series.end() ? nullptr : &it->second;
+}
+
+// --------------------------------------------------------- single-tracer conv
+int ngrtd_conv(ngrtd_ctx* ctx, int32_t series_id, int32_t mod_type, int32_t accum, const double* tau,
+               const double* eta, const double* D, const double* t_half, double t_half_const,
+               const double* J, double J_const, int64_t n, double* out, int32_t mem) {
+    if (!ctx) return NGRTD_ESTATE;
+    const SeriesHost* s = find_series(ctx, series_id);
+    if (!s) return set_err(ctx, NGRTD_ESTATE, "unknown series %d", series_id);
+    if (mod_type < NGRTD_MOD_PISTON || mod_type > NGRTD_MOD_DISPERSION)
+        return set_err(ctx, NGRTD_EINVAL, "bad mod_type %d", mod_type);
+    if (accum < 0 || accum > 3) return set_err(ctx, NGRTD_EINVAL, "bad accum %d", accum);
+    if (!tau || !out || n < 0) return set_err(ctx, NGRTD_EINVAL, "tau/out required");
+    if (mod_type == NGRTD_MOD_EXP_PIST_FLOW && !eta) return set_err(ctx, NGRTD_EINVAL, "eta required");
+    if (mod_type == NGRTD_MOD_DISPERSION && !D) return set_err(ctx, NGRTD_EINVAL, "D required");
+    if (n == 0) return NGRTD_OK;
+    const bool lamw = t_half != nullptr;
+    const double lam = lamw ? 0.0 : lam_of(t_half_const);
+    uint64_t lb;
+    std::memcpy(&lb, &lam, 8);
+    auto key = std::make_tuple((int)series_id, lb, (int)accum, (int)lamw);
+    auto it = ctx->tables.find(key);
+    if (it == ctx->tables.end()) {
+        auto t = std::make_unique<TableDev>();
+        NG_CHECK(build_table(ctx, {TracerBuild{s, accum, lam, lamw}}, *t));
+        it = ctx->tables.emplace(key, std::move(t)).first;
+    }
+    const TableDev& tab = *it->second;
+    // theta rows: 0 tau, 1 eta, 2 D, 3 t_half, 4 J (device, [5][n])
+    HIP_TRY(ctx, ctx->stage[0].ensure((size_t)5 * n * sizeof(double)));
+    double* th = ctx->stage[0].d();
+    const double* rows[5] = {tau, eta, D, t_half, J};
+    const hipMemcpyKind kind = (mem == NGRTD_MEM_DEVICE) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    for (int r = 0; r < 5; ++r)
+        if (rows[r]) HIP_TRY(ctx, hipMemcpyAsync(th + (size_t)r * n, rows[r], (size_t)n * sizeof(double), kind, S(ctx)));
+    RtdArgs a{};
+    a.theta = th; a.U = n;
+    a.row_tau[0] = 0; a.row_tau[1] = -1;
+    a.row_eta[0] = eta ? 1 : -1; a.row_eta[1] = -1;
+    a.row_D[0] = D ? 2 : -1; a.row_D[1] = -1;
+    a.row_f1 = -1; a.row_lamsf6 = -1;
+    a.row_thalf = lamw ? 3 : -1; a.thalf_a = 1.0; a.thalf_b = 0.0;
+    a.row_J = J ? 4 : -1; a.J_is_log10 = 0;
+    a.tab = tab.buf.d(); a.N = (int)s->n; a.C = tab.C; a.CP = tab.CP;
+    a.tp0 = (0.0 + 1e-5) + s->dtp; a.dtp = s->dtp;
+    a.mod[0] = mod_type; a.mod[1] = MOD_NONE;
+    a.K = 1;
+    for (int c = 0; c < tab.C; ++c) { a.chan_tracer[c] = tab.chan_tracer[c]; a.chan_isB[c] = tab.chan_isB[c]; a.chan_lamw[c] = tab.chan_lamw[c]; }
+    a.tr_sf6[0] = 0; a.tr_J[0] = J_const;
+    if (mem == NGRTD_MEM_DEVICE) {
+        a.conc = out;
+    } else {
+        HIP_TRY(ctx, ctx->stage[1].ensure((size_t)n * sizeof(double)));
+        a.conc = ctx->stage[1].d();
+    }
+    NG_CHECK(launch_rtd(ctx, a, lamw, S(ctx)));
+    if (mem != NGRTD_MEM_DEVICE) {
+        HIP_TRY(ctx, hipMemcpyAsync(out, a.conc, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, S(ctx)));
+        HIP_TRY(ctx, hipStreamSynchronize(S(ctx)));
+    }
+    return NGRTD_OK;
+}
+
+int ngrtd_rtd_weights(ngrtd_ctx* ctx, int32_t series_id, int32_t mod_type, double tau, double eta, double D,
+                      double* g_out, int32_t mem) {
+    if (!ctx) return NGRTD_ESTATE;
+    const SeriesHost* s = find_series(ctx, series_id);
+    if (!s) return set_err(ctx, NGRTD_ESTATE, "unknown series %d", series_id);
+    if (mod_type < NGRTD_MOD_PISTON || mod_type > NGRTD_MOD_DISPERSION || !g_out)
+        return set_err(ctx, NGRTD_EINVAL, "bad mod_type/g_out");
+    double* g = g_out;
+    if (mem != NGRTD_MEM_DEVICE) {
+        HIP_TRY(ctx, ctx->stage[2].ensure((size_t)s->n * sizeof(double)));
+        g = ctx->stage[2].d();
+    }
+    hipLaunchKernelGGL(rtd_weights_kernel, dim3(1), dim3(1024), 0, S(ctx), mod_type, tau, eta, D,
+                       (0.0 + 1e-5) + s->dtp, s->dtp, (int)s->n, g);
+    HIP_TRY(ctx, hipGetLastError());
+    if (mem != NGRTD_MEM_DEVICE) {
+        HIP_TRY(ctx, hipMemcpyAsync(g_out, g, (size_t)s->n * sizeof(double), hipMemcpyDeviceToHost, S(ctx)));
+        HIP_TRY(ctx, hipStreamSynchronize(S(ctx)));
+    }
+    return NGRTD_OK;
+}
+
+int ngrtd_conv_dot(ngrtd_ctx* ctx, int32_t series_id, const double* g, double t_half, int32_t accum, double J,
+                   double* out, int32_t mem) {
+    if (!ctx) return NGRTD_ESTATE;
+    const SeriesHost* s = find_series(ctx, series_id);
+    if (!s) return set_err(ctx, NGRTD_ESTATE, "unknown series %d", series_id);
+    if (!g || !out || accum < 0 || accum > 3) return set_err(ctx, NGRTD_EINVAL, "bad arguments");
+    const int64_t n = s->n;
+    HIP_TRY(ctx, ctx->stage[3].ensure((size_t)2 * n * sizeof(double)));
+    double* cs = ctx->stage[3].d();
+    HIP_TRY(ctx, hipMemcpyAsync(cs, s->c.data(), n * sizeof(double), hipMemcpyHostToDevice, S(ctx)));
+    HIP_TRY(ctx, hipMemcpyAsync(cs + n, s->idx.data(), n * sizeof(double), hipMemcpyHostToDevice, S(ctx)));
+    const double* gd;
+    NG_CHECK(stage_in(ctx, 4, g, n, mem, &gd));
+    double* o = out;
+    if (mem != NGRTD_MEM_DEVICE) {
+        HIP_TRY(ctx, ctx->stage[5].ensure(sizeof(double)));
+        o = ctx->stage[5].d();
+    }
+    hipLaunchKernelGGL(conv_dot_kernel, dim3(1), dim3(1024), 0, S(ctx), cs, cs + n, gd, lam_of(t_half), accum, J,
+                       (0.0 + 1e-5) + s->dtp, s->dtp, (int)n, o);
+    HIP_TRY(ctx, hipGetLastError());
+    if (mem != NGRTD_MEM_DEVICE) {
+        HIP_TRY(ctx, hipMemcpyAsync(out, o, sizeof(double), hipMemcpyDeviceToHost, S(ctx)));
+        HIP_TRY(ctx, hipStreamSynchronize(S(ctx)));
+    }
+    return NGRTD_OK;
+}
+
+// ---------------------------------------------------------------------- plans
+static int upload(ngrtd_ctx* ctx, DevBuf& b, const double* src, size_t n) {
+    HIP_TRY(ctx, b.ensure(n * sizeof(double) + 16));
+    if (n) HIP_TRY(ctx, hipMemcpy(b.p, src, n * sizeof(double), hipMemcpyHostToDevice));
+    return NGRTD_OK;
+}
+
+int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_walkers, ngrtd_plan** out) {
+    if (!ctx) return NGRTD_ESTATE;
+    if (!d || !out || max_walkers <= 0) return set_err(ctx, NGRTD_EINVAL, "bad plan arguments");
+    *out = nullptr;
+    const int L = d->n_wells;
+    if (L <= 0 || d->n_params <= 0) return set_err(ctx, NGRTD_EINVAL, "n_wells/n_params must be > 0");
+    if (!d->ce_enabled && !d->rtd_enabled) return set_err(ctx, NGRTD_EINVAL, "plan needs a CE or an RTD block");
+    const int* ri = d->role_index;
+    for (int r = 0; r < NGRTD_ROLE_COUNT; ++r)
+        if (ri[r] >= d->n_params) return set_err(ctx, NGRTD_EINVAL, "role %d row %d >= n_params", r, ri[r]);
+    auto p = std::make_unique<ngrtd_plan>();
+    p->ctx = ctx;
+    p->desc = *d;
+    p->max_w = max_walkers;
+    const int64_t Umax = (int64_t)L * max_walkers;
+    UnitArgs& u = p->unit;
+    u.L = L;
+    u.flags = d->flags;
+    if (d->ce_enabled) {
+        for (int r = NGRTD_ROLE_AE_BETA; r <= NGRTD_ROLE_NU_CE_BETA; ++r)
+            if (ri[r] < 0) return set_err(ctx, NGRTD_EINVAL, "CE block needs role %d", r);
+        if (d->ce_n_gases < 1 || d->ce_n_gases > kMaxGas) return set_err(ctx, NGRTD_EINVAL, "ce_n_gases must be 1..5");
+        if (!d->ce_obs || !d->ce_sd || !d->ce_E_min) return set_err(ctx, NGRTD_EINVAL, "CE obs/sd/E_min required");
+        const int G = d->ce_n_gases;
+        NG_CHECK(upload(ctx, p->ce_obs, d->ce_obs, (size_t)L * G));
+        NG_CHECK(upload(ctx, p->ce_sd, d->ce_sd, (size_t)L * G));
+        NG_CHECK(upload(ctx, p->ce_emin, d->ce_E_min, (size_t)L));
+        u.ce_on = 1; u.G = G;
+        for (int j = 0; j < G; ++j) {
+            if (d->ce_gas_ids[j] < 0 || d->ce_gas_ids[j] > 4) return set_err(ctx, NGRTD_EINVAL, "bad gas id");
+            u.gas[j] = d->ce_gas_ids[j];
+        }
+        for (int i = 0; i < 6; ++i) u.row_ce[i] = ri[NGRTD_ROLE_AE_BETA + i];
+        u.ce_obs = p->ce_obs.d(); u.ce_sd = p->ce_sd.d(); u.ce_Emin = p->ce_emin.d();
+        u.E_max = d->ce_E_max; u.logA_min = d->ce_logA_min; u.logA_max = d->ce_logA_max;
+        u.logF_min = d->ce_logF_min; u.logF_max = d->ce_logF_max; u.b_min = d->ce_b_min; u.b_max = d->ce_b_max;
+        u.nu_min = d->ce_nu_min; u.nu_max = d->ce_nu_max;
+        u.m_mu = d->ce_m_mu;
+        u.m_tau = std::pow(d->ce_m_sd, -2.0);
+        u.m_log_tau_2pi = std::log(u.m_tau / M_PI / 2.0);
+        for (int i = 0; i < 5; ++i) {
+            u.ce_ba[i] = d->ce_beta_a[i]; u.ce_bb[i] = d->ce_beta_b[i];
+            u.ce_betaln[i] = host_betaln(d->ce_beta_a[i], d->ce_beta_b[i]);
+        }
+    }
+    if (d->rtd_enabled) {
+        const int K = d->n_tracers;
+        if (K < 1 || K > kMaxTracer) return set_err(ctx, NGRTD_EINVAL, "n_tracers must be 1..8");
+        if (ri[NGRTD_ROLE_TAU1] < 0 || ri[NGRTD_ROLE_NU_RTD_BETA] < 0)
+            return set_err(ctx, NGRTD_EINVAL, "RTD block needs tau1 and nu roles");
+        if (d->mod_type1 < 0 || d->mod_type1 > 3 || d->mod_type2 < -1 || d->mod_type2 > 3)
+            return set_err(ctx, NGRTD_EINVAL, "bad RTD model types");
+        if (d->mod_type2 >= 0 && ri[NGRTD_ROLE_TAU2] < 0) return set_err(ctx, NGRTD_EINVAL, "BMM needs tau2");
+        if ((d->mod_type1 == NGRTD_MOD_EXP_PIST_FLOW && ri[NGRTD_ROLE_ETA1] < 0) ||
+            (d->mod_type2 == NGRTD_MOD_EXP_PIST_FLOW && ri[NGRTD_ROLE_ETA2] < 0) ||
+            (d->mod_type1 == NGRTD_MOD_DISPERSION && ri[NGRTD_ROLE_D1] < 0) ||
+            (d->mod_type2 == NGRTD_MOD_DISPERSION && ri[NGRTD_ROLE_D2] < 0))
+            return set_err(ctx, NGRTD_EINVAL, "model type needs its eta/D role");
+        if (!d->rtd_obs || !d->rtd_sd) return set_err(ctx, NGRTD_EINVAL, "RTD obs/sd required");
+        std::vector<TracerBuild> trs;
+        const bool thalf_role = ri[NGRTD_ROLE_THALF_BETA] >= 0;
+        bool any_lamw = false;
+        for (int t = 0; t < K; ++t) {
+            const ngrtd_tracer_desc& td = d->tracers[t];
+            const SeriesHost* s = find_series(ctx, td.series_id);
+            if (!s) return set_err(ctx, NGRTD_ESTATE, "unknown series %d", td.series_id);
+            if (td.accum < 0 || td.accum > 3) return set_err(ctx, NGRTD_EINVAL, "bad accum");
+            const bool lamw = thalf_role && td.is_cfc12;
+            any_lamw |= lamw;
+            trs.push_back(TracerBuild{s, td.accum, lamw ? 0.0 : lam_of(td.t_half), lamw});
+        }
+        NG_CHECK(build_table(ctx, trs, p->table));
+        p->N = (int)trs[0].s->n;
+        p->dtp = trs[0].s->dtp;
+        for (auto& tb : trs)
+            if (tb.s->dtp != p->dtp) return set_err(ctx, NGRTD_EINVAL, "tracers must share dtp");
+        p->tp0 = (0.0 + 1e-5) + p->dtp;
+        NG_CHECK(upload(ctx, p->rtd_obs, d->rtd_obs, (size_t)L * K));
+        NG_CHECK(upload(ctx, p->rtd_sd, d->rtd_sd, (size_t)L * K));
+        HIP_TRY(ctx, p->conc.ensure((size_t)K * Umax * sizeof(double)));
+        RtdArgs& a = p->rtd;
+        a.row_tau[0] = ri[NGRTD_ROLE_TAU1]; a.row_tau[1] = ri[NGRTD_ROLE_TAU2];
+        a.row_eta[0] = ri[NGRTD_ROLE_ETA1]; a.row_eta[1] = ri[NGRTD_ROLE_ETA2];
+        a.row_D[0] = ri[NGRTD_ROLE_D1]; a.row_D[1] = ri[NGRTD_ROLE_D2];
+        a.row_f1 = ri[NGRTD_ROLE_F1];
+        a.row_J = ri[NGRTD_ROLE_J]; a.J_is_log10 = 1;
+        a.row_thalf = any_lamw ? ri[NGRTD_ROLE_THALF_BETA] : -1;
+        a.thalf_a = d->thalf_hi - d->thalf_lo; a.thalf_b = d->thalf_lo;
+        a.row_lamsf6 = ri[NGRTD_ROLE_LAMSF6];
+        a.tab = p->table.buf.d(); a.N = p->N; a.C = p->table.C; a.CP = p->table.CP;
+        a.tp0 = p->tp0; a.dtp = p->dtp;
+        a.mod[0] = d->mod_type1; a.mod[1] = d->mod_type2 >= 0 ? d->mod_type2 : MOD_NONE;
+        a.K = K;
+        for (int c = 0; c < p->table.C; ++c) {
+            a.chan_tracer[c] = p->table.chan_tracer[c]; a.chan_isB[c] = p->table.chan_isB[c];
+            a.chan_lamw[c] = p->table.chan_lamw[c];
+        }
+        for (int t = 0; t < K; ++t) { a.tr_sf6[t] = d->tracers[t].is_sf6; a.tr_J[t] = d->tracers[t].J; }
+        a.conc = p->conc.d();
+        u.rtd_on = 1; u.K = K;
+        u.rtd_obs = p->rtd_obs.d(); u.rtd_sd = p->rtd_sd.d(); u.conc = p->conc.d();
+        u.row_tau1 = ri[NGRTD_ROLE_TAU1]; u.row_nu = ri[NGRTD_ROLE_NU_RTD_BETA]; u.row_tau2 = ri[NGRTD_ROLE_TAU2];
+        u.row_f1 = ri[NGRTD_ROLE_F1]; u.row_eta1 = ri[NGRTD_ROLE_ETA1]; u.row_eta2 = ri[NGRTD_ROLE_ETA2];
+        u.row_D1 = ri[NGRTD_ROLE_D1]; u.row_D2 = ri[NGRTD_ROLE_D2]; u.row_J = ri[NGRTD_ROLE_J];
+        u.row_thalf = ri[NGRTD_ROLE_THALF_BETA]; u.row_lamsf6 = ri[NGRTD_ROLE_LAMSF6];
+        auto nlw = [](double lo, double hi) { return -std::log(hi - lo); };
+        u.tau1_lo = d->tau1_lo; u.tau1_hi = d->tau1_hi; u.tau1_nlw = nlw(d->tau1_lo, d->tau1_hi);
+        u.tau2_lo = d->tau2_lo; u.tau2_hi = d->tau2_hi; u.tau2_nlw = nlw(d->tau2_lo, d->tau2_hi);
+        u.f1_lo = d->f1_lo; u.f1_hi = d->f1_hi; u.f1_nlw = nlw(d->f1_lo, d->f1_hi);
+        u.eta1_lo = d->eta1_lo; u.eta1_hi = d->eta1_hi; u.eta1_nlw = nlw(d->eta1_lo, d->eta1_hi);
+        u.eta2_lo = d->eta2_lo; u.eta2_hi = d->eta2_hi; u.eta2_nlw = nlw(d->eta2_lo, d->eta2_hi);
+        u.D1_lo = d->D1_lo; u.D1_hi = d->D1_hi; u.D1_nlw = nlw(d->D1_lo, d->D1_hi);
+        u.D2_lo = d->D2_lo; u.D2_hi = d->D2_hi; u.D2_nlw = nlw(d->D2_lo, d->D2_hi);
+        u.J_mu = d->J_mu; u.J_tau = std::pow(d->J_sd, -2.0); u.J_log_tau_2pi = std::log(u.J_tau / M_PI / 2.0);
+        u.th_a = d->thalf_a; u.th_b = d->thalf_b; u.th_betaln = host_betaln(d->thalf_a, d->thalf_b);
+        u.ls_tau = std::pow(d->lamsf6_sd, -2.0); u.ls_half_log = 0.5 * std::log(u.ls_tau * 2.0 / M_PI);
+        u.rnu_min = d->rtd_nu_min; u.rnu_max = d->rtd_nu_max; u.rnu_a = d->rtd_nu_a; u.rnu_b = d->rtd_nu_b;
+        u.rnu_betaln = host_betaln(d->rtd_nu_a, d->rtd_nu_b);
+    }
+    HIP_TRY(ctx, p->ulogp.ensure((size_t)Umax * sizeof(double)));
+    u.ulogp = p->ulogp.d();
+    *out = p.release();
+    return NGRTD_OK;
+}
+
+int ngrtd_plan_destroy(ngrtd_plan* p) {
+    if (!p) return NGRTD_ESTATE;
+    (void)hipStreamSynchronize(p->ctx->stream);
+    (void)drain_timings(p);
+    delete p;
+    return NGRTD_OK;
+}
+
+// Enqueue the plan's kernels for theta (device) -> logp (device) / forward outputs.
+// Timing without host synchronisation: each profiled launch is bracketed by two events
+// recorded on the launch stream; ngrtd_plan_kernel_stats() reads them back later.
+static int timed_begin(ngrtd_plan* p, bool prof, hipStream_t st, hipEvent_t* a) {
+    if (!prof) return NGRTD_OK;
+    *a = p->ctx->take_event();
+    HIP_TRY(p->ctx, hipEventRecord(*a, st));
+    return NGRTD_OK;
+}
+static int timed_end(ngrtd_plan* p, bool prof, hipStream_t st, int kind, hipEvent_t a) {
+    if (!prof) return NGRTD_OK;
+    hipEvent_t b = p->ctx->take_event();
+    HIP_TRY(p->ctx, hipEventRecord(b, st));
+    p->pending.push_back(PendingTiming{kind, a, b});
+    return NGRTD_OK;
+}
+
+static int drain_timings(ngrtd_plan* p) {
+    for (auto& t : p->pending) {
+        HIP_TRY(p->ctx, hipEventSynchronize(t.b));
+        float ms = 0.f;
+        HIP_TRY(p->ctx, hipEventElapsedTime(&ms, t.a, t.b));
+        p->stats.ms[t.kind] += ms;
+        p->stats.n[t.kind] += 1;
+        p->ctx->event_pool.push_back(t.a);
+        p->ctx->event_pool.push_back(t.b);
+    }
+    p->pending.clear();
+    return NGRTD_OK;
+}
+
+// Enqueue the plan's kernels for theta (device) -> logp (device) / forward outputs.
+static int plan_run(ngrtd_plan* p, const double* theta, int64_t W, double* logp, double* ce_out, double* rtd_out) {
+    ngrtd_ctx* ctx = p->ctx;
+    const int64_t U = (int64_t)p->desc.n_wells * W;
+    const bool prof = ctx->profiling;
+    hipStream_t st = S(ctx);
+    hipEvent_t ev = nullptr;
+    if (prof && p->pending.size() > 4096) NG_CHECK(drain_timings(p));
+    if (p->desc.rtd_enabled) {
+        RtdArgs a = p->rtd;
+        a.theta = theta; a.U = U;
+        if (rtd_out) a.conc = rtd_out;
+        NG_CHECK(timed_begin(p, prof, st, &ev));
+        NG_CHECK(launch_rtd(ctx, a, a.row_thalf >= 0, st));
+        NG_CHECK(timed_end(p, prof, st, 0, ev));
+    }
+    if (logp || ce_out) {
+        UnitArgs u = p->unit;
+        u.theta = theta; u.U = U; u.W = W;
+        if (rtd_out) u.conc = rtd_out;
+        u.ce_out = ce_out;
+        if (!logp) u.flags = 0;
+        NG_CHECK(timed_begin(p, prof, st, &ev));
+        hipLaunchKernelGGL(unit_logp_kernel, dim3((unsigned)cdiv(U, 256)), dim3(256), 0, st, u);
+        HIP_TRY(ctx, hipGetLastError());
+        NG_CHECK(timed_end(p, prof, st, 1, ev));
+        if (logp) {
+            NG_CHECK(timed_begin(p, prof, st, &ev));
+            hipLaunchKernelGGL(walker_reduce_kernel, dim3((unsigned)cdiv(W, 256)), dim3(256), 0, st,
+                               (const double*)p->ulogp.d(), W, p->desc.n_wells, logp);
+            HIP_TRY(ctx, hipGetLastError());
+            NG_CHECK(timed_end(p, prof, st, 2, ev));
+        }
+    }
+    return NGRTD_OK;
+}
+
+int ngrtd_logp(ngrtd_plan* p, const double* theta, int64_t W, double* logp, int32_t mem) {
+    if (!p) return NGRTD_ESTATE;
+    ngrtd_ctx* ctx = p->ctx;
+    if (!theta || !logp || W < 0 || W > p->max_w) return set_err(ctx, NGRTD_EINVAL, "bad theta/logp/W (max %lld)", (long long)p->max_w);
+    if (W == 0) return NGRTD_OK;
+    const int64_t nth = (int64_t)p->desc.n_params * p->desc.n_wells * W;
+    if (mem == NGRTD_MEM_DEVICE) return plan_run(p, theta, W, logp, nullptr, nullptr);
+    HIP_TRY(ctx, p->theta_stage.ensure((size_t)nth * sizeof(double)));
+    HIP_TRY(ctx, p->out_stage.ensure((size_t)W * sizeof(double)));
+    HIP_TRY(ctx, hipMemcpyAsync(p->theta_stage.p, theta, nth * sizeof(double), hipMemcpyHostToDevice, S(ctx)));
+    NG_CHECK(plan_run(p, p->theta_stage.d(), W, p->out_stage.d(), nullptr, nullptr));
+    HIP_TRY(ctx, hipMemcpyAsync(logp, p->out_stage.p, W * sizeof(double), hipMemcpyDeviceToHost, S(ctx)));
+    HIP_TRY(ctx, hipStreamSynchronize(S(ctx)));
+    return NGRTD_OK;
+}
+
+int ngrtd_forward(ngrtd_plan* p, const double* theta, int64_t W, double* ce_out, double* rtd_out, int32_t mem) {
+    if (!p) return NGRTD_ESTATE;
+    ngrtd_ctx* ctx = p->ctx;
+    if (!theta || W < 0 || W > p->max_w) return set_err(ctx, NGRTD_EINVAL, "bad theta/W");
+    if (ce_out && !p->desc.ce_enabled) return set_err(ctx, NGRTD_EINVAL, "plan has no CE block");
+    if (rtd_out && !p->desc.rtd_enabled) return set_err(ctx, NGRTD_EINVAL, "plan has no RTD block");
+    if (W == 0) return NGRTD_OK;
+    const int64_t U = (int64_t)p->desc.n_wells * W;
+    if (mem == NGRTD_MEM_DEVICE) return plan_run(p, theta, W, nullptr, ce_out, rtd_out);
+    const int64_t nth = (int64_t)p->desc.n_params * U;
+    const int G = p->desc.ce_n_gases, K = p->desc.n_tracers;
+    HIP_TRY(ctx, p->theta_stage.ensure((size_t)nth * sizeof(double)));
+    HIP_TRY(ctx, hipMemcpyAsync(p->theta_stage.p, theta, nth * sizeof(double), hipMemcpyHostToDevice, S(ctx)));
+    double* dce = nullptr;
+    if (ce_out) {
+        HIP_TRY(ctx, p->ce_stage.ensure((size_t)G * U * sizeof(double)));
+        dce = p->ce_stage.d();
+    }
+    double* drtd = (rtd_out && p->desc.rtd_enabled) ? p->conc.d() : nullptr;
+    NG_CHECK(plan_run(p, p->theta_stage.d(), W, nullptr, dce, nullptr));
+    if (ce_out) HIP_TRY(ctx, hipMemcpyAsync(ce_out, dce, (size_t)G * U * sizeof(double), hipMemcpyDeviceToHost, S(ctx)));
+    if (drtd) HIP_TRY(ctx, hipMemcpyAsync(rtd_out, drtd, (size_t)K * U * sizeof(double), hipMemcpyDeviceToHost, S(ctx)));
+    HIP_TRY(ctx, hipStreamSynchronize(S(ctx)));
+    return NGRTD_OK;
+}
+
+int ngrtd_plan_kernel_stats(ngrtd_plan* p, double* times_ms, int64_t* counts, int32_t n, int32_t reset) {
+    if (!p) return NGRTD_ESTATE;
+    NG_CHECK(drain_timings(p));
+    for (int i = 0; i < n && i < 3; ++i) {
+        if (times_ms) times_ms[i] = p->stats.ms[i];
+        if (counts) counts[i] = p->stats.n[i];
+    }
+    if (reset) p->stats = LaunchStats{};
+    return NGRTD_OK;
+}
+
+int ngrtd_plan_info(ngrtd_plan* p, int64_t W, int64_t* info, int32_t n) {
+    if (!p) return NGRTD_ESTATE;
+    const int64_t U = (int64_t)p->desc.n_wells * W;
+    int64_t v[8] = {0};
+    if (p->desc.rtd_enabled) {
+        const RtdGeom g = rtd_geometry(U, p->N, p->table.C, p->rtd.row_thalf >= 0);
+        v[0] = g.R; v[1] = g.NW; v[2] = g.blocks; v[3] = (int64_t)g.LW * g.NW; v[4] = p->table.C;
+        v[5] = p->N; v[6] = (int64_t)g.lds;
+    }
+    v[7] = U;
+    for (int i = 0; i < n && i < 8; ++i) info[i] = v[i];
+    return NGRTD_OK;
+}
+
+}  // extern "C"

