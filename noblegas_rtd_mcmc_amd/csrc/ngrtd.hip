@@ -10,6 +10,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -46,6 +47,8 @@ struct SeriesHost {
 
 struct TableDev {
     DevBuf buf;
+    DevBuf frag;            // MFMA A-operand fragments (rtd_exp_mfma_kernel)
+    int S_seg = 1, Lseg = 0, nsteps = 0;
     int C = 0, CP = 0;
     int chan_tracer[kMaxChan] = {}, chan_isB[kMaxChan] = {}, chan_lamw[kMaxChan] = {};
 };
@@ -86,7 +89,7 @@ struct ngrtd_plan {
     ngrtd_model_desc desc{};
     int64_t max_w = 0;
     // device copies of the model data
-    DevBuf ce_obs, ce_sd, ce_emin, rtd_obs, rtd_sd;
+    DevBuf ce_obs, ce_sd, ce_emin, rtd_obs, rtd_sd, ce_lam, rtd_lam;
     TableDev table;
     int N = 0;
     double tp0 = 1e-5, dtp = 0.0;
@@ -188,7 +191,38 @@ static int build_table(ngrtd_ctx* ctx, const std::vector<TracerBuild>& trs, Tabl
         for (int64_t k = 0; k < N; ++k) h[(size_t)k * tab.CP + c] = cols[c][k];
     HIP_TRY(ctx, tab.buf.ensure(h.size() * sizeof(double) + 16));
     HIP_TRY(ctx, hipMemcpy(tab.buf.p, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
+    // MFMA fragment table: GEMM rows i = (channel c, age segment s), i < C * S_seg <= 16;
+    // row i covers ages 1 + s*Lseg + [0, Lseg); entry [step][mm][lane] is the A operand of
+    // lane (row lane&15, k-slot lane>>4) for ages 1 + s*Lseg + 16*step + 4*mm + (lane>>4).
+    if (C >= 1 && C <= 16) {
+        const int S = 16 / C;
+        int64_t Lseg = cdiv(std::max<int64_t>(N - 1, 0), S);
+        Lseg = cdiv(Lseg, 16) * 16;
+        tab.S_seg = S;
+        tab.Lseg = (int)Lseg;
+        tab.nsteps = (int)(Lseg / 16);
+        std::vector<double> fr((size_t)tab.nsteps * 256, 0.0);
+        for (int step = 0; step < tab.nsteps; ++step)
+            for (int mm = 0; mm < 4; ++mm)
+                for (int lane = 0; lane < 64; ++lane) {
+                    const int i = lane & 15, t = lane >> 4;
+                    if (i >= C * S) continue;
+                    const int c = i / S, sg = i % S;
+                    const int64_t k = 1 + sg * Lseg + 16 * step + 4 * mm + t;
+                    if (k < N) fr[(size_t)(step * 4 + mm) * 64 + lane] = cols[c][k];
+                }
+        HIP_TRY(ctx, tab.frag.ensure(fr.size() * sizeof(double) + 16));
+        if (!fr.empty())
+            HIP_TRY(ctx, hipMemcpy(tab.frag.p, fr.data(), fr.size() * sizeof(double), hipMemcpyHostToDevice));
+    }
     return NGRTD_OK;
+}
+
+static void set_frag(RtdArgs& a, const TableDev& tab) {
+    a.frag = tab.frag.d();
+    a.nsteps = tab.nsteps;
+    a.S_seg = tab.S_seg;
+    a.Lseg = tab.Lseg;
 }
 
 // ------------------------------------------------------- RTD kernel dispatch
@@ -239,10 +273,40 @@ static RtdGeom rtd_geometry(int64_t U, int N, int C, bool lamw) {
     return g;
 }
 
-static int launch_rtd(ngrtd_ctx* ctx, RtdArgs a, bool lamw, hipStream_t st, RtdGeom* out_geom = nullptr) {
+static bool mfma_path(const RtdArgs& a, bool lamw) {
+    static const bool disabled = std::getenv("NGRTD_NO_MFMA") != nullptr;
+    return !disabled && a.mod[0] == MOD_EXP && a.mod[1] == MOD_NONE && !lamw && a.C >= 1 && a.C <= 16 &&
+           a.frag != nullptr;
+}
+
+static int mfma_nt(int64_t U) {
+    if (cdiv(U, 64) >= 1024) return 4;
+    if (cdiv(U, 32) >= 1024) return 2;
+    return 1;
+}
+
+// Enqueue the RTD kernel.  On the MFMA path with `ua` non-null the kernel also evaluates
+// the per-unit log-prob (fused epilogue); *fused reports whether it did.
+static int launch_rtd(ngrtd_ctx* ctx, RtdArgs a, bool lamw, hipStream_t st, const UnitArgs* ua = nullptr,
+                      bool* fused = nullptr) {
+    if (fused) *fused = false;
     if (a.U <= 0) return NGRTD_OK;
+    if (mfma_path(a, lamw)) {
+        const int NT = mfma_nt(a.U);
+        const unsigned blocks = (unsigned)cdiv(a.U, 64 * NT);
+        UnitArgs u{};
+        int32_t fuse = 0;
+        if (ua) { u = *ua; fuse = 1; }
+        const size_t lds = std::max<size_t>((size_t)std::min(a.nsteps, kMfmaChunkSteps) * 256 * sizeof(double),
+                                            (size_t)4 * NT * 16 * 17 * sizeof(double));
+        if (NT == 4) hipLaunchKernelGGL(rtd_exp_mfma_kernel<4>, dim3(blocks), dim3(256), lds, st, a, u, fuse);
+        else if (NT == 2) hipLaunchKernelGGL(rtd_exp_mfma_kernel<2>, dim3(blocks), dim3(256), lds, st, a, u, fuse);
+        else hipLaunchKernelGGL(rtd_exp_mfma_kernel<1>, dim3(blocks), dim3(256), lds, st, a, u, fuse);
+        HIP_TRY(ctx, hipGetLastError());
+        if (fused) *fused = fuse != 0;
+        return NGRTD_OK;
+    }
     const RtdGeom g = rtd_geometry(a.U, a.N, a.C, lamw);
-    if (out_geom) *out_geom = g;
     RtdKernel k = pick_rtd(g.R, a.C, lamw);
     if (!k) return set_err(ctx, NGRTD_EINVAL, "no RTD kernel for R=%d C=%d", g.R, a.C);
     a.LW = g.LW;
@@ -441,6 +505,7 @@ int ngrtd_conv(ngrtd_ctx* ctx, int32_t series_id, int32_t mod_type, int32_t accu
     a.K = 1;
     for (int c = 0; c < tab.C; ++c) { a.chan_tracer[c] = tab.chan_tracer[c]; a.chan_isB[c] = tab.chan_isB[c]; a.chan_lamw[c] = tab.chan_lamw[c]; }
     a.tr_sf6[0] = 0; a.tr_J[0] = J_const;
+    set_frag(a, tab);
     if (mem == NGRTD_MEM_DEVICE) {
         a.conc = out;
     } else {
@@ -512,6 +577,19 @@ static int upload(ngrtd_ctx* ctx, DevBuf& b, const double* src, size_t n) {
     return NGRTD_OK;
 }
 
+// StudentT precision terms per observation: lam = sd^-2 and 0.5*log(lam), laid out as
+// [lam(L*n) | hll(L*n)]; sd <= 0 (or NaN) stores lam = -1 so the bound gives -inf.
+static int upload_lam(ngrtd_ctx* ctx, DevBuf& b, const double* sd, size_t n) {
+    std::vector<double> h(2 * n);
+    for (size_t i = 0; i < n; ++i) {
+        const double lam = std::pow(sd[i], -2.0);
+        const bool ok = sd[i] > 0 && lam > 0;
+        h[i] = ok ? lam : -1.0;
+        h[n + i] = ok ? 0.5 * std::log(lam) : 0.0;
+    }
+    return upload(ctx, b, h.data(), 2 * n);
+}
+
 int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_walkers, ngrtd_plan** out) {
     if (!ctx) return NGRTD_ESTATE;
     if (!d || !out || max_walkers <= 0) return set_err(ctx, NGRTD_EINVAL, "bad plan arguments");
@@ -539,6 +617,8 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
         NG_CHECK(upload(ctx, p->ce_obs, d->ce_obs, (size_t)L * G));
         NG_CHECK(upload(ctx, p->ce_sd, d->ce_sd, (size_t)L * G));
         NG_CHECK(upload(ctx, p->ce_emin, d->ce_E_min, (size_t)L));
+        NG_CHECK(upload_lam(ctx, p->ce_lam, d->ce_sd, (size_t)L * G));
+        u.ce_lam = p->ce_lam.d(); u.ce_hll = p->ce_lam.d() + (size_t)L * G;
         u.ce_on = 1; u.G = G;
         for (int j = 0; j < G; ++j) {
             if (d->ce_gas_ids[j] < 0 || d->ce_gas_ids[j] > 4) return set_err(ctx, NGRTD_EINVAL, "bad gas id");
@@ -591,6 +671,8 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
         p->tp0 = (0.0 + 1e-5) + p->dtp;
         NG_CHECK(upload(ctx, p->rtd_obs, d->rtd_obs, (size_t)L * K));
         NG_CHECK(upload(ctx, p->rtd_sd, d->rtd_sd, (size_t)L * K));
+        NG_CHECK(upload_lam(ctx, p->rtd_lam, d->rtd_sd, (size_t)L * K));
+        u.rtd_lam = p->rtd_lam.d(); u.rtd_hll = p->rtd_lam.d() + (size_t)L * K;
         HIP_TRY(ctx, p->conc.ensure((size_t)K * Umax * sizeof(double)));
         RtdArgs& a = p->rtd;
         a.row_tau[0] = ri[NGRTD_ROLE_TAU1]; a.row_tau[1] = ri[NGRTD_ROLE_TAU2];
@@ -611,6 +693,7 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
         }
         for (int t = 0; t < K; ++t) { a.tr_sf6[t] = d->tracers[t].is_sf6; a.tr_J[t] = d->tracers[t].J; }
         a.conc = p->conc.d();
+        set_frag(a, p->table);
         u.rtd_on = 1; u.K = K;
         u.rtd_obs = p->rtd_obs.d(); u.rtd_sd = p->rtd_sd.d(); u.conc = p->conc.d();
         u.row_tau1 = ri[NGRTD_ROLE_TAU1]; u.row_nu = ri[NGRTD_ROLE_NU_RTD_BETA]; u.row_tau2 = ri[NGRTD_ROLE_TAU2];
@@ -684,27 +767,44 @@ static int plan_run(ngrtd_plan* p, const double* theta, int64_t W, double* logp,
     hipStream_t st = S(ctx);
     hipEvent_t ev = nullptr;
     if (prof && p->pending.size() > 4096) NG_CHECK(drain_timings(p));
+    UnitArgs u = p->unit;
+    u.theta = theta; u.U = U; u.W = W;
+    u.ce_out = ce_out;
+    if (!logp) u.flags = 0;
+    bool fused = false;
     if (p->desc.rtd_enabled) {
         RtdArgs a = p->rtd;
         a.theta = theta; a.U = U;
         if (rtd_out) a.conc = rtd_out;
+        if (rtd_out) u.conc = rtd_out;
+        // Fusing the per-unit CE / likelihood epilogue into the MFMA kernel saves the
+        // concentration round trip but runs that VALU-bound epilogue at the MFMA kernel's
+        // occupancy (2 waves/SIMD at c4); measured slower than two kernels, so
+        // it is opt-in (NGRTD_FUSE=1).
+        static const bool fuse_env = std::getenv("NGRTD_FUSE") != nullptr;
+        const bool want_unit = fuse_env && (logp || ce_out);
+        // the fused MFMA kernel keeps concentrations in registers: store them only on request
+        if (want_unit && !rtd_out && mfma_path(a, a.row_thalf >= 0)) a.conc = nullptr;
         NG_CHECK(timed_begin(p, prof, st, &ev));
-        NG_CHECK(launch_rtd(ctx, a, a.row_thalf >= 0, st));
+        NG_CHECK(launch_rtd(ctx, a, a.row_thalf >= 0, st, want_unit ? &u : nullptr, &fused));
         NG_CHECK(timed_end(p, prof, st, 0, ev));
     }
-    if (logp || ce_out) {
-        UnitArgs u = p->unit;
-        u.theta = theta; u.U = U; u.W = W;
-        if (rtd_out) u.conc = rtd_out;
-        u.ce_out = ce_out;
-        if (!logp) u.flags = 0;
+    if ((logp || ce_out) && fused) {
+        if (logp) {
+            NG_CHECK(timed_begin(p, prof, st, &ev));
+            hipLaunchKernelGGL(walker_reduce_kernel, dim3((unsigned)cdiv(W, 64)), dim3(1024), 0, st,
+                               (const double*)p->ulogp.d(), W, p->desc.n_wells, logp);
+            HIP_TRY(ctx, hipGetLastError());
+            NG_CHECK(timed_end(p, prof, st, 2, ev));
+        }
+    } else if (logp || ce_out) {
         NG_CHECK(timed_begin(p, prof, st, &ev));
         hipLaunchKernelGGL(unit_logp_kernel, dim3((unsigned)cdiv(U, 256)), dim3(256), 0, st, u);
         HIP_TRY(ctx, hipGetLastError());
         NG_CHECK(timed_end(p, prof, st, 1, ev));
         if (logp) {
             NG_CHECK(timed_begin(p, prof, st, &ev));
-            hipLaunchKernelGGL(walker_reduce_kernel, dim3((unsigned)cdiv(W, 256)), dim3(256), 0, st,
+            hipLaunchKernelGGL(walker_reduce_kernel, dim3((unsigned)cdiv(W, 64)), dim3(1024), 0, st,
                                (const double*)p->ulogp.d(), W, p->desc.n_wells, logp);
             HIP_TRY(ctx, hipGetLastError());
             NG_CHECK(timed_end(p, prof, st, 2, ev));
@@ -748,7 +848,7 @@ int ngrtd_forward(ngrtd_plan* p, const double* theta, int64_t W, double* ce_out,
         dce = p->ce_stage.d();
     }
     double* drtd = (rtd_out && p->desc.rtd_enabled) ? p->conc.d() : nullptr;
-    NG_CHECK(plan_run(p, p->theta_stage.d(), W, nullptr, dce, nullptr));
+    NG_CHECK(plan_run(p, p->theta_stage.d(), W, nullptr, dce, drtd));
     if (ce_out) HIP_TRY(ctx, hipMemcpyAsync(ce_out, dce, (size_t)G * U * sizeof(double), hipMemcpyDeviceToHost, S(ctx)));
     if (drtd) HIP_TRY(ctx, hipMemcpyAsync(rtd_out, drtd, (size_t)K * U * sizeof(double), hipMemcpyDeviceToHost, S(ctx)));
     HIP_TRY(ctx, hipStreamSynchronize(S(ctx)));
@@ -769,14 +869,24 @@ int ngrtd_plan_kernel_stats(ngrtd_plan* p, double* times_ms, int64_t* counts, in
 int ngrtd_plan_info(ngrtd_plan* p, int64_t W, int64_t* info, int32_t n) {
     if (!p) return NGRTD_ESTATE;
     const int64_t U = (int64_t)p->desc.n_wells * W;
-    int64_t v[8] = {0};
+    int64_t v[11] = {0};
     if (p->desc.rtd_enabled) {
-        const RtdGeom g = rtd_geometry(U, p->N, p->table.C, p->rtd.row_thalf >= 0);
-        v[0] = g.R; v[1] = g.NW; v[2] = g.blocks; v[3] = (int64_t)g.LW * g.NW; v[4] = p->table.C;
-        v[5] = p->N; v[6] = (int64_t)g.lds;
+        RtdArgs a = p->rtd;
+        a.U = U;
+        const bool lamw = a.row_thalf >= 0;
+        if (mfma_path(a, lamw)) {
+            const int NT = mfma_nt(U);
+            v[0] = NT; v[1] = 4; v[2] = cdiv(U, 64 * NT); v[3] = a.Lseg;
+            v[6] = std::max<int64_t>((int64_t)std::min(a.nsteps, kMfmaChunkSteps) * 2048, (int64_t)4 * NT * 16 * 17 * 8);
+            v[8] = 1; v[9] = a.S_seg; v[10] = a.nsteps;
+        } else {
+            const RtdGeom g = rtd_geometry(U, p->N, p->table.C, lamw);
+            v[0] = g.R; v[1] = g.NW; v[2] = g.blocks; v[3] = (int64_t)g.LW * g.NW; v[6] = (int64_t)g.lds;
+        }
+        v[4] = p->table.C; v[5] = p->N;
     }
     v[7] = U;
-    for (int i = 0; i < n && i < 8; ++i) info[i] = v[i];
+    for (int i = 0; i < n && i < 11; ++i) info[i] = v[i];
     return NGRTD_OK;
 }
 

@@ -30,6 +30,9 @@ struct RtdArgs {
     int32_t tr_sf6[kMaxTracer];     // apply (1 + lamsf6)
     double tr_J[kMaxTracer];        // fixed J per tracer when row_J < 0
     double* conc;           // out [K][U]
+    // MFMA Horner fragments (rtd_exp_mfma_kernel): rows = (channel, age segment)
+    const double* frag;     // [nsteps][4][64] A-operand fragments of v_mfma_f64_16x16x4f64
+    int32_t nsteps, S_seg, Lseg;
 };
 
 // Per-unit CE + likelihood + prior launch (unit_logp_kernel)
@@ -44,6 +47,8 @@ struct UnitArgs {
     int32_t row_ce[6];      // Ae_beta, F_beta, E_beta, m, b_beta, nu_ce_beta
     const double* ce_obs;   // [L][G]
     const double* ce_sd;
+    const double* ce_lam;   // [L][G] sd^-2 (<= 0 when sd <= 0: StudentT bound -> -inf)
+    const double* ce_hll;   // [L][G] 0.5 * log(sd^-2)
     const double* ce_Emin;  // [L]
     double E_max, logA_min, logA_max, logF_min, logF_max, b_min, b_max, nu_min, nu_max;
     double m_mu, m_tau, m_log_tau_2pi;
@@ -52,6 +57,8 @@ struct UnitArgs {
     const double* conc;     // [K][U] model concentrations from rtd_conc_kernel
     const double* rtd_obs;  // [L][K]
     const double* rtd_sd;
+    const double* rtd_lam;  // [L][K]
+    const double* rtd_hll;
     int32_t row_tau1, row_nu, row_tau2, row_f1, row_eta1, row_eta2, row_D1, row_D2, row_J, row_thalf, row_lamsf6;
     double tau1_lo, tau1_hi, tau1_nlw, tau2_lo, tau2_hi, tau2_nlw, f1_lo, f1_hi, f1_nlw;
     double eta1_lo, eta1_hi, eta1_nlw, eta2_lo, eta2_hi, eta2_nlw;

@@ -381,9 +381,65 @@ __global__ void __launch_bounds__(256) rtd_conc_kernel(const RtdArgs a) {
 }
 
 // ------------------------------------------------- per-unit CE + likelihood
-__global__ void __launch_bounds__(256) unit_logp_kernel(const UnitArgs a) {
-    const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (u >= a.U) return;
+// CE concentrations of one (walker, well) for the likelihood gases, with S = 0 (the
+// reference models never pass a salinity): the Setchenow factor exp(0 * setch) is 1
+// whenever setch is finite and NaN otherwise (noble_gas_utils.py:154-156), so it is
+// decided without the exp/log; the He branch reuses the Ar exponential (:172).
+__device__ __forceinline__ void ce_model_s0(const UnitArgs& a, double T, double P, double Ae, double F,
+                                            double* mod) {
+    const double Pv = vapor_pressure(T);
+    const double T_k = T + 273.15;
+    const double x = .001 * T_k, x2 = x * x, x3 = x * x * x;
+    const double x1 = .01 * T_k;
+    double gamma = 1.;
+    if (T < 65.) {
+        const bool fin = (x1 > 0.0) && (x1 < __builtin_inf());
+        gamma = fin ? 1. : __builtin_nan("");
+    }
+    const GasCoef ar = gas_coef(2);
+    double exp_ar = 0.0;
+    bool have_ar = false;
+    for (int j = 0; j < a.G; ++j) {
+        const int g = a.gas[j];
+        const GasCoef c = gas_coef(g);
+        // Setchenow with S = 0: exp(0 * setch) -- finite setch gives exactly 1
+        double gj = gamma;
+        if (T < 65. && gj == 1.) gj = isfinite(c.G2 / x1) ? 1. : __builtin_nan("");
+        double K;
+        if (g == 0) {
+            if (!have_ar) { exp_ar = exp(ar.A0 + (ar.A1 / x) + (ar.A2 / x2) + (ar.A3 / x3)); have_ar = true; }
+            const double Fh = exp(c.A0 + (c.A1 / x) + (c.A2 / x2) + (c.A3 / x3));
+            const double X_Ar_water = 1. / exp_ar * 9.31e-3;
+            const double X_he_water = Fh * (5.24e-6 / 9.31e-3) * X_Ar_water;
+            K = gj * (5.24e-6 / X_he_water);
+        } else {
+            const double e = exp(c.A0 + (c.A1 / x) + (c.A2 / x2) + (c.A3 / x3));
+            if (g == 2 && !have_ar) { exp_ar = e; have_ar = true; }
+            K = gj * e;
+        }
+        const double ceq = equil_conc_dry(g, T, P, Pv, K);
+        mod[j] = ce_excess(g, Ae, F, ceq) + ceq;
+    }
+}
+
+// Student-t sum over observations sharing nu, with lam = sigma^-2 and 0.5*log(lam)
+// precomputed per observation on the host (lam <= 0 encodes sigma <= 0 -> -inf).
+__device__ __forceinline__ double st_sum(int n, const double* obs, const double* mu, const double* lam,
+                                         const double* hll, double nu) {
+    const double c0 = st_const(nu) - 0.5 * log(nu * kPi);
+    const double hn = (nu + 1.0) / 2.0;
+    double s = 0.0;
+    for (int j = 0; j < n; ++j) {
+        const double d = obs[j] - mu[j];
+        const double v = c0 + hll[j] - hn * log1p(lam[j] * (d * d) / nu);
+        s += (lam[j] > 0 && nu > 0) ? v : kNegInf;
+    }
+    return s;
+}
+
+// log-prob contribution of one (walker, well) unit: priors, CE model + likelihood,
+// RTD likelihood on the unit's model concentrations `conc` (K values).
+__device__ __forceinline__ double unit_logp(const UnitArgs& a, int64_t u, const double* conc) {
     const int l = (int)(u / a.W);
     const bool want_like = a.flags & NGRTD_WANT_LIKE;
     const bool want_prior = a.flags & NGRTD_WANT_PRIOR;
@@ -411,20 +467,12 @@ __global__ void __launch_bounds__(256) unit_logp_kernel(const UnitArgs a) {
             const double b = p[4] * (a.b_max - a.b_min) + a.b_min;
             const double T = (E - b) / p[3];
             const double nu = p[5] * (a.nu_max - a.nu_min) + a.nu_min;
-            const double Ae = pow(10.0, Ae_log), F = pow(10.0, F_log);
-            const double P = lapse_rate(E);
-            const double Pv = vapor_pressure(T);
-            const double c0 = st_const(nu);
-            double like = 0.0;
-            for (int j = 0; j < a.G; ++j) {
-                const int g = a.gas[j];
-                const double K = solubility(g, T, 0.0);
-                const double ceq = equil_conc_dry(g, T, P, Pv, K);
-                const double mod = ce_excess(g, Ae, F, ceq) + ceq;
-                if (a.ce_out) a.ce_out[(int64_t)j * a.U + u] = mod;
-                like += c0 + st_term(a.ce_obs[l * a.G + j], mod, a.ce_sd[l * a.G + j], nu);
-            }
-            if (want_like) lp += like;
+            double mod[kMaxGas];
+            ce_model_s0(a, T, lapse_rate(E), exp10(Ae_log), exp10(F_log), mod);
+            if (a.ce_out)
+                for (int j = 0; j < a.G; ++j) a.ce_out[(int64_t)j * a.U + u] = mod[j];
+            if (want_like)
+                lp += st_sum(a.G, a.ce_obs + l * a.G, mod, a.ce_lam + l * a.G, a.ce_hll + l * a.G, nu);
         }
     }
     if (a.rtd_on) {
@@ -460,25 +508,160 @@ __global__ void __launch_bounds__(256) unit_logp_kernel(const UnitArgs a) {
             }
         }
         if (want_like) {
-            const double nu = nub * (a.rnu_max - a.rnu_min) + a.rnu_min;   // :292
-            const double c0 = st_const(nu);
-            double like = 0.0;
-            for (int t = 0; t < a.K; ++t)
-                like += c0 + st_term(a.rtd_obs[l * a.K + t], a.conc[(int64_t)t * a.U + u], a.rtd_sd[l * a.K + t], nu);
-            lp += like;
+            const double nu = nub * (a.rnu_max - a.rnu_min) + a.rnu_min;   // run_age_mcmc_utils.py:292
+            lp += st_sum(a.K, a.rtd_obs + l * a.K, conc, a.rtd_lam + l * a.K, a.rtd_hll + l * a.K, nu);
         }
     }
-    a.ulogp[u] = lp;
+    return lp;
 }
 
-// logp[w] = sum_l ulogp[l*W + w], fixed order (deterministic)
-__global__ void __launch_bounds__(256) walker_reduce_kernel(const double* __restrict__ ulogp, int64_t W,
-                                                            int32_t L, double* __restrict__ logp) {
-    const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= W) return;
+__global__ void __launch_bounds__(256) unit_logp_kernel(const UnitArgs a) {
+    const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= a.U) return;
+    double conc[kMaxTracer];
+    if (a.rtd_on)
+        for (int t = 0; t < a.K; ++t) conc[t] = a.conc[(int64_t)t * a.U + u];
+    a.ulogp[u] = unit_logp(a, u, conc);
+}
+
+// ------------------------------------------- exponential RTD on the matrix cores
+// Single-component exponential model (convolution_integral_utils.py:184) with every decay
+// folded into the channel table.  The polynomials sum_k A_{c,k} q_u^(k-1) of all units u
+// and channels c form a small GEMM: rows i = (channel c, age segment s), columns = 16
+// units, K = 4 consecutive ages per v_mfma_f64_16x16x4f64.  Lane l supplies
+//   A[i = l&15][t = l>>4] = A_{c, 1 + s*Lseg + 16*step + 4*mm + t}   (fragment table)
+//   B[t = l>>4][j = l&15] = q_j^(16*step + 4*mm + t)                (per-unit powers)
+// so the accumulator (row (l>>4)+4r, column l&15 in register r) ends as
+//   P_{c,s} = sum_j A_{c,1+s*Lseg+j} q^j ;   Y_c = sum_s q^(s*Lseg) P_{c,s}.
+// The powers advance by one multiply per step (B *= q^16), accumulators stay in the
+// matrix register file.  FP64 MFMA runs at 2x the FP64 VALU FMA rate on gfx950
+// (tools/ubench_fp64.hip: 78 vs 38 TFLOP/s).  With `fuse`, the epilogue also evaluates
+// the CE model, both Student-t likelihoods and the priors of the unit (one per lane).
+typedef double ngrtd_v4d __attribute__((ext_vector_type(4)));
+
+constexpr int kMfmaChunkSteps = 32;   // Horner steps of fragments staged in LDS at a time (64 KiB)
+
+template <int NT>
+__global__ void __launch_bounds__(256) rtd_exp_mfma_kernel(const RtdArgs a, const UnitArgs ua, int32_t fuse) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int col = lane & 15, tq = lane >> 4;
+    const int64_t u0 = ((int64_t)blockIdx.x * 4 + wave) * (16 * NT);
+    const int64_t Umax = a.U - 1;
+
+    double q16[NT], pw[NT][4];
+    ngrtd_v4d acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        int64_t u = u0 + 16 * t + col;
+        u = u < Umax ? u : Umax;
+        const double beta = 1. / a.theta[(int64_t)a.row_tau[0] * a.U + u];
+        const double q = exp(-beta);
+        const double q2 = q * q, q4 = q2 * q2;
+        const double qt = (tq == 0) ? 1.0 : (tq == 1) ? q : (tq == 2) ? q2 : q2 * q;
+        pw[t][0] = qt;
+        pw[t][1] = qt * q4;
+        pw[t][2] = pw[t][1] * q4;
+        pw[t][3] = pw[t][2] * q4;
+        const double q8 = q4 * q4;
+        q16[t] = q8 * q8;
+        acc[t] = ngrtd_v4d{0.0, 0.0, 0.0, 0.0};
+    }
+    const int nsteps = a.nsteps;
+    for (int c0 = 0; c0 < nsteps; c0 += kMfmaChunkSteps) {
+        const int cn = (nsteps - c0) < kMfmaChunkSteps ? (nsteps - c0) : kMfmaChunkSteps;
+        // stage fragments of steps [c0, c0+cn) (cn * 2 KiB, contiguous) into LDS
+        __syncthreads();
+        {
+            const double2* src = reinterpret_cast<const double2*>(a.frag + (int64_t)c0 * 256);
+            double2* dst = reinterpret_cast<double2*>(lds);
+            for (int i = threadIdx.x; i < cn * 128; i += 256) dst[i] = src[i];
+        }
+        __syncthreads();
+        const double* f = lds + lane;
+        for (int step = 0; step < cn; ++step, f += 256) {
+            const double A0 = f[0], A1 = f[64], A2 = f[128], A3 = f[192];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(A0, pw[t][0], acc[t], 0, 0, 0);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(A1, pw[t][1], acc[t], 0, 0, 0);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(A2, pw[t][2], acc[t], 0, 0, 0);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(A3, pw[t][3], acc[t], 0, 0, 0);
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int mm = 0; mm < 4; ++mm) pw[t][mm] *= q16[t];
+        }
+    }
+    __syncthreads();
+    double (*sh)[NT * 16][17] = reinterpret_cast<double (*)[NT * 16][17]>(lds);
+    // transpose the accumulator tiles through LDS: one unit per lane
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sh[wave][16 * t + col][tq + 4 * r] = acc[t][r];
+    __syncthreads();
+    if (lane >= 16 * NT) return;
+    const int64_t u = u0 + lane;
+    if (u > Umax) return;
+    const double beta = 1. / a.theta[(int64_t)a.row_tau[0] * a.U + u];
+    const double Qs = exp(-beta * (double)a.Lseg);
+    const double* P = sh[wave][lane];
+    const int N = a.N;
+    const double s01 = exp(-beta * ((1.0 + a.dtp) - a.tp0));
+    const int n = N - 1;
+    const double G = (n > 0) ? expm1(-beta * (double)n) / expm1(-beta) : 0.0;
+    const double den = 1.0 + s01 * G;
+    double num[kMaxChan];
+    for (int c = 0; c < a.C; ++c) {
+        double y = P[c * a.S_seg + a.S_seg - 1];
+        for (int s = a.S_seg - 2; s >= 0; --s) y = fma(y, Qs, P[c * a.S_seg + s]);
+        num[c] = a.tab[c] + s01 * y;
+    }
+    const double fmix = (a.row_f1 >= 0) ? a.theta[(int64_t)a.row_f1 * a.U + u] : 1.0;
+    double Jw = 0.0;
+    if (a.row_J >= 0) {
+        const double jv = a.theta[(int64_t)a.row_J * a.U + u];
+        Jw = a.J_is_log10 ? exp10(jv) : jv;
+    }
+    double conc[kMaxTracer];
+    for (int t = 0; t < a.K; ++t) {
+        double sA = 0.0, sB = 0.0;
+        bool hasB = false;
+        for (int c = 0; c < a.C; ++c) {
+            if (a.chan_tracer[c] != t) continue;
+            if (a.chan_isB[c]) { sB = num[c]; hasB = true; }
+            else sA = num[c];
+        }
+        const double cc = hasB ? (sA + ((a.row_J >= 0) ? Jw : a.tr_J[t]) * sB) / den : sA / den;
+        double cout = fmix * cc + 0.0 * 0.0;   // f1*cout1 + f2*cout2, run_age_mcmc_utils.py:154
+        if (a.tr_sf6[t] && a.row_lamsf6 >= 0) cout *= (1 + a.theta[(int64_t)a.row_lamsf6 * a.U + u]);
+        conc[t] = cout;
+        if (a.conc) a.conc[(int64_t)t * a.U + u] = cout;
+    }
+    if (fuse) ua.ulogp[u] = unit_logp(ua, u, conc);
+}
+
+// logp[w] = sum over wells of ulogp[l*W + w]: 16 fixed well groups per walker summed
+// in registers, then combined in a fixed order through LDS (deterministic, no atomics).
+__global__ void __launch_bounds__(1024) walker_reduce_kernel(const double* __restrict__ ulogp, int64_t W,
+                                                             int32_t L, double* __restrict__ logp) {
+    __shared__ double sh[16][64];
+    const int wl = threadIdx.x & 63, g = threadIdx.x >> 6;
+    const int64_t w = (int64_t)blockIdx.x * 64 + wl;
     double s = 0.0;
-    for (int l = 0; l < L; ++l) s += ulogp[(int64_t)l * W + w];
-    logp[w] = s;
+    if (w < W)
+        for (int l = g; l < L; l += 16) s += ulogp[(int64_t)l * W + w];
+    sh[g][wl] = s;
+    __syncthreads();
+    if (g == 0 && w < W) {
+        double t = sh[0][wl];
+        for (int i = 1; i < 16; ++i) t += sh[i][wl];
+        logp[w] = t;
+    }
 }
 
 // ------------------------------------------ gen_g_tp() materialised weights

@@ -177,9 +177,10 @@ class LogProb:
         return {"rtd": (ms[0], n[0]), "unit": (ms[1], n[1]), "reduce": (ms[2], n[2])}
 
     def info(self, W):
-        v = (C.c_int64 * 8)()
-        self.ctx.check(self.lib.ngrtd_plan_info(self.plan, int(W), v, 8), "plan_info")
-        keys = ("R", "NW", "blocks", "slice_ages", "channels", "N", "lds_bytes", "units")
+        v = (C.c_int64 * 11)()
+        self.ctx.check(self.lib.ngrtd_plan_info(self.plan, int(W), v, 11), "plan_info")
+        keys = ("R", "NW", "blocks", "slice_ages", "channels", "N", "lds_bytes", "units", "mfma", "S_seg",
+                "nsteps")
         return dict(zip(keys, list(v)))
 
     def close(self):
