@@ -1,0 +1,176 @@
+"""Drop-in for the reference's ``utils/convolution_integral_utils.py`` on the GPU.
+
+    conv = tracer_conv_integral(C_t, t_samp)
+    conv.update_pars(tau=37.3, mod_type='exponential', t_half=12.34)
+    conv.convolve()        # -> float, as convolution_integral_utils.py:284-340
+
+``tau`` (and ``eta``/``D``/``t_half``/``J``) may also be numpy arrays: the convolutions of
+all parameter sets then run in one launch and ``convolve`` returns an array -- the batched
+form of the reference's posterior-predictive and sweep loops (run_age_mcmc.py:251-319,
+age_modeling_mcmc.prep.py:739-778).
+
+Supported models: piston, exponential, exp_pist_flow, dispersion (the hot-path models,
+SURVEY.md §8a-a19).  The matrix-diffusion models 'frac_inf_diff*' are not implemented in
+this version and raise NotImplementedError.
+"""
+import ctypes as C
+import hashlib
+
+import numpy as np
+
+from . import _lib
+from .spec import ACCUM_IDS, MOD_IDS
+
+_series_cache = {}
+
+
+def _series_arrays(C_t, rad_accum):
+    """(values, index) of C_t in the reference's DataFrame order (oldest age first).
+
+    The 4He branch reads the 'He4_ter' column when present (:322-327); otherwise the
+    frame must hold a single column (convolve ravels it, :336).
+    """
+    try:
+        import pandas as pd
+    except ImportError:  # pragma: no cover
+        pd = None
+    if pd is not None and isinstance(C_t, pd.DataFrame):
+        if rad_accum == "4He" and "He4_ter" in C_t.columns:
+            s = C_t["He4_ter"]
+            return s.to_numpy(dtype=np.float64), np.asarray(s.index)
+        if rad_accum == "SF6" and "SF6" in C_t.columns:
+            s = C_t["SF6"]
+            return s.to_numpy(dtype=np.float64), np.asarray(s.index)
+        if C_t.shape[1] != 1:
+            raise ValueError("C_t must hold a single tracer column (convolution_integral_utils.py:336)")
+        return C_t.to_numpy(dtype=np.float64).ravel(), np.asarray(C_t.index)
+    if pd is not None and isinstance(C_t, pd.Series):
+        return C_t.to_numpy(dtype=np.float64), np.asarray(C_t.index)
+    v = np.asarray(C_t, dtype=np.float64).ravel()
+    return v, np.arange(len(v) - 1, -1, -1)
+
+
+def _series_id(ctx, values, index, t_samp):
+    c_by_age = np.ascontiguousarray(np.flip(values))
+    idx_by_age = np.ascontiguousarray(np.flip(index.astype(np.float64)))
+    dtp = float(np.floor(t_samp - index[-1]))
+    h = hashlib.blake2b(c_by_age.tobytes(), digest_size=16)
+    h.update(idx_by_age.tobytes())
+    key = (ctx.pid, ctx.device, h.hexdigest(), dtp)
+    sid = _series_cache.get(key)
+    if sid is None:
+        sid = ctx.series_create(c_by_age, idx_by_age, dtp)
+        _series_cache[key] = sid
+    return sid, len(c_by_age)
+
+
+def _arr(x, n):
+    return None if x is None or x is False else np.ascontiguousarray(np.broadcast_to(np.asarray(x, dtype=np.float64), (n,)))
+
+
+class tracer_conv_integral:
+    """convolution_integral_utils.py:105-340 (same constructor, attributes and methods)."""
+
+    def __init__(self, C_t, t_samp, device=0):
+        self.C_t = C_t
+        self.t_samp = t_samp
+        self._device = device
+
+    def update_pars(self, **kwargs):
+        """:111-142 -- missing kwargs reset to None/False exactly like the reference."""
+        self.tau = kwargs.get('tau', None)
+        self.mod_type = kwargs.get('mod_type', None)
+        self.t_half = kwargs.get('t_half', False)
+        if np.any(np.asarray(self.t_half, dtype=object) != False):  # noqa: E712
+            self.thalf_2_lambda(self.t_half)
+        else:
+            self.lamba = 0.0
+        self.rad_accum = kwargs.get('rad_accum', False)
+        self.J = kwargs.get('J', False)
+        self.eta = kwargs.get('eta', None)
+        self.D = kwargs.get('D', None)
+        self.bbar = kwargs.get('bbar', None)
+        self.Phi_im = kwargs.get('Phi_im', None)
+        self.J_sf6 = kwargs.get('J_sf6', None)
+        self.f_tadv_ext = kwargs.get('f_tadv_ext', None)
+
+    def thalf_2_lambda(self, t_half):
+        """:146-152."""
+        lamba = -1 * np.log(0.5) / np.asarray(t_half, dtype=np.float64)
+        self.lamba = float(lamba) if np.ndim(lamba) == 0 else lamba
+        self._thalf_src = (t_half, self.lamba)
+        return self.lamba
+
+    def _check_model(self):
+        if self.mod_type not in MOD_IDS:
+            if isinstance(self.mod_type, str) and self.mod_type.startswith("frac_inf_diff"):
+                raise NotImplementedError("frac_inf_diff models are not implemented (SURVEY.md §8f rank 3)")
+            raise ValueError("unsupported mod_type %r" % (self.mod_type,))
+
+    def _t_half_arg(self):
+        # the device recomputes lamba from the half-life exactly as thalf_2_lambda does; use
+        # the half-life that produced self.lamba when it is still current
+        src = getattr(self, "_thalf_src", None)
+        if src is not None and src[1] is self.lamba:
+            return np.asarray(src[0], dtype=np.float64)
+        lam = np.asarray(self.lamba, dtype=np.float64)
+        with np.errstate(divide="ignore"):
+            th = np.where(lam != 0.0, -1 * np.log(0.5) / np.where(lam != 0.0, lam, 1.0), 0.0)
+        return th
+
+    def gen_g_tp(self):
+        """:155-281 -- normalised weights g(tp) (N,) for scalar parameters."""
+        self._check_model()
+        ctx = _lib.Context.get(self._device)
+        v, i = _series_arrays(self.C_t, self.rad_accum)
+        sid, n = _series_id(ctx, v, i, self.t_samp)
+        g = np.empty(n)
+        eta = float(self.eta) if self.eta is not None and self.eta is not False else 0.0
+        D = float(self.D) if self.D is not None and self.D is not False else 0.0
+        ctx.check(ctx.lib.ngrtd_rtd_weights(ctx.h, sid, MOD_IDS[self.mod_type], float(self.tau), eta, D,
+                                            g.ctypes.data_as(C.c_void_p), _lib.MEM_HOST), "ngrtd_rtd_weights")
+        t = np.arange(0, n).astype(float)
+        t[0] += 1e-5
+        self.tau_list = t + np.floor(self.t_samp - i[-1])
+        return g
+
+    def convolve(self, **kwargs):
+        """:284-340 -- concentration at the sampling time (float, or array for array params)."""
+        g_tau = kwargs.get('g_tau', None)
+        ctx = _lib.Context.get(self._device)
+        v, i = _series_arrays(self.C_t, self.rad_accum)
+        sid, n = _series_id(ctx, v, i, self.t_samp)
+        accum = ACCUM_IDS.get(self.rad_accum if self.rad_accum in ("3He", "4He", "SF6") else None, 0)
+        Jv = self.J_sf6 if self.rad_accum == "SF6" else self.J
+        if g_tau is not None:
+            g = np.ascontiguousarray(g_tau, dtype=np.float64)
+            out = np.empty(1)
+            th = float(self._t_half_arg())
+            ctx.check(ctx.lib.ngrtd_conv_dot(ctx.h, sid, g.ctypes.data_as(C.c_void_p), th, accum,
+                                             float(Jv or 0.0), out.ctypes.data_as(C.c_void_p), _lib.MEM_HOST),
+                      "ngrtd_conv_dot")
+            self.g_tp = g
+            self.C_i = float(out[0])
+            return self.C_i
+        self._check_model()
+        tau = np.asarray(self.tau, dtype=np.float64)
+        shape = np.broadcast_shapes(tau.shape, np.shape(self.eta if self.eta is not None else 0),
+                                    np.shape(self.D if self.D is not None else 0), np.shape(self.lamba),
+                                    np.shape(Jv if Jv is not None else 0))
+        m = int(np.prod(shape)) if shape else 1
+        taus = _arr(tau, m)
+        etas = _arr(self.eta, m) if self.mod_type == "exp_pist_flow" else None
+        Ds = _arr(self.D, m) if self.mod_type == "dispersion" else None
+        th = self._t_half_arg()
+        per_th = np.ndim(th) > 0
+        ths = _arr(th, m) if per_th else None
+        per_J = np.ndim(Jv) > 0 if Jv is not None else False
+        Js = _arr(Jv, m) if per_J else None
+        out = np.empty(m)
+        p = lambda a: a.ctypes.data_as(C.c_void_p) if a is not None else None  # noqa: E731
+        ctx.check(ctx.lib.ngrtd_conv(ctx.h, sid, MOD_IDS[self.mod_type], accum, p(taus), p(etas), p(Ds), p(ths),
+                                     0.0 if per_th else float(th), p(Js),
+                                     0.0 if (per_J or Jv is None or Jv is False) else float(Jv),
+                                     m, out.ctypes.data_as(C.c_void_p), _lib.MEM_HOST), "ngrtd_conv")
+        self.C_i = float(out[0]) if shape == () else out.reshape(shape)
+        return self.C_i

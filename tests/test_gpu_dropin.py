@@ -1,0 +1,160 @@
+"""GPU tests of the reference-shaped drop-in modules (noble_gas_utils, convolution_
+integral_utils, run_age_mcmc_utils.ForwardMod / conv_mcmc, noble_gas_mcmc) against the
+golden vectors, plus the c1 sampler plumbing checked statistically against the
+reference's posterior summary ng_interp/ng_optPLM1.csv."""
+import numpy as np
+import pandas as pd
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GASES = ["He", "Ne", "Ar", "Kr", "Xe"]
+
+
+def close(a, b, rtol=1e-12, atol=0.0):
+    a, b = np.asarray(a), np.asarray(b)
+    ok = (np.isnan(a) & np.isnan(b)) | (np.isinf(a) & np.isinf(b) & (np.sign(a) == np.sign(b)))
+    ok |= np.abs(a - b) <= atol + rtol * np.abs(b)
+    return ok
+
+
+def test_noble_gas_fun_scalar_and_batched(golden):
+    from noblegas_rtd_mcmc_amd import noble_gas_utils as ng
+    z = golden("ce_golden.npz")
+    sel = np.nonzero(z["pmode"] == 0)[0][:40]
+    for i in sel[:8]:            # scalar calls: floats, like the reference
+        o = ng.noble_gas_fun(gases=GASES, E=float(z["E"][i]), T=float(z["T"][i]), Ae=float(z["Ae"][i]),
+                             F=float(z["F"][i]), P="lapse_rate", S=float(z["S"][i]))
+        r = o.ce_exc(True)
+        assert all(isinstance(r[g], float) for g in GASES)
+        assert close([r[g] for g in GASES], z["ce_total"][i]).all()
+        assert close(o.vapor_pressure(), z["vapor"][i], 1e-13)
+        assert close(o.solubility("Xe"), z["solubility"][i, 4])
+    o = ng.noble_gas_fun(gases=GASES, E=z["E"][sel], T=z["T"][sel], Ae=z["Ae"][sel], F=z["F"][sel], P="lapse_rate")
+    for key, d in (("ce_total", o.ce_exc(True)), ("ce_excess", o.ce_exc(False)), ("equil_dry", o.equil_conc_dry()),
+                   ("equil", o.equil_conc())):
+        assert close(np.stack([d[g] for g in GASES], 1), z[key][sel]).all(), key
+    one = ng.noble_gas_fun(gases=GASES, E=3000., T=5., Ae=0.01, F=0.5, P="1atm")
+    assert one.P == 0.000101325
+    one.update_pars(T=5., Ae=0.01, F=0.5, E=3000.)
+    r = one.ce_exc(True)     # SURVEY.md §8c measured value of the reference at these inputs
+    assert close(r["He"], 4.8383457752e-08, 1e-10) and close(r["Xe"], 1.1721013542e-08, 1e-10)
+
+
+def test_ce_exc_wrapper(golden):
+    from noblegas_rtd_mcmc_amd.noble_gas_mcmc import ce_exc_wrapper
+    z = golden("ce_golden.npz")
+    th = z["wrap_theta"]
+    for i in range(0, th.shape[1], 97):
+        assert close(ce_exc_wrapper(th[:, i]), z["wrap_out"][i]).all()
+
+
+TRACERS = {"CFC12": ("CFC12", False, False, False), "SF6": ("SF6", False, False, False),
+           "H3": ("H3", 12.34, False, False), "He3": ("H3", 12.34, "3He", False),
+           "He4_ter": ("He4_ter", False, "4He", 3.30885e-11)}
+MODS = ["piston", "exponential", "exp_pist_flow", "dispersion"]
+
+
+def frame(tname, n):
+    from noblegas_rtd_mcmc_amd.workloads import atmos_series
+    sname = TRACERS[tname][0]
+    s = atmos_series(sname, n)
+    c = s.c_by_age * (0.0 if tname == "He4_ter" else 1.0)
+    return pd.DataFrame({tname: np.flip(c)}, index=np.arange(n - 1, -1, -1))
+
+
+@pytest.mark.parametrize("tname", list(TRACERS))
+def test_tracer_conv_integral(golden, tname):
+    from noblegas_rtd_mcmc_amd.convolution_integral_utils import tracer_conv_integral
+    z = golden("conv_golden.npz")
+    _, t_half, accum, J = TRACERS[tname]
+    df = frame(tname, 1200)
+    for mod in MODS:
+        key = "%s_%s_1200" % (tname, mod)
+        tau, eta, D, ref = z[key + "_tau"], z[key + "_eta"], z[key + "_D"], z[key + "_out"]
+        cm = tracer_conv_integral(df.copy(), df.index[-1])
+        for i in range(3):      # scalar path: one convolution per call, like ForwardMod
+            cm.update_pars(tau=float(tau[i]), mod_type=mod, t_half=t_half, rad_accum=accum, J=J,
+                           eta=float(eta[i]), D=float(D[i]), bbar=False, Phi_im=False)
+            assert close(cm.convolve(), ref[i], 1e-12, 1e-300)
+        cm.update_pars(tau=tau, mod_type=mod, t_half=t_half, rad_accum=accum, J=J, eta=eta, D=D)
+        got = cm.convolve()      # batched path: all parameter sets in one launch
+        assert close(got, ref, 1e-12, 1e-300).all(), key
+    cm.update_pars(tau=37.3, mod_type="exponential", t_half=t_half, rad_accum=accum, J=J)
+    with pytest.raises(NotImplementedError):
+        cm.update_pars(tau=1.0, mod_type="frac_inf_diff")
+        cm.convolve()
+
+
+def test_gen_g_tp_and_g_tau(golden):
+    from noblegas_rtd_mcmc_amd.convolution_integral_utils import tracer_conv_integral
+    z = golden("conv_golden.npz")
+    df = frame("CFC12", 1200)
+    cm = tracer_conv_integral(df, df.index[-1])
+    for (mi, tau, eta, D), g in zip(z["gtp_params"], z["gtp"]):
+        cm.update_pars(tau=tau, mod_type=MODS[int(mi)], eta=eta, D=D)
+        assert close(cm.gen_g_tp(), g, 1e-12, 1e-300).all()
+    cm.update_pars(tau=10.0, mod_type="exponential", t_half=12.34)
+    assert close(cm.convolve(g_tau=z["gext"]), z["gext_out"], 1e-12)
+
+
+FWD_CASES = [("exp_J_thalf_lamsf6", "exponential", False, ["tau1", "J", "thalf_cfc", "lamsf6"]),
+             ("epm", "exp_pist_flow", False, ["tau1", "eta1"]),
+             ("bmm_exp_piston", "exponential", "piston", ["tau1", "tau2", "f1", "f2"]),
+             ("bmm_disp_exp", "dispersion", "exponential", ["tau1", "tau2", "f1", "f2", "D1"])]
+
+
+@pytest.mark.parametrize("case", FWD_CASES, ids=[c[0] for c in FWD_CASES])
+def test_forward_mod_perform_and_batch(golden, case):
+    from noblegas_rtd_mcmc_amd.run_age_mcmc_utils import ForwardMod
+    z = golden("fwd_golden.npz")
+    name, m1, m2, pn = case
+    th = z[name + "_theta"]
+    for tname, (_, t_half, accum, _) in TRACERS.items():
+        kw = {"C_t": frame(tname, 1200), "mod_type1": m1, "mod_type2": m2, "t_half": t_half, "rad_accum": accum}
+        op = ForwardMod(kw, pn, tname)
+        ref = z["%s_%s" % (name, tname)]
+        out = [[None]]
+        op.perform(None, [th[0]], out)          # the Theano Op boundary, W = 1
+        assert isinstance(out[0][0], np.ndarray) and out[0][0].ndim == 0
+        assert close(out[0][0], ref[0], 1e-12, 1e-300)
+        assert close(ForwardMod(kw, pn, tname).batch(th), ref, 1e-12, 1e-300).all(), (name, tname)
+
+
+def test_conv_mcmc_logp_matches_oracle():
+    import oracle.models as om
+    from noblegas_rtd_mcmc_amd.run_age_mcmc_utils import conv_mcmc
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    rng = np.random.default_rng(9)
+    tracers = ["CFC12", "SF6", "H3", "He4_ter"]
+    okw = {t: {"obs_df": pd.Series(rng.lognormal(0, 0.1, 50) * v), "obs_perr": 0.05}
+           for t, v in zip(tracers, (36.4, 1.25, 4.9, 8.8e-9))}
+    ckw = {"mod_type1": "exponential", "mod_type2": False}
+    for t in tracers:
+        ckw[t] = {"C_t": frame(t, 1200)}
+        if t == "He4_ter":
+            ckw[t]["rad_accum"] = "4He"
+        if t == "H3":
+            ckw[t]["t_half"] = 12.34
+    pkw = {"tau1_low": 1.0, "tau1_high": 1000.0, "J_mu": -10.42, "J_sd": 0.33, "par_names": ["tau1", "J"]}
+    m = conv_mcmc("PLM1", tracers, okw, ckw, pkw, "", 1)
+    lp = m.build_mcmc_model_joint_sT()
+    th = wl.sample_prior(lp.spec, 40, rng)
+    assert close(lp(th, soa=True), om.log_prob(lp.spec, th), 1e-12, 1e-9).all()
+
+
+def test_c1_sampler_recovers_reference_posterior():
+    """c1: CE model of PLM1 (Ne, Ar, Kr, Xe), 100 walkers x 500 steps on the GPU log-prob.
+    The posterior means must land within the reference run's posterior spread
+    (ng_interp/ng_optPLM1.csv: T 1.33 +- 0.87 C, E 2974 +- 88 m) -- a statistical, not
+    bitwise, check (PyMC3's DEMetropolisZ is not available here: parity unpinned)."""
+    from noblegas_rtd_mcmc_amd.noble_gas_mcmc import CEModel
+    from noblegas_rtd_mcmc_amd.workloads import field_data
+    fd = field_data()
+    m = CEModel(fd["obs"], ["PLM1"], max_walkers=128)
+    res = m.sample(nwalkers=100, tune=300, draws=200, seed=12345, tune_interval=50)
+    assert 0.02 < res["accept_rate"] < 0.9
+    s = res["samples"][::4]                       # [n, 6, 1, W]
+    det = m.deterministics(np.moveaxis(s, 0, -1).reshape(6, 1, -1))
+    T, E = det["T"].mean(), det["E"].mean()
+    assert abs(T - 1.325) < 0.87 and abs(E - 2974.2) < 88.1, (T, E)

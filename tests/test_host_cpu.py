@@ -1,0 +1,106 @@
+"""CPU tests of the host-side logic: specs, layouts, workloads, sampler mechanics, and the
+drop-in modules' argument handling (no device calls)."""
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+from noblegas_rtd_mcmc_amd import spec as S
+from noblegas_rtd_mcmc_amd import workloads as wl
+
+
+def test_roles_and_layout():
+    spec = wl.c4_spec(L=3, N=50)
+    assert spec.roles == ["Ae_beta", "F_beta", "E_beta", "m", "b_beta", "nu_ce_beta", "tau1", "nu_rtd_beta"]
+    th = wl.sample_prior(spec, 5, np.random.default_rng(0))
+    assert th.shape == (8, 3, 5)
+    wlp = spec.theta_wlp(th)
+    assert wlp.shape == (5, 3, 8)
+    assert np.array_equal(spec.theta_soa(wlp), th)
+    assert np.array_equal(spec.theta_soa(wlp.reshape(5, 24)), th)
+    ri = spec.role_index()
+    assert ri[S.ROLE_IDS["tau1"]] == 6 and ri[S.ROLE_IDS["J"]] == -1
+
+
+def test_spec_validation():
+    fd = wl.field_data()
+    with pytest.raises(ValueError):
+        S.ModelSpec(n_wells=1)
+    with pytest.raises(ValueError):
+        S.CEBlock(obs=np.ones((2, 3)), sd=np.ones((2, 3)), E_min=np.ones(2), gases=("Ne", "Ar"))
+    t = wl.tracer("CFC12", 10)
+    with pytest.raises(ValueError):
+        S.RTDBlock(tracers=[t], obs=np.ones((1, 1)), sd=np.ones((1, 1)), mod_type1="frac_inf_diff")
+    with pytest.raises(ValueError):
+        S.RTDBlock(tracers=[t, wl.tracer("SF6", 11)], obs=np.ones((1, 2)), sd=np.ones((1, 2)))
+    assert fd["well_elev"]["PLM1"] == 2786.889893
+
+
+def test_bmm_roles_and_priors_sampling():
+    spec = wl.c4_spec(L=2, N=40, mod_type1="exp_pist_flow", mod_type2="piston",
+                      par_names=("tau1", "tau2", "f1", "eta1", "J", "thalf_cfc", "lamsf6"))
+    th = wl.sample_prior(spec, 200, np.random.default_rng(1))
+    r = dict(zip(spec.roles, th))
+    assert (r["tau2"] >= 50).all() and (r["tau2"] <= 15000).all()
+    assert (r["f1"] >= 0.01).all() and (r["lamsf6"] >= 0).all()
+    assert ((r["thalf_cfc_beta"] > 0) & (r["thalf_cfc_beta"] < 1)).all()
+
+
+def test_workload_shapes():
+    spec, th = wl.c2(W=16)
+    assert spec.n_wells == 3 and spec.ce.gases == ("He", "Ne", "Ar", "Kr", "Xe") and th.shape == (6, 3, 16)
+    spec, th = wl.c3(W=16)
+    assert spec.rtd.n_ages == 1200 and spec.roles == ["tau1", "nu_rtd_beta", "J"]
+    spec, th = wl.c1()
+    assert th.shape == (6, 1, 100)
+    s = wl.atmos_series("H3", 25256)
+    assert s.n == 25256 and s.c_by_age[-1] == 3.3273 and s.c_by_age[0] > 0
+
+
+def test_series_from_reference_frames():
+    from noblegas_rtd_mcmc_amd.convolution_integral_utils import _series_arrays
+    idx = np.arange(9, -1, -1)
+    df = pd.DataFrame({"He4_ter": np.zeros(10), "other": np.ones(10)}, index=idx)
+    v, i = _series_arrays(df, "4He")
+    assert np.array_equal(v, np.zeros(10)) and np.array_equal(i, idx)
+    with pytest.raises(ValueError):
+        _series_arrays(df, False)
+    v, i = _series_arrays(pd.DataFrame({"x": np.arange(10.0)}, index=idx), False)
+    assert np.array_equal(v, np.arange(10.0))
+    ser = S.Series.from_reference_frame(v, i, 3.7)
+    assert ser.dtp == 3.0 and ser.c_by_age[0] == 9.0
+
+
+def test_de_sampler_gaussian():
+    """Population DE-MC recovers a correlated 2-D Gaussian (CPU, torch)."""
+    from noblegas_rtd_mcmc_amd.sampler import DEMetropolis
+    cov = np.array([[1.0, 0.6], [0.6, 2.0]])
+    P = torch.from_numpy(np.linalg.inv(cov))
+
+    def lp(x):   # x [2, W]
+        return -0.5 * torch.einsum("iw,ij,jw->w", x, P, x)
+    x0 = torch.from_numpy(np.random.default_rng(0).normal(size=(2, 64)) * 3)
+    res = DEMetropolis(lp, tune_interval=50, seed=1).run(x0, tune=400, draws=800)
+    s = res["samples"].permute(0, 2, 1).reshape(-1, 2).numpy()
+    assert np.allclose(s.mean(0), 0, atol=0.12)
+    assert np.allclose(np.cov(s.T), cov, atol=0.3)
+    assert 0.05 < res["accept_rate"] < 0.9
+    again = DEMetropolis(lp, tune_interval=50, seed=1).run(x0, tune=400, draws=800)
+    assert torch.equal(again["samples"], res["samples"])
+
+
+def test_pymc3_tune_schedule():
+    from noblegas_rtd_mcmc_amd.sampler import pymc3_tune
+    assert pymc3_tune(1.0, 0.0005) == 0.1 and pymc3_tune(1.0, 0.96) == 10.0 and pymc3_tune(1.0, 0.3) == 1.0
+
+
+def test_ce_sampler_plumbing_with_cpu_logp():
+    """c1 plumbing: the DE sampler driving the CE log-prob (oracle as the CPU log-prob)."""
+    import oracle.models as om
+    from noblegas_rtd_mcmc_amd.sampler import DEMetropolis
+    spec, th = wl.c1(W=12)
+
+    def lp(x):
+        return torch.from_numpy(om.log_prob(spec, x.numpy()))
+    res = DEMetropolis(lp, tune_interval=5, seed=2).run(torch.from_numpy(th), tune=10, draws=5)
+    assert res["samples"].shape == (5, 6, 1, 12) and torch.isfinite(res["logp"]).all()
