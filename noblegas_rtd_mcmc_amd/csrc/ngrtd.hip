@@ -579,15 +579,26 @@ static int upload(ngrtd_ctx* ctx, DevBuf& b, const double* src, size_t n) {
 
 // StudentT precision terms per observation: lam = sd^-2 and 0.5*log(lam), laid out as
 // [lam(L*n) | hll(L*n)]; sd <= 0 (or NaN) stores lam = -1 so the bound gives -inf.
-static int upload_lam(ngrtd_ctx* ctx, DevBuf& b, const double* sd, size_t n) {
-    std::vector<double> h(2 * n);
-    for (size_t i = 0; i < n; ++i) {
+// ... followed by per-well sums of 0.5*log(lam) ([L]) for st_block.
+static int upload_lam(ngrtd_ctx* ctx, DevBuf& b, const double* sd, size_t L, size_t n) {
+    const size_t m = L * n;
+    std::vector<double> h(2 * m + L, 0.0);
+    for (size_t i = 0; i < m; ++i) {
         const double lam = std::pow(sd[i], -2.0);
         const bool ok = sd[i] > 0 && lam > 0;
         h[i] = ok ? lam : -1.0;
-        h[n + i] = ok ? 0.5 * std::log(lam) : 0.0;
+        h[m + i] = ok ? 0.5 * std::log(lam) : 0.0;
+        h[2 * m + i / n] += h[m + i];
     }
-    return upload(ctx, b, h.data(), 2 * n);
+    return upload(ctx, b, h.data(), h.size());
+}
+
+// a-1 / b-1 when both are small non-negative integers (beta_logp_fast), else -1
+static void beta_int(double a, double b, int32_t* ia, int32_t* ib) {
+    const double x = a - 1, y = b - 1;
+    const bool ok = x >= 0 && y >= 0 && x <= 4 && y <= 4 && x == std::floor(x) && y == std::floor(y);
+    *ia = ok ? (int32_t)x : -1;
+    *ib = ok ? (int32_t)y : -1;
 }
 
 int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_walkers, ngrtd_plan** out) {
@@ -617,8 +628,9 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
         NG_CHECK(upload(ctx, p->ce_obs, d->ce_obs, (size_t)L * G));
         NG_CHECK(upload(ctx, p->ce_sd, d->ce_sd, (size_t)L * G));
         NG_CHECK(upload(ctx, p->ce_emin, d->ce_E_min, (size_t)L));
-        NG_CHECK(upload_lam(ctx, p->ce_lam, d->ce_sd, (size_t)L * G));
+        NG_CHECK(upload_lam(ctx, p->ce_lam, d->ce_sd, (size_t)L, (size_t)G));
         u.ce_lam = p->ce_lam.d(); u.ce_hll = p->ce_lam.d() + (size_t)L * G;
+        u.ce_hll_sum = p->ce_lam.d() + (size_t)2 * L * G;
         u.ce_on = 1; u.G = G;
         for (int j = 0; j < G; ++j) {
             if (d->ce_gas_ids[j] < 0 || d->ce_gas_ids[j] > 4) return set_err(ctx, NGRTD_EINVAL, "bad gas id");
@@ -635,6 +647,7 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
         for (int i = 0; i < 5; ++i) {
             u.ce_ba[i] = d->ce_beta_a[i]; u.ce_bb[i] = d->ce_beta_b[i];
             u.ce_betaln[i] = host_betaln(d->ce_beta_a[i], d->ce_beta_b[i]);
+            beta_int(d->ce_beta_a[i], d->ce_beta_b[i], &u.ce_bia[i], &u.ce_bib[i]);
         }
     }
     if (d->rtd_enabled) {
@@ -671,8 +684,9 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
         p->tp0 = (0.0 + 1e-5) + p->dtp;
         NG_CHECK(upload(ctx, p->rtd_obs, d->rtd_obs, (size_t)L * K));
         NG_CHECK(upload(ctx, p->rtd_sd, d->rtd_sd, (size_t)L * K));
-        NG_CHECK(upload_lam(ctx, p->rtd_lam, d->rtd_sd, (size_t)L * K));
+        NG_CHECK(upload_lam(ctx, p->rtd_lam, d->rtd_sd, (size_t)L, (size_t)K));
         u.rtd_lam = p->rtd_lam.d(); u.rtd_hll = p->rtd_lam.d() + (size_t)L * K;
+        u.rtd_hll_sum = p->rtd_lam.d() + (size_t)2 * L * K;
         HIP_TRY(ctx, p->conc.ensure((size_t)K * Umax * sizeof(double)));
         RtdArgs& a = p->rtd;
         a.row_tau[0] = ri[NGRTD_ROLE_TAU1]; a.row_tau[1] = ri[NGRTD_ROLE_TAU2];
@@ -713,6 +727,8 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
         u.ls_tau = std::pow(d->lamsf6_sd, -2.0); u.ls_half_log = 0.5 * std::log(u.ls_tau * 2.0 / M_PI);
         u.rnu_min = d->rtd_nu_min; u.rnu_max = d->rtd_nu_max; u.rnu_a = d->rtd_nu_a; u.rnu_b = d->rtd_nu_b;
         u.rnu_betaln = host_betaln(d->rtd_nu_a, d->rtd_nu_b);
+        beta_int(d->rtd_nu_a, d->rtd_nu_b, &u.rnu_ia, &u.rnu_ib);
+        beta_int(d->thalf_a, d->thalf_b, &u.th_ia, &u.th_ib);
     }
     HIP_TRY(ctx, p->ulogp.ensure((size_t)Umax * sizeof(double)));
     u.ulogp = p->ulogp.d();
@@ -797,6 +813,16 @@ static int plan_run(ngrtd_plan* p, const double* theta, int64_t W, double* logp,
             HIP_TRY(ctx, hipGetLastError());
             NG_CHECK(timed_end(p, prof, st, 2, ev));
         }
+    } else if (logp && p->desc.n_wells <= 512) {
+        // per-unit log-prob + per-walker sum over wells, one launch
+        int LS = 1;
+        while (LS < p->desc.n_wells) LS *= 2;
+        const int WB = 512 / LS;
+        NG_CHECK(timed_begin(p, prof, st, &ev));
+        hipLaunchKernelGGL(unit_walker_kernel, dim3((unsigned)cdiv(W, WB)), dim3(512), (size_t)512 * sizeof(double),
+                           st, u, WB, LS, logp);
+        HIP_TRY(ctx, hipGetLastError());
+        NG_CHECK(timed_end(p, prof, st, 1, ev));
     } else if (logp || ce_out) {
         NG_CHECK(timed_begin(p, prof, st, &ev));
         hipLaunchKernelGGL(unit_logp_kernel, dim3((unsigned)cdiv(U, 256)), dim3(256), 0, st, u);

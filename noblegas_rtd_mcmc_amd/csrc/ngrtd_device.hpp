@@ -49,6 +49,8 @@ struct UnitArgs {
     const double* ce_sd;
     const double* ce_lam;   // [L][G] sd^-2 (<= 0 when sd <= 0: StudentT bound -> -inf)
     const double* ce_hll;   // [L][G] 0.5 * log(sd^-2)
+    const double* ce_hll_sum;   // [L] sum over gases of ce_hll
+    int32_t ce_bia[5], ce_bib[5];   // integer Beta exponents a-1, b-1 (or -1): beta_logp_fast
     const double* ce_Emin;  // [L]
     double E_max, logA_min, logA_max, logF_min, logF_max, b_min, b_max, nu_min, nu_max;
     double m_mu, m_tau, m_log_tau_2pi;
@@ -59,6 +61,8 @@ struct UnitArgs {
     const double* rtd_sd;
     const double* rtd_lam;  // [L][K]
     const double* rtd_hll;
+    const double* rtd_hll_sum;  // [L]
+    int32_t rnu_ia, rnu_ib, th_ia, th_ib;
     int32_t row_tau1, row_nu, row_tau2, row_f1, row_eta1, row_eta2, row_D1, row_D2, row_J, row_thalf, row_lamsf6;
     double tau1_lo, tau1_hi, tau1_nlw, tau2_lo, tau2_hi, tau2_nlw, f1_lo, f1_hi, f1_nlw;
     double eta1_lo, eta1_hi, eta1_nlw, eta2_lo, eta2_hi, eta2_nlw;

@@ -387,7 +387,7 @@ __global__ void __launch_bounds__(256) rtd_conc_kernel(const RtdArgs a) {
 // decided without the exp/log; the He branch reuses the Ar exponential (:172).
 __device__ __forceinline__ void ce_model_s0(const UnitArgs& a, double T, double P, double Ae, double F,
                                             double* mod) {
-    const double Pv = vapor_pressure(T);
+    const double Pv = vapor_pressure_fast(T);
     const double T_k = T + 273.15;
     const double x = .001 * T_k, x2 = x * x, x3 = x * x * x;
     const double x1 = .01 * T_k;
@@ -407,13 +407,13 @@ __device__ __forceinline__ void ce_model_s0(const UnitArgs& a, double T, double 
         if (T < 65. && gj == 1.) gj = isfinite(c.G2 / x1) ? 1. : __builtin_nan("");
         double K;
         if (g == 0) {
-            if (!have_ar) { exp_ar = exp(ar.A0 + (ar.A1 / x) + (ar.A2 / x2) + (ar.A3 / x3)); have_ar = true; }
-            const double Fh = exp(c.A0 + (c.A1 / x) + (c.A2 / x2) + (c.A3 / x3));
+            if (!have_ar) { exp_ar = fexp(ar.A0 + (ar.A1 / x) + (ar.A2 / x2) + (ar.A3 / x3)); have_ar = true; }
+            const double Fh = fexp(c.A0 + (c.A1 / x) + (c.A2 / x2) + (c.A3 / x3));
             const double X_Ar_water = 1. / exp_ar * 9.31e-3;
             const double X_he_water = Fh * (5.24e-6 / 9.31e-3) * X_Ar_water;
             K = gj * (5.24e-6 / X_he_water);
         } else {
-            const double e = exp(c.A0 + (c.A1 / x) + (c.A2 / x2) + (c.A3 / x3));
+            const double e = fexp(c.A0 + (c.A1 / x) + (c.A2 / x2) + (c.A3 / x3));
             if (g == 2 && !have_ar) { exp_ar = e; have_ar = true; }
             K = gj * e;
         }
@@ -450,12 +450,12 @@ __device__ __forceinline__ double unit_logp(const UnitArgs& a, int64_t u, const 
 #pragma unroll
         for (int i = 0; i < 6; ++i) p[i] = a.theta[(int64_t)a.row_ce[i] * a.U + u];
         if (want_prior) {
-            lp += beta_logp(p[0], a.ce_ba[0], a.ce_bb[0], a.ce_betaln[0]);
-            lp += beta_logp(p[1], a.ce_ba[1], a.ce_bb[1], a.ce_betaln[1]);
-            lp += beta_logp(p[2], a.ce_ba[2], a.ce_bb[2], a.ce_betaln[2]);
+            lp += beta_logp_fast(p[0], a.ce_ba[0], a.ce_bb[0], a.ce_betaln[0], a.ce_bia[0], a.ce_bib[0]);
+            lp += beta_logp_fast(p[1], a.ce_ba[1], a.ce_bb[1], a.ce_betaln[1], a.ce_bia[1], a.ce_bib[1]);
+            lp += beta_logp_fast(p[2], a.ce_ba[2], a.ce_bb[2], a.ce_betaln[2], a.ce_bia[2], a.ce_bib[2]);
             lp += normal_logp(p[3], a.m_mu, a.m_tau, a.m_log_tau_2pi);
-            lp += beta_logp(p[4], a.ce_ba[3], a.ce_bb[3], a.ce_betaln[3]);
-            lp += beta_logp(p[5], a.ce_ba[4], a.ce_bb[4], a.ce_betaln[4]);
+            lp += beta_logp_fast(p[4], a.ce_ba[3], a.ce_bb[3], a.ce_betaln[3], a.ce_bia[3], a.ce_bib[3]);
+            lp += beta_logp_fast(p[5], a.ce_ba[4], a.ce_bb[4], a.ce_betaln[4], a.ce_bia[4], a.ce_bib[4]);
             if (jac) lp += jac_logodds(p[0]) + jac_logodds(p[1]) + jac_logodds(p[2]) + jac_logodds(p[4]) + jac_logodds(p[5]);
         }
         if (want_like || a.ce_out) {
@@ -468,11 +468,11 @@ __device__ __forceinline__ double unit_logp(const UnitArgs& a, int64_t u, const 
             const double T = (E - b) / p[3];
             const double nu = p[5] * (a.nu_max - a.nu_min) + a.nu_min;
             double mod[kMaxGas];
-            ce_model_s0(a, T, lapse_rate(E), exp10(Ae_log), exp10(F_log), mod);
+            ce_model_s0(a, T, lapse_rate_fast(E), exp10_fast(Ae_log), exp10_fast(F_log), mod);
             if (a.ce_out)
                 for (int j = 0; j < a.G; ++j) a.ce_out[(int64_t)j * a.U + u] = mod[j];
             if (want_like)
-                lp += st_sum(a.G, a.ce_obs + l * a.G, mod, a.ce_lam + l * a.G, a.ce_hll + l * a.G, nu);
+                lp += st_block(a.G, a.ce_obs + l * a.G, mod, a.ce_lam + l * a.G, a.ce_hll_sum[l], nu);
         }
     }
     if (a.rtd_on) {
@@ -480,7 +480,7 @@ __device__ __forceinline__ double unit_logp(const UnitArgs& a, int64_t u, const 
         const double nub = a.theta[(int64_t)a.row_nu * a.U + u];
         if (want_prior) {
             lp += uniform_logp(tau1, a.tau1_lo, a.tau1_hi, a.tau1_nlw);
-            lp += beta_logp(nub, a.rnu_a, a.rnu_b, a.rnu_betaln);
+            lp += beta_logp_fast(nub, a.rnu_a, a.rnu_b, a.rnu_betaln, a.rnu_ia, a.rnu_ib);
             if (jac) lp += jac_interval(tau1, a.tau1_lo, a.tau1_hi) + jac_logodds(nub);
 #define NGRTD_UNIF(row, lo, hi, nlw)                                                   \
     if (a.row >= 0) {                                                                  \
@@ -498,7 +498,7 @@ __device__ __forceinline__ double unit_logp(const UnitArgs& a, int64_t u, const 
             if (a.row_J >= 0) lp += normal_logp(a.theta[(int64_t)a.row_J * a.U + u], a.J_mu, a.J_tau, a.J_log_tau_2pi);
             if (a.row_thalf >= 0) {
                 const double x = a.theta[(int64_t)a.row_thalf * a.U + u];
-                lp += beta_logp(x, a.th_a, a.th_b, a.th_betaln);
+                lp += beta_logp_fast(x, a.th_a, a.th_b, a.th_betaln, a.th_ia, a.th_ib);
                 if (jac) lp += jac_logodds(x);
             }
             if (a.row_lamsf6 >= 0) {
@@ -509,7 +509,7 @@ __device__ __forceinline__ double unit_logp(const UnitArgs& a, int64_t u, const 
         }
         if (want_like) {
             const double nu = nub * (a.rnu_max - a.rnu_min) + a.rnu_min;   // run_age_mcmc_utils.py:292
-            lp += st_sum(a.K, a.rtd_obs + l * a.K, conc, a.rtd_lam + l * a.K, a.rtd_hll + l * a.K, nu);
+            lp += st_block(a.K, a.rtd_obs + l * a.K, conc, a.rtd_lam + l * a.K, a.rtd_hll_sum[l], nu);
         }
     }
     return lp;
@@ -522,6 +522,31 @@ __global__ void __launch_bounds__(256) unit_logp_kernel(const UnitArgs a) {
     if (a.rtd_on)
         for (int t = 0; t < a.K; ++t) conc[t] = a.conc[(int64_t)t * a.U + u];
     a.ulogp[u] = unit_logp(a, u, conc);
+}
+
+// Per-unit log-prob AND the per-walker sum over wells in one launch (L <= 512): a block
+// owns WB walkers x LS >= L well slots, one unit per thread; the wells of each walker are
+// then added in well order through LDS (deterministic, no atomics, no second launch).
+__global__ void __launch_bounds__(512) unit_walker_kernel(const UnitArgs a, int32_t WB, int32_t LS,
+                                                          double* __restrict__ logp) {
+    extern __shared__ __attribute__((aligned(16))) double part[];   // [LS][WB]
+    const int wl = threadIdx.x % WB, l = threadIdx.x / WB;
+    const int64_t w = (int64_t)blockIdx.x * WB + wl;
+    double s = 0.0;
+    if (w < a.W && l < a.L) {
+        const int64_t u = (int64_t)l * a.W + w;
+        double conc[kMaxTracer];
+        if (a.rtd_on)
+            for (int t = 0; t < a.K; ++t) conc[t] = a.conc[(int64_t)t * a.U + u];
+        s = unit_logp(a, u, conc);
+    }
+    part[l * WB + wl] = s;
+    __syncthreads();
+    if (l == 0 && w < a.W) {
+        double tot = part[wl];
+        for (int i = 1; i < a.L; ++i) tot += part[i * WB + wl];
+        logp[w] = tot;
+    }
 }
 
 // ------------------------------------------- exponential RTD on the matrix cores

@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include "ngrtd_fastmath.hpp"
+
 #define NGRTD_HD __host__ __device__ __forceinline__
 
 namespace ngrtd {
@@ -44,6 +46,25 @@ NGRTD_HD double vapor_pressure(double T) {
     if (T <= 99.0) { A = 8.07131; B = 1730.63; C = 233.426; }
     else           { A = 8.14019; B = 1810.94; C = 244.485; }
     double P = pow(10.0, A - (B / (C + T)));
+    P = P / 760. * 101325;
+    return P / 1.0e9;
+}
+
+// ---- likelihood-path variants (one call per (walker, well) in the batched log-prob).
+// OCML's pow/exp10/log1p are double-double accurate (~0.5 ulp) and several times the cost
+// of exp/log.  Here 10**y = exp(y ln10) and b**c = exp(c log b): the argument rounding
+// adds |y ln10| * 2^-53 (< 3e-15 for the CE ranges) relative error -- far inside the
+// 1e-12 parity bar (DESIGN.md 'Numerics').
+constexpr double kLn10 = 2.302585092994045684;
+NGRTD_HD double exp10_fast(double y) { return fexp(y * kLn10); }
+NGRTD_HD double lapse_rate_fast(double E) {
+    return fexp(5.2561 * flog(1 - .0065 * E / 288.15)) * 0.000101325;
+}
+NGRTD_HD double vapor_pressure_fast(double T) {
+    double A, B, C;
+    if (T <= 99.0) { A = 8.07131; B = 1730.63; C = 233.426; }
+    else           { A = 8.14019; B = 1810.94; C = 244.485; }
+    double P = exp10_fast(A - (B / (C + T)));
     P = P / 760. * 101325;
     return P / 1.0e9;
 }
@@ -100,16 +121,116 @@ NGRTD_HD double ce_excess(int g, double Ae, double F, double C_eq) {
 }
 
 // ---------------------------------------------------------------- log densities
+// lgamma(x + 1/2) - lgamma(x) for x > 0, without two general lgamma() calls (the
+// StudentT normaliser needs only this difference).  Shift x up by the recurrence
+// lgamma(y+1) = lgamma(y) + log(y) until y >= 12, then the asymptotic series
+//   D(y) = 1/2 log y + sum_{m>=1} (2^(1-2m) - 2) B_2m / (2m (2m-1) y^(2m-1))
+// (Bernoulli numbers B_2m), truncated after y^-13: the first omitted term is
+// < 5e-18 at y = 12.  Branch-free (fixed 12-step shift with selects) so the lanes of a
+// wavefront never diverge.
+NGRTD_HD double lgamma_half_diff(double x) {
+    double P = 1.0, Q = 1.0, y = x;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        const bool s = y < 12.0;
+        P = s ? P * (y + 0.5) : P;
+        Q = s ? Q * y : Q;
+        y = s ? y + 1.0 : y;
+    }
+    const double r = 1.0 / y, r2 = r * r;
+    double t = -5461.0 / 425984.0;
+    t = fma(t, r2, 691.0 / 180224.0);
+    t = fma(t, r2, -31.0 / 18432.0);
+    t = fma(t, r2, 17.0 / 14336.0);
+    t = fma(t, r2, -1.0 / 640.0);
+    t = fma(t, r2, 1.0 / 192.0);
+    t = fma(t, r2, -0.125);
+    return 0.5 * log(y) + t * r - log(P / Q);
+}
+
 // StudentT.logp, summed over observations that share nu: the caller adds
 //   st_const(nu) + st_term(x, mu, sigma, nu)
+// st_const = lgamma((nu+1)/2) - lgamma(nu/2), as PyMC3 writes it.
 NGRTD_HD double st_const(double nu) {
-    return lgamma((nu + 1.0) / 2.0) - lgamma(nu / 2.0);
+    return lgamma_half_diff(nu / 2.0);
 }
 NGRTD_HD double st_term(double x, double mu, double sigma, double nu) {
     const double lam = 1.0 / (sigma * sigma);
     const double d = x - mu;
     const double v = 0.5 * log(lam / (nu * kPi)) - (nu + 1.0) / 2.0 * log1p(lam * (d * d) / nu);
     return (lam > 0 && nu > 0 && sigma > 0) ? v : kNegInf;
+}
+
+// Beta.logp with small integer exponents (a-1, b-1 in 0..4, e.g. Beta(2,2), Beta(2,4)):
+// (a-1) log x + (b-1) log1p(-x) = log(x^(a-1) (1-x)^(b-1)) -- one log instead of two.
+// ia/ib < 0 selects the general two-log form.
+NGRTD_HD double ipow_small(double v, int k) {
+    double r = 1.0;
+    for (int i = 0; i < k; ++i) r *= v;
+    return r;
+}
+NGRTD_HD double beta_logp_fast(double x, double a, double b, double betaln_ab, int ia, int ib) {
+    double lp;
+    if (ia >= 0 && ib >= 0) {
+        lp = flog(ipow_small(x, ia) * ipow_small(1 - x, ib)) - betaln_ab;
+    } else {
+        // log1p(-x) as log(1 - x): absolute error <= 2^-53 (parity bar is absolute on logp)
+        const double t1 = (a == 1.0) ? 0.0 : (a - 1) * flog(x);
+        const double t2 = (b == 1.0) ? 0.0 : (b - 1) * flog(1 - x);
+        lp = t1 + t2 - betaln_ab;
+    }
+    return (x >= 0 && x <= 1) ? lp : kNegInf;
+}
+
+// StudentT sum over n observations sharing nu (one likelihood block of a unit):
+//   sum_j [ lgamma((nu+1)/2) - lgamma(nu/2) + 0.5 log(lam_j/(nu pi)) - (nu+1)/2 log1p(z_j) ]
+// with z_j = lam_j (x_j - mu_j)^2 / nu, evaluated as
+//   n * c0 + sum_j 0.5 log lam_j - (nu+1)/2 * log(prod_j (1 + z_j)),
+//   c0 = lgamma((nu+1)/2) - lgamma(nu/2) - 0.5 log(nu pi) in ONE log (see lgamma_half_diff),
+// i.e. 2 logs per block instead of 3 + n.  log(1 + z) vs log1p(z) differs by < 2^-53 per
+// factor.  Very large z (poor fits: z >= 1e15) take the per-observation log1p path so
+// the product cannot overflow.  hll_sum = sum_j 0.5 log lam_j (host precomputed).
+NGRTD_HD double st_block(int n, const double* obs, const double* mu, const double* lam, double hll_sum,
+                         double nu) {
+    double P = 1.0, Q = 1.0, y = nu / 2.0;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        const bool s = y < 12.0;
+        P = s ? P * (y + 0.5) : P;
+        Q = s ? Q * y : Q;
+        y = s ? y + 1.0 : y;
+    }
+    const double r = 1.0 / y, r2 = r * r;
+    double t = -5461.0 / 425984.0;
+    t = fma(t, r2, 691.0 / 180224.0);
+    t = fma(t, r2, -31.0 / 18432.0);
+    t = fma(t, r2, 17.0 / 14336.0);
+    t = fma(t, r2, -1.0 / 640.0);
+    t = fma(t, r2, 1.0 / 192.0);
+    t = fma(t, r2, -0.125);
+    const double qp = Q / P;
+    const double c0 = 0.5 * flog(y * qp * qp / (nu * kPi)) + t * r;
+    double prod = 1.0;
+    bool big = false, ok = nu > 0;
+    for (int j = 0; j < n; ++j) {
+        const double d = obs[j] - mu[j];
+        const double z = lam[j] * (d * d) / nu;
+        prod *= (1.0 + z);
+        big |= !(z < 1.0e15);
+        ok &= lam[j] > 0;
+    }
+    double Lg;
+    if (!big) {
+        Lg = flog(prod);
+    } else {
+        Lg = 0.0;
+        for (int j = 0; j < n; ++j) {
+            const double d = obs[j] - mu[j];
+            Lg += log1p(lam[j] * (d * d) / nu);
+        }
+    }
+    const double v = (double)n * c0 + hll_sum - (nu + 1.0) / 2.0 * Lg;
+    return ok ? v : kNegInf;
 }
 
 // Beta.logp with precomputed betaln(a, b)
