@@ -1,0 +1,84 @@
+"""Accuracy of the device math helpers (fexp, flog, lgamma_half_diff), compiled for the
+host from the same headers the gfx950 kernels include (tools/fastmath_host.cpp).
+
+fexp/flog are measured in ulps against 80-bit long double; lgamma_half_diff against
+scipy.special.gammaln and, for large arguments where gammaln's own cancellation would
+dominate, through the recurrence D(x+1) - D(x) = log1p(1/(2x)).
+"""
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(HERE, "..", "tools", "fastmath_host.cpp")
+
+
+@pytest.fixture(scope="module")
+def host_tool(tmp_path_factory):
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    exe = str(tmp_path_factory.mktemp("fm") / "fm_host")
+    subprocess.run([hipcc, "-O2", "-ffp-contract=off", "-x", "hip", "--offload-arch=gfx950", SRC, "-o", exe],
+                   check=True, capture_output=True)
+
+    def run(op, xs):
+        xs = np.ascontiguousarray(xs, dtype=np.float64)
+        inp = "".join("%s %x\n" % (op, b) for b in xs.view(np.uint64))
+        out = subprocess.run([exe], input=inp, capture_output=True, text=True, check=True).stdout.split()
+        return np.array([int(h, 16) for h in out], dtype=np.uint64).view(np.float64)
+    return run
+
+
+def ulp_err(got, ref_ld):
+    ref = ref_ld.astype(np.float64)
+    ulp = np.spacing(np.abs(ref))
+    return np.abs((got.astype(np.longdouble) - ref_ld) / ulp.astype(np.longdouble)).astype(np.float64)
+
+
+def test_fexp_ulp(host_tool):
+    if np.finfo(np.longdouble).nmant < 60:
+        pytest.skip("long double is not 80-bit here")
+    rng = np.random.default_rng(1)
+    x = np.concatenate([rng.uniform(-745.0, 709.7, 20000), rng.uniform(-1, 1, 5000),
+                        rng.uniform(-40, 5, 5000), [0.0, -0.0, 1e-300, -1e-300, 709.78, -708.3]])
+    got = host_tool("e", x)
+    ref = np.exp(x.astype(np.longdouble))
+    normal = ref.astype(np.float64) > np.finfo(np.float64).tiny
+    assert ulp_err(got[normal], ref[normal]).max() <= 1.0
+    sub = ~normal & (ref > 0)        # subnormal results: absolute error within one subnormal step
+    assert np.all(np.abs(got[sub] - ref[sub].astype(np.float64)) <= 2 * 4.9406564584124654e-324)
+    sp = host_tool("e", np.array([np.nan, np.inf, -np.inf, 710.0, -746.0]))
+    assert np.isnan(sp[0]) and sp[1] == np.inf and sp[2] == 0.0 and sp[3] == np.inf and sp[4] == 0.0
+
+
+def test_flog_ulp(host_tool):
+    if np.finfo(np.longdouble).nmant < 60:
+        pytest.skip("long double is not 80-bit here")
+    rng = np.random.default_rng(2)
+    bits = rng.integers(0x0010000000000000, 0x7FEFFFFFFFFFFFFF, 20000, dtype=np.uint64)
+    x = np.concatenate([bits.view(np.float64), rng.uniform(0.5, 2.0, 10000), 1.0 + rng.uniform(-1e-6, 1e-6, 2000),
+                        [1.0, 2.0, 0.5, 5e-324, 1e-310, 1.7976931348623157e308]])
+    got = host_tool("l", x)
+    ref = np.log(x.astype(np.longdouble))
+    nz = ref != 0
+    assert ulp_err(got[nz], ref[nz]).max() <= 2.0
+    assert got[~nz].max() == 0.0 and got[~nz].min() == 0.0
+    sp = host_tool("l", np.array([0.0, -1.0, np.inf, np.nan, -0.0]))
+    assert sp[0] == -np.inf and np.isnan(sp[1]) and sp[2] == np.inf and np.isnan(sp[3]) and sp[4] == -np.inf
+
+
+def test_lgamma_half_diff(host_tool):
+    from scipy.special import gammaln
+    x = np.concatenate([np.geomspace(1e-3, 100.0, 4000), np.linspace(11.5, 12.5, 200)])
+    got = host_tool("g", x)
+    ref = gammaln(x + 0.5) - gammaln(x)
+    assert np.all(np.abs(got - ref) <= 4e-15 * np.maximum(1.0, np.abs(gammaln(x))))
+    big = np.geomspace(10.0, 1e8, 2000)
+    D0, D1 = host_tool("g", big), host_tool("g", big + 1.0)
+    assert np.all(np.abs((D1 - D0) - np.log1p(0.5 / big)) <= 4 * np.spacing(D1))   # 4 ulp of D
+    big = big[big >= 1e4]        # next asymptotic term 1/(192 x^3) < 1e-14 here
+    assert np.allclose(host_tool("g", big), 0.5 * np.log(big) - 1.0 / (8 * big), rtol=1e-13, atol=0)
