@@ -24,7 +24,8 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 METRIC = "log-likelihood evals/sec (CE + RTD-conv), 2048 walkers, 1/2/4/8 MI355X"
-FP64_VALU_PEAK = 78.6e12     # 256 CU x 4 SIMD x 16 lanes x 2 FLOP (FMA) x 2.4 GHz
+FP64_MFMA_PEAK = 78.6e12     # dense FP64 matrix peak, 256 CU x 4 SIMD x 32 FLOP/clk x 2.4 GHz
+                             # (tools/ubench_fp64.hip measures 78.3: profiles/r01_ubench_fp64.txt)
 HBM_PEAK = 8.0e12            # MI355X_MICROARCH.md chip table
 
 
@@ -158,9 +159,9 @@ def main():
                                    "RTD exponential, N=%d ages)" % (W, args.wells, N),
                        "walkers_per_gpu": W, "wells": args.wells, "gases": 5, "tracers": 5, "ages": N,
                        "parallelism": "walker blocks per GPU + RCCL all-gather of logp" if world > 1 else "single GPU"},
-            "roofline": {"bound": "valu_fp64", "achieved": achieved / 1e12, "peak": FP64_VALU_PEAK / 1e12,
-                         "unit": "TFLOP/s", "frac": achieved / FP64_VALU_PEAK, "traffic": traffic,
-                         "kernel": "rtd_conc_kernel", "kernel_ms": rtd_ms, "flop_per_launch": flops,
+            "roofline": {"bound": "mfma", "achieved": achieved / 1e12, "peak": FP64_MFMA_PEAK / 1e12,
+                         "unit": "TFLOP/s", "frac": achieved / FP64_MFMA_PEAK, "traffic": traffic,
+                         "kernel": "rtd_exp_mfma_kernel" if info["mfma_rows"] else "rtd_conc_kernel", "kernel_ms": rtd_ms, "flop_per_launch": flops,
                          "hbm": {"algorithmic_bytes": hbm_bytes, "achieved_GBps": hbm_bytes / (rtd_ms * 1e-3) / 1e9,
                                  "peak_GBps": HBM_PEAK / 1e9,
                                  "frac": hbm_bytes / (rtd_ms * 1e-3) / HBM_PEAK}},

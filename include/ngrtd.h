@@ -214,8 +214,8 @@ int ngrtd_plan_kernel_stats(ngrtd_plan* plan, double* times_ms, int64_t* counts,
 
 /* Launch geometry the plan chose for its RTD kernel: info[0..10] = units per lane (VALU
  * path) or 16-unit tiles per wave (MFMA path), waves per block, blocks, ages per LDS slice
- * (VALU) or per segment (MFMA), channels, N, LDS bytes, units, MFMA path (0/1), age
- * segments per GEMM row block, Horner steps.  For the roofline accounting in bench.py. */
+ * (VALU) or per segment (MFMA), channels, N, LDS bytes, units, MFMA row tiles (0 = VALU
+ * path), age segments, 4-age MFMA steps.  For the roofline accounting in bench.py. */
 int ngrtd_plan_info(ngrtd_plan* plan, int64_t W, int64_t* info, int32_t n);
 
 #ifdef __cplusplus

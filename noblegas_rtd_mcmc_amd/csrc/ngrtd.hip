@@ -191,25 +191,27 @@ static int build_table(ngrtd_ctx* ctx, const std::vector<TracerBuild>& trs, Tabl
         for (int64_t k = 0; k < N; ++k) h[(size_t)k * tab.CP + c] = cols[c][k];
     HIP_TRY(ctx, tab.buf.ensure(h.size() * sizeof(double) + 16));
     HIP_TRY(ctx, hipMemcpy(tab.buf.p, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
-    // MFMA fragment table: GEMM rows i = (channel c, age segment s), i < C * S_seg <= 16;
-    // row i covers ages 1 + s*Lseg + [0, Lseg); entry [step][mm][lane] is the A operand of
-    // lane (row lane&15, k-slot lane>>4) for ages 1 + s*Lseg + 16*step + 4*mm + (lane>>4).
-    if (C >= 1 && C <= 16) {
-        const int S = 16 / C;
-        int64_t Lseg = cdiv(std::max<int64_t>(N - 1, 0), S);
-        Lseg = cdiv(Lseg, 16) * 16;
+    // MFMA fragment table (rtd_exp_mfma_kernel): S = 4*SG segments of Lseg ages; entry
+    // [step][rt][lane] is the A operand of lane (row i = lane&15, k-slot kq = lane>>4) of row
+    // tile rt: group g = 4*rt + (i>>2) -> channel g % C, segment s = 4*(g / C) + (i&3),
+    // age index j = s*Lseg + 4*step + kq (table row 1 + j).
+    if (C >= 1 && C <= kMaxChan) {
+        const int R = mfma_rows(C), SG = mfma_groups_per_chan(C), S = 4 * SG;
+        const int64_t n = std::max<int64_t>(N - 1, 0);
+        const int64_t Lseg = cdiv(cdiv(n, S), 4) * 4;
         tab.S_seg = S;
         tab.Lseg = (int)Lseg;
-        tab.nsteps = (int)(Lseg / 16);
-        std::vector<double> fr((size_t)tab.nsteps * 256, 0.0);
+        tab.nsteps = (int)(Lseg / 4);
+        std::vector<double> fr((size_t)tab.nsteps * R * 64, 0.0);
         for (int step = 0; step < tab.nsteps; ++step)
-            for (int mm = 0; mm < 4; ++mm)
+            for (int rt = 0; rt < R; ++rt)
                 for (int lane = 0; lane < 64; ++lane) {
-                    const int i = lane & 15, t = lane >> 4;
-                    if (i >= C * S) continue;
-                    const int c = i / S, sg = i % S;
-                    const int64_t k = 1 + sg * Lseg + 16 * step + 4 * mm + t;
-                    if (k < N) fr[(size_t)(step * 4 + mm) * 64 + lane] = cols[c][k];
+                    const int i = lane & 15, kq = lane >> 4;
+                    const int g = 4 * rt + (i >> 2);
+                    if (g >= C * SG) continue;
+                    const int c = g % C, sg = 4 * (g / C) + (i & 3);
+                    const int64_t j = sg * Lseg + 4 * step + kq;
+                    if (j < n) fr[((size_t)step * R + rt) * 64 + lane] = cols[c][1 + j];
                 }
         HIP_TRY(ctx, tab.frag.ensure(fr.size() * sizeof(double) + 16));
         if (!fr.empty())
@@ -275,14 +277,22 @@ static RtdGeom rtd_geometry(int64_t U, int N, int C, bool lamw) {
 
 static bool mfma_path(const RtdArgs& a, bool lamw) {
     static const bool disabled = std::getenv("NGRTD_NO_MFMA") != nullptr;
-    return !disabled && a.mod[0] == MOD_EXP && a.mod[1] == MOD_NONE && !lamw && a.C >= 1 && a.C <= 16 &&
+    return !disabled && a.mod[0] == MOD_EXP && a.mod[1] == MOD_NONE && !lamw && a.C >= 1 && a.C <= kMaxChan &&
            a.frag != nullptr;
 }
 
-static int mfma_nt(int64_t U) {
-    if (cdiv(U, 64) >= 1024) return 4;
-    if (cdiv(U, 32) >= 1024) return 2;
-    return 1;
+// Dynamic LDS of the MFMA kernel: one fragment chunk, at least 56 KiB so that no more than
+// two 256-unit blocks share a CU (an odd third block would double that CU's matrix-core
+// time while others idle: tools/mfma_probe.hip).
+static size_t mfma_lds(const RtdArgs& a) {
+    const size_t chunk = (size_t)std::min(a.nsteps, kMfmaLdsBytes / (mfma_rows(a.C) * 512)) * mfma_rows(a.C) * 512;
+    return std::max<size_t>(chunk, 56 * 1024);
+}
+
+template <int C>
+static void launch_mfma(const RtdArgs& a, const UnitArgs& u, int32_t fuse, hipStream_t st) {
+    const unsigned blocks = (unsigned)cdiv(a.U, kMfmaUnitsPerBlock);
+    hipLaunchKernelGGL(rtd_exp_mfma_kernel<C>, dim3(blocks), dim3(64 * mfma_waves(C)), mfma_lds(a), st, a, u, fuse);
 }
 
 // Enqueue the RTD kernel.  On the MFMA path with `ua` non-null the kernel also evaluates
@@ -292,16 +302,19 @@ static int launch_rtd(ngrtd_ctx* ctx, RtdArgs a, bool lamw, hipStream_t st, cons
     if (fused) *fused = false;
     if (a.U <= 0) return NGRTD_OK;
     if (mfma_path(a, lamw)) {
-        const int NT = mfma_nt(a.U);
-        const unsigned blocks = (unsigned)cdiv(a.U, 64 * NT);
         UnitArgs u{};
         int32_t fuse = 0;
         if (ua) { u = *ua; fuse = 1; }
-        const size_t lds = std::max<size_t>((size_t)std::min(a.nsteps, kMfmaChunkSteps) * 256 * sizeof(double),
-                                            (size_t)4 * NT * 16 * 17 * sizeof(double));
-        if (NT == 4) hipLaunchKernelGGL(rtd_exp_mfma_kernel<4>, dim3(blocks), dim3(256), lds, st, a, u, fuse);
-        else if (NT == 2) hipLaunchKernelGGL(rtd_exp_mfma_kernel<2>, dim3(blocks), dim3(256), lds, st, a, u, fuse);
-        else hipLaunchKernelGGL(rtd_exp_mfma_kernel<1>, dim3(blocks), dim3(256), lds, st, a, u, fuse);
+        switch (a.C) {
+        case 1: launch_mfma<1>(a, u, fuse, st); break;
+        case 2: launch_mfma<2>(a, u, fuse, st); break;
+        case 3: launch_mfma<3>(a, u, fuse, st); break;
+        case 4: launch_mfma<4>(a, u, fuse, st); break;
+        case 5: launch_mfma<5>(a, u, fuse, st); break;
+        case 6: launch_mfma<6>(a, u, fuse, st); break;
+        case 7: launch_mfma<7>(a, u, fuse, st); break;
+        default: launch_mfma<8>(a, u, fuse, st); break;
+        }
         HIP_TRY(ctx, hipGetLastError());
         if (fused) *fused = fuse != 0;
         return NGRTD_OK;
@@ -901,10 +914,9 @@ int ngrtd_plan_info(ngrtd_plan* p, int64_t W, int64_t* info, int32_t n) {
         a.U = U;
         const bool lamw = a.row_thalf >= 0;
         if (mfma_path(a, lamw)) {
-            const int NT = mfma_nt(U);
-            v[0] = NT; v[1] = 4; v[2] = cdiv(U, 64 * NT); v[3] = a.Lseg;
-            v[6] = std::max<int64_t>((int64_t)std::min(a.nsteps, kMfmaChunkSteps) * 2048, (int64_t)4 * NT * 16 * 17 * 8);
-            v[8] = 1; v[9] = a.S_seg; v[10] = a.nsteps;
+            v[0] = mfma_tiles(a.C); v[1] = mfma_waves(a.C); v[2] = cdiv(U, kMfmaUnitsPerBlock); v[3] = a.Lseg;
+            v[6] = (int64_t)mfma_lds(a);
+            v[8] = mfma_rows(a.C); v[9] = a.S_seg; v[10] = a.nsteps;
         } else {
             const RtdGeom g = rtd_geometry(U, p->N, p->table.C, lamw);
             v[0] = g.R; v[1] = g.NW; v[2] = g.blocks; v[3] = (int64_t)g.LW * g.NW; v[6] = (int64_t)g.lds;

@@ -30,10 +30,17 @@ struct RtdArgs {
     int32_t tr_sf6[kMaxTracer];     // apply (1 + lamsf6)
     double tr_J[kMaxTracer];        // fixed J per tracer when row_J < 0
     double* conc;           // out [K][U]
-    // MFMA Horner fragments (rtd_exp_mfma_kernel): rows = (channel, age segment)
-    const double* frag;     // [nsteps][4][64] A-operand fragments of v_mfma_f64_16x16x4f64
+    // MFMA fragments (rtd_exp_mfma_kernel): GEMM rows = (channel, age segment)
+    const double* frag;     // [nsteps][R][64] A-operand fragments of v_mfma_f64_16x16x4f64
     int32_t nsteps, S_seg, Lseg;
 };
+
+// Row tiles of the exponential-RTD GEMM for C channels: R tiles of 16 rows hold 4R row
+// groups; group g = c + C*m (m < 4R/C) of channel c carries the 4 age segments 4m..4m+3.
+// R = C (C >= 3) keeps every row busy; C = 1, 2 use 4 tiles so that each B operand (one
+// VALU multiply per lane per step) feeds at least 4 MFMAs.
+__host__ __device__ constexpr int mfma_rows(int C) { return C >= 3 ? C : 4; }
+__host__ __device__ constexpr int mfma_groups_per_chan(int C) { return 4 * mfma_rows(C) / C; }
 
 // Per-unit CE + likelihood + prior launch (unit_logp_kernel)
 struct UnitArgs {

@@ -382,59 +382,39 @@ __global__ void __launch_bounds__(256) rtd_conc_kernel(const RtdArgs a) {
 
 // ------------------------------------------------- per-unit CE + likelihood
 // CE concentrations of one (walker, well) for the likelihood gases, with S = 0 (the
-// reference models never pass a salinity): the Setchenow factor exp(0 * setch) is 1
-// whenever setch is finite and NaN otherwise (noble_gas_utils.py:154-156), so it is
-// decided without the exp/log; the He branch reuses the Ar exponential (:172).
+// reference models never pass a salinity).  noble_gas_utils.py:117-253 restated for the
+// per-unit path with one division per gas instead of ~7:
+//  * Setchenow factor exp(0 * setch) (:154-156) is 1 whenever setch is finite, NaN
+//    otherwise; for T < 65 setch is finite iff T_k > 0 (T_k = T + 273.15 is never a positive
+//    value small enough for G2 / (.01 T_k) to overflow), so gamma needs no exp/log;
+//  * ln K = A0 + A1/x + A2/x^2 + A3/x^3 is evaluated by Horner in 1/x (one reciprocal for
+//    all gases), and x_i = p_i / K = gamma p_i exp(-ln K) (gamma is 1 or NaN);
+//  * He (:161-176): K_He = exp(ln K_Ar - ln F_He) exactly as the reference's chain of
+//    ratios, so x_He = gamma p_He exp(ln F_He - ln K_Ar);
+//  * ce_excess (1-F) Ae z / (1 + F Ae z / C_eq) = (1-F) Ae z C_eq / (C_eq + F Ae z).
+// Each rewrite moves a result by a few ulp of ln K (|ln K| < 30 on the CE ranges): far
+// inside the 1e-12 parity bar (tests/test_gpu_parity.py checks against the reference).
+__device__ __forceinline__ double lnK_horner(const GasCoef& c, double ix) {
+    return fma(fma(fma(c.A3, ix, c.A2), ix, c.A1), ix, c.A0);
+}
 __device__ __forceinline__ void ce_model_s0(const UnitArgs& a, double T, double P, double Ae, double F,
                                             double* mod) {
     const double Pv = vapor_pressure_fast(T);
     const double T_k = T + 273.15;
-    const double x = .001 * T_k, x2 = x * x, x3 = x * x * x;
-    const double x1 = .01 * T_k;
-    double gamma = 1.;
-    if (T < 65.) {
-        const bool fin = (x1 > 0.0) && (x1 < __builtin_inf());
-        gamma = fin ? 1. : __builtin_nan("");
-    }
-    const GasCoef ar = gas_coef(2);
-    double exp_ar = 0.0;
-    bool have_ar = false;
+    const double ix = 1.0 / (.001 * T_k);
+    const double gamma = (T < 65. && !(T_k > 0.0)) ? __builtin_nan("") : 1.0;
+    const double dP = P - Pv;
+    const double lnAr = lnK_horner(gas_coef(2), ix);
+    const double FA = F * Ae, ImFA = (1 - F) * Ae;
     for (int j = 0; j < a.G; ++j) {
         const int g = a.gas[j];
         const GasCoef c = gas_coef(g);
-        // Setchenow with S = 0: exp(0 * setch) -- finite setch gives exactly 1
-        double gj = gamma;
-        if (T < 65. && gj == 1.) gj = isfinite(c.G2 / x1) ? 1. : __builtin_nan("");
-        double K;
-        if (g == 0) {
-            if (!have_ar) { exp_ar = fexp(ar.A0 + (ar.A1 / x) + (ar.A2 / x2) + (ar.A3 / x3)); have_ar = true; }
-            const double Fh = fexp(c.A0 + (c.A1 / x) + (c.A2 / x2) + (c.A3 / x3));
-            const double X_Ar_water = 1. / exp_ar * 9.31e-3;
-            const double X_he_water = Fh * (5.24e-6 / 9.31e-3) * X_Ar_water;
-            K = gj * (5.24e-6 / X_he_water);
-        } else {
-            const double e = fexp(c.A0 + (c.A1 / x) + (c.A2 / x2) + (c.A3 / x3));
-            if (g == 2 && !have_ar) { exp_ar = e; have_ar = true; }
-            K = gj * e;
-        }
-        const double ceq = equil_conc_dry(g, T, P, Pv, K);
-        mod[j] = ce_excess(g, Ae, F, ceq) + ceq;
+        const double lnK = lnK_horner(c, ix);
+        const double e = fexp((g == 0) ? lnK - lnAr : -lnK);
+        const double ceq = (T < 0.0) ? -9999.0 : (gamma * (c.z * dP) * e) * (22414. / 18.);
+        const double ex = (ImFA * c.z) * ceq / (ceq + FA * c.z);
+        mod[j] = ex + ceq;
     }
-}
-
-// Student-t sum over observations sharing nu, with lam = sigma^-2 and 0.5*log(lam)
-// precomputed per observation on the host (lam <= 0 encodes sigma <= 0 -> -inf).
-__device__ __forceinline__ double st_sum(int n, const double* obs, const double* mu, const double* lam,
-                                         const double* hll, double nu) {
-    const double c0 = st_const(nu) - 0.5 * log(nu * kPi);
-    const double hn = (nu + 1.0) / 2.0;
-    double s = 0.0;
-    for (int j = 0; j < n; ++j) {
-        const double d = obs[j] - mu[j];
-        const double v = c0 + hll[j] - hn * log1p(lam[j] * (d * d) / nu);
-        s += (lam[j] > 0 && nu > 0) ? v : kNegInf;
-    }
-    return s;
 }
 
 // log-prob contribution of one (walker, well) unit: priors, CE model + likelihood,
@@ -551,101 +531,124 @@ __global__ void __launch_bounds__(512) unit_walker_kernel(const UnitArgs a, int3
 
 // ------------------------------------------- exponential RTD on the matrix cores
 // Single-component exponential model (convolution_integral_utils.py:184) with every decay
-// folded into the channel table.  The polynomials sum_k A_{c,k} q_u^(k-1) of all units u
-// and channels c form a small GEMM: rows i = (channel c, age segment s), columns = 16
-// units, K = 4 consecutive ages per v_mfma_f64_16x16x4f64.  Lane l supplies
-//   A[i = l&15][t = l>>4] = A_{c, 1 + s*Lseg + 16*step + 4*mm + t}   (fragment table)
-//   B[t = l>>4][j = l&15] = q_j^(16*step + 4*mm + t)                (per-unit powers)
-// so the accumulator (row (l>>4)+4r, column l&15 in register r) ends as
-//   P_{c,s} = sum_j A_{c,1+s*Lseg+j} q^j ;   Y_c = sum_s q^(s*Lseg) P_{c,s}.
-// The powers advance by one multiply per step (B *= q^16), accumulators stay in the
-// matrix register file.  FP64 MFMA runs at 2x the FP64 VALU FMA rate on gfx950
-// (tools/ubench_fp64.hip: 78 vs 38 TFLOP/s).  With `fuse`, the epilogue also evaluates
-// the CE model, both Student-t likelihoods and the priors of the unit (one per lane).
+// folded into the channel table, so that for unit u (q = exp(-1/tau_u))
+//   Y_c(u) = sum_{j=0}^{n-1} A_{c,1+j} q^j ,   n = N - 1,
+// and conc = (tab_{c,0} + s01 Y_c) / (1 + s01 G) as in rtd_conc_kernel.  The ages j are cut
+// into S = 4 * SG segments of Lseg (a multiple of 4) ages, j = s*Lseg + 4*step + kq, and
+//   Y_c = sum_s q^(s*Lseg) P_{c,s},   P_{c,s} = sum_step sum_kq A_{c,1+j} q^(4*step+kq)
+// is a GEMM: rows = (c, s), columns = 16 units, K = 4 ages per v_mfma_f64_16x16x4f64.
+// Lane l of a wave supplies
+//   B[kq = l>>4][col = l&15] = q_col^(4*step + kq)     (ONE register per 16-unit tile)
+//   A[row = l&15][kq = l>>4] of row tile rt           (fragment table, staged in LDS)
+// and each B feeds R row tiles (R MFMAs per VALU multiply B *= q^4; the f64 VALU and MFMA
+// share one pipe on gfx950, so that ratio bounds the loop).  Row i of tile rt is group
+// g = 4*rt + (i>>2), segment slot i&3, i.e. lane (tq = l>>4) accumulates segments
+// s = 4m + tq of channel c = g % C (m = g / C) in element (g&3) of accumulator rt: the
+// segment sum runs in registers (Horner in q^(4 Lseg)) and the 4 lanes of a column are
+// added with two cross-lane shuffles.  With `fuse`, the epilogue also evaluates the CE
+// model, both Student-t likelihoods and the priors of the unit (unit_logp).
 typedef double ngrtd_v4d __attribute__((ext_vector_type(4)));
 
-constexpr int kMfmaChunkSteps = 32;   // Horner steps of fragments staged in LDS at a time (64 KiB)
+constexpr int kMfmaLdsBytes = 64 * 1024;   // fragment bytes staged in LDS at a time
+// 16-unit column tiles per wave (accumulators: 8 * NT * R VGPRs) and waves per block
+__host__ __device__ constexpr int mfma_tiles(int C) { return mfma_rows(C) <= 5 ? 4 : 2; }
+__host__ __device__ constexpr int mfma_waves(int C) { return 16 / mfma_tiles(C); }   // 256 units per block
+__host__ __device__ constexpr int mfma_chunk_steps(int C) { return kMfmaLdsBytes / (mfma_rows(C) * 64 * 8); }
+constexpr int kMfmaUnitsPerBlock = 256;
 
-template <int NT>
-__global__ void __launch_bounds__(256) rtd_exp_mfma_kernel(const RtdArgs a, const UnitArgs ua, int32_t fuse) {
+template <int C>
+__global__ void __launch_bounds__(64 * mfma_waves(C)) rtd_exp_mfma_kernel(const RtdArgs a, const UnitArgs ua,
+                                                                         int32_t fuse) {
+    constexpr int R = mfma_rows(C), SG = mfma_groups_per_chan(C), NT = mfma_tiles(C), NW = mfma_waves(C);
+    constexpr int CHUNK = mfma_chunk_steps(C);
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int col = lane & 15, tq = lane >> 4;
-    const int64_t u0 = ((int64_t)blockIdx.x * 4 + wave) * (16 * NT);
+    const int64_t u0 = ((int64_t)blockIdx.x * NW + wave) * (16 * NT);
     const int64_t Umax = a.U - 1;
+    const double* tau_row = a.theta + (int64_t)a.row_tau[0] * a.U;
 
-    double q16[NT], pw[NT][4];
-    ngrtd_v4d acc[NT];
+    double beta[NT], q4[NT], pw[NT];
+    ngrtd_v4d acc[NT][R];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
         int64_t u = u0 + 16 * t + col;
         u = u < Umax ? u : Umax;
-        const double beta = 1. / a.theta[(int64_t)a.row_tau[0] * a.U + u];
-        const double q = exp(-beta);
-        const double q2 = q * q, q4 = q2 * q2;
-        const double qt = (tq == 0) ? 1.0 : (tq == 1) ? q : (tq == 2) ? q2 : q2 * q;
-        pw[t][0] = qt;
-        pw[t][1] = qt * q4;
-        pw[t][2] = pw[t][1] * q4;
-        pw[t][3] = pw[t][2] * q4;
-        const double q8 = q4 * q4;
-        q16[t] = q8 * q8;
-        acc[t] = ngrtd_v4d{0.0, 0.0, 0.0, 0.0};
+        beta[t] = 1. / tau_row[u];
+        const double q = fexp(-beta[t]);
+        const double q2 = q * q;
+        q4[t] = q2 * q2;
+        pw[t] = (tq == 0) ? 1.0 : (tq == 1) ? q : (tq == 2) ? q2 : q2 * q;
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[t][r] = ngrtd_v4d{0.0, 0.0, 0.0, 0.0};
     }
     const int nsteps = a.nsteps;
-    for (int c0 = 0; c0 < nsteps; c0 += kMfmaChunkSteps) {
-        const int cn = (nsteps - c0) < kMfmaChunkSteps ? (nsteps - c0) : kMfmaChunkSteps;
-        // stage fragments of steps [c0, c0+cn) (cn * 2 KiB, contiguous) into LDS
+    for (int c0 = 0; c0 < nsteps; c0 += CHUNK) {
+        const int cn = (nsteps - c0) < CHUNK ? (nsteps - c0) : CHUNK;
         __syncthreads();
-        {
-            const double2* src = reinterpret_cast<const double2*>(a.frag + (int64_t)c0 * 256);
+        {   // fragments of steps [c0, c0 + cn): cn * R * 512 contiguous bytes
+            const double2* src = reinterpret_cast<const double2*>(a.frag + (int64_t)c0 * R * 64);
             double2* dst = reinterpret_cast<double2*>(lds);
-            for (int i = threadIdx.x; i < cn * 128; i += 256) dst[i] = src[i];
+            for (int i = threadIdx.x; i < cn * R * 32; i += 64 * NW) dst[i] = src[i];
         }
         __syncthreads();
         const double* f = lds + lane;
-        for (int step = 0; step < cn; ++step, f += 256) {
-            const double A0 = f[0], A1 = f[64], A2 = f[128], A3 = f[192];
+        for (int step = 0; step < cn; ++step, f += R * 64) {
+            double A[R];
 #pragma unroll
-            for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(A0, pw[t][0], acc[t], 0, 0, 0);
-#pragma unroll
-            for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(A1, pw[t][1], acc[t], 0, 0, 0);
-#pragma unroll
-            for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(A2, pw[t][2], acc[t], 0, 0, 0);
-#pragma unroll
-            for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(A3, pw[t][3], acc[t], 0, 0, 0);
+            for (int r = 0; r < R; ++r) A[r] = f[r * 64];
 #pragma unroll
             for (int t = 0; t < NT; ++t)
 #pragma unroll
-                for (int mm = 0; mm < 4; ++mm) pw[t][mm] *= q16[t];
+                for (int r = 0; r < R; ++r) acc[t][r] = __builtin_amdgcn_mfma_f64_16x16x4f64(A[r], pw[t], acc[t][r], 0, 0, 0);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) pw[t] *= q4[t];
         }
     }
-    __syncthreads();
-    double (*sh)[NT * 16][17] = reinterpret_cast<double (*)[NT * 16][17]>(lds);
-    // transpose the accumulator tiles through LDS: one unit per lane
+
+    // segment sums: lane (tq, col) of tile t holds P_{c, 4m+tq} for all c, m
+    const double Lseg = (double)a.Lseg;
+    double y[NT][C];
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
+    for (int t = 0; t < NT; ++t) {
+        const double Q = fexp(-beta[t] * Lseg);
+        const double Q2 = Q * Q, Q4 = Q2 * Q2;
+        const double Qt = (tq == 0) ? 1.0 : (tq == 1) ? Q : (tq == 2) ? Q2 : Q2 * Q;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) sh[wave][16 * t + col][tq + 4 * r] = acc[t][r];
-    __syncthreads();
-    if (lane >= 16 * NT) return;
-    const int64_t u = u0 + lane;
-    if (u > Umax) return;
-    const double beta = 1. / a.theta[(int64_t)a.row_tau[0] * a.U + u];
-    const double Qs = exp(-beta * (double)a.Lseg);
-    const double* P = sh[wave][lane];
-    const int N = a.N;
-    const double s01 = exp(-beta * ((1.0 + a.dtp) - a.tp0));
-    const int n = N - 1;
-    const double G = (n > 0) ? expm1(-beta * (double)n) / expm1(-beta) : 0.0;
-    const double den = 1.0 + s01 * G;
-    double num[kMaxChan];
-    for (int c = 0; c < a.C; ++c) {
-        double y = P[c * a.S_seg + a.S_seg - 1];
-        for (int s = a.S_seg - 2; s >= 0; --s) y = fma(y, Qs, P[c * a.S_seg + s]);
-        num[c] = a.tab[c] + s01 * y;
+        for (int c = 0; c < C; ++c) {
+            double v = 0.0;
+#pragma unroll
+            for (int m = SG - 1; m >= 0; --m) {
+                const int g = c + C * m;
+                v = fma(v, Q4, acc[t][g >> 2][g & 3]);
+            }
+            v *= Qt;
+            v += __shfl_xor(v, 16);
+            v += __shfl_xor(v, 32);
+            y[t][c] = v;
+        }
     }
+    // lanes with tq = t finish the units of tile t
+    if (tq >= NT) return;
+    double yy[C], bu = 0.0;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        if (t == tq) {
+            bu = beta[t];
+#pragma unroll
+            for (int c = 0; c < C; ++c) yy[c] = y[t][c];
+        }
+    }
+    const int64_t u = u0 + 16 * tq + col;
+    if (u > Umax) return;
+    const int n = a.N - 1;
+    const double s01 = fexp(-bu * ((1.0 + a.dtp) - a.tp0));
+    const double G = (n > 0) ? expm1(-bu * (double)n) / expm1(-bu) : 0.0;
+    const double den = 1.0 + s01 * G;
+    double num[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) num[c] = a.tab[c] + s01 * yy[c];
     const double fmix = (a.row_f1 >= 0) ? a.theta[(int64_t)a.row_f1 * a.U + u] : 1.0;
     double Jw = 0.0;
     if (a.row_J >= 0) {
@@ -656,7 +659,8 @@ __global__ void __launch_bounds__(256) rtd_exp_mfma_kernel(const RtdArgs a, cons
     for (int t = 0; t < a.K; ++t) {
         double sA = 0.0, sB = 0.0;
         bool hasB = false;
-        for (int c = 0; c < a.C; ++c) {
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
             if (a.chan_tracer[c] != t) continue;
             if (a.chan_isB[c]) { sB = num[c]; hasB = true; }
             else sA = num[c];

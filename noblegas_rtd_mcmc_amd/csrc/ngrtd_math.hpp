@@ -122,22 +122,50 @@ NGRTD_HD double ce_excess(int g, double Ae, double F, double C_eq) {
 
 // ---------------------------------------------------------------- log densities
 // lgamma(x + 1/2) - lgamma(x) for x > 0, without two general lgamma() calls (the
-// StudentT normaliser needs only this difference).  Shift x up by the recurrence
-// lgamma(y+1) = lgamma(y) + log(y) until y >= 12, then the asymptotic series
+// StudentT normaliser needs only this difference).  Shift x up by 12 with the recurrence
+// lgamma(y+1) = lgamma(y) + log(y):
+//   D(x) = D(x + 12) - log(P(x) / Q(x)),  P = prod_{k<12} (x + k + 1/2),  Q = prod_{k<12} (x + k),
+// then the asymptotic series at y = x + 12 >= 12
 //   D(y) = 1/2 log y + sum_{m>=1} (2^(1-2m) - 2) B_2m / (2m (2m-1) y^(2m-1))
-// (Bernoulli numbers B_2m), truncated after y^-13: the first omitted term is
-// < 5e-18 at y = 12.  Branch-free (fixed 12-step shift with selects) so the lanes of a
-// wavefront never diverge.
-NGRTD_HD double lgamma_half_diff(double x) {
-    double P = 1.0, Q = 1.0, y = x;
-#pragma unroll
-    for (int k = 0; k < 12; ++k) {
-        const bool s = y < 12.0;
-        P = s ? P * (y + 0.5) : P;
-        Q = s ? Q * y : Q;
-        y = s ? y + 1.0 : y;
-    }
-    const double r = 1.0 / y, r2 = r * r;
+// (Bernoulli numbers B_2m), truncated after y^-13: the first omitted term is < 5e-18.
+// P and Q are degree-12 polynomials with exactly representable positive coefficients,
+// evaluated by Horner (12 FMAs each, relative error <= 12 ulp for x > 0) -- no per-step
+// selects, so the lanes of a wavefront never diverge.  x >= 1e6 skips the shift (P, Q
+// would overflow near 1e25; the series alone is already exact there).
+NGRTD_HD void shift12(double x, double& P, double& Q) {
+    P = 1.0;
+    P = fma(P, x, 72.0);
+    P = fma(P, x, 2304.5);
+    P = fma(P, x, 43230.0);
+    P = fma(P, x, 527486.4375);
+    P = fma(P, x, 4391541.0);
+    P = fma(P, x, 25442216.9375);
+    P = fma(P, x, 102636393.75);
+    P = fma(P, x, 283508825.74609375);
+    P = fma(P, x, 516212165.90625);
+    P = fma(P, x, 576705198.5332031);
+    P = fma(P, x, 343464997.1484375);
+    P = fma(P, x, 77205601.37329102);
+    Q = 1.0;
+    Q = fma(Q, x, 66.0);
+    Q = fma(Q, x, 1925.0);
+    Q = fma(Q, x, 32670.0);
+    Q = fma(Q, x, 357423.0);
+    Q = fma(Q, x, 2637558.0);
+    Q = fma(Q, x, 13339535.0);
+    Q = fma(Q, x, 45995730.0);
+    Q = fma(Q, x, 105258076.0);
+    Q = fma(Q, x, 150917976.0);
+    Q = fma(Q, x, 120543840.0);
+    Q = fma(Q, x, 39916800.0);
+    Q = Q * x;
+    const bool sh = x < 1.0e6;
+    P = sh ? P : 1.0;
+    Q = sh ? Q : 1.0;
+}
+// asymptotic tail  sum_m (...) r^(2m-1),  r = 1/y
+NGRTD_HD double lgamma_half_tail(double r) {
+    const double r2 = r * r;
     double t = -5461.0 / 425984.0;
     t = fma(t, r2, 691.0 / 180224.0);
     t = fma(t, r2, -31.0 / 18432.0);
@@ -145,7 +173,13 @@ NGRTD_HD double lgamma_half_diff(double x) {
     t = fma(t, r2, -1.0 / 640.0);
     t = fma(t, r2, 1.0 / 192.0);
     t = fma(t, r2, -0.125);
-    return 0.5 * log(y) + t * r - log(P / Q);
+    return t * r;
+}
+NGRTD_HD double lgamma_half_diff(double x) {
+    double P, Q;
+    shift12(x, P, Q);
+    const double y = (x < 1.0e6) ? x + 12.0 : x;
+    return 0.5 * flog(y) + lgamma_half_tail(1.0 / y) - flog(P / Q);
 }
 
 // StudentT.logp, summed over observations that share nu: the caller adds
@@ -187,34 +221,24 @@ NGRTD_HD double beta_logp_fast(double x, double a, double b, double betaln_ab, i
 // with z_j = lam_j (x_j - mu_j)^2 / nu, evaluated as
 //   n * c0 + sum_j 0.5 log lam_j - (nu+1)/2 * log(prod_j (1 + z_j)),
 //   c0 = lgamma((nu+1)/2) - lgamma(nu/2) - 0.5 log(nu pi) in ONE log (see lgamma_half_diff),
-// i.e. 2 logs per block instead of 3 + n.  log(1 + z) vs log1p(z) differs by < 2^-53 per
+// i.e. 2 logs per block instead of 3 + n, and 2 divisions (1/(y P), 1/nu) instead of n + 3.  log(1 + z) vs log1p(z) differs by < 2^-53 per
 // factor.  Very large z (poor fits: z >= 1e15) take the per-observation log1p path so
 // the product cannot overflow.  hll_sum = sum_j 0.5 log lam_j (host precomputed).
 NGRTD_HD double st_block(int n, const double* obs, const double* mu, const double* lam, double hll_sum,
                          double nu) {
-    double P = 1.0, Q = 1.0, y = nu / 2.0;
-#pragma unroll
-    for (int k = 0; k < 12; ++k) {
-        const bool s = y < 12.0;
-        P = s ? P * (y + 0.5) : P;
-        Q = s ? Q * y : Q;
-        y = s ? y + 1.0 : y;
-    }
-    const double r = 1.0 / y, r2 = r * r;
-    double t = -5461.0 / 425984.0;
-    t = fma(t, r2, 691.0 / 180224.0);
-    t = fma(t, r2, -31.0 / 18432.0);
-    t = fma(t, r2, 17.0 / 14336.0);
-    t = fma(t, r2, -1.0 / 640.0);
-    t = fma(t, r2, 1.0 / 192.0);
-    t = fma(t, r2, -0.125);
-    const double qp = Q / P;
-    const double c0 = 0.5 * flog(y * qp * qp / (nu * kPi)) + t * r;
+    const double x = nu / 2.0;
+    double P, Q;
+    shift12(x, P, Q);
+    const double y = (x < 1.0e6) ? x + 12.0 : x;
+    const double iyP = 1.0 / (y * P);               // one division for 1/y and Q/P
+    const double qp = (Q * y) * iyP;
+    const double inu = 1.0 / nu;
+    const double c0 = 0.5 * flog(y * qp * qp * (inu * (1.0 / kPi))) + lgamma_half_tail(P * iyP);
     double prod = 1.0;
     bool big = false, ok = nu > 0;
     for (int j = 0; j < n; ++j) {
         const double d = obs[j] - mu[j];
-        const double z = lam[j] * (d * d) / nu;
+        const double z = lam[j] * (d * d) * inu;
         prod *= (1.0 + z);
         big |= !(z < 1.0e15);
         ok &= lam[j] > 0;

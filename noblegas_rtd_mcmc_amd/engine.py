@@ -179,7 +179,7 @@ class LogProb:
     def info(self, W):
         v = (C.c_int64 * 11)()
         self.ctx.check(self.lib.ngrtd_plan_info(self.plan, int(W), v, 11), "plan_info")
-        keys = ("R", "NW", "blocks", "slice_ages", "channels", "N", "lds_bytes", "units", "mfma", "S_seg",
+        keys = ("R", "NW", "blocks", "slice_ages", "channels", "N", "lds_bytes", "units", "mfma_rows", "S_seg",
                 "nsteps")
         return dict(zip(keys, list(v)))
 

@@ -79,6 +79,6 @@ def test_lgamma_half_diff(host_tool):
     assert np.all(np.abs(got - ref) <= 4e-15 * np.maximum(1.0, np.abs(gammaln(x))))
     big = np.geomspace(10.0, 1e8, 2000)
     D0, D1 = host_tool("g", big), host_tool("g", big + 1.0)
-    assert np.all(np.abs((D1 - D0) - np.log1p(0.5 / big)) <= 4 * np.spacing(D1))   # 4 ulp of D
+    assert np.all(np.abs((D1 - D0) - np.log1p(0.5 / big)) <= 8 * np.spacing(D1))   # 2 x 4 ulp of D
     big = big[big >= 1e4]        # next asymptotic term 1/(192 x^3) < 1e-14 here
     assert np.allclose(host_tool("g", big), 0.5 * np.log(big) - 1.0 / (8 * big), rtol=1e-13, atol=0)
