@@ -208,7 +208,8 @@ int ngrtd_forward(ngrtd_plan* plan, const double* theta, int64_t W, double* ce_o
 
 /* Accumulated device time (ms) and launch count of each kernel the plan launched while
  * profiling was on: index 0 = RTD convolution kernel, 1 = per-unit CE/likelihood kernel,
- * 2 = per-walker reduction.  times_ms/counts have room for n entries; resets if reset. */
+ * 2 = per-walker reduction, 3 = single-launch log-prob kernel (RTD + CE + likelihood +
+ * per-walker sum).  times_ms/counts have room for n entries; resets if reset. */
 int ngrtd_plan_kernel_stats(ngrtd_plan* plan, double* times_ms, int64_t* counts, int32_t n,
                             int32_t reset);
 

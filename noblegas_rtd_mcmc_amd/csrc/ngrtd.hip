@@ -54,8 +54,8 @@ struct TableDev {
 };
 
 struct LaunchStats {
-    double ms[3] = {0, 0, 0};
-    int64_t n[3] = {0, 0, 0};
+    double ms[4] = {0, 0, 0, 0};
+    int64_t n[4] = {0, 0, 0, 0};
 };
 
 }  // namespace
@@ -293,6 +293,36 @@ template <int C>
 static void launch_mfma(const RtdArgs& a, const UnitArgs& u, int32_t fuse, hipStream_t st) {
     const unsigned blocks = (unsigned)cdiv(a.U, kMfmaUnitsPerBlock);
     hipLaunchKernelGGL(rtd_exp_mfma_kernel<C>, dim3(blocks), dim3(64 * mfma_waves(C)), mfma_lds(a), st, a, u, fuse);
+}
+
+// Single-launch log-prob (logp_fused_kernel): exponential RTD on the MFMA path with 4
+// tiles per wave (C <= 5), the whole fragment table in LDS next to the 512 per-unit
+// partial sums, and L <= 512 wells.
+static size_t fused_lds(const RtdArgs& a) {
+    return (size_t)a.nsteps * mfma_rows(a.C) * 512 + kFusedUnits * sizeof(double);
+}
+static bool fused_path(const RtdArgs& a, int L) {
+    static const bool disabled = std::getenv("NGRTD_NO_FUSED") != nullptr;
+    return !disabled && mfma_path(a, a.row_thalf >= 0) && a.C <= 5 && L >= 1 && L <= kFusedUnits &&
+           fused_lds(a) <= 64 * 1024;
+}
+template <int C>
+static void launch_fused_c(const RtdArgs& a, const UnitArgs& u, int WB, int64_t W, double* logp, hipStream_t st) {
+    hipLaunchKernelGGL(logp_fused_kernel<C>, dim3((unsigned)cdiv(W, WB)), dim3(64 * kFusedWaves), fused_lds(a), st,
+                       a, u, WB, logp);
+}
+static int launch_fused(ngrtd_ctx* ctx, const RtdArgs& a, const UnitArgs& u, int64_t W, int L, double* logp,
+                        hipStream_t st) {
+    const int WB = kFusedUnits / L;
+    switch (a.C) {
+    case 1: launch_fused_c<1>(a, u, WB, W, logp, st); break;
+    case 2: launch_fused_c<2>(a, u, WB, W, logp, st); break;
+    case 3: launch_fused_c<3>(a, u, WB, W, logp, st); break;
+    case 4: launch_fused_c<4>(a, u, WB, W, logp, st); break;
+    default: launch_fused_c<5>(a, u, WB, W, logp, st); break;
+    }
+    HIP_TRY(ctx, hipGetLastError());
+    return NGRTD_OK;
 }
 
 // Enqueue the RTD kernel.  On the MFMA path with `ua` non-null the kernel also evaluates
@@ -801,6 +831,16 @@ static int plan_run(ngrtd_plan* p, const double* theta, int64_t W, double* logp,
     u.ce_out = ce_out;
     if (!logp) u.flags = 0;
     bool fused = false;
+    if (logp && !ce_out && !rtd_out && p->desc.rtd_enabled) {
+        RtdArgs a = p->rtd;
+        a.theta = theta; a.U = U; a.conc = nullptr;
+        if (fused_path(a, p->desc.n_wells)) {
+            NG_CHECK(timed_begin(p, prof, st, &ev));
+            NG_CHECK(launch_fused(ctx, a, u, W, p->desc.n_wells, logp, st));
+            NG_CHECK(timed_end(p, prof, st, 3, ev));
+            return NGRTD_OK;
+        }
+    }
     if (p->desc.rtd_enabled) {
         RtdArgs a = p->rtd;
         a.theta = theta; a.U = U;
@@ -897,7 +937,7 @@ int ngrtd_forward(ngrtd_plan* p, const double* theta, int64_t W, double* ce_out,
 int ngrtd_plan_kernel_stats(ngrtd_plan* p, double* times_ms, int64_t* counts, int32_t n, int32_t reset) {
     if (!p) return NGRTD_ESTATE;
     NG_CHECK(drain_timings(p));
-    for (int i = 0; i < n && i < 3; ++i) {
+    for (int i = 0; i < n && i < 4; ++i) {
         if (times_ms) times_ms[i] = p->stats.ms[i];
         if (counts) counts[i] = p->stats.n[i];
     }

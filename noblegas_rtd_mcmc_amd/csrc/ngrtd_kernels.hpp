@@ -417,10 +417,9 @@ __device__ __forceinline__ void ce_model_s0(const UnitArgs& a, double T, double 
     }
 }
 
-// log-prob contribution of one (walker, well) unit: priors, CE model + likelihood,
-// RTD likelihood on the unit's model concentrations `conc` (K values).
-__device__ __forceinline__ double unit_logp(const UnitArgs& a, int64_t u, const double* conc) {
-    const int l = (int)(u / a.W);
+// log-prob contribution of one (walker, well) unit that depends on theta only: priors,
+// CE model + likelihood, RTD priors (the RTD likelihood is added by unit_like_rtd).
+__device__ __forceinline__ double unit_logp_theta(const UnitArgs& a, int64_t u, int l) {
     const bool want_like = a.flags & NGRTD_WANT_LIKE;
     const bool want_prior = a.flags & NGRTD_WANT_PRIOR;
     const bool jac = a.flags & NGRTD_WANT_JACOBIAN;
@@ -487,12 +486,22 @@ __device__ __forceinline__ double unit_logp(const UnitArgs& a, int64_t u, const 
                 if (jac) lp += log(x);
             }
         }
-        if (want_like) {
-            const double nu = nub * (a.rnu_max - a.rnu_min) + a.rnu_min;   // run_age_mcmc_utils.py:292
-            lp += st_block(a.K, a.rtd_obs + l * a.K, conc, a.rtd_lam + l * a.K, a.rtd_hll_sum[l], nu);
-        }
     }
     return lp;
+}
+
+// Student-t likelihood of the unit's K model concentrations (run_age_mcmc_utils.py:292-296)
+__device__ __forceinline__ double unit_like_rtd(const UnitArgs& a, int64_t u, int l, const double* conc) {
+    if (!a.rtd_on || !(a.flags & NGRTD_WANT_LIKE)) return 0.0;
+    const double nub = a.theta[(int64_t)a.row_nu * a.U + u];
+    const double nu = nub * (a.rnu_max - a.rnu_min) + a.rnu_min;
+    return st_block(a.K, a.rtd_obs + l * a.K, conc, a.rtd_lam + l * a.K, a.rtd_hll_sum[l], nu);
+}
+
+// full log-prob contribution of one unit (same addition order as the reference's sum)
+__device__ __forceinline__ double unit_logp(const UnitArgs& a, int64_t u, const double* conc) {
+    const int l = (int)(u / a.W);
+    return unit_logp_theta(a, u, l) + unit_like_rtd(a, u, l, conc);
 }
 
 __global__ void __launch_bounds__(256) unit_logp_kernel(const UnitArgs a) {
@@ -556,92 +565,75 @@ __host__ __device__ constexpr int mfma_waves(int C) { return 16 / mfma_tiles(C);
 __host__ __device__ constexpr int mfma_chunk_steps(int C) { return kMfmaLdsBytes / (mfma_rows(C) * 64 * 8); }
 constexpr int kMfmaUnitsPerBlock = 256;
 
+// One wave's share of the matrix-core RTD: NT column tiles of 16 units (unit of lane
+// column `col` in tile t given by uoff[t]).  init() sets the powers, steps() runs the
+// MFMA recurrence over fragments already staged in LDS (callable chunk after chunk),
+// finish() forms the per-tile channel sums Y_c (identical in the 4 lanes of a column).
 template <int C>
-__global__ void __launch_bounds__(64 * mfma_waves(C)) rtd_exp_mfma_kernel(const RtdArgs a, const UnitArgs ua,
-                                                                         int32_t fuse) {
-    constexpr int R = mfma_rows(C), SG = mfma_groups_per_chan(C), NT = mfma_tiles(C), NW = mfma_waves(C);
-    constexpr int CHUNK = mfma_chunk_steps(C);
-    extern __shared__ __attribute__((aligned(16))) double lds[];
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const int col = lane & 15, tq = lane >> 4;
-    const int64_t u0 = ((int64_t)blockIdx.x * NW + wave) * (16 * NT);
-    const int64_t Umax = a.U - 1;
-    const double* tau_row = a.theta + (int64_t)a.row_tau[0] * a.U;
-
+struct MfmaWave {
+    static constexpr int R = mfma_rows(C), SG = mfma_groups_per_chan(C), NT = mfma_tiles(C);
     double beta[NT], q4[NT], pw[NT];
     ngrtd_v4d acc[NT][R];
+
+    __device__ __forceinline__ void init(const RtdArgs& a, const int64_t* uoff) {
+        const int tq = (threadIdx.x & 63) >> 4;
+        const double* tau_row = a.theta + (int64_t)a.row_tau[0] * a.U;
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-        int64_t u = u0 + 16 * t + col;
-        u = u < Umax ? u : Umax;
-        beta[t] = 1. / tau_row[u];
-        const double q = fexp(-beta[t]);
-        const double q2 = q * q;
-        q4[t] = q2 * q2;
-        pw[t] = (tq == 0) ? 1.0 : (tq == 1) ? q : (tq == 2) ? q2 : q2 * q;
+        for (int t = 0; t < NT; ++t) {
+            beta[t] = 1. / tau_row[uoff[t]];
+            const double q = fexp(-beta[t]);
+            const double q2 = q * q;
+            q4[t] = q2 * q2;
+            pw[t] = (tq == 0) ? 1.0 : (tq == 1) ? q : (tq == 2) ? q2 : q2 * q;
 #pragma unroll
-        for (int r = 0; r < R; ++r) acc[t][r] = ngrtd_v4d{0.0, 0.0, 0.0, 0.0};
-    }
-    const int nsteps = a.nsteps;
-    for (int c0 = 0; c0 < nsteps; c0 += CHUNK) {
-        const int cn = (nsteps - c0) < CHUNK ? (nsteps - c0) : CHUNK;
-        __syncthreads();
-        {   // fragments of steps [c0, c0 + cn): cn * R * 512 contiguous bytes
-            const double2* src = reinterpret_cast<const double2*>(a.frag + (int64_t)c0 * R * 64);
-            double2* dst = reinterpret_cast<double2*>(lds);
-            for (int i = threadIdx.x; i < cn * R * 32; i += 64 * NW) dst[i] = src[i];
+            for (int r = 0; r < R; ++r) acc[t][r] = ngrtd_v4d{0.0, 0.0, 0.0, 0.0};
         }
-        __syncthreads();
-        const double* f = lds + lane;
-        for (int step = 0; step < cn; ++step, f += R * 64) {
+    }
+    __device__ __forceinline__ void steps(const double* __restrict__ fr, int nsteps) {
+        const double* f = fr + (threadIdx.x & 63);
+        for (int step = 0; step < nsteps; ++step, f += R * 64) {
             double A[R];
 #pragma unroll
             for (int r = 0; r < R; ++r) A[r] = f[r * 64];
 #pragma unroll
             for (int t = 0; t < NT; ++t)
 #pragma unroll
-                for (int r = 0; r < R; ++r) acc[t][r] = __builtin_amdgcn_mfma_f64_16x16x4f64(A[r], pw[t], acc[t][r], 0, 0, 0);
+                for (int r = 0; r < R; ++r)
+                    acc[t][r] = __builtin_amdgcn_mfma_f64_16x16x4f64(A[r], pw[t], acc[t][r], 0, 0, 0);
 #pragma unroll
             for (int t = 0; t < NT; ++t) pw[t] *= q4[t];
         }
     }
-
     // segment sums: lane (tq, col) of tile t holds P_{c, 4m+tq} for all c, m
-    const double Lseg = (double)a.Lseg;
-    double y[NT][C];
+    __device__ __forceinline__ void finish(const RtdArgs& a, double (*y)[C]) const {
+        const int tq = (threadIdx.x & 63) >> 4;
+        const double Lseg = (double)a.Lseg;
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-        const double Q = fexp(-beta[t] * Lseg);
-        const double Q2 = Q * Q, Q4 = Q2 * Q2;
-        const double Qt = (tq == 0) ? 1.0 : (tq == 1) ? Q : (tq == 2) ? Q2 : Q2 * Q;
+        for (int t = 0; t < NT; ++t) {
+            const double Q = fexp(-beta[t] * Lseg);
+            const double Q2 = Q * Q, Q4 = Q2 * Q2;
+            const double Qt = (tq == 0) ? 1.0 : (tq == 1) ? Q : (tq == 2) ? Q2 : Q2 * Q;
 #pragma unroll
-        for (int c = 0; c < C; ++c) {
-            double v = 0.0;
+            for (int c = 0; c < C; ++c) {
+                double v = 0.0;
 #pragma unroll
-            for (int m = SG - 1; m >= 0; --m) {
-                const int g = c + C * m;
-                v = fma(v, Q4, acc[t][g >> 2][g & 3]);
+                for (int m = SG - 1; m >= 0; --m) {
+                    const int g = c + C * m;
+                    v = fma(v, Q4, acc[t][g >> 2][g & 3]);
+                }
+                v *= Qt;
+                v += __shfl_xor(v, 16);
+                v += __shfl_xor(v, 32);
+                y[t][c] = v;
             }
-            v *= Qt;
-            v += __shfl_xor(v, 16);
-            v += __shfl_xor(v, 32);
-            y[t][c] = v;
         }
     }
-    // lanes with tq = t finish the units of tile t
-    if (tq >= NT) return;
-    double yy[C], bu = 0.0;
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-        if (t == tq) {
-            bu = beta[t];
-#pragma unroll
-            for (int c = 0; c < C; ++c) yy[c] = y[t][c];
-        }
-    }
-    const int64_t u = u0 + 16 * tq + col;
-    if (u > Umax) return;
+};
+
+// Channel sums -> tracer concentrations of unit u (rtd_conc_kernel's combination step)
+template <int C>
+__device__ __forceinline__ void mfma_unit_conc(const RtdArgs& a, int64_t u, double bu, const double* yy,
+                                               double* conc) {
     const int n = a.N - 1;
     const double s01 = fexp(-bu * ((1.0 + a.dtp) - a.tp0));
     const double G = (n > 0) ? expm1(-bu * (double)n) / expm1(-bu) : 0.0;
@@ -655,7 +647,6 @@ __global__ void __launch_bounds__(64 * mfma_waves(C)) rtd_exp_mfma_kernel(const 
         const double jv = a.theta[(int64_t)a.row_J * a.U + u];
         Jw = a.J_is_log10 ? exp10(jv) : jv;
     }
-    double conc[kMaxTracer];
     for (int t = 0; t < a.K; ++t) {
         double sA = 0.0, sB = 0.0;
         bool hasB = false;
@@ -669,9 +660,137 @@ __global__ void __launch_bounds__(64 * mfma_waves(C)) rtd_exp_mfma_kernel(const 
         double cout = fmix * cc + 0.0 * 0.0;   // f1*cout1 + f2*cout2, run_age_mcmc_utils.py:154
         if (a.tr_sf6[t] && a.row_lamsf6 >= 0) cout *= (1 + a.theta[(int64_t)a.row_lamsf6 * a.U + u]);
         conc[t] = cout;
-        if (a.conc) a.conc[(int64_t)t * a.U + u] = cout;
     }
+}
+
+// lanes with tq = t finish the units of tile t: select that tile's sums
+template <int C>
+__device__ __forceinline__ void mfma_pick_tile(const double (*y)[C], const double* beta, double* yy, double& bu) {
+    constexpr int NT = mfma_tiles(C);
+    const int tq = (threadIdx.x & 63) >> 4;
+    bu = 0.0;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        if (t == tq) {
+            bu = beta[t];
+#pragma unroll
+            for (int c = 0; c < C; ++c) yy[c] = y[t][c];
+        }
+    }
+}
+
+template <int C>
+__global__ void __launch_bounds__(64 * mfma_waves(C)) rtd_exp_mfma_kernel(const RtdArgs a, const UnitArgs ua,
+                                                                         int32_t fuse) {
+    constexpr int R = mfma_rows(C), NT = mfma_tiles(C), NW = mfma_waves(C);
+    constexpr int CHUNK = mfma_chunk_steps(C);
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int col = lane & 15, tq = lane >> 4;
+    const int64_t u0 = ((int64_t)blockIdx.x * NW + wave) * (16 * NT);
+    const int64_t Umax = a.U - 1;
+    int64_t uoff[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const int64_t u = u0 + 16 * t + col;
+        uoff[t] = u < Umax ? u : Umax;
+    }
+    MfmaWave<C> mw;
+    mw.init(a, uoff);
+    for (int c0 = 0; c0 < a.nsteps; c0 += CHUNK) {
+        const int cn = (a.nsteps - c0) < CHUNK ? (a.nsteps - c0) : CHUNK;
+        if (c0 > 0) __syncthreads();
+        // fragments of steps [c0, c0 + cn): cn * R * 512 contiguous bytes
+        const double2* src = reinterpret_cast<const double2*>(a.frag + (int64_t)c0 * R * 64);
+        double2* dst = reinterpret_cast<double2*>(lds);
+        for (int i = threadIdx.x; i < cn * R * 32; i += 64 * NW) dst[i] = src[i];
+        __syncthreads();
+        mw.steps(lds, cn);
+    }
+    double y[NT][C];
+    mw.finish(a, y);
+    if (tq >= NT) return;
+    double yy[C], bu;
+    mfma_pick_tile<C>(y, mw.beta, yy, bu);
+    const int64_t u = u0 + 16 * tq + col;
+    if (u > Umax) return;
+    double conc[kMaxTracer];
+    mfma_unit_conc<C>(a, u, bu, yy, conc);
+    if (a.conc)
+        for (int t = 0; t < a.K; ++t) a.conc[(int64_t)t * a.U + u] = conc[t];
     if (fuse) ua.ulogp[u] = unit_logp(ua, u, conc);
+}
+
+// The whole batched log-prob in ONE launch (exponential single-component RTD with
+// C <= 5 channels so that a wave owns 4 tiles = 64 units, table in LDS, L <= 512).  A
+// block of 8 waves owns WB = 512 / L walkers x all L wells (block-local unit
+// i = l * WB + w'); lane `lane` of wave `wave` owns unit i = 64 * wave + lane for all of
+// its work: the matrix-core RTD of the wave's 4 tiles, the unit's concentrations and RTD
+// Student-t likelihood, and the theta-only part (CE model + likelihood, all priors).
+// f64 MFMA and f64 VALU share one pipe on gfx950 and a lone wave leaves it idle while it
+// waits on dependencies, so waves 0-3 run RTD then CE and waves 4-7 run CE then RTD: the
+// two waves sharing a SIMD (wave w and w + 4) always interleave an MFMA stream with a VALU
+// stream.  Per-walker sums over wells run through LDS in well order (deterministic, same
+// order as unit_walker_kernel).  One block per CU (VGPRs), 256 blocks at c4: one round.
+constexpr int kFusedWaves = 8;
+constexpr int kFusedUnits = 64 * kFusedWaves;
+
+template <int C>
+__global__ void __launch_bounds__(64 * kFusedWaves) logp_fused_kernel(const RtdArgs a, const UnitArgs ua,
+                                                                     int32_t WB, double* __restrict__ logp) {
+    constexpr int R = mfma_rows(C), NT = mfma_tiles(C);
+    static_assert(NT == 4, "one unit per lane needs 4 tiles per wave");
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    double* part = lds + (size_t)a.nsteps * R * 64;          // [512] per-unit log-prob
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const int col = lane & 15, tq = lane >> 4;
+    const int L = ua.L;
+    const int64_t W = ua.W;
+    const int64_t w0 = (int64_t)blockIdx.x * WB;
+    {
+        const double2* src = reinterpret_cast<const double2*>(a.frag);
+        double2* dst = reinterpret_cast<double2*>(lds);
+        for (int i = tid; i < a.nsteps * R * 32; i += 64 * kFusedWaves) dst[i] = src[i];
+    }
+    // this lane's unit and the units of the wave's tiles
+    const int mi = 64 * wave + lane;
+    const int mwl = mi % WB, ml = mi / WB;
+    const bool mvalid = ml < L && w0 + mwl < W;
+    const int64_t mu = mvalid ? (int64_t)ml * W + w0 + mwl : 0;
+    int64_t uoff[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const int i = (wave * NT + t) * 16 + col;
+        const int wl = i % WB, l = i / WB;
+        uoff[t] = (l < L && w0 + wl < W) ? (int64_t)l * W + w0 + wl : 0;
+    }
+    __syncthreads();
+    const bool rtd_first = wave < kFusedWaves / 2;
+    double th = 0.0;
+    if (!rtd_first && mvalid) th = unit_logp_theta(ua, mu, ml);
+    MfmaWave<C> mw;
+    mw.init(a, uoff);
+    mw.steps(lds, a.nsteps);
+    double y[NT][C];
+    mw.finish(a, y);
+    double yy[C], bu;
+    mfma_pick_tile<C>(y, mw.beta, yy, bu);       // tile tq holds this lane's unit
+    double like = 0.0;
+    if (mvalid) {
+        double conc[kMaxTracer];
+        mfma_unit_conc<C>(a, mu, bu, yy, conc);
+        like = unit_like_rtd(ua, mu, ml, conc);
+        if (rtd_first) th = unit_logp_theta(ua, mu, ml);
+    }
+    part[mi] = th + like;
+    __syncthreads();
+    if (tid < WB && w0 + tid < W) {
+        double tot = part[tid];
+        for (int l = 1; l < L; ++l) tot += part[l * WB + tid];
+        logp[w0 + tid] = tot;
+    }
 }
 
 // logp[w] = sum over wells of ulogp[l*W + w]: 16 fixed well groups per walker summed

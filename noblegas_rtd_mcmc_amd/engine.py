@@ -171,10 +171,10 @@ class LogProb:
         return ce, rt
 
     def kernel_stats(self, reset=False):
-        ms = (C.c_double * 3)()
-        n = (C.c_int64 * 3)()
-        self.ctx.check(self.lib.ngrtd_plan_kernel_stats(self.plan, ms, n, 3, int(reset)), "kernel_stats")
-        return {"rtd": (ms[0], n[0]), "unit": (ms[1], n[1]), "reduce": (ms[2], n[2])}
+        ms = (C.c_double * 4)()
+        n = (C.c_int64 * 4)()
+        self.ctx.check(self.lib.ngrtd_plan_kernel_stats(self.plan, ms, n, 4, int(reset)), "kernel_stats")
+        return {"rtd": (ms[0], n[0]), "unit": (ms[1], n[1]), "reduce": (ms[2], n[2]), "fused": (ms[3], n[3])}
 
     def info(self, W):
         v = (C.c_int64 * 11)()

@@ -221,8 +221,11 @@ def test_edge_walkers():
 
 
 def test_mfma_and_valu_paths_agree():
-    """The exponential model runs on the matrix cores (rtd_exp_mfma_kernel); the general
-    VALU Horner kernel (forced with NGRTD_NO_MFMA=1) must give the same answer."""
+    """The exponential model runs on the matrix cores: by default the log-prob is ONE
+    launch (logp_fused_kernel) and forward() uses rtd_exp_mfma_kernel.  The general VALU
+    Horner kernel (NGRTD_NO_MFMA=1), the two-launch MFMA path (NGRTD_NO_FUSED=1) and the
+    MFMA kernel with the per-unit epilogue fused (NGRTD_FUSE=1, NGRTD_NO_FUSED=1) must give
+    the same answer."""
     import os
     import subprocess
     import sys
@@ -234,6 +237,11 @@ def test_mfma_and_valu_paths_agree():
     assert lp.info(300)["mfma_rows"] >= 1
     _, rt = lp.forward(th, soa=True)
     a = lp(th, soa=True)
+    lp.ctx.set_profiling(True)
+    lp.kernel_stats(reset=True)
+    lp(th, soa=True)
+    assert lp.kernel_stats(reset=True)["fused"][1] == 1
+    lp.ctx.set_profiling(False)
     lp.close()
     code = ("import numpy as np, sys; sys.path.insert(0, %r); from noblegas_rtd_mcmc_amd import workloads as wl;"
             "from noblegas_rtd_mcmc_amd.engine import LogProb; spec = wl.c4_spec(L=8, N=1200);"
@@ -241,17 +249,12 @@ def test_mfma_and_valu_paths_agree():
             "assert (lp.info(300)['mfma_rows'] > 0) == MFMA; _, rt = lp.forward(th, soa=True);"
             "np.save(sys.argv[1], np.concatenate([rt.ravel(), lp(th, soa=True)]))"
             % os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    out = "/tmp/ngrtd_valu_%d.npy" % os.getpid()
-    env = dict(os.environ, NGRTD_NO_MFMA="1")
-    subprocess.run([sys.executable, "-c", "MFMA = False; " + code, out], check=True, env=env, timeout=300)
-    b = np.load(out)
-    os.remove(out)
-    assert close(rt.ravel(), b[:rt.size], 1e-12).all()
-    assert close(a, b[rt.size:], 1e-12, 1e-9).all()
-    # the fused MFMA + CE/likelihood epilogue variant (NGRTD_FUSE=1)
-    env = dict(os.environ, NGRTD_FUSE="1")
-    subprocess.run([sys.executable, "-c", "MFMA = True; " + code, out], check=True, env=env, timeout=300)
-    c = np.load(out)
-    os.remove(out)
-    assert close(rt.ravel(), c[:rt.size], 1e-12).all()
-    assert close(a, c[rt.size:], 1e-12, 1e-9).all()
+    out = "/tmp/ngrtd_paths_%d.npy" % os.getpid()
+    for extra, mfma in (({"NGRTD_NO_MFMA": "1"}, False), ({"NGRTD_NO_FUSED": "1"}, True),
+                        ({"NGRTD_FUSE": "1", "NGRTD_NO_FUSED": "1"}, True)):
+        env = dict(os.environ, **extra)
+        subprocess.run([sys.executable, "-c", "MFMA = %s; " % mfma + code, out], check=True, env=env, timeout=300)
+        b = np.load(out)
+        os.remove(out)
+        assert close(rt.ravel(), b[:rt.size], 1e-12).all(), extra
+        assert close(a, b[rt.size:], 1e-12, 1e-9).all(), extra

@@ -39,10 +39,23 @@ def main():
     for name, spec in variants.items():
         th = torch.from_numpy(workloads.sample_prior(spec, W, np.random.default_rng(1))).cuda()
         lp = LogProb(spec, max_walkers=W)
+        import time
+        out_t = torch.empty(W, dtype=torch.float64, device=th.device)
         for _ in range(5):
-            lp(th)
+            lp(th, out=out_t)
         torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            lp(th, out=out_t)
+        torch.cuda.synchronize()
+        wall_off = (time.perf_counter() - t0) / args.steps * 1e6
         lp.ctx.set_profiling(True)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            lp(th, out=out_t)
+        torch.cuda.synchronize()
+        wall_on = (time.perf_counter() - t0) / args.steps * 1e6
+        lp.kernel_stats(reset=True)
         lp.kernel_stats(reset=True)
         for _ in range(args.steps):
             lp(th)
@@ -56,7 +69,7 @@ def main():
         else:
             kf = {}
         lp.ctx.set_profiling(False)
-        out[name] = {"logp_us": {k: 1e3 * v[0] / max(v[1], 1) for k, v in ks.items() if v[1]},
+        out[name] = {"wall_us_events_off": wall_off, "wall_us_events_on": wall_on, "logp_us": {k: 1e3 * v[0] / max(v[1], 1) for k, v in ks.items() if v[1]},
                      "forward_us": {k: 1e3 * v[0] / max(v[1], 1) for k, v in kf.items() if v[1]}}
         lp.close()
         print(name, json.dumps(out[name]), flush=True)

@@ -165,7 +165,50 @@ __global__ void __launch_bounds__(64 * NWAVE) probe_rt(const double* __restrict_
     __syncthreads();
     if (threadIdx.x == 0) s.w1 = wall_clock64();
     const double* f = (MODE == 2 ? frag : lds) + lane;
-    if (MODE == 1) {
+    if (MODE == 3 || MODE == 4) {
+        double A[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) A[r] = f[r * 64];
+        for (int step = 0; step < nsteps; ++step) {
+            if (MODE == 4) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) A[r] = f[r * 64 + step * R * 64];
+            }
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int r = 0; r < R; ++r) acc[t][r] = __builtin_amdgcn_mfma_f64_16x16x4f64(A[r], pw[t], acc[t][r], 0, 0, 0);
+            if (MODE == 3) {
+#pragma unroll
+                for (int t = 0; t < NT; ++t) pw[t] *= q4[t];
+            }
+        }
+    } else if (MODE == 5) {
+        // two steps per iteration, A of the next pair loaded while this pair runs
+        double A0[R], A1[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) { A0[r] = f[r * 64]; A1[r] = f[R * 64 + r * 64]; }
+        for (int step = 0; step < nsteps; step += 2) {
+            f += 2 * R * 64;
+            double B0[R], B1[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) { B0[r] = f[r * 64]; B1[r] = f[R * 64 + r * 64]; }
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int r = 0; r < R; ++r) acc[t][r] = __builtin_amdgcn_mfma_f64_16x16x4f64(A0[r], pw[t], acc[t][r], 0, 0, 0);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) pw[t] *= q4[t];
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int r = 0; r < R; ++r) acc[t][r] = __builtin_amdgcn_mfma_f64_16x16x4f64(A1[r], pw[t], acc[t][r], 0, 0, 0);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) pw[t] *= q4[t];
+#pragma unroll
+            for (int r = 0; r < R; ++r) { A0[r] = B0[r]; A1[r] = B1[r]; }
+        }
+    } else if (MODE == 1) {
         double A[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) A[r] = f[r * 64];
@@ -356,13 +399,13 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&dst, 8192 * sizeof(Stamp)));
     CK(hipMemcpy(dth, th.data(), U * 8, hipMemcpyHostToDevice));
     CK(hipMemcpy(dfr, fr.data(), fr.size() * 8, hipMemcpyHostToDevice));
-    run<4, 4, 0>("r1a NT4 W4 pad64K", dth, dfr, U, dconc, dst, reps, 64 << 10);
-    run_rt<5, 4, 4, 0>("rt R5 NT4 W4 lds (prod)", dth, dfr, U, dconc, dst, reps);
-    run_rt<5, 4, 4, 1>("rt R5 NT4 W4 lds-pipelined", dth, dfr, U, dconc, dst, reps);
-    run_rt<5, 4, 4, 2>("rt R5 NT4 W4 global-A", dth, dfr, U, dconc, dst, reps);
-    run_rt<5, 2, 8, 0>("rt R5 NT2 W8 lds", dth, dfr, U, dconc, dst, reps);
-    run_rt<5, 2, 8, 1>("rt R5 NT2 W8 lds-pipelined", dth, dfr, U, dconc, dst, reps);
-    run_rt<5, 4, 8, 1>("rt R5 NT4 W8 lds-pipe 1blk", dth, dfr, U, dconc, dst, reps, 96 << 10);
-    run_rt<5, 4, 4, 0>("rt R5 NT4 W4 lds (prod) again", dth, dfr, U, dconc, dst, reps);
+    run_rt<5, 4, 4, 0>("W4 lds56K (prod)", dth, dfr, U, dconc, dst, reps);
+    run_rt<5, 4, 4, 0>("W4 lds96K", dth, dfr, U, dconc, dst, reps, 96 << 10);
+    run_rt<5, 4, 8, 0>("W8 lds56K", dth, dfr, U, dconc, dst, reps, 56 << 10);
+    run_rt<5, 4, 8, 0>("W8 lds64K", dth, dfr, U, dconc, dst, reps, 64 << 10);
+    run_rt<5, 4, 8, 0>("W8 lds80K", dth, dfr, U, dconc, dst, reps, 80 << 10);
+    run_rt<5, 4, 8, 0>("W8 lds96K", dth, dfr, U, dconc, dst, reps, 96 << 10);
+    run_rt<5, 4, 16, 0>("W16 lds96K", dth, dfr, U, dconc, dst, reps, 96 << 10);
+    run_rt<5, 4, 4, 0>("W4 lds56K (prod) again", dth, dfr, U, dconc, dst, reps);
     return 0;
 }
