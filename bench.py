@@ -27,6 +27,7 @@ METRIC = "log-likelihood evals/sec (CE + RTD-conv), 2048 walkers, 1/2/4/8 MI355X
 FP64_MFMA_PEAK = 78.6e12     # dense FP64 matrix peak, 256 CU x 4 SIMD x 32 FLOP/clk x 2.4 GHz
                              # (tools/ubench_fp64.hip measures 78.3: profiles/r01_ubench_fp64.txt)
 HBM_PEAK = 8.0e12            # MI355X_MICROARCH.md chip table
+PMC_SUMMARY = "r01_pmc.json"
 
 
 def parse():
@@ -142,14 +143,23 @@ def main():
         # (unit, channel, age >= 1) -- the Horner evaluation (DESIGN.md 'Roofline')
         flops = 2.0 * U * C * (N - 1)
         achieved = flops / (rtd_ms * 1e-3)
-        # algorithmic HBM bytes of the same launch: theta rows read + concentrations written
-        n_rows = 1 + (1 if "J" in spec.roles else 0)
-        hbm_bytes = U * 8.0 * n_rows + U * 8.0 * len(spec.rtd.tracers) + N * ((C + 1) // 2 * 2) * 8.0
+        # algorithmic HBM bytes of the same launch: every theta row read once, plus the
+        # output (logp per walker for the single-launch kernel; concentrations otherwise)
+        # and the MFMA fragment table once per block (L2-served after the first block)
+        theta_bytes = U * 8.0 * len(spec.roles)
+        out_bytes = W * 8.0 if kname == "fused" else U * 8.0 * len(spec.rtd.tracers)
+        hbm_bytes = theta_bytes + out_bytes + info["nsteps"] * max(info["mfma_rows"], 1) * 512.0
+        # HBM bytes per launch from the committed PMC summary of the same command
+        # (tools/gpu_profile.sh + tools/profile_summary.py; FETCH_SIZE doubled per the
+        # MI355X guide, plus WRITE_SIZE); null when no summary for this kernel is committed
         traffic = None
-        pmc = os.path.join(REPO, "profiles", "pmc_rtd_summary.json")
+        pmc = os.path.join(REPO, "profiles", PMC_SUMMARY)
         if os.path.exists(pmc):
             with open(pmc) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
+                for k, e in json.load(f).items():
+                    if (("logp_fused_kernel" if kname == "fused" else "rtd_exp_mfma_kernel") in k
+                            and "hbm_bytes_per_launch" in e):
+                        traffic = e["hbm_bytes_per_launch"]
         evals = W * world * args.steps
         line = {
             "metric": METRIC,

@@ -38,19 +38,45 @@ void run(const char* name, int blocks, size_t lds, long long cycles, double* d) 
            1e3 * ms / reps);
 }
 
+template <int NTH, int VG>
+void run2(const char* name, int blocks, size_t lds, long long cycles, double* d, int nsplit) {
+    auto k = spin<NTH, VG>;
+    hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipStream_t s0, s[4];
+    hipStreamCreate(&s0);
+    for (int i = 0; i < nsplit; ++i) hipStreamCreateWithFlags(&s[i], hipStreamNonBlocking);
+    hipEvent_t fork[64], join[4][64];
+    for (int i = 0; i < 64; ++i) { hipEventCreateWithFlags(&fork[i], hipEventDisableTiming);
+        for (int j = 0; j < 4; ++j) hipEventCreateWithFlags(&join[j][i], hipEventDisableTiming); }
+    auto step = [&](int it) {
+        hipEventRecord(fork[it & 63], s0);
+        for (int i = 0; i < nsplit; ++i) {
+            hipStreamWaitEvent(s[i], fork[it & 63], 0);
+            hipLaunchKernelGGL(k, dim3(blocks / nsplit), dim3(NTH), lds, s[i], d, cycles);
+            hipEventRecord(join[i][it & 63], s[i]);
+            hipStreamWaitEvent(s0, join[i][it & 63], 0);
+        }
+    };
+    for (int i = 0; i < 5; ++i) step(i);
+    hipDeviceSynchronize();
+    hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
+    const int reps = 200;
+    hipEventRecord(a, s0);
+    for (int i = 0; i < reps; ++i) step(i);
+    hipEventRecord(b, s0); hipEventSynchronize(b);
+    float ms; hipEventElapsedTime(&ms, a, b);
+    printf("%-34s blocks %5d split %d  spin %.2f us  per step %.2f us\n", name, blocks, nsplit, cycles / 2.4e3,
+           1e3 * ms / reps);
+}
+
 int main() {
     double* d; hipMalloc(&d, 1 << 20); hipMemset(d, 0, 1 << 20);
     const long long cyc = 48000;   // ~20 us at 2.4 GHz
-    (void)cyc;
-    run<256, 8>("256thr VG8", 512, 0, 0, d);
-    run<256, 16>("256thr VG16", 512, 0, 0, d);
-    run<256, 32>("256thr VG32", 512, 0, 0, d);
-    run<256, 48>("256thr VG48", 512, 0, 0, d);
-    run<256, 64>("256thr VG64", 512, 0, 0, d);
-    run<256, 96>("256thr VG96", 512, 0, 0, d);
-    run<256, 8>("256thr VG8 x4 blocks", 2048, 0, 0, d);
-    run<256, 32>("256thr VG32 x4 blocks", 2048, 0, 0, d);
-    run<256, 48>("256thr VG48 x4 blocks", 2048, 0, 0, d);
-    run<256, 8>("256thr VG8 x16 blocks", 8192, 0, 0, d);
+    run<256, 96>("256thr VG96 1 stream", 512, 57344, cyc, d);
+    run2<256, 96>("256thr VG96 streams", 512, 57344, cyc, d, 1);
+    run2<256, 96>("256thr VG96 streams", 512, 57344, cyc, d, 2);
+    run2<256, 96>("256thr VG96 streams", 512, 57344, cyc, d, 4);
+    run<256, 96>("256thr VG96 1 stream nospin", 512, 57344, 0, d);
+    run2<256, 96>("256thr VG96 streams nospin", 512, 57344, 0, d, 2);
     return 0;
 }

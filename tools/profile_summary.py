@@ -1,0 +1,42 @@
+#!/usr/bin/env python3
+"""Condense a tools/gpu_profile.sh run into the files committed under profiles/:
+
+    python tools/profile_summary.py gpurun_out/TAG profiles/rNN
+
+writes rNN_kernel_stats.csv (rocprofv3 --stats of the bench command), rNN_pmc.json (per
+launch averages of every PMC counter for the ngrtd kernels, plus HBM bytes per launch:
+FETCH_SIZE doubled per MI355X_MICROARCH.md 'HBM' + WRITE_SIZE, both KiB counters) and
+rNN_bench.json (the bench line)."""
+import json
+import os
+import shutil
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from pmc_summary import summarize  # noqa: E402
+
+
+def main(src, prefix):
+    os.makedirs(os.path.dirname(prefix) or ".", exist_ok=True)
+    stats = os.path.join(src, "prof", "stats_kernel_stats.csv")
+    if os.path.exists(stats):
+        shutil.copy(stats, prefix + "_kernel_stats.csv")
+    if os.path.exists(os.path.join(src, "bench.json")):
+        shutil.copy(os.path.join(src, "bench.json"), prefix + "_bench.json")
+    res = summarize([os.path.join(src, d) for d in ("pmc_fetch", "pmc_write", "pmc_sq")])
+    out = {}
+    for k, d in res.items():
+        if "ngrtd" not in k:
+            continue
+        e = {c: v for c, v in d.items()}
+        if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+            e["hbm_bytes_per_launch"] = (2.0 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024.0
+        out[k] = e
+    with open(prefix + "_pmc.json", "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+    print(json.dumps({k[:60]: {c: round(v, 1) for c, v in e.items() if not c.startswith("dur")}
+                      for k, e in out.items()}, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
