@@ -130,6 +130,16 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     assert torch.isfinite(out).any()
+    # PCIe-inclusive rate: theta handed over as host memory (staged H2D per call, results
+    # copied back) -- reported beside `value`, never as it (DESIGN.md 'Measurement')
+    host_staged = None
+    if rank == 0:
+        hs = max(5, args.steps // 20)
+        lp(theta_h, soa=True)
+        t1 = time.perf_counter()
+        for _ in range(hs):
+            lp(theta_h, soa=True)
+        host_staged = W * hs / (time.perf_counter() - t1)
 
     if rank == 0:
         info = lp.info(W)
@@ -185,6 +195,7 @@ def main():
                          "hbm": {"algorithmic_bytes": hbm_bytes, "achieved_GBps": hbm_bytes / (rtd_ms * 1e-3) / 1e9,
                                  "peak_GBps": HBM_PEAK / 1e9,
                                  "frac": hbm_bytes / (rtd_ms * 1e-3) / HBM_PEAK}},
+            "host_staged_value": host_staged,
             "kernels_ms": {k: v[0] / max(v[1], 1) for k, v in ks.items()},
             "geometry": info,
         }
