@@ -213,11 +213,25 @@ int ngrtd_forward(ngrtd_plan* plan, const double* theta, int64_t W, double* ce_o
 int ngrtd_plan_kernel_stats(ngrtd_plan* plan, double* times_ms, int64_t* counts, int32_t n,
                             int32_t reset);
 
-/* Launch geometry the plan chose for its RTD kernel: info[0..10] = units per lane (VALU
+/* Launch geometry the plan chose for its RTD kernel: info[0..12] = units per lane (VALU
  * path) or 16-unit tiles per wave (MFMA path), waves per block, blocks, ages per LDS slice
  * (VALU) or per segment (MFMA), channels, N, LDS bytes, units, MFMA row tiles (0 = VALU
- * path), age segments, 4-age MFMA steps.  For the roofline accounting in bench.py. */
+ * path), age segments, 4-age MFMA steps, Chebyshev surrogate in use (0/1), the
+ * surrogate's validated max relative error in units of 1e-18 (-1: not built).  For the
+ * roofline accounting in bench.py. */
 int ngrtd_plan_info(ngrtd_plan* plan, int64_t W, int64_t* info, int32_t n);
+
+/* Host-only (no device needed): build the piecewise-Chebyshev surrogate the exponential
+ * log-prob kernel uses for the channel sums Y_c(tau) = sum_{j>=0} A_c[1+j] exp(-j/tau)
+ * (the exponential g(tp) of convolution_integral_utils.py:184 times the decay-folded
+ * series, :305-340) and validate it against a long-double evaluation of the same sums.
+ * cols: [C][N] channel columns (age order); coef (may be NULL): receives
+ * [NGRTD_CHEB_PIECES][NGRTD_CHEB_N][(C+1)&~1]; *max_rel_err: max |surrogate - exact| /
+ * sum_j |A_c[1+j]| exp(-j/tau) over the validation points.  Plans use the surrogate only
+ * when this is <= 5e-14. */
+#define NGRTD_CHEB_N 18
+#define NGRTD_CHEB_PIECES 27
+int ngrtd_surrogate_check(const double* cols, int32_t C, int64_t N, double* coef, double* max_rel_err);
 
 #ifdef __cplusplus
 }

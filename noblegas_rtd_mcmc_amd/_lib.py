@@ -10,7 +10,8 @@ import threading
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libngrtd.so")
+# NGRTD_LIB selects an instrumented build (tools/section_probe.py); default: the product library
+LIB_PATH = os.environ.get("NGRTD_LIB") or os.path.join(_HERE, "libngrtd.so")
 
 NGRTD_OK, NGRTD_EINVAL, NGRTD_EDEVICE, NGRTD_ENOMEM, NGRTD_ESTATE = 0, -1, -2, -3, -4
 MEM_HOST, MEM_DEVICE = 0, 1
@@ -80,6 +81,7 @@ PROTOTYPES = {
     "ngrtd_forward": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int32]),
     "ngrtd_plan_kernel_stats": (C.c_int, [C.c_void_p, _dp, _i64p, C.c_int32, C.c_int32]),
     "ngrtd_plan_info": (C.c_int, [C.c_void_p, C.c_int64, _i64p, C.c_int32]),
+    "ngrtd_surrogate_check": (C.c_int, [_dp, C.c_int32, C.c_int64, _dp, _dp]),
 }
 
 

@@ -48,6 +48,10 @@ struct SeriesHost {
 struct TableDev {
     DevBuf buf;
     DevBuf frag;            // MFMA A-operand fragments (rtd_exp_mfma_kernel)
+    DevBuf cheb;            // Chebyshev surrogate of the exponential channel sums (cheb_build)
+    bool cheb_ok = false;
+    double cheb_err = -1.0; // max relative error measured by the validation (-1: not built)
+    std::vector<std::vector<double>> cols_host;   // channel columns (kept for cheb_build)
     int S_seg = 1, Lseg = 0, nsteps = 0;
     int C = 0, CP = 0;
     int chan_tracer[kMaxChan] = {}, chan_isB[kMaxChan] = {}, chan_lamw[kMaxChan] = {};
@@ -186,6 +190,7 @@ static int build_table(ngrtd_ctx* ctx, const std::vector<TracerBuild>& trs, Tabl
     }
     tab.C = C;
     tab.CP = (C + 1) & ~1;
+    tab.cols_host = cols;
     std::vector<double> h((size_t)N * tab.CP, 0.0);
     for (int c = 0; c < C; ++c)
         for (int64_t k = 0; k < N; ++k) h[(size_t)k * tab.CP + c] = cols[c][k];
@@ -217,6 +222,98 @@ static int build_table(ngrtd_ctx* ctx, const std::vector<TracerBuild>& trs, Tabl
         if (!fr.empty())
             HIP_TRY(ctx, hipMemcpy(tab.frag.p, fr.data(), fr.size() * sizeof(double), hipMemcpyHostToDevice));
     }
+    return NGRTD_OK;
+}
+
+// ------------------------------------------------- Chebyshev surrogate tables
+static_assert(kChebN == NGRTD_CHEB_N && kChebPieces == NGRTD_CHEB_PIECES, "surrogate geometry vs ngrtd.h");
+// Y_c(s) = sum_{j=0}^{N-2} A_{c,1+j} e^{-j s} (s = 1/tau) in long double: the reference sum
+// the surrogate is fitted to and validated against.  `absval` sums |A| instead (the scale
+// the relative error is measured on, so that cancelling series are judged fairly).
+static long double cheb_exact(const std::vector<double>& A, long double s, bool absval) {
+    const long double q = expl(-s);
+    long double y = 0.0L;
+    for (size_t j = A.size(); j-- > 1;) y = y * q + (absval ? fabsl((long double)A[j]) : (long double)A[j]);
+    return y;
+}
+
+// Fit kChebN Chebyshev coefficients per piece and channel (interpolation at the Chebyshev
+// nodes of each piece), then validate every piece at 26 points per piece through the same
+// cheb_piece/cheb_sums code the kernel runs.  Returns the max relative error.
+// Channels with negative entries are not expanded (HUGE_VAL): for non-negative columns the
+// error measure below is exactly relative to |Y|, for mixed signs it would not be.
+static double cheb_build(const std::vector<std::vector<double>>& cols, int C, int CP, std::vector<double>& coef) {
+    const int n = kChebN;
+    coef.assign((size_t)kChebPieces * n * CP, 0.0);
+    for (int c = 0; c < C; ++c)
+        for (double v : cols[c])
+            if (!(v >= 0.0) || !std::isfinite(v)) return HUGE_VAL;
+    const long double PI = 3.14159265358979323846264338327950288L;
+    std::vector<long double> f(n);
+    for (int p = 0; p < kChebPieces; ++p) {
+        for (int c = 0; c < C; ++c) {
+            for (int k = 0; k < n; ++k) {
+                const long double xk = cosl(PI * (k + 0.5L) / n);
+                long double sv;
+                if (p < kChebLogPieces) {
+                    const long double u = (long double)kChebU0 + (p + 0.5L) * 0.5L + 0.25L * xk;
+                    sv = expl(-u);
+                } else {
+                    sv = 0.5L * (long double)kChebSHi * (1.0L + xk);
+                }
+                f[k] = cheb_exact(cols[c], sv, false);
+            }
+            for (int j = 0; j < n; ++j) {
+                long double acc = 0.0L;
+                for (int k = 0; k < n; ++k) acc += f[k] * cosl(PI * j * (k + 0.5L) / n);
+                acc *= 2.0L / n;
+                if (j == 0) acc *= 0.5L;
+                coef[((size_t)p * n + j) * CP + c] = (double)acc;
+            }
+        }
+    }
+    double worst = 0.0;
+    const int M = 24;
+    for (int p = 0; p < kChebPieces; ++p) {
+        for (int i = 0; i <= M + 1; ++i) {
+            double tau;
+            if (p < kChebLogPieces) {
+                const long double t = (i == 0) ? p : (i == M + 1) ? p + 1 - 1e-12L : p + (i - 0.5L) / M;
+                tau = (double)expl((long double)kChebU0 + 0.5L * t);
+            } else {
+                const long double sv = (long double)kChebSHi * (i / (long double)(M + 1));
+                tau = (sv == 0.0L) ? HUGE_VAL : (double)(1.0L / sv);
+            }
+            double x = 0.0;
+            const int pp = cheb_piece(tau, x);
+            if (pp < 0) return HUGE_VAL;
+            const long double sv = 1.0L / (long double)tau;
+            for (int c = 0; c < C; ++c) {
+                double y = 0.0;
+                cheb_sums<1>(coef.data() + (size_t)pp * n * CP + c, CP, x, &y);
+                const long double ex = cheb_exact(cols[c], sv, false);
+                const long double sc = cheb_exact(cols[c], sv, true);
+                const double e = (sc > 0) ? (double)(fabsl((long double)y - ex) / sc) : (y == 0.0 ? 0.0 : HUGE_VAL);
+                if (!(e <= worst)) worst = e;   // NaN -> worst = NaN
+            }
+        }
+    }
+    return worst;
+}
+
+// Surrogate for a table whose exponential plan runs logp_fused_kernel.  Used only when the
+// validation bound holds (kChebTol), else the kernel takes the exact matrix-core path.
+constexpr double kChebTol = 5e-14;
+static int cheb_prepare(ngrtd_ctx* ctx, TableDev& tab) {
+    static const bool disabled = std::getenv("NGRTD_NO_CHEB") != nullptr;
+    tab.cheb_ok = false;
+    if (disabled || tab.C < 1 || tab.cols_host.empty() || tab.cols_host[0].size() < 2) return NGRTD_OK;
+    std::vector<double> coef;
+    tab.cheb_err = cheb_build(tab.cols_host, tab.C, tab.CP, coef);
+    if (!(tab.cheb_err <= kChebTol)) return NGRTD_OK;
+    HIP_TRY(ctx, tab.cheb.ensure(coef.size() * sizeof(double)));
+    HIP_TRY(ctx, hipMemcpy(tab.cheb.p, coef.data(), coef.size() * sizeof(double), hipMemcpyHostToDevice));
+    tab.cheb_ok = true;
     return NGRTD_OK;
 }
 
@@ -298,8 +395,10 @@ static void launch_mfma(const RtdArgs& a, const UnitArgs& u, int32_t fuse, hipSt
 // Single-launch log-prob (logp_fused_kernel): exponential RTD on the MFMA path with 4
 // tiles per wave (C <= 5), the whole fragment table in LDS next to the 512 per-unit
 // partial sums, and L <= 512 wells.
+// LDS: the 512 per-unit partial sums and the surrogate table (the exact path's fragments
+// are read from global memory: they are needed only by waves with an uncovered tau)
 static size_t fused_lds(const RtdArgs& a) {
-    return (size_t)a.nsteps * mfma_rows(a.C) * 512 + kFusedUnits * sizeof(double);
+    return (size_t)(kFusedUnits + kChebPieces * kChebN * ((a.C + 1) & ~1)) * sizeof(double);
 }
 static bool fused_path(const RtdArgs& a, int L) {
     static const bool disabled = std::getenv("NGRTD_NO_FUSED") != nullptr;
@@ -679,6 +778,11 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
             if (d->ce_gas_ids[j] < 0 || d->ce_gas_ids[j] > 4) return set_err(ctx, NGRTD_EINVAL, "bad gas id");
             u.gas[j] = d->ce_gas_ids[j];
         }
+        for (int j = 0; j < kMaxGas; ++j) {
+            const GasCoef gc = gas_coef(u.gas[j < G ? j : 0]);
+            u.gz[j] = gc.z; u.gA0[j] = gc.A0; u.gA1[j] = gc.A1; u.gA2[j] = gc.A2; u.gA3[j] = gc.A3;
+            u.g_he[j] = u.gas[j < G ? j : 0] == 0;
+        }
         for (int i = 0; i < 6; ++i) u.row_ce[i] = ri[NGRTD_ROLE_AE_BETA + i];
         u.ce_obs = p->ce_obs.d(); u.ce_sd = p->ce_sd.d(); u.ce_Emin = p->ce_emin.d();
         u.E_max = d->ce_E_max; u.logA_min = d->ce_logA_min; u.logA_max = d->ce_logA_max;
@@ -751,6 +855,11 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
         for (int t = 0; t < K; ++t) { a.tr_sf6[t] = d->tracers[t].is_sf6; a.tr_J[t] = d->tracers[t].J; }
         a.conc = p->conc.d();
         set_frag(a, p->table);
+        a.cheb = nullptr;
+        if (a.mod[0] == MOD_EXP && a.mod[1] == MOD_NONE && !any_lamw && p->table.C <= 5) {
+            NG_CHECK(cheb_prepare(ctx, p->table));
+            if (p->table.cheb_ok) a.cheb = p->table.cheb.d();
+        }
         u.rtd_on = 1; u.K = K;
         u.rtd_obs = p->rtd_obs.d(); u.rtd_sd = p->rtd_sd.d(); u.conc = p->conc.d();
         u.row_tau1 = ri[NGRTD_ROLE_TAU1]; u.row_nu = ri[NGRTD_ROLE_NU_RTD_BETA]; u.row_tau2 = ri[NGRTD_ROLE_TAU2];
@@ -945,12 +1054,25 @@ int ngrtd_plan_kernel_stats(ngrtd_plan* p, double* times_ms, int64_t* counts, in
     return NGRTD_OK;
 }
 
+int ngrtd_surrogate_check(const double* cols, int32_t C, int64_t N, double* coef, double* max_rel_err) {
+    if (!cols || C < 1 || C > kMaxChan || N < 2 || !max_rel_err) return NGRTD_EINVAL;
+    std::vector<std::vector<double>> cv((size_t)C);
+    for (int c = 0; c < C; ++c) cv[c].assign(cols + (size_t)c * N, cols + (size_t)(c + 1) * N);
+    std::vector<double> co;
+    *max_rel_err = cheb_build(cv, C, (C + 1) & ~1, co);
+    if (coef) std::copy(co.begin(), co.end(), coef);
+    return NGRTD_OK;
+}
+
 int ngrtd_plan_info(ngrtd_plan* p, int64_t W, int64_t* info, int32_t n) {
     if (!p) return NGRTD_ESTATE;
     const int64_t U = (int64_t)p->desc.n_wells * W;
-    int64_t v[11] = {0};
+    int64_t v[13] = {0};
     if (p->desc.rtd_enabled) {
         RtdArgs a = p->rtd;
+        v[11] = a.cheb != nullptr;
+        v[12] = (p->table.cheb_err >= 0 && p->table.cheb_err < 1.0) ? (int64_t)llround(p->table.cheb_err * 1e18)
+                                                                    : -1;
         a.U = U;
         const bool lamw = a.row_thalf >= 0;
         if (mfma_path(a, lamw)) {
@@ -964,8 +1086,16 @@ int ngrtd_plan_info(ngrtd_plan* p, int64_t W, int64_t* info, int32_t n) {
         v[4] = p->table.C; v[5] = p->N;
     }
     v[7] = U;
-    for (int i = 0; i < n && i < 11; ++i) info[i] = v[i];
+    for (int i = 0; i < n && i < 13; ++i) info[i] = v[i];
     return NGRTD_OK;
 }
 
 }  // extern "C"
+
+#ifdef NGRTD_SECTION_PROBE
+// probe build only (tools/section_probe.py): copy the s_memtime stamps of the last launch
+extern "C" int ngrtd_probe_read(unsigned long long* dst, int64_t n) {
+    if (n > (int64_t)(sizeof(g_probe) / sizeof(g_probe[0]))) n = sizeof(g_probe) / sizeof(g_probe[0]);
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_probe), (size_t)n * sizeof(unsigned long long)) == hipSuccess ? 0 : -2;
+}
+#endif

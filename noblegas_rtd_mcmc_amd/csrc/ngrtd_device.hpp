@@ -33,7 +33,21 @@ struct RtdArgs {
     // MFMA fragments (rtd_exp_mfma_kernel): GEMM rows = (channel, age segment)
     const double* frag;     // [nsteps][R][64] A-operand fragments of v_mfma_f64_16x16x4f64
     int32_t nsteps, S_seg, Lseg;
+    // Chebyshev surrogate of the exponential channel sums (logp_fused_kernel), or null
+    const double* cheb;     // [kChebPieces][kChebN][CP]
 };
+
+// Chebyshev surrogate of Y_c(tau) = sum_{j>=0} A_{c,1+j} exp(-j / tau) (the exponential
+// RTD channel sums): piecewise in u = log(tau), kChebLogPieces pieces of width 1/2 from
+// tau = 1/2 (u0 = log 1/2), then one piece in s = 1/tau over [0, kChebSHi] for the tail up
+// to tau = inf.  kChebN coefficients per piece and channel.  Built and validated per plan
+// on the host (ngrtd.hip cheb_build); tau < 1/2, NaN take the exact matrix-core path.
+constexpr int kChebN = 18;
+constexpr int kChebLogPieces = 26;                 // u in [u0, u0 + 13]: tau up to 221 206.9
+constexpr int kChebPieces = kChebLogPieces + 1;
+constexpr double kChebTauLo = 0.5;
+constexpr double kChebU0 = -0.69314718055994530942;   // log(0.5)
+constexpr double kChebSHi = 4.55e-6;               // > 1 / (0.5 e^13)
 
 // Row tiles of the exponential-RTD GEMM for C channels: R tiles of 16 rows hold 4R row
 // groups; group g = c + C*m (m < 4R/C) of channel c carries the 4 age segments 4m..4m+3.
@@ -51,6 +65,10 @@ struct UnitArgs {
     int32_t flags;          // NGRTD_WANT_*
     int32_t ce_on, G;
     int32_t gas[kMaxGas];
+    // per likelihood slot j < kMaxGas: coefficients of gas[j] (slots >= G repeat slot 0), so
+    // the per-unit CE loop is unrolled over constant slots with uniform (SGPR) coefficients
+    double gz[kMaxGas], gA0[kMaxGas], gA1[kMaxGas], gA2[kMaxGas], gA3[kMaxGas];
+    int32_t g_he[kMaxGas];
     int32_t row_ce[6];      // Ae_beta, F_beta, E_beta, m, b_beta, nu_ce_beta
     const double* ce_obs;   // [L][G]
     const double* ce_sd;

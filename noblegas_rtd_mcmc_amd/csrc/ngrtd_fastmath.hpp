@@ -81,4 +81,36 @@ NGRTD_FM double flog(double x) {
     return res;
 }
 
+// expm1(x) = 2^k (e^r - 1) + (2^k - 1), x = k ln2 + r, |r| <= ln2/2: e^r - 1 by its Taylor
+// series to r^14/14! (truncation < 2e-19 relative), then ONE fma with the exact 2^k - 1
+// (|k| <= 57 below), so there is no cancellation for small |x| and <= 2 ulp everywhere
+// (tests/test_fastmath_cpu.py).  x <= -40 rounds to -1 exactly; NaN/inf as libm.
+NGRTD_FM double fexpm1(double x) {
+    const double LOG2E = 1.4426950408889634074;
+    const double LN2_HI = 6.93147180369123816490e-01;
+    const double LN2_LO = 1.90821492927058770002e-10;
+    const double kd = rint(fmin(fmax(x, -40.0), 40.0) * LOG2E);
+    double r = fma(-kd, LN2_HI, x);
+    r = fma(-kd, LN2_LO, r);
+    double p = 1.0 / 87178291200.0;
+    p = fma(p, r, 1.0 / 6227020800.0);
+    p = fma(p, r, 1.0 / 479001600.0);
+    p = fma(p, r, 1.0 / 39916800.0);
+    p = fma(p, r, 1.0 / 3628800.0);
+    p = fma(p, r, 1.0 / 362880.0);
+    p = fma(p, r, 1.0 / 40320.0);
+    p = fma(p, r, 1.0 / 5040.0);
+    p = fma(p, r, 1.0 / 720.0);
+    p = fma(p, r, 1.0 / 120.0);
+    p = fma(p, r, 1.0 / 24.0);
+    p = fma(p, r, 1.0 / 6.0);
+    p = fma(p, r, 0.5);
+    const double em = fma(r * r, p, r);                     // e^r - 1
+    const double t = ldexp(1.0, (int)kd);                   // exact, |kd| <= 58
+    double res = (kd == 0.0) ? em : fma(t, em, t - 1.0);
+    if (x > 40.0) res = fexp(x) - 1.0;                      // e^x >= 2^57: the -1 is below 1 ulp
+    if (x < -40.0) res = -1.0;
+    return (x != x) ? x : res;
+}
+
 }  // namespace ngrtd

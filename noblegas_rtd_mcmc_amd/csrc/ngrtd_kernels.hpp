@@ -29,6 +29,22 @@
 
 namespace ngrtd {
 
+// Section-timing probe (tools/section_probe.py builds a separate library with
+// -DNGRTD_SECTION_PROBE): lane 0 of every wave of logp_fused_kernel records the shader
+// clock (s_memtime) at fixed points.  Compiled out of the product library.
+#ifdef NGRTD_SECTION_PROBE
+constexpr int kProbeSlots = 8;
+__device__ unsigned long long g_probe[8192 * kProbeSlots];
+#define NGRTD_PROBE(k)                                                                        \
+    do {                                                                                     \
+        if ((threadIdx.x & 63) == 0)                                                          \
+            g_probe[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * kProbeSlots + (k)] = \
+                __builtin_amdgcn_s_memtime();                                                \
+    } while (0)
+#else
+#define NGRTD_PROBE(k) do {} while (0)
+#endif
+
 // ------------------------------------------------------------------ CE forward
 struct CeArgs {
     int32_t what, p_mode, G;
@@ -406,13 +422,13 @@ __device__ __forceinline__ void ce_model_s0(const UnitArgs& a, double T, double 
     const double dP = P - Pv;
     const double lnAr = lnK_horner(gas_coef(2), ix);
     const double FA = F * Ae, ImFA = (1 - F) * Ae;
-    for (int j = 0; j < a.G; ++j) {
-        const int g = a.gas[j];
-        const GasCoef c = gas_coef(g);
-        const double lnK = lnK_horner(c, ix);
-        const double e = fexp((g == 0) ? lnK - lnAr : -lnK);
-        const double ceq = (T < 0.0) ? -9999.0 : (gamma * (c.z * dP) * e) * (22414. / 18.);
-        const double ex = (ImFA * c.z) * ceq / (ceq + FA * c.z);
+    const bool neg = T < 0.0;
+#pragma unroll
+    for (int j = 0; j < kMaxGas; ++j) {
+        const double lnK = fma(fma(fma(a.gA3[j], ix, a.gA2[j]), ix, a.gA1[j]), ix, a.gA0[j]);
+        const double e = fexp(a.g_he[j] ? lnK - lnAr : -lnK);
+        const double ceq = neg ? -9999.0 : (gamma * (a.gz[j] * dP) * e) * (22414. / 18.);
+        const double ex = (ImFA * a.gz[j]) * ceq / (ceq + FA * a.gz[j]);
         mod[j] = ex + ceq;
     }
 }
@@ -451,7 +467,7 @@ __device__ __forceinline__ double unit_logp_theta(const UnitArgs& a, int64_t u, 
             if (a.ce_out)
                 for (int j = 0; j < a.G; ++j) a.ce_out[(int64_t)j * a.U + u] = mod[j];
             if (want_like)
-                lp += st_block(a.G, a.ce_obs + l * a.G, mod, a.ce_lam + l * a.G, a.ce_hll_sum[l], nu);
+                lp += st_block<kMaxGas>(a.G, a.ce_obs + l * a.G, mod, a.ce_lam + l * a.G, a.ce_hll_sum[l], nu);
         }
     }
     if (a.rtd_on) {
@@ -495,7 +511,7 @@ __device__ __forceinline__ double unit_like_rtd(const UnitArgs& a, int64_t u, in
     if (!a.rtd_on || !(a.flags & NGRTD_WANT_LIKE)) return 0.0;
     const double nub = a.theta[(int64_t)a.row_nu * a.U + u];
     const double nu = nub * (a.rnu_max - a.rnu_min) + a.rnu_min;
-    return st_block(a.K, a.rtd_obs + l * a.K, conc, a.rtd_lam + l * a.K, a.rtd_hll_sum[l], nu);
+    return st_block<kMaxTracer>(a.K, a.rtd_obs + l * a.K, conc, a.rtd_lam + l * a.K, a.rtd_hll_sum[l], nu);
 }
 
 // full log-prob contribution of one unit (same addition order as the reference's sum)
@@ -630,14 +646,54 @@ struct MfmaWave {
     }
 };
 
+// ---------------------------------------------- Chebyshev surrogate (see ngrtd_device.hpp)
+// Piece of tau and its local coordinate x in [-1, 1]; -1 when tau is not covered (tau < 1/2
+// or NaN).  Host and device run this same code (the host validates the table with it).
+__host__ __device__ __forceinline__ int cheb_piece(double tau, double& x) {
+    if (!(tau >= kChebTauLo)) return -1;
+    const double u = flog(tau);
+    const double t = (u - kChebU0) * 2.0;            // piece width 1/2
+    if (t >= (double)kChebLogPieces) {
+        const double sv = 1.0 / tau;
+        x = sv * (2.0 / kChebSHi) - 1.0;
+        return kChebLogPieces;
+    }
+    int p = (int)floor(t);
+    p = p < 0 ? 0 : p;
+    const double mid = kChebU0 + ((double)p + 0.5) * 0.5;
+    x = (u - mid) * 4.0;
+    return p;
+}
+
+// Clenshaw sums of C channels at x from one piece's coefficients [kChebN][CP]
+template <int C>
+__host__ __device__ __forceinline__ void cheb_sums(const double* __restrict__ pc, int CP, double x, double* y) {
+    const double x2 = x + x;
+    double b1[C], b2[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) { b1[c] = 0.0; b2[c] = 0.0; }
+#pragma unroll 3
+    for (int k = kChebN - 1; k >= 1; --k) {
+        const double* row = pc + k * CP;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const double t = fma(x2, b1[c], row[c] - b2[c]);
+            b2[c] = b1[c];
+            b1[c] = t;
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) y[c] = fma(x, b1[c], pc[c] - b2[c]);
+}
+
 // Channel sums -> tracer concentrations of unit u (rtd_conc_kernel's combination step)
 template <int C>
 __device__ __forceinline__ void mfma_unit_conc(const RtdArgs& a, int64_t u, double bu, const double* yy,
                                                double* conc) {
     const int n = a.N - 1;
     const double s01 = fexp(-bu * ((1.0 + a.dtp) - a.tp0));
-    const double G = (n > 0) ? expm1(-bu * (double)n) / expm1(-bu) : 0.0;
-    const double den = 1.0 + s01 * G;
+    const double G = (n > 0) ? fexpm1(-bu * (double)n) / fexpm1(-bu) : 0.0;
+    const double rden = 1.0 / (1.0 + s01 * G);     // one division for the K tracers (<= 1 ulp)
     double num[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) num[c] = a.tab[c] + s01 * yy[c];
@@ -656,7 +712,7 @@ __device__ __forceinline__ void mfma_unit_conc(const RtdArgs& a, int64_t u, doub
             if (a.chan_isB[c]) { sB = num[c]; hasB = true; }
             else sA = num[c];
         }
-        const double cc = hasB ? (sA + ((a.row_J >= 0) ? Jw : a.tr_J[t]) * sB) / den : sA / den;
+        const double cc = hasB ? (sA + ((a.row_J >= 0) ? Jw : a.tr_J[t]) * sB) * rden : sA * rden;
         double cout = fmix * cc + 0.0 * 0.0;   // f1*cout1 + f2*cout2, run_age_mcmc_utils.py:154
         if (a.tr_sf6[t] && a.row_lamsf6 >= 0) cout *= (1 + a.theta[(int64_t)a.row_lamsf6 * a.U + u]);
         conc[t] = cout;
@@ -723,74 +779,128 @@ __global__ void __launch_bounds__(64 * mfma_waves(C)) rtd_exp_mfma_kernel(const 
 }
 
 // The whole batched log-prob in ONE launch (exponential single-component RTD with
-// C <= 5 channels so that a wave owns 4 tiles = 64 units, table in LDS, L <= 512).  A
-// block of 8 waves owns WB = 512 / L walkers x all L wells (block-local unit
-// i = l * WB + w'); lane `lane` of wave `wave` owns unit i = 64 * wave + lane for all of
-// its work: the matrix-core RTD of the wave's 4 tiles, the unit's concentrations and RTD
-// Student-t likelihood, and the theta-only part (CE model + likelihood, all priors).
-// f64 MFMA and f64 VALU share one pipe on gfx950 and a lone wave leaves it idle while it
-// waits on dependencies, so waves 0-3 run RTD then CE and waves 4-7 run CE then RTD: the
-// two waves sharing a SIMD (wave w and w + 4) always interleave an MFMA stream with a VALU
-// stream.  Per-walker sums over wells run through LDS in well order (deterministic, same
-// order as unit_walker_kernel).  One block per CU (VGPRs), 256 blocks at c4: one round.
+// C <= 5 channels, L <= 512).  A block of 8 waves owns WB = 512 / L walkers x all L wells
+// (block-local unit i = l * WB + w'); lane `lane` of wave `wave` owns unit
+// i = 64 * wave + lane for all of its work:
+//  1. the theta-only part: CE model + likelihood and all priors (the surrogate table's
+//     global loads, issued first into registers, land meanwhile);
+//  2. the channel sums Y_c(tau) from the Chebyshev surrogate (a.cheb, staged in LDS; about
+//     C * 2 * kChebN FP64 ops per unit instead of C * (N - 1) FMAs).  A wave with a lane
+//     whose tau the surrogate does not cover (tau < 1/2, NaN) evaluates the exact sums of
+//     all 4 of its 16-unit tiles on the matrix cores instead (MfmaWave; fragments read
+//     from global memory / L2, the exact path of rtd_exp_mfma_kernel); so does every wave
+//     when the plan has no validated surrogate (a.cheb == nullptr);
+//  3. the unit's concentrations and RTD Student-t likelihood.
+// Per-walker sums over wells run through LDS: for WB a power of two <= 64, lane
+// (g, w') of wave 0 adds wells g, g + 64/WB, ... in order and the 64/WB partials are
+// combined by a fixed xor-shuffle tree; otherwise WB lanes add the L wells in order.
+// Both orders are fixed (deterministic, no atomics).
 constexpr int kFusedWaves = 8;
 constexpr int kFusedUnits = 64 * kFusedWaves;
+constexpr int kFusedPrefetch = 3;   // double2 per thread: covers kChebPieces*kChebN*6 doubles
 
 template <int C>
 __global__ void __launch_bounds__(64 * kFusedWaves) logp_fused_kernel(const RtdArgs a, const UnitArgs ua,
                                                                      int32_t WB, double* __restrict__ logp) {
-    constexpr int R = mfma_rows(C), NT = mfma_tiles(C);
+    constexpr int NT = mfma_tiles(C);
+    constexpr int CP = (C + 1) & ~1;
+    constexpr int TAB2 = kChebPieces * kChebN * CP / 2;   // double2 entries of the surrogate table
     static_assert(NT == 4, "one unit per lane needs 4 tiles per wave");
+    static_assert(TAB2 <= kFusedPrefetch * 64 * kFusedWaves, "prefetch covers the table");
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    double* part = lds + (size_t)a.nsteps * R * 64;          // [512] per-unit log-prob
+    double* part = lds;                                   // [512] per-unit log-prob
+    double* cheb = lds + kFusedUnits;                     // [kChebPieces][kChebN][CP]
+    NGRTD_PROBE(0);
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
-    const int col = lane & 15, tq = lane >> 4;
+    const int col = lane & 15;
     const int L = ua.L;
     const int64_t W = ua.W;
-    const int64_t w0 = (int64_t)blockIdx.x * WB;
-    {
-        const double2* src = reinterpret_cast<const double2*>(a.frag);
-        double2* dst = reinterpret_cast<double2*>(lds);
-        for (int i = tid; i < a.nsteps * R * 32; i += 64 * kFusedWaves) dst[i] = src[i];
+    // XCD-aware walker blocks: the dispatcher deals block b to XCD b % 8, so consecutive
+    // walker blocks (which share the 128-B lines of every theta row when WB * 8 < 128) are
+    // renumbered onto the same XCD and its L2 serves the second (profiles: FETCH_SIZE)
+    const int nb = gridDim.x;
+    const int bl = (nb & 7) == 0 ? ((int)blockIdx.x & 7) * (nb >> 3) + ((int)blockIdx.x >> 3) : (int)blockIdx.x;
+    const int64_t w0 = (int64_t)bl * WB;
+    // surrogate table -> registers (written to LDS after the theta-only part)
+    double2 pre[kFusedPrefetch];
+    if (a.cheb) {
+        const double2* src = reinterpret_cast<const double2*>(a.cheb);
+#pragma unroll
+        for (int r = 0; r < kFusedPrefetch; ++r) {
+            const int i = tid + r * 64 * kFusedWaves;
+            pre[r] = i < TAB2 ? src[i] : double2{0.0, 0.0};
+        }
     }
-    // this lane's unit and the units of the wave's tiles
+    // this lane's unit
     const int mi = 64 * wave + lane;
     const int mwl = mi % WB, ml = mi / WB;
     const bool mvalid = ml < L && w0 + mwl < W;
     const int64_t mu = mvalid ? (int64_t)ml * W + w0 + mwl : 0;
-    int64_t uoff[NT];
+    const double tau = mvalid ? a.theta[(int64_t)a.row_tau[0] * a.U + mu] : 1.0;
+    NGRTD_PROBE(1);
+    const double th = mvalid ? unit_logp_theta(ua, mu, ml) : 0.0;
+    NGRTD_PROBE(2);
+    if (a.cheb) {
+        double2* dst = reinterpret_cast<double2*>(cheb);
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-        const int i = (wave * NT + t) * 16 + col;
-        const int wl = i % WB, l = i / WB;
-        uoff[t] = (l < L && w0 + wl < W) ? (int64_t)l * W + w0 + wl : 0;
+        for (int r = 0; r < kFusedPrefetch; ++r) {
+            const int i = tid + r * 64 * kFusedWaves;
+            if (i < TAB2) dst[i] = pre[r];
+        }
     }
+    double cx = 0.0;
+    const int cpc = a.cheb ? cheb_piece(tau, cx) : -1;
+    const bool exact = __any(cpc < 0);                    // wave-uniform
     __syncthreads();
-    const bool rtd_first = wave < kFusedWaves / 2;
-    double th = 0.0;
-    if (!rtd_first && mvalid) th = unit_logp_theta(ua, mu, ml);
-    MfmaWave<C> mw;
-    mw.init(a, uoff);
-    mw.steps(lds, a.nsteps);
-    double y[NT][C];
-    mw.finish(a, y);
     double yy[C], bu;
-    mfma_pick_tile<C>(y, mw.beta, yy, bu);       // tile tq holds this lane's unit
+    if (exact) {
+        int64_t uoff[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int i = (wave * NT + t) * 16 + col;
+            const int wl = i % WB, l = i / WB;
+            uoff[t] = (l < L && w0 + wl < W) ? (int64_t)l * W + w0 + wl : 0;
+        }
+        MfmaWave<C> mw;
+        mw.init(a, uoff);
+        NGRTD_PROBE(3);
+        mw.steps(a.frag, a.nsteps);
+        NGRTD_PROBE(4);
+        double y[NT][C];
+        mw.finish(a, y);
+        mfma_pick_tile<C>(y, mw.beta, yy, bu);   // tile tq holds this lane's unit
+    } else {
+        NGRTD_PROBE(3);
+        bu = 1. / tau;
+        cheb_sums<C>(cheb + cpc * (kChebN * CP), CP, cx, yy);
+        NGRTD_PROBE(4);
+    }
+    NGRTD_PROBE(5);
     double like = 0.0;
     if (mvalid) {
         double conc[kMaxTracer];
         mfma_unit_conc<C>(a, mu, bu, yy, conc);
         like = unit_like_rtd(ua, mu, ml, conc);
-        if (rtd_first) th = unit_logp_theta(ua, mu, ml);
     }
     part[mi] = th + like;
+    NGRTD_PROBE(6);
     __syncthreads();
-    if (tid < WB && w0 + tid < W) {
+    if (WB <= 64 && (WB & (WB - 1)) == 0) {
+        if (wave == 0) {
+            const int G = 64 / WB;                        // well groups (power of two)
+            const int wl = lane % WB, g = lane / WB;
+            double tot = 0.0;
+            for (int l = g; l < L; l += G) tot += part[l * WB + wl];
+            for (int off = WB; off < 64; off <<= 1) tot += __shfl_xor(tot, off);
+            if (g == 0 && w0 + wl < W) logp[w0 + wl] = tot;
+        }
+    } else if (tid < WB && w0 + tid < W) {
         double tot = part[tid];
         for (int l = 1; l < L; ++l) tot += part[l * WB + tid];
         logp[w0 + tid] = tot;
     }
+    NGRTD_PROBE(7);
 }
 
 // logp[w] = sum over wells of ulogp[l*W + w]: 16 fixed well groups per walker summed

@@ -58,15 +58,15 @@ NGRTD_HD double vapor_pressure(double T) {
 constexpr double kLn10 = 2.302585092994045684;
 NGRTD_HD double exp10_fast(double y) { return fexp(y * kLn10); }
 NGRTD_HD double lapse_rate_fast(double E) {
-    return fexp(5.2561 * flog(1 - .0065 * E / 288.15)) * 0.000101325;
+    // .0065 * E / 288.15 as one multiply by the folded constant (<= 1 ulp)
+    return fexp(5.2561 * flog(1 - E * (.0065 / 288.15))) * 0.000101325;
 }
 NGRTD_HD double vapor_pressure_fast(double T) {
     double A, B, C;
     if (T <= 99.0) { A = 8.07131; B = 1730.63; C = 233.426; }
     else           { A = 8.14019; B = 1810.94; C = 244.485; }
-    double P = exp10_fast(A - (B / (C + T)));
-    P = P / 760. * 101325;
-    return P / 1.0e9;
+    // P / 760 * 101325 / 1e9 as one multiply by the folded constant (<= 2 ulp)
+    return exp10_fast(A - (B / (C + T))) * (101325. / 760. / 1.0e9);
 }
 
 // Setchenow salting factor of solubility(), :154-159.  With S = 0 this is exp(0*s) = 1
@@ -199,9 +199,12 @@ NGRTD_HD double st_term(double x, double mu, double sigma, double nu) {
 // (a-1) log x + (b-1) log1p(-x) = log(x^(a-1) (1-x)^(b-1)) -- one log instead of two.
 // ia/ib < 0 selects the general two-log form.
 NGRTD_HD double ipow_small(double v, int k) {
-    double r = 1.0;
-    for (int i = 0; i < k; ++i) r *= v;
-    return r;
+    // k in 0..4 (beta_int on the host): branch-free selects, no loop
+    const double v2 = v * v;
+    const double lo = (k & 1) ? v : 1.0;
+    const double hi = (k & 2) ? v2 : 1.0;
+    const double r = lo * hi;
+    return (k & 4) ? v2 * v2 : r;
 }
 NGRTD_HD double beta_logp_fast(double x, double a, double b, double betaln_ab, int ia, int ib) {
     double lp;
@@ -224,6 +227,7 @@ NGRTD_HD double beta_logp_fast(double x, double a, double b, double betaln_ab, i
 // i.e. 2 logs per block instead of 3 + n, and 2 divisions (1/(y P), 1/nu) instead of n + 3.  log(1 + z) vs log1p(z) differs by < 2^-53 per
 // factor.  Very large z (poor fits: z >= 1e15) take the per-observation log1p path so
 // the product cannot overflow.  hll_sum = sum_j 0.5 log lam_j (host precomputed).
+template <int NMAX>
 NGRTD_HD double st_block(int n, const double* obs, const double* mu, const double* lam, double hll_sum,
                          double nu) {
     const double x = nu / 2.0;
@@ -234,14 +238,18 @@ NGRTD_HD double st_block(int n, const double* obs, const double* mu, const doubl
     const double qp = (Q * y) * iyP;
     const double inu = 1.0 / nu;
     const double c0 = 0.5 * flog(y * qp * qp * (inu * (1.0 / kPi))) + lgamma_half_tail(P * iyP);
+    // unrolled over NMAX constant slots (slots j >= n masked; their loads clamp to n - 1)
     double prod = 1.0;
     bool big = false, ok = nu > 0;
-    for (int j = 0; j < n; ++j) {
-        const double d = obs[j] - mu[j];
-        const double z = lam[j] * (d * d) * inu;
-        prod *= (1.0 + z);
-        big |= !(z < 1.0e15);
-        ok &= lam[j] > 0;
+#pragma unroll
+    for (int j = 0; j < NMAX; ++j) {
+        const int jj = j < n ? j : n - 1;
+        const double d = obs[jj] - mu[j];
+        const double z = lam[jj] * (d * d) * inu;
+        const bool on = j < n;
+        prod *= on ? (1.0 + z) : 1.0;
+        big |= on && !(z < 1.0e15);
+        ok &= !on || lam[jj] > 0;
     }
     double Lg;
     if (!big) {

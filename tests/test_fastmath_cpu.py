@@ -1,4 +1,4 @@
-"""Accuracy of the device math helpers (fexp, flog, lgamma_half_diff), compiled for the
+"""Accuracy of the device math helpers (fexp, flog, fexpm1, lgamma_half_diff), compiled for the
 host from the same headers the gfx950 kernels include (tools/fastmath_host.cpp).
 
 fexp/flog are measured in ulps against 80-bit long double; lgamma_half_diff against
@@ -69,6 +69,22 @@ def test_flog_ulp(host_tool):
     assert got[~nz].max() == 0.0 and got[~nz].min() == 0.0
     sp = host_tool("l", np.array([0.0, -1.0, np.inf, np.nan, -0.0]))
     assert sp[0] == -np.inf and np.isnan(sp[1]) and sp[2] == np.inf and np.isnan(sp[3]) and sp[4] == -np.inf
+
+
+def test_fexpm1_ulp(host_tool):
+    if np.finfo(np.longdouble).nmant < 60:
+        pytest.skip("long double is not 80-bit here")
+    rng = np.random.default_rng(3)
+    x = np.concatenate([rng.uniform(-1, 1, 10000), rng.uniform(-1e-3, 1e-3, 3000), rng.uniform(-50, 50, 10000),
+                        -np.geomspace(1e-3, 1200, 3000), np.geomspace(1e-300, 1e-5, 1000),
+                        rng.uniform(40, 709, 2000), [0.0, -0.0, 0.3465, -0.3466, 40.0, -40.0, 1e-310]])
+    got = host_tool("m", x)
+    ref = np.expm1(x.astype(np.longdouble))
+    nz = ref != 0
+    assert ulp_err(got[nz], ref[nz]).max() <= 2.0
+    assert np.array_equal(got[~nz], x[~nz])
+    sp = host_tool("m", np.array([np.nan, np.inf, -np.inf, 710.0, -1e4]))
+    assert np.isnan(sp[0]) and sp[1] == np.inf and sp[2] == -1.0 and sp[3] == np.inf and sp[4] == -1.0
 
 
 def test_lgamma_half_diff(host_tool):

@@ -251,10 +251,52 @@ def test_mfma_and_valu_paths_agree():
             % os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     out = "/tmp/ngrtd_paths_%d.npy" % os.getpid()
     for extra, mfma in (({"NGRTD_NO_MFMA": "1"}, False), ({"NGRTD_NO_FUSED": "1"}, True),
-                        ({"NGRTD_FUSE": "1", "NGRTD_NO_FUSED": "1"}, True)):
+                        ({"NGRTD_FUSE": "1", "NGRTD_NO_FUSED": "1"}, True), ({"NGRTD_NO_CHEB": "1"}, True)):
         env = dict(os.environ, **extra)
         subprocess.run([sys.executable, "-c", "MFMA = %s; " % mfma + code, out], check=True, env=env, timeout=300)
         b = np.load(out)
         os.remove(out)
         assert close(rt.ravel(), b[:rt.size], 1e-12).all(), extra
         assert close(a, b[rt.size:], 1e-12, 1e-9).all(), extra
+
+
+def test_surrogate_vs_exact_over_tau_range():
+    """The single-launch log-prob evaluates the exponential channel sums from the validated
+    Chebyshev surrogate; waves holding a tau it does not cover (< 1/2, NaN) take the exact
+    matrix-core path.  Walkers spread over tau in [0.05, 1e7] (prior support is [1, 1000]:
+    the likelihood is switched off so every walker's value depends on the convolution) must
+    agree with the exact path (NGRTD_NO_CHEB=1) and with the oracle."""
+    import os
+    import subprocess
+    import sys
+    import oracle.models as om
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+    spec = wl.c4_spec(L=8, N=1200)
+    spec.include_prior = False
+    W = 640
+    th = wl.sample_prior(spec, W, np.random.default_rng(21))
+    taus = np.exp(np.random.default_rng(22).uniform(np.log(0.05), np.log(1e7), (8, W)))
+    taus[:, 64:128] = np.exp(np.random.default_rng(23).uniform(np.log(0.5), np.log(3e5), (8, 64)))
+    th[spec.roles.index("tau1")] = taus
+    th[spec.roles.index("tau1"), 3, 200] = np.nan
+    path = "/tmp/ngrtd_sur_%d.npy" % os.getpid()
+    np.save(path, th)
+    lp = LogProb(spec, max_walkers=W)
+    assert lp.info(W)["surrogate"] == 1
+    got = lp(th, soa=True)
+    code = ("import numpy as np, sys; sys.path.insert(0, %r); from noblegas_rtd_mcmc_amd import workloads as wl;"
+            "from noblegas_rtd_mcmc_amd.engine import LogProb; spec = wl.c4_spec(L=8, N=1200);"
+            "spec.include_prior = False; th = np.load(sys.argv[1]); lp = LogProb(spec, max_walkers=th.shape[2]);"
+            "assert lp.info(th.shape[2])['surrogate'] == 0; np.save(sys.argv[1], lp(th, soa=True))"
+            % os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    subprocess.run([sys.executable, "-c", code, path], check=True, timeout=300,
+                   env=dict(os.environ, NGRTD_NO_CHEB="1"))
+    exact = np.load(path)
+    os.remove(path)
+    assert close(got, exact, 1e-12, 1e-9).all(), np.nonzero(~close(got, exact, 1e-12, 1e-9))
+    assert np.isnan(got[200]) and np.isnan(exact[200])
+    walkers = [0, 65, 100, 127, 300, 639]
+    ref = om.log_prob(spec, th, walkers=walkers)
+    assert close(got[walkers], ref, 1e-12, 1e-9).all(), (got[walkers], ref)
+    lp.close()

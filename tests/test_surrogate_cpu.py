@@ -1,0 +1,108 @@
+"""The piecewise-Chebyshev surrogate of the exponential RTD channel sums (host-only part of
+libngrtd: ngrtd_surrogate_check, no GPU needed).
+
+The log-prob kernel replaces Y_c(tau) = sum_{j>=0} A_c[1+j] exp(-j/tau) -- the exponential
+weights of convolution_integral_utils.py:184 against the decay-folded input series
+(:305-340) -- by a Chebyshev expansion in log(tau).  A plan uses it only when the library's
+own validation bound (5e-14 relative) holds; these tests check that the bound holds for
+the shipped series at both input lengths and for the c4 workload, and evaluate the
+returned coefficients independently in NumPy against a direct float64 sum.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from noblegas_rtd_mcmc_amd import workloads
+
+N_COEF, PIECES = 18, 27
+U0, S_HI = np.log(0.5), 4.55e-6
+
+
+@pytest.fixture(scope="module")
+def lib():
+    import __graft_entry__ as g
+    g.build()
+    from noblegas_rtd_mcmc_amd import _lib
+    return _lib.load()
+
+
+def channels(tracers):
+    """Channel columns as the plan builds them (ngrtd.hip build_table)."""
+    cols = []
+    for t in tracers:
+        s = t.series
+        tp = np.arange(s.n, dtype=np.float64) + s.dtp
+        tp[0] = 1e-5 + s.dtp
+        lam = -np.log(0.5) / t.t_half if t.t_half else 0.0
+        e = np.exp(-lam * tp)
+        d = (1 - e) if t.rad_accum == "3He" else e
+        hasB = t.rad_accum in ("4He", "SF6")
+        if np.any(s.c_by_age != 0) or not hasB:
+            cols.append(s.c_by_age * d)
+        if hasB:
+            cols.append(s.idx_by_age * d)
+    return np.ascontiguousarray(cols, dtype=np.float64)
+
+
+def check(lib, cols):
+    Cn, N = cols.shape
+    CP = (Cn + 1) & ~1
+    coef = np.zeros(PIECES * N_COEF * CP)
+    err = C.c_double()
+    dp = C.POINTER(C.c_double)
+    assert lib.ngrtd_surrogate_check(cols.ctypes.data_as(dp), Cn, N, coef.ctypes.data_as(dp), C.byref(err)) == 0
+    return err.value, coef.reshape(PIECES, N_COEF, CP)
+
+
+def numpy_surrogate(coef, tau, c):
+    u = np.log(tau)
+    t = (u - U0) * 2.0
+    if t >= PIECES - 1:
+        p, x = PIECES - 1, (1.0 / tau) * (2.0 / S_HI) - 1.0
+    else:
+        p = max(int(np.floor(t)), 0)
+        x = (u - (U0 + (p + 0.5) * 0.5)) * 4.0
+    return np.polynomial.chebyshev.chebval(x, coef[p, :, c])
+
+
+@pytest.mark.parametrize("n", [1200, 25256])
+def test_shipped_series_within_bound(lib, n):
+    trs = [workloads.tracer(name, n) for name in ("CFC11", "CFC12", "CFC113", "SF6", "H3", "He4_ter")]
+    err, coef = check(lib, channels(trs))
+    assert err <= 5e-14, err
+    cols = channels(trs)
+    j = np.arange(n - 1, dtype=np.float64)
+    for tau in (0.5, 0.731, 1.0, 7.3, 37.3, 333.3, 1000.0, 2.2e5, 3e6, np.inf):
+        q = np.exp(-j / tau)
+        for c in range(cols.shape[0]):
+            ref = np.dot(cols[c, 1:], q)
+            scale = np.dot(np.abs(cols[c, 1:]), q)
+            assert abs(numpy_surrogate(coef, tau, c) - ref) <= 1e-13 * scale, (tau, c)
+
+
+def test_c4_workload_series_within_bound(lib):
+    spec = workloads.c4_spec(L=4)
+    err, _ = check(lib, channels(spec.rtd.tracers))
+    assert err <= 5e-14, err
+
+
+def test_positive_rough_series_within_bound(lib):
+    """Non-negative columns of any roughness stay within the bound: each term exp(-j/tau)
+    is analytic in log(tau) with |.| <= 1 in the strip |Im log tau| < pi/2, whatever A is."""
+    rng = np.random.default_rng(5)
+    col = 10.0 ** rng.uniform(-8, 8, 1200)
+    err, _ = check(lib, np.ascontiguousarray(col[None, :]))
+    assert err <= 5e-14, err
+
+
+def test_signed_or_nonfinite_series_is_rejected(lib):
+    """Mixed signs (no relative bound) or NaN/inf entries: the plan keeps the exact path."""
+    rng = np.random.default_rng(6)
+    col = rng.standard_normal(1200)
+    err, _ = check(lib, np.ascontiguousarray(col[None, :]))
+    assert not err <= 5e-14
+    col = np.abs(col)
+    col[7] = np.nan
+    err, _ = check(lib, np.ascontiguousarray(col[None, :]))
+    assert not err <= 5e-14

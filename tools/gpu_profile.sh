@@ -1,7 +1,7 @@
 #!/bin/bash
-# One GPU session: parity tests, bench, rocprofv3 kernel stats of the bench command, PMC
-# passes (FETCH_SIZE, WRITE_SIZE, SQ busy/MFMA counters -- each in its own pass, never with
-# a trace domain).  Outputs under gpurun_out/$TAG/; tools/profile_summary.py condenses them.
+# One GPU session: parity tests, bench, rocprofv3 kernel stats of the bench command, then
+# PMC passes (each group in its own rocprofv3 run, never combined with a trace domain).
+# Outputs under gpurun_out/$TAG/; tools/profile_summary.py condenses them into profiles/.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${1:-run}
@@ -16,10 +16,16 @@ step bench
 timeout -k 10 300 python bench.py --steps 400 --warmup 40 --cpu-seconds 15 > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed rc=$?" >> $OUT/steps.log; exit 1; }
 step rocprof-stats
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o stats -- python3 bench.py --steps 400 --warmup 40 --no-cpu-baseline > $OUT/prof_bench.json 2> $OUT/prof.err || { echo "rocprof failed rc=$?" >> $OUT/steps.log; exit 1; }
-step pmc-fetch
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o fetch -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > /dev/null 2> $OUT/pmc_fetch.err || { echo "pmc fetch failed rc=$?" >> $OUT/steps.log; exit 1; }
-step pmc-write
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o write -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > /dev/null 2> $OUT/pmc_write.err || { echo "pmc write failed rc=$?" >> $OUT/steps.log; exit 1; }
-step pmc-sq
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $OUT/pmc_sq -o sq -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > /dev/null 2> $OUT/pmc_sq.err || { echo "pmc sq failed rc=$?" >> $OUT/steps.log; exit 1; }
+i=0
+for grp in "FETCH_SIZE" "WRITE_SIZE" \
+           "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS" \
+           "SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64" \
+           "SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_FLOPS_FP64_TRANS SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64" \
+           "SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY" \
+           "SQ_INSTS_MFMA SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_CVT" \
+           "GRBM_GUI_ACTIVE SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT"; do
+  i=$((i+1))
+  step "pmc$i $grp"
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d $OUT/pmc$i -o pmc$i -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > /dev/null 2> $OUT/pmc$i.err || { echo "pmc$i failed rc=$?" >> $OUT/steps.log; exit 1; }
+done
 step done

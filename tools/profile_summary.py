@@ -23,14 +23,22 @@ def main(src, prefix):
         shutil.copy(stats, prefix + "_kernel_stats.csv")
     if os.path.exists(os.path.join(src, "bench.json")):
         shutil.copy(os.path.join(src, "bench.json"), prefix + "_bench.json")
-    res = summarize([os.path.join(src, d) for d in ("pmc_fetch", "pmc_write", "pmc_sq")])
+    import glob
+    res = summarize(sorted(glob.glob(os.path.join(src, "pmc*"))))
     out = {}
     for k, d in res.items():
         if "ngrtd" not in k:
             continue
         e = {c: v for c, v in d.items()}
         if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+            # FETCH_SIZE reports half the bytes for 8- and 16-byte-per-lane loads on gfx950
+            # (MI355X_MICROARCH.md 'HBM'; tools/fetch_calib.hip: profiles/r01_fetch_calib.txt)
             e["hbm_bytes_per_launch"] = (2.0 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024.0
+        if "SQ_INSTS_VALU_FLOPS_FP64" in d:
+            # FP64 FLOPs per launch: VALU FP64 FLOPs (fma = 2, counted per lane by the SQ) +
+            # MFMA FP64 (MOPS x 512 per 16x16x4 op: the counter unit is 512 FLOP)
+            e["fp64_flop_per_launch"] = (d["SQ_INSTS_VALU_FLOPS_FP64"] + d.get("SQ_INSTS_VALU_FLOPS_FP64_TRANS", 0.0)
+                                         + 512.0 * d.get("SQ_INSTS_VALU_MFMA_MOPS_F64", 0.0))
         out[k] = e
     with open(prefix + "_pmc.json", "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
