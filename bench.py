@@ -26,6 +26,7 @@ sys.path.insert(0, REPO)
 METRIC = "log-likelihood evals/sec (CE + RTD-conv), 2048 walkers, 1/2/4/8 MI355X"
 FP64_MFMA_PEAK = 78.6e12     # dense FP64 matrix peak, 256 CU x 4 SIMD x 32 FLOP/clk x 2.4 GHz
                              # (tools/ubench_fp64.hip measures 78.3: profiles/r01_ubench_fp64.txt)
+FP64_VALU_PEAK = 38.3e12     # v_fma_f64 throughput measured by tools/ubench_fp64.hip (profiles/r01_ubench_fp64.txt)
 HBM_PEAK = 8.0e12            # MI355X_MICROARCH.md chip table
 PMC_SUMMARY = "r01_pmc.json"
 
@@ -148,28 +149,31 @@ def main():
         N = spec.rtd.n_ages
         # dominant kernel: the single-launch log-prob kernel when the plan uses it
         kname = "fused" if ks["fused"][1] else "rtd"
-        rtd_ms = ks[kname][0] / max(ks[kname][1], 1)
-        # algorithmic work of the RTD kernel per launch: one FMA (2 FLOP) per
-        # (unit, channel, age >= 1) -- the Horner evaluation (DESIGN.md 'Roofline')
-        flops = 2.0 * U * C * (N - 1)
-        achieved = flops / (rtd_ms * 1e-3)
-        # algorithmic HBM bytes of the same launch: every theta row read once, plus the
-        # output (logp per walker for the single-launch kernel; concentrations otherwise)
-        # and the MFMA fragment table once per block (L2-served after the first block)
-        theta_bytes = U * 8.0 * len(spec.roles)
-        out_bytes = W * 8.0 if kname == "fused" else U * 8.0 * len(spec.rtd.tracers)
-        hbm_bytes = theta_bytes + out_bytes + info["nsteps"] * max(info["mfma_rows"], 1) * 512.0
-        # HBM bytes per launch from the committed PMC summary of the same command
-        # (tools/gpu_profile.sh + tools/profile_summary.py; FETCH_SIZE doubled per the
-        # MI355X guide, plus WRITE_SIZE); null when no summary for this kernel is committed
-        traffic = None
-        pmc = os.path.join(REPO, "profiles", PMC_SUMMARY)
-        if os.path.exists(pmc):
-            with open(pmc) as f:
+        kms = ks[kname][0] / max(ks[kname][1], 1)
+        kfull = {"fused": "logp_fused_kernel", "rtd": "rtd_exp_mfma_kernel" if info["mfma_rows"] else "rtd_conc_kernel"}[kname]
+        # committed PMC summary of the same command (tools/gpu_profile.sh -> tools/profile_summary.py)
+        pmc = {}
+        path = os.path.join(REPO, "profiles", PMC_SUMMARY)
+        if os.path.exists(path):
+            with open(path) as f:
                 for k, e in json.load(f).items():
-                    if (("logp_fused_kernel" if kname == "fused" else "rtd_exp_mfma_kernel") in k
-                            and "hbm_bytes_per_launch" in e):
-                        traffic = e["hbm_bytes_per_launch"]
+                    if kfull in k:
+                        pmc = e
+        traffic = pmc.get("hbm_bytes_per_launch")   # FETCH_SIZE x 2 (calibrated) + WRITE_SIZE
+        if info.get("surrogate"):
+            # FP64 work of the launch: PMC-counted FP64 FLOPs per (walker, well) unit of this
+            # kernel (SQ_INSTS_VALU_FLOPS_FP64 x 64 lanes, fma = 2) x units
+            fpu = pmc.get("fp64_flop_per_unit")
+            flops = fpu * U if fpu else None
+            flop_src = "PMC fp64_flop_per_unit %s x %d units (profiles/%s)" % (
+                "%.1f" % fpu if fpu else "n/a", U, PMC_SUMMARY)
+        else:
+            # exact matrix-core path: one FMA (2 FLOP) per (unit, channel, age >= 1)
+            flops = 2.0 * U * C * (N - 1)
+            flop_src = "2 * units * channels * (N - 1) (matrix-core Horner)"
+        achieved = flops / (kms * 1e-3) if flops else None
+        # algorithmic HBM bytes of the same launch: every theta row read once + logp out
+        hbm_bytes = U * 8.0 * len(spec.roles) + (W * 8.0 if kname == "fused" else U * 8.0 * len(spec.rtd.tracers))
         evals = W * world * args.steps
         line = {
             "metric": METRIC,
@@ -188,13 +192,15 @@ def main():
                                    "RTD exponential, N=%d ages)" % (W, args.wells, N),
                        "walkers_per_gpu": W, "wells": args.wells, "gases": 5, "tracers": 5, "ages": N,
                        "parallelism": "walker blocks per GPU + RCCL all-gather of logp" if world > 1 else "single GPU"},
-            "roofline": {"bound": "mfma", "achieved": achieved / 1e12, "peak": FP64_MFMA_PEAK / 1e12,
-                         "unit": "TFLOP/s", "frac": achieved / FP64_MFMA_PEAK, "traffic": traffic,
-                         "kernel": ("logp_fused_kernel" if kname == "fused" else
-                                    "rtd_exp_mfma_kernel" if info["mfma_rows"] else "rtd_conc_kernel"), "kernel_ms": rtd_ms, "flop_per_launch": flops,
-                         "hbm": {"algorithmic_bytes": hbm_bytes, "achieved_GBps": hbm_bytes / (rtd_ms * 1e-3) / 1e9,
-                                 "peak_GBps": HBM_PEAK / 1e9,
-                                 "frac": hbm_bytes / (rtd_ms * 1e-3) / HBM_PEAK}},
+            "roofline": {"bound": "mfma", "achieved": achieved / 1e12 if achieved else None,
+                         "peak": FP64_MFMA_PEAK / 1e12, "unit": "TFLOP/s",
+                         "frac": achieved / FP64_MFMA_PEAK if achieved else None, "traffic": traffic,
+                         "kernel": kfull, "kernel_ms": kms, "flop_per_launch": flops, "flop_source": flop_src,
+                         "pipe": "FP64 (gfx950 FP64 VALU and MFMA share one pipe; the surrogate path is VALU)",
+                         "fp64_valu_peak_measured": FP64_VALU_PEAK / 1e12,
+                         "frac_of_fp64_valu_peak": achieved / FP64_VALU_PEAK if achieved else None,
+                         "hbm": {"algorithmic_bytes": hbm_bytes, "achieved_GBps": hbm_bytes / (kms * 1e-3) / 1e9,
+                                 "peak_GBps": HBM_PEAK / 1e9, "frac": hbm_bytes / (kms * 1e-3) / HBM_PEAK}},
             "host_staged_value": host_staged,
             "kernels_ms": {k: v[0] / max(v[1], 1) for k, v in ks.items()},
             "geometry": info,

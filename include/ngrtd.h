@@ -229,8 +229,8 @@ int ngrtd_plan_info(ngrtd_plan* plan, int64_t W, int64_t* info, int32_t n);
  * [NGRTD_CHEB_PIECES][NGRTD_CHEB_N][(C+1)&~1]; *max_rel_err: max |surrogate - exact| /
  * sum_j |A_c[1+j]| exp(-j/tau) over the validation points.  Plans use the surrogate only
  * when this is <= 5e-14. */
-#define NGRTD_CHEB_N 18
-#define NGRTD_CHEB_PIECES 27
+#define NGRTD_CHEB_N 12
+#define NGRTD_CHEB_PIECES 53
 int ngrtd_surrogate_check(const double* cols, int32_t C, int64_t N, double* coef, double* max_rel_err);
 
 #ifdef __cplusplus

@@ -256,7 +256,7 @@ static double cheb_build(const std::vector<std::vector<double>>& cols, int C, in
                 const long double xk = cosl(PI * (k + 0.5L) / n);
                 long double sv;
                 if (p < kChebLogPieces) {
-                    const long double u = (long double)kChebU0 + (p + 0.5L) * 0.5L + 0.25L * xk;
+                    const long double u = (long double)kChebU0 + (p + 0.5L) * kChebW + 0.5L * kChebW * xk;
                     sv = expl(-u);
                 } else {
                     sv = 0.5L * (long double)kChebSHi * (1.0L + xk);
@@ -279,7 +279,7 @@ static double cheb_build(const std::vector<std::vector<double>>& cols, int C, in
             double tau;
             if (p < kChebLogPieces) {
                 const long double t = (i == 0) ? p : (i == M + 1) ? p + 1 - 1e-12L : p + (i - 0.5L) / M;
-                tau = (double)expl((long double)kChebU0 + 0.5L * t);
+                tau = (double)expl((long double)kChebU0 + (long double)kChebW * t);
             } else {
                 const long double sv = (long double)kChebSHi * (i / (long double)(M + 1));
                 tau = (sv == 0.0L) ? HUGE_VAL : (double)(1.0L / sv);
@@ -881,6 +881,31 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
         u.rnu_betaln = host_betaln(d->rtd_nu_a, d->rtd_nu_b);
         beta_int(d->rtd_nu_a, d->rtd_nu_b, &u.rnu_ia, &u.rnu_ib);
         beta_int(d->thalf_a, d->thalf_b, &u.th_ia, &u.th_ib);
+    }
+    // Beta-prior slots (beta_block): exponents a-1, b-1 (+1 each with the logodds Jacobian)
+    // split into integer parts (0..7, one shared product) and non-integer coefficients
+    {
+        const bool jac = d->flags & NGRTD_WANT_JACOBIAN;
+        auto add_beta = [&](int row, double A, double B) {
+            const int i = u.bt_n++;
+            u.bt_row[i] = row;
+            const double ca = (A - 1) + (jac ? 1.0 : 0.0), cb = (B - 1) + (jac ? 1.0 : 0.0);
+            const bool ia_ok = ca >= 0 && ca <= 7 && ca == std::floor(ca);
+            const bool ib_ok = cb >= 0 && cb <= 7 && cb == std::floor(cb);
+            u.bt_ia[i] = ia_ok ? (int)ca : 0; u.bt_fa[i] = ia_ok ? 0.0 : ca;
+            u.bt_ib[i] = ib_ok ? (int)cb : 0; u.bt_fb[i] = ib_ok ? 0.0 : cb;
+            u.bt_betaln += host_betaln(A, B);
+        };
+        u.bt_n = 0; u.bt_betaln = 0.0;
+        if (d->ce_enabled) {
+            const int rows[5] = {ri[NGRTD_ROLE_AE_BETA], ri[NGRTD_ROLE_F_BETA], ri[NGRTD_ROLE_E_BETA],
+                                 ri[NGRTD_ROLE_B_BETA], ri[NGRTD_ROLE_NU_CE_BETA]};
+            for (int i = 0; i < 5; ++i) add_beta(rows[i], d->ce_beta_a[i], d->ce_beta_b[i]);
+        }
+        if (d->rtd_enabled) {
+            add_beta(ri[NGRTD_ROLE_NU_RTD_BETA], d->rtd_nu_a, d->rtd_nu_b);
+            if (ri[NGRTD_ROLE_THALF_BETA] >= 0) add_beta(ri[NGRTD_ROLE_THALF_BETA], d->thalf_a, d->thalf_b);
+        }
     }
     HIP_TRY(ctx, p->ulogp.ensure((size_t)Umax * sizeof(double)));
     u.ulogp = p->ulogp.d();

@@ -7,6 +7,7 @@ namespace ngrtd {
 constexpr int kMaxChan = 8;     // RTD channels (tracer A/B tables) per launch
 constexpr int kMaxTracer = 8;
 constexpr int kMaxGas = 5;
+constexpr int kMaxBeta = 7;     // Beta-prior slots per unit (5 CE + RTD nu + thalf_cfc)
 
 enum Mod { MOD_NONE = -1, MOD_PISTON = 0, MOD_EXP = 1, MOD_EPM = 2, MOD_DISP = 3 };
 
@@ -38,12 +39,13 @@ struct RtdArgs {
 };
 
 // Chebyshev surrogate of Y_c(tau) = sum_{j>=0} A_{c,1+j} exp(-j / tau) (the exponential
-// RTD channel sums): piecewise in u = log(tau), kChebLogPieces pieces of width 1/2 from
+// RTD channel sums): piecewise in u = log(tau), kChebLogPieces pieces of width kChebW from
 // tau = 1/2 (u0 = log 1/2), then one piece in s = 1/tau over [0, kChebSHi] for the tail up
 // to tau = inf.  kChebN coefficients per piece and channel.  Built and validated per plan
 // on the host (ngrtd.hip cheb_build); tau < 1/2, NaN take the exact matrix-core path.
-constexpr int kChebN = 18;
-constexpr int kChebLogPieces = 26;                 // u in [u0, u0 + 13]: tau up to 221 206.9
+constexpr int kChebN = 12;
+constexpr double kChebW = 0.25;                    // piece width in log(tau) (exact in binary)
+constexpr int kChebLogPieces = 52;                 // u in [u0, u0 + 13]: tau up to 221 206.9
 constexpr int kChebPieces = kChebLogPieces + 1;
 constexpr double kChebTauLo = 0.5;
 constexpr double kChebU0 = -0.69314718055994530942;   // log(0.5)
@@ -98,6 +100,14 @@ struct UnitArgs {
     double rnu_min, rnu_max, rnu_a, rnu_b, rnu_betaln;
     double* ulogp;          // out [U]
     double* ce_out;         // optional out [G][U] (forward)
+    // All Beta priors of a unit (CE: Ae, F, E, b, nu; RTD: nu, thalf_cfc), with their
+    // logodds Jacobians folded in (beta_block): slot i reads theta row bt_row[i] = x and
+    // contributes x^bt_ia (1-x)^bt_ib to ONE product (integer exponents 0..7) plus
+    // bt_fa log x + bt_fb log(1-x) for non-integer exponents; bt_betaln = sum of betaln.
+    int32_t bt_n;
+    int32_t bt_row[kMaxBeta], bt_ia[kMaxBeta], bt_ib[kMaxBeta];
+    double bt_fa[kMaxBeta], bt_fb[kMaxBeta];
+    double bt_betaln;
 };
 
 }  // namespace ngrtd

@@ -1,82 +1,110 @@
 // ngrtd_fastmath.hpp -- exp/log in float64 for the per-(walker, well) likelihood path.
 //
 // OCML's f64 exp/log are double-double compensated (~0.5 ulp, ~60-80 instructions each);
-// the CE + Student-t + prior block of one unit calls them ~30 times, which made that
-// block VALU-bound.  These are the classic single-precision-free reductions with a short
-// polynomial (Horner on FMAs): max error <= 2 ulp over the full double range
-// (tests/test_fastmath_cpu.py measures it against 80-bit long double), far inside the
-// 1e-12 parity bar.  Special values follow IEEE/libm: exp(NaN)=NaN, exp(+-inf)=inf/0,
-// log(x<0)=NaN, log(0)=-inf, log(inf)=inf, subnormals handled via frexp/ldexp.
+// the CE + Student-t + prior block of one unit calls them ~20 times, and FP64 VALU issue
+// is what bounds the log-prob kernel.  These are table-driven (64-entry 2^(j/64) and
+// 65-entry log(1 + i/64) tables, hi + lo, in LDS) with short Taylor polynomials on FMAs:
+// <= 1 ulp over the full double range (tests/test_fastmath_cpu.py measures against 80-bit
+// long double), far inside the 1e-12 parity bar.  Special values follow IEEE/libm:
+// exp(NaN)=NaN, exp(+-inf)=inf/0, log(x<0)=NaN, log(0)=-inf, log(inf)=inf, subnormals.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <math.h>
+
+#include "ngrtd_fmtab.hpp"
 
 namespace ngrtd {
 
 #define NGRTD_FM __host__ __device__ __forceinline__
 
-NGRTD_FM double fexp(double x) {
-    const double LOG2E = 1.4426950408889634074;
-    const double LN2_HI = 6.93147180369123816490e-01;   // 0x3fe62e42fee00000 (k*LN2_HI exact)
-    const double LN2_LO = 1.90821492927058770002e-10;
-    const double k = rint(x * LOG2E);
-    double r = fma(-k, LN2_HI, x);
-    r = fma(-k, LN2_LO, r);                               // |r| <= ln2/2 + tiny
-    // e^r, Taylor to r^13/13! (truncation < 4e-18 relative at |r| = 0.347)
-    double p = 1.0 / 6227020800.0;
-    p = fma(p, r, 1.0 / 479001600.0);
-    p = fma(p, r, 1.0 / 39916800.0);
-    p = fma(p, r, 1.0 / 3628800.0);
-    p = fma(p, r, 1.0 / 362880.0);
-    p = fma(p, r, 1.0 / 40320.0);
-    p = fma(p, r, 1.0 / 5040.0);
-    p = fma(p, r, 1.0 / 720.0);
-    p = fma(p, r, 1.0 / 120.0);
-    p = fma(p, r, 1.0 / 24.0);
-    p = fma(p, r, 1.0 / 6.0);
-    p = fma(p, r, 0.5);
-    p = fma(p, r, 1.0);
-    p = fma(p, r, 1.0);
-    // 2^k with k in [-1075, 1024]: split so each ldexp factor stays representable
-    const int ki = (int)fmax(fmin(k, 2100.0), -2100.0);
-    const int k1 = ki / 2;
-    double res = ldexp(ldexp(p, k1), ki - k1);
-    if (x > 709.782712893384) res = __builtin_inf();
-    if (x < -745.1332191019412) res = 0.0;
-    return (x != x) ? x : res;
+// Lookup tables (ngrtd_fmtab.hpp): kernels read them from LDS -- every kernel that
+// evaluates fexp/flog (or anything built on them) runs fm_lds_init() and a barrier first --
+// and host code from the constant array, so host and device execute the same arithmetic.
+#if defined(__HIP_DEVICE_COMPILE__)
+__shared__ double g_fm_lds[kFmTabDoubles];
+#define NGRTD_FMT g_fm_lds
+#else
+#define NGRTD_FMT kFmTab
+#endif
+
+__device__ __forceinline__ void fm_lds_init() {
+#if defined(__HIP_DEVICE_COMPILE__)
+    for (int i = threadIdx.x; i < kFmTabDoubles; i += blockDim.x) g_fm_lds[i] = kFmTab[i];
+#endif
 }
 
+NGRTD_FM unsigned fm_hi(double x) {
+    unsigned long long b;
+    __builtin_memcpy(&b, &x, 8);
+    return (unsigned)(b >> 32);
+}
+NGRTD_FM double fm_with_hi(double x, unsigned hi) {
+    unsigned long long b;
+    __builtin_memcpy(&b, &x, 8);
+    b = (b & 0xFFFFFFFFull) | ((unsigned long long)hi << 32);
+    double r;
+    __builtin_memcpy(&r, &b, 8);
+    return r;
+}
+
+// e^x: x = (64 m + j) ln2/64 + r, |r| <= ln2/128; e^x = 2^m 2^(j/64) e^r with 2^(j/64) as
+// hi + lo from the table and e^r - 1 by its Taylor series to r^6/720 (truncation
+// < 3e-20).  <= 1 ulp (tests/test_fastmath_cpu.py).  NaN -> NaN, overflow -> inf,
+// underflow -> 0 / subnormal.
+NGRTD_FM double fexp(double x) {
+    const double L64E = 92.332482616893656;              // 64 / ln 2
+    const double L2HI = 6.93147180369123816490e-01 / 64; // (k ln2/64 exact for |k| < 2^21)
+    const double L2LO = 1.90821492927058770002e-10 / 64;
+    const double xc = fmin(fmax(x, -800.0), 800.0);
+    const double kd = rint(xc * L64E);
+    double r = fma(-kd, L2HI, xc);
+    r = fma(-kd, L2LO, r);
+    double q = 1.0 / 720.0;
+    q = fma(q, r, 1.0 / 120.0);
+    q = fma(q, r, 1.0 / 24.0);
+    q = fma(q, r, 1.0 / 6.0);
+    q = fma(q, r, 0.5);
+    const double p = fma(r * r, q, r);                   // e^r - 1
+    const int k = (int)kd;
+    const int j = k & 63;
+    const double th = NGRTD_FMT[2 * j], tl = NGRTD_FMT[2 * j + 1];
+    const double res = ldexp(th + fma(th, p, tl), k >> 6);
+    return (x == x) ? res : x;
+}
+
+// log x: x = 2^e m, m in [1 - 2^-7, 2 - 2^-7) taken from the bit pattern, c_i = 1 + i/64
+// the nearest table point, r = (m - c_i) / c_i (m - c_i exact, |r| < 2^-7); log x = e ln2 + log c_i +
+// log1p(r), log1p by its Taylor series to r^8/8 (truncation < 2e-20).  <= 1 ulp.
+// log(0) = -inf, log(x < 0) = NaN, log(inf) = inf, subnormals scaled by 2^54 first.
 NGRTD_FM double flog(double x) {
     const double LN2_HI = 6.93147180369123816490e-01;
     const double LN2_LO = 1.90821492927058770002e-10;
-    int e;
-    double m = frexp(x, &e);                              // x = m 2^e, m in [0.5, 1)
-    const bool lo = m < 0.70710678118654752440;
-    m = lo ? m + m : m;                                   // m in [sqrt(1/2), sqrt(2))
-    e = lo ? e - 1 : e;
-    const double f = m - 1.0;
-    const double s = f / (2.0 + f);                       // |s| <= 0.1716
-    const double s2 = s * s;
-    // log(m) = 2 atanh(s) = 2s (1 + s^2/3 + s^4/5 + ...), truncated after s^24/25
-    double q = 1.0 / 25.0;
-    q = fma(q, s2, 1.0 / 23.0);
-    q = fma(q, s2, 1.0 / 21.0);
-    q = fma(q, s2, 1.0 / 19.0);
-    q = fma(q, s2, 1.0 / 17.0);
-    q = fma(q, s2, 1.0 / 15.0);
-    q = fma(q, s2, 1.0 / 13.0);
-    q = fma(q, s2, 1.0 / 11.0);
-    q = fma(q, s2, 1.0 / 9.0);
-    q = fma(q, s2, 1.0 / 7.0);
-    q = fma(q, s2, 1.0 / 5.0);
-    q = fma(q, s2, 1.0 / 3.0);
-    const double hs = s * s2 * q;                         // 2s - f + ... computed as f - 2s*... below
-    // log(m) = 2s + 2 s^3 q  ; write 2s = f - s f (exactly: 2s = f - s*f since s(2+f) = f)
-    const double lm = fma(-s, f, f) + 2.0 * hs;
+    const bool sub = x < 2.2250738585072014e-308;
+    const double xs = sub ? x * 18014398509481984.0 : x;    // 2^54
+    const unsigned hi = fm_hi(xs);
+    const int i64 = (int)(((hi >> 13) & 127) + 1) >> 1;      // nearest 1/64: 0..64
+    // i = 64 (m within 2^-7 of 2) is taken as m/2 next to c_0 = 1 with e + 1, so that
+    // x just below 1 gives log x = log1p(r) with no cancellation against e ln2
+    const bool wrap = i64 == 64;
+    const int i = wrap ? 0 : i64;
+    const int e = (int)((hi >> 20) & 0x7FF) - 1023 - (sub ? 54 : 0) + (wrap ? 1 : 0);
+    const double m = fm_with_hi(xs, (hi & 0x000FFFFFu) | (wrap ? 0x3FE00000u : 0x3FF00000u));
+    const double f = m - (1.0 + (double)i * 0.015625);
+    const double r = f * NGRTD_FMT[2 * kFmExpN + 3 * i];
+    double q = -0.125;
+    q = fma(q, r, 1.0 / 7.0);
+    q = fma(q, r, -1.0 / 6.0);
+    q = fma(q, r, 0.2);
+    q = fma(q, r, -0.25);
+    q = fma(q, r, 1.0 / 3.0);
+    q = fma(q, r, -0.5);
+    const double l1p = fma(r * r, q, r);
     const double ed = (double)e;
-    double res = fma(ed, LN2_HI, fma(ed, LN2_LO, lm));
+    const double t1 = fma(ed, LN2_HI, NGRTD_FMT[2 * kFmExpN + 3 * i + 1]);
+    const double t2 = fma(ed, LN2_LO, NGRTD_FMT[2 * kFmExpN + 3 * i + 2]) + l1p;
+    double res = t1 + t2;
     if (x == 0.0) res = -__builtin_inf();
-    if (x < 0.0 || x != x) res = __builtin_nan("");
+    if (!(x >= 0.0)) res = __builtin_nan("");
     if (x == __builtin_inf()) res = x;
     return res;
 }

@@ -435,24 +435,55 @@ __device__ __forceinline__ void ce_model_s0(const UnitArgs& a, double T, double 
 
 // log-prob contribution of one (walker, well) unit that depends on theta only: priors,
 // CE model + likelihood, RTD priors (the RTD likelihood is added by unit_like_rtd).
+// Sum of all Beta-prior log densities of a unit (and their logodds Jacobians):
+//   sum_i [(a_i-1) log x_i + (b_i-1) log(1-x_i) - betaln(a_i, b_i)]
+// as ONE log of the product of the integer-exponent factors plus one log per non-integer
+// exponent (c4: 4 logs instead of 9).  -inf when any x_i is outside [0, 1] (or NaN), as
+// PyMC3's bound.  A product below 1e-280 (x within ~1e-40 of 0 or 1) redoes the sum
+// term by term so that it cannot underflow.  Differs from the term-by-term sum by a few
+// ulp of the largest log (the logp parity bar is atol 1e-9).
+__device__ __forceinline__ double beta_block(const UnitArgs& a, int64_t u) {
+    double pint = 1.0, lsum = 0.0;
+    bool inb = true;
+    double xs[kMaxBeta];
+#pragma unroll
+    for (int i = 0; i < kMaxBeta; ++i) {
+        if (i < a.bt_n) {
+            const double x = a.theta[(int64_t)a.bt_row[i] * a.U + u];
+            xs[i] = x;
+            inb &= (x >= 0 && x <= 1);
+            pint *= ipow_small(x, a.bt_ia[i]) * ipow_small(1 - x, a.bt_ib[i]);
+            if (a.bt_fa[i] != 0.0) lsum += a.bt_fa[i] * flog(x);
+            if (a.bt_fb[i] != 0.0) lsum += a.bt_fb[i] * flog(1 - x);
+        }
+    }
+    double lint;
+    if (pint >= 1e-280) {
+        lint = flog(pint);
+    } else {
+        lint = 0.0;
+#pragma unroll
+        for (int i = 0; i < kMaxBeta; ++i) {
+            if (i < a.bt_n) {
+                if (a.bt_ia[i]) lint += (double)a.bt_ia[i] * flog(xs[i]);
+                if (a.bt_ib[i]) lint += (double)a.bt_ib[i] * flog(1 - xs[i]);
+            }
+        }
+    }
+    return inb ? (lint + lsum) - a.bt_betaln : kNegInf;
+}
+
 __device__ __forceinline__ double unit_logp_theta(const UnitArgs& a, int64_t u, int l) {
     const bool want_like = a.flags & NGRTD_WANT_LIKE;
     const bool want_prior = a.flags & NGRTD_WANT_PRIOR;
     const bool jac = a.flags & NGRTD_WANT_JACOBIAN;
     double lp = 0.0;
+    if (want_prior) lp += beta_block(a, u);
     if (a.ce_on) {
         double p[6];
 #pragma unroll
         for (int i = 0; i < 6; ++i) p[i] = a.theta[(int64_t)a.row_ce[i] * a.U + u];
-        if (want_prior) {
-            lp += beta_logp_fast(p[0], a.ce_ba[0], a.ce_bb[0], a.ce_betaln[0], a.ce_bia[0], a.ce_bib[0]);
-            lp += beta_logp_fast(p[1], a.ce_ba[1], a.ce_bb[1], a.ce_betaln[1], a.ce_bia[1], a.ce_bib[1]);
-            lp += beta_logp_fast(p[2], a.ce_ba[2], a.ce_bb[2], a.ce_betaln[2], a.ce_bia[2], a.ce_bib[2]);
-            lp += normal_logp(p[3], a.m_mu, a.m_tau, a.m_log_tau_2pi);
-            lp += beta_logp_fast(p[4], a.ce_ba[3], a.ce_bb[3], a.ce_betaln[3], a.ce_bia[3], a.ce_bib[3]);
-            lp += beta_logp_fast(p[5], a.ce_ba[4], a.ce_bb[4], a.ce_betaln[4], a.ce_bia[4], a.ce_bib[4]);
-            if (jac) lp += jac_logodds(p[0]) + jac_logodds(p[1]) + jac_logodds(p[2]) + jac_logodds(p[4]) + jac_logodds(p[5]);
-        }
+        if (want_prior) lp += normal_logp(p[3], a.m_mu, a.m_tau, a.m_log_tau_2pi);
         if (want_like || a.ce_out) {
             // noble_gas_mcmc.py:229-250 parameter mapping, then ce_exc_wrapper (:205-213)
             const double Emin = a.ce_Emin[l];
@@ -472,11 +503,9 @@ __device__ __forceinline__ double unit_logp_theta(const UnitArgs& a, int64_t u, 
     }
     if (a.rtd_on) {
         const double tau1 = a.theta[(int64_t)a.row_tau1 * a.U + u];
-        const double nub = a.theta[(int64_t)a.row_nu * a.U + u];
         if (want_prior) {
             lp += uniform_logp(tau1, a.tau1_lo, a.tau1_hi, a.tau1_nlw);
-            lp += beta_logp_fast(nub, a.rnu_a, a.rnu_b, a.rnu_betaln, a.rnu_ia, a.rnu_ib);
-            if (jac) lp += jac_interval(tau1, a.tau1_lo, a.tau1_hi) + jac_logodds(nub);
+            if (jac) lp += jac_interval(tau1, a.tau1_lo, a.tau1_hi);
 #define NGRTD_UNIF(row, lo, hi, nlw)                                                   \
     if (a.row >= 0) {                                                                  \
         const double x = a.theta[(int64_t)a.row * a.U + u];                            \
@@ -491,11 +520,6 @@ __device__ __forceinline__ double unit_logp_theta(const UnitArgs& a, int64_t u, 
             NGRTD_UNIF(row_D2, D2_lo, D2_hi, D2_nlw)
 #undef NGRTD_UNIF
             if (a.row_J >= 0) lp += normal_logp(a.theta[(int64_t)a.row_J * a.U + u], a.J_mu, a.J_tau, a.J_log_tau_2pi);
-            if (a.row_thalf >= 0) {
-                const double x = a.theta[(int64_t)a.row_thalf * a.U + u];
-                lp += beta_logp_fast(x, a.th_a, a.th_b, a.th_betaln, a.th_ia, a.th_ib);
-                if (jac) lp += jac_logodds(x);
-            }
             if (a.row_lamsf6 >= 0) {
                 const double x = a.theta[(int64_t)a.row_lamsf6 * a.U + u];
                 lp += halfnormal_logp(x, a.ls_tau, a.ls_half_log);
@@ -507,11 +531,14 @@ __device__ __forceinline__ double unit_logp_theta(const UnitArgs& a, int64_t u, 
 }
 
 // Student-t likelihood of the unit's K model concentrations (run_age_mcmc_utils.py:292-296)
+// (NMAX: compile-time bound on K -- the single-launch kernel passes its channel count,
+// K <= C since every tracer owns at least one channel)
+template <int NMAX = kMaxTracer>
 __device__ __forceinline__ double unit_like_rtd(const UnitArgs& a, int64_t u, int l, const double* conc) {
     if (!a.rtd_on || !(a.flags & NGRTD_WANT_LIKE)) return 0.0;
     const double nub = a.theta[(int64_t)a.row_nu * a.U + u];
     const double nu = nub * (a.rnu_max - a.rnu_min) + a.rnu_min;
-    return st_block<kMaxTracer>(a.K, a.rtd_obs + l * a.K, conc, a.rtd_lam + l * a.K, a.rtd_hll_sum[l], nu);
+    return st_block<NMAX>(a.K, a.rtd_obs + l * a.K, conc, a.rtd_lam + l * a.K, a.rtd_hll_sum[l], nu);
 }
 
 // full log-prob contribution of one unit (same addition order as the reference's sum)
@@ -521,6 +548,8 @@ __device__ __forceinline__ double unit_logp(const UnitArgs& a, int64_t u, const 
 }
 
 __global__ void __launch_bounds__(256) unit_logp_kernel(const UnitArgs a) {
+    fm_lds_init();
+    __syncthreads();
     const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (u >= a.U) return;
     double conc[kMaxTracer];
@@ -535,6 +564,8 @@ __global__ void __launch_bounds__(256) unit_logp_kernel(const UnitArgs a) {
 __global__ void __launch_bounds__(512) unit_walker_kernel(const UnitArgs a, int32_t WB, int32_t LS,
                                                           double* __restrict__ logp) {
     extern __shared__ __attribute__((aligned(16))) double part[];   // [LS][WB]
+    fm_lds_init();
+    __syncthreads();
     const int wl = threadIdx.x % WB, l = threadIdx.x / WB;
     const int64_t w = (int64_t)blockIdx.x * WB + wl;
     double s = 0.0;
@@ -652,7 +683,7 @@ struct MfmaWave {
 __host__ __device__ __forceinline__ int cheb_piece(double tau, double& x) {
     if (!(tau >= kChebTauLo)) return -1;
     const double u = flog(tau);
-    const double t = (u - kChebU0) * 2.0;            // piece width 1/2
+    const double t = (u - kChebU0) * (1.0 / kChebW);
     if (t >= (double)kChebLogPieces) {
         const double sv = 1.0 / tau;
         x = sv * (2.0 / kChebSHi) - 1.0;
@@ -660,8 +691,8 @@ __host__ __device__ __forceinline__ int cheb_piece(double tau, double& x) {
     }
     int p = (int)floor(t);
     p = p < 0 ? 0 : p;
-    const double mid = kChebU0 + ((double)p + 0.5) * 0.5;
-    x = (u - mid) * 4.0;
+    const double mid = kChebU0 + ((double)p + 0.5) * kChebW;
+    x = (u - mid) * (2.0 / kChebW);
     return p;
 }
 
@@ -672,7 +703,7 @@ __host__ __device__ __forceinline__ void cheb_sums(const double* __restrict__ pc
     double b1[C], b2[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) { b1[c] = 0.0; b2[c] = 0.0; }
-#pragma unroll 3
+#pragma unroll
     for (int k = kChebN - 1; k >= 1; --k) {
         const double* row = pc + k * CP;
 #pragma unroll
@@ -746,6 +777,8 @@ __global__ void __launch_bounds__(64 * mfma_waves(C)) rtd_exp_mfma_kernel(const 
     const int col = lane & 15, tq = lane >> 4;
     const int64_t u0 = ((int64_t)blockIdx.x * NW + wave) * (16 * NT);
     const int64_t Umax = a.U - 1;
+    fm_lds_init();
+    __syncthreads();
     int64_t uoff[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -797,7 +830,7 @@ __global__ void __launch_bounds__(64 * mfma_waves(C)) rtd_exp_mfma_kernel(const 
 // Both orders are fixed (deterministic, no atomics).
 constexpr int kFusedWaves = 8;
 constexpr int kFusedUnits = 64 * kFusedWaves;
-constexpr int kFusedPrefetch = 3;   // double2 per thread: covers kChebPieces*kChebN*6 doubles
+constexpr int kFusedPrefetch = 4;   // double2 per thread: covers kChebPieces*kChebN*6 doubles
 
 template <int C>
 __global__ void __launch_bounds__(64 * kFusedWaves) logp_fused_kernel(const RtdArgs a, const UnitArgs ua,
@@ -838,6 +871,8 @@ __global__ void __launch_bounds__(64 * kFusedWaves) logp_fused_kernel(const RtdA
     const bool mvalid = ml < L && w0 + mwl < W;
     const int64_t mu = mvalid ? (int64_t)ml * W + w0 + mwl : 0;
     const double tau = mvalid ? a.theta[(int64_t)a.row_tau[0] * a.U + mu] : 1.0;
+    fm_lds_init();                                        // fexp/flog tables
+    __syncthreads();
     NGRTD_PROBE(1);
     const double th = mvalid ? unit_logp_theta(ua, mu, ml) : 0.0;
     NGRTD_PROBE(2);
@@ -881,7 +916,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves) logp_fused_kernel(const RtdA
     if (mvalid) {
         double conc[kMaxTracer];
         mfma_unit_conc<C>(a, mu, bu, yy, conc);
-        like = unit_like_rtd(ua, mu, ml, conc);
+        like = unit_like_rtd<C>(ua, mu, ml, conc);
     }
     part[mi] = th + like;
     NGRTD_PROBE(6);

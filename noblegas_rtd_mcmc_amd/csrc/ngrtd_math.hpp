@@ -199,12 +199,12 @@ NGRTD_HD double st_term(double x, double mu, double sigma, double nu) {
 // (a-1) log x + (b-1) log1p(-x) = log(x^(a-1) (1-x)^(b-1)) -- one log instead of two.
 // ia/ib < 0 selects the general two-log form.
 NGRTD_HD double ipow_small(double v, int k) {
-    // k in 0..4 (beta_int on the host): branch-free selects, no loop
+    // k in 0..7: branch-free selects, no loop
     const double v2 = v * v;
     const double lo = (k & 1) ? v : 1.0;
     const double hi = (k & 2) ? v2 : 1.0;
     const double r = lo * hi;
-    return (k & 4) ? v2 * v2 : r;
+    return (k & 4) ? r * (v2 * v2) : r;
 }
 NGRTD_HD double beta_logp_fast(double x, double a, double b, double betaln_ab, int ia, int ib) {
     double lp;
@@ -225,8 +225,8 @@ NGRTD_HD double beta_logp_fast(double x, double a, double b, double betaln_ab, i
 //   n * c0 + sum_j 0.5 log lam_j - (nu+1)/2 * log(prod_j (1 + z_j)),
 //   c0 = lgamma((nu+1)/2) - lgamma(nu/2) - 0.5 log(nu pi) in ONE log (see lgamma_half_diff),
 // i.e. 2 logs per block instead of 3 + n, and 2 divisions (1/(y P), 1/nu) instead of n + 3.  log(1 + z) vs log1p(z) differs by < 2^-53 per
-// factor.  Very large z (poor fits: z >= 1e15) take the per-observation log1p path so
-// the product cannot overflow.  hll_sum = sum_j 0.5 log lam_j (host precomputed).
+// factor.  Very large z (z >= 1e38, inf, NaN) take a per-observation log path so the
+// product cannot overflow (the T < 0 sentinel -9999 gives z ~ 1e28: still one log).  hll_sum = sum_j 0.5 log lam_j (host precomputed).
 template <int NMAX>
 NGRTD_HD double st_block(int n, const double* obs, const double* mu, const double* lam, double hll_sum,
                          double nu) {
@@ -248,17 +248,18 @@ NGRTD_HD double st_block(int n, const double* obs, const double* mu, const doubl
         const double z = lam[jj] * (d * d) * inu;
         const bool on = j < n;
         prod *= on ? (1.0 + z) : 1.0;
-        big |= on && !(z < 1.0e15);
+        big |= on && !(z < 1.0e38);      // (1 + 1e38)^8 < DBL_MAX: the product cannot overflow
         ok &= !on || lam[jj] > 0;
     }
     double Lg;
     if (!big) {
         Lg = flog(prod);
     } else {
+        // inf/NaN z or z >= 1e38: one log per factor (log(1 + z) = log1p(z) + O(2^-53))
         Lg = 0.0;
         for (int j = 0; j < n; ++j) {
             const double d = obs[j] - mu[j];
-            Lg += log1p(lam[j] * (d * d) / nu);
+            Lg += flog(1.0 + lam[j] * (d * d) * inu);
         }
     }
     const double v = (double)n * c0 + hll_sum - (nu + 1.0) / 2.0 * Lg;

@@ -15,7 +15,7 @@ import pytest
 
 from noblegas_rtd_mcmc_amd import workloads
 
-N_COEF, PIECES = 18, 27
+N_COEF, PIECES, WIDTH = 12, 53, 0.25
 U0, S_HI = np.log(0.5), 4.55e-6
 
 
@@ -57,12 +57,12 @@ def check(lib, cols):
 
 def numpy_surrogate(coef, tau, c):
     u = np.log(tau)
-    t = (u - U0) * 2.0
+    t = (u - U0) / WIDTH
     if t >= PIECES - 1:
         p, x = PIECES - 1, (1.0 / tau) * (2.0 / S_HI) - 1.0
     else:
         p = max(int(np.floor(t)), 0)
-        x = (u - (U0 + (p + 0.5) * 0.5)) * 4.0
+        x = (u - (U0 + (p + 0.5) * WIDTH)) * (2.0 / WIDTH)
     return np.polynomial.chebyshev.chebval(x, coef[p, :, c])
 
 

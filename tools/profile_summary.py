@@ -25,6 +25,12 @@ def main(src, prefix):
         shutil.copy(os.path.join(src, "bench.json"), prefix + "_bench.json")
     import glob
     res = summarize(sorted(glob.glob(os.path.join(src, "pmc*"))))
+    units = None
+    try:
+        with open(os.path.join(src, "bench.json")) as f:
+            units = json.loads(f.read().strip().splitlines()[-1])["geometry"]["units"]
+    except Exception:
+        pass
     out = {}
     for k, d in res.items():
         if "ngrtd" not in k:
@@ -35,10 +41,16 @@ def main(src, prefix):
             # (MI355X_MICROARCH.md 'HBM'; tools/fetch_calib.hip: profiles/r01_fetch_calib.txt)
             e["hbm_bytes_per_launch"] = (2.0 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024.0
         if "SQ_INSTS_VALU_FLOPS_FP64" in d:
-            # FP64 FLOPs per launch: VALU FP64 FLOPs (fma = 2, counted per lane by the SQ) +
-            # MFMA FP64 (MOPS x 512 per 16x16x4 op: the counter unit is 512 FLOP)
-            e["fp64_flop_per_launch"] = (d["SQ_INSTS_VALU_FLOPS_FP64"] + d.get("SQ_INSTS_VALU_FLOPS_FP64_TRANS", 0.0)
-                                         + 512.0 * d.get("SQ_INSTS_VALU_MFMA_MOPS_F64", 0.0))
+            # FP64 FLOPs per launch.  SQ_INSTS_VALU_FLOPS_FP64 counts per wave instruction
+            # (add/mul = 1, fma = 2: it equals ADD_F64 + MUL_F64 + 2 FMA_F64 of the same
+            # launch), so x 64 lanes; transcendental (v_rcp/v_sqrt...) ops count 1 per lane;
+            # MFMA FP64 adds MOPS x 512 (one 16x16x4 op = 2048 FLOP = 4 MOPS).
+            e["fp64_flop_per_launch"] = 64.0 * (d["SQ_INSTS_VALU_FLOPS_FP64"]
+                                                + d.get("SQ_INSTS_VALU_FLOPS_FP64_TRANS", 0.0)) \
+                + 512.0 * d.get("SQ_INSTS_VALU_MFMA_MOPS_F64", 0.0)
+        if units and "fp64_flop_per_launch" in e:
+            e["units"] = units          # (walker, well) units per launch of the profiled command
+            e["fp64_flop_per_unit"] = e["fp64_flop_per_launch"] / units
         out[k] = e
     with open(prefix + "_pmc.json", "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
