@@ -104,28 +104,46 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    # which kernels does one step launch? (one profiled step after the warm-up)
+    lp.ctx.set_profiling(True)
+    lp.kernel_stats(reset=True)
+    step()
+    lp.ctx.set_profiling(False)
+    kinds = {k for k, v in lp.kernel_stats(reset=True).items() if v[1]}
+    single_kernel = kinds == {"fused"}
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    # timed region.  The kernels of every k-th step are bracketed by HIP events on the
-    # launch stream (read back after the region; no host syncs inside it): the per-kernel
-    # average for the roofline is measured live without an event pair on every launch.
+    # timed region.  Kernel time for the roofline, measured live with HIP events on the
+    # launch stream (torch's current stream, which the plan enqueues on):
+    #  * N = 1: one event pair around the whole region; every launch in it is the
+    #    single-launch log-prob kernel, so region / steps is its average duration
+    #    (back-to-back, as rocprofv3 --kernel-trace sees it);
+    #  * N > 1: the all-gather shares the stream, so the kernels of every k-th step are
+    #    bracketed by their own event pair (read back after the region, no host syncs).
     lp.kernel_stats(reset=True)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev0.record()
     for i in range(args.steps):
-        sample = i % args.event_every == 0
+        sample = (world > 1 or not single_kernel) and i % args.event_every == 0
         if sample:
             lp.ctx.set_profiling(True)
         step()
         if sample:
             lp.ctx.set_profiling(False)
+    ev1.record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     ks = lp.kernel_stats(reset=True)
+    if world == 1 and single_kernel:
+        ks = dict(ks)
+        ks["fused"] = (ev0.elapsed_time(ev1), args.steps)
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
