@@ -222,16 +222,19 @@ int ngrtd_plan_kernel_stats(ngrtd_plan* plan, double* times_ms, int64_t* counts,
 int ngrtd_plan_info(ngrtd_plan* plan, int64_t W, int64_t* info, int32_t n);
 
 /* Host-only (no device needed): build the piecewise-Chebyshev surrogate the exponential
- * log-prob kernel uses for the channel sums Y_c(tau) = sum_{j>=0} A_c[1+j] exp(-j/tau)
- * (the exponential g(tp) of convolution_integral_utils.py:184 times the decay-folded
- * series, :305-340) and validate it against a long-double evaluation of the same sums.
+ * log-prob kernel uses for its channel sums and validate it against a long-double
+ * evaluation of the same sums.  With s = 1/tau and s01 = exp(-(tp_1 - tp_0) s) (tp as in
+ * gen_g_tp, convolution_integral_utils.py:168-174, for dtp = floor(t_samp - C_t.index[-1])):
+ *   Z_c(tau) = s01 sum_{j>=0} A_c[1+j] exp(-j s)      c < C  (exponential g(tp), :184, times
+ *                                                             the decay-folded series, :305-340)
+ *   Z_C(tau) = s01 sum_{j=0}^{N-2} exp(-j s)                  (the normaliser g.sum(), :270)
  * cols: [C][N] channel columns (age order); coef (may be NULL): receives
- * [NGRTD_CHEB_PIECES][NGRTD_CHEB_N][(C+1)&~1]; *max_rel_err: max |surrogate - exact| /
- * sum_j |A_c[1+j]| exp(-j/tau) over the validation points.  Plans use the surrogate only
- * when this is <= 5e-14. */
+ * [NGRTD_CHEB_PIECES][NGRTD_CHEB_N][(C+2)&~1]; *max_rel_err: max |surrogate - exact| / exact
+ * over the validation points.  Plans use the surrogate only when this is <= 5e-14. */
 #define NGRTD_CHEB_N 12
 #define NGRTD_CHEB_PIECES 53
-int ngrtd_surrogate_check(const double* cols, int32_t C, int64_t N, double* coef, double* max_rel_err);
+int ngrtd_surrogate_check(const double* cols, int32_t C, int64_t N, double dtp, double* coef,
+                          double* max_rel_err);
 
 #ifdef __cplusplus
 }

@@ -81,7 +81,7 @@ PROTOTYPES = {
     "ngrtd_forward": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int32]),
     "ngrtd_plan_kernel_stats": (C.c_int, [C.c_void_p, _dp, _i64p, C.c_int32, C.c_int32]),
     "ngrtd_plan_info": (C.c_int, [C.c_void_p, C.c_int64, _i64p, C.c_int32]),
-    "ngrtd_surrogate_check": (C.c_int, [_dp, C.c_int32, C.c_int64, _dp, _dp]),
+    "ngrtd_surrogate_check": (C.c_int, [_dp, C.c_int32, C.c_int64, C.c_double, _dp, _dp]),
 }
 
 

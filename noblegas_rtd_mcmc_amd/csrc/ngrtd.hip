@@ -93,7 +93,7 @@ struct ngrtd_plan {
     ngrtd_model_desc desc{};
     int64_t max_w = 0;
     // device copies of the model data
-    DevBuf ce_obs, ce_sd, ce_emin, rtd_obs, rtd_sd, ce_lam, rtd_lam;
+    DevBuf ce_obs, ce_sd, ce_emin, rtd_obs, rtd_sd, ce_lam, rtd_lam, welldata;
     TableDev table;
     int N = 0;
     double tp0 = 1e-5, dtp = 0.0;
@@ -227,31 +227,35 @@ static int build_table(ngrtd_ctx* ctx, const std::vector<TracerBuild>& trs, Tabl
 
 // ------------------------------------------------- Chebyshev surrogate tables
 static_assert(kChebN == NGRTD_CHEB_N && kChebPieces == NGRTD_CHEB_PIECES, "surrogate geometry vs ngrtd.h");
-// Y_c(s) = sum_{j=0}^{N-2} A_{c,1+j} e^{-j s} (s = 1/tau) in long double: the reference sum
-// the surrogate is fitted to and validated against.  `absval` sums |A| instead (the scale
-// the relative error is measured on, so that cancelling series are judged fairly).
-static long double cheb_exact(const std::vector<double>& A, long double s, bool absval) {
+
+// s01(s) * sum_{j=0}^{N-2} A_{1+j} e^{-j s} (s = 1/tau, s01 = e^{-d01 s}) in long double:
+// the function the surrogate is fitted to and validated against.  `ones` sums 1 instead
+// of A (the normaliser Z_G).
+static long double cheb_exact(const std::vector<double>& A, long double s, long double d01, bool ones) {
     const long double q = expl(-s);
     long double y = 0.0L;
-    for (size_t j = A.size(); j-- > 1;) y = y * q + (absval ? fabsl((long double)A[j]) : (long double)A[j]);
-    return y;
+    for (size_t j = A.size(); j-- > 1;) y = y * q + (ones ? 1.0L : (long double)A[j]);
+    return y * expl(-d01 * s);
 }
 
-// Fit kChebN Chebyshev coefficients per piece and channel (interpolation at the Chebyshev
-// nodes of each piece), then validate every piece at 26 points per piece through the same
-// cheb_piece/cheb_sums code the kernel runs.  Returns the max relative error.
-// Channels with negative entries are not expanded (HUGE_VAL): for non-negative columns the
-// error measure below is exactly relative to |Y|, for mixed signs it would not be.
-static double cheb_build(const std::vector<std::vector<double>>& cols, int C, int CP, std::vector<double>& coef) {
-    const int n = kChebN;
+// Fit kChebN Chebyshev coefficients per piece for the C channel functions and the
+// normaliser (interpolation at the Chebyshev nodes of each piece), then validate every
+// piece at 26 points per piece through the same cheb_piece/cheb_sums code the kernel runs.
+// Returns the max relative error.  Channels with negative or non-finite entries are not
+// expanded (HUGE_VAL): for non-negative columns the error is relative to |value|.
+// d01 = tp_1 - tp_0 as the kernel forms it: (1 + dtp) - (1e-5 + dtp).
+static double cheb_build(const std::vector<std::vector<double>>& cols, int C, double d01, std::vector<double>& coef) {
+    const int n = kChebN, CP = cheb_cp(C);
     coef.assign((size_t)kChebPieces * n * CP, 0.0);
     for (int c = 0; c < C; ++c)
         for (double v : cols[c])
             if (!(v >= 0.0) || !std::isfinite(v)) return HUGE_VAL;
     const long double PI = 3.14159265358979323846264338327950288L;
+    const long double dd = d01;
     std::vector<long double> f(n);
     for (int p = 0; p < kChebPieces; ++p) {
-        for (int c = 0; c < C; ++c) {
+        for (int c = 0; c <= C; ++c) {
+            const std::vector<double>& col = cols[c < C ? c : 0];
             for (int k = 0; k < n; ++k) {
                 const long double xk = cosl(PI * (k + 0.5L) / n);
                 long double sv;
@@ -261,7 +265,7 @@ static double cheb_build(const std::vector<std::vector<double>>& cols, int C, in
                 } else {
                     sv = 0.5L * (long double)kChebSHi * (1.0L + xk);
                 }
-                f[k] = cheb_exact(cols[c], sv, false);
+                f[k] = cheb_exact(col, sv, dd, c == C);
             }
             for (int j = 0; j < n; ++j) {
                 long double acc = 0.0L;
@@ -288,12 +292,11 @@ static double cheb_build(const std::vector<std::vector<double>>& cols, int C, in
             const int pp = cheb_piece(tau, x);
             if (pp < 0) return HUGE_VAL;
             const long double sv = 1.0L / (long double)tau;
-            for (int c = 0; c < C; ++c) {
+            for (int c = 0; c <= C; ++c) {
                 double y = 0.0;
                 cheb_sums<1>(coef.data() + (size_t)pp * n * CP + c, CP, x, &y);
-                const long double ex = cheb_exact(cols[c], sv, false);
-                const long double sc = cheb_exact(cols[c], sv, true);
-                const double e = (sc > 0) ? (double)(fabsl((long double)y - ex) / sc) : (y == 0.0 ? 0.0 : HUGE_VAL);
+                const long double ex = cheb_exact(cols[c < C ? c : 0], sv, dd, c == C);
+                const double e = (ex > 0) ? (double)(fabsl((long double)y - ex) / ex) : (y == 0.0 ? 0.0 : HUGE_VAL);
                 if (!(e <= worst)) worst = e;   // NaN -> worst = NaN
             }
         }
@@ -304,12 +307,12 @@ static double cheb_build(const std::vector<std::vector<double>>& cols, int C, in
 // Surrogate for a table whose exponential plan runs logp_fused_kernel.  Used only when the
 // validation bound holds (kChebTol), else the kernel takes the exact matrix-core path.
 constexpr double kChebTol = 5e-14;
-static int cheb_prepare(ngrtd_ctx* ctx, TableDev& tab) {
+static int cheb_prepare(ngrtd_ctx* ctx, TableDev& tab, double d01) {
     static const bool disabled = std::getenv("NGRTD_NO_CHEB") != nullptr;
     tab.cheb_ok = false;
     if (disabled || tab.C < 1 || tab.cols_host.empty() || tab.cols_host[0].size() < 2) return NGRTD_OK;
     std::vector<double> coef;
-    tab.cheb_err = cheb_build(tab.cols_host, tab.C, tab.CP, coef);
+    tab.cheb_err = cheb_build(tab.cols_host, tab.C, d01, coef);
     if (!(tab.cheb_err <= kChebTol)) return NGRTD_OK;
     HIP_TRY(ctx, tab.cheb.ensure(coef.size() * sizeof(double)));
     HIP_TRY(ctx, hipMemcpy(tab.cheb.p, coef.data(), coef.size() * sizeof(double), hipMemcpyHostToDevice));
@@ -318,6 +321,8 @@ static int cheb_prepare(ngrtd_ctx* ctx, TableDev& tab) {
 }
 
 static void set_frag(RtdArgs& a, const TableDev& tab) {
+    for (int c = 0; c < kMaxChan; ++c)
+        a.tab0[c] = (c < tab.C && !tab.cols_host.empty()) ? tab.cols_host[c][0] : 0.0;
     a.frag = tab.frag.d();
     a.nsteps = tab.nsteps;
     a.S_seg = tab.S_seg;
@@ -397,18 +402,36 @@ static void launch_mfma(const RtdArgs& a, const UnitArgs& u, int32_t fuse, hipSt
 // partial sums, and L <= 512 wells.
 // LDS: the 512 per-unit partial sums and the surrogate table (the exact path's fragments
 // are read from global memory: they are needed only by waves with an uncovered tau)
-static size_t fused_lds(const RtdArgs& a) {
-    return (size_t)(kFusedUnits + kChebPieces * kChebN * ((a.C + 1) & ~1)) * sizeof(double);
+// LDS: the 512 per-unit partial sums, the surrogate table and the per-well observation
+// data (ce obs, 1/sd^2, sums of 0.5 log 1/sd^2, E_min; rtd obs, 1/sd^2, sums).
+static size_t fused_lds(const RtdArgs& a, const UnitArgs& u) {
+    const size_t wells = (size_t)u.L * ((u.ce_on ? 2 * u.G + 2 : 0) + (u.rtd_on ? 2 * u.K + 1 : 0));
+    return (size_t)(kFusedUnits + kChebPieces * kChebN * cheb_cp(a.C) + wells) * sizeof(double);
 }
-static bool fused_path(const RtdArgs& a, int L) {
+constexpr size_t kFusedMaxLds = 150 * 1024;
+static bool fused_path(const RtdArgs& a, const UnitArgs& u) {
     static const bool disabled = std::getenv("NGRTD_NO_FUSED") != nullptr;
-    return !disabled && mfma_path(a, a.row_thalf >= 0) && a.C <= 5 && L >= 1 && L <= kFusedUnits &&
-           fused_lds(a) <= 64 * 1024;
+    return !disabled && mfma_path(a, a.row_thalf >= 0) && a.C <= 5 && u.L >= 1 && u.L <= kFusedUnits &&
+           fused_lds(a, u) <= kFusedMaxLds;
 }
+template <int C, bool FULL>
+static void launch_fused_cf(const RtdArgs& a, const UnitArgs& u, int WB, int64_t W, double* logp, hipStream_t st) {
+    static const bool attr = [] {   // dynamic LDS above 64 KiB (many wells) needs the opt-in
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&logp_fused_kernel<C, FULL>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFusedMaxLds);
+        return true;
+    }();
+    (void)attr;
+    hipLaunchKernelGGL((logp_fused_kernel<C, FULL>), dim3((unsigned)cdiv(W, WB)), dim3(64 * kFusedWaves),
+                       fused_lds(a, u), st, a, u, WB, logp);
+}
+// FULL instance: CE + RTD blocks, priors and likelihoods on, no Jacobians (the joint model)
 template <int C>
 static void launch_fused_c(const RtdArgs& a, const UnitArgs& u, int WB, int64_t W, double* logp, hipStream_t st) {
-    hipLaunchKernelGGL(logp_fused_kernel<C>, dim3((unsigned)cdiv(W, WB)), dim3(64 * kFusedWaves), fused_lds(a), st,
-                       a, u, WB, logp);
+    const bool full = u.ce_on && u.rtd_on && (u.flags & NGRTD_WANT_LIKE) && (u.flags & NGRTD_WANT_PRIOR) &&
+                      !(u.flags & NGRTD_WANT_JACOBIAN);
+    if (full) launch_fused_cf<C, true>(a, u, WB, W, logp, st);
+    else launch_fused_cf<C, false>(a, u, WB, W, logp, st);
 }
 static int launch_fused(ngrtd_ctx* ctx, const RtdArgs& a, const UnitArgs& u, int64_t W, int L, double* logp,
                         hipStream_t st) {
@@ -857,7 +880,7 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
         set_frag(a, p->table);
         a.cheb = nullptr;
         if (a.mod[0] == MOD_EXP && a.mod[1] == MOD_NONE && !any_lamw && p->table.C <= 5) {
-            NG_CHECK(cheb_prepare(ctx, p->table));
+            NG_CHECK(cheb_prepare(ctx, p->table, (1.0 + p->dtp) - p->tp0));
             if (p->table.cheb_ok) a.cheb = p->table.cheb.d();
         }
         u.rtd_on = 1; u.K = K;
@@ -906,6 +929,31 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
             add_beta(ri[NGRTD_ROLE_NU_RTD_BETA], d->rtd_nu_a, d->rtd_nu_b);
             if (ri[NGRTD_ROLE_THALF_BETA] >= 0) add_beta(ri[NGRTD_ROLE_THALF_BETA], d->thalf_a, d->thalf_b);
         }
+    }
+    // per-well data packed for the single-launch kernel's LDS copy (UnitArgs.wd_src)
+    {
+        std::vector<double> wd;
+        auto add = [&](const DevBuf& b, size_t off, size_t n) {
+            std::vector<double> h(n);
+            if (n) (void)hipMemcpy(h.data(), b.d() + off, n * sizeof(double), hipMemcpyDeviceToHost);
+            wd.insert(wd.end(), h.begin(), h.end());
+        };
+        if (d->ce_enabled) {
+            const size_t LG = (size_t)L * d->ce_n_gases;
+            wd.insert(wd.end(), d->ce_obs, d->ce_obs + LG);
+            add(p->ce_lam, 0, LG);
+            add(p->ce_lam, 2 * LG, (size_t)L);
+            wd.insert(wd.end(), d->ce_E_min, d->ce_E_min + L);
+        }
+        if (d->rtd_enabled) {
+            const size_t LK = (size_t)L * d->n_tracers;
+            wd.insert(wd.end(), d->rtd_obs, d->rtd_obs + LK);
+            add(p->rtd_lam, 0, LK);
+            add(p->rtd_lam, 2 * LK, (size_t)L);
+        }
+        NG_CHECK(upload(ctx, p->welldata, wd.data(), wd.size()));
+        u.wd_src = p->welldata.d();
+        u.wd_n = (int32_t)wd.size();
     }
     HIP_TRY(ctx, p->ulogp.ensure((size_t)Umax * sizeof(double)));
     u.ulogp = p->ulogp.d();
@@ -968,7 +1016,7 @@ static int plan_run(ngrtd_plan* p, const double* theta, int64_t W, double* logp,
     if (logp && !ce_out && !rtd_out && p->desc.rtd_enabled) {
         RtdArgs a = p->rtd;
         a.theta = theta; a.U = U; a.conc = nullptr;
-        if (fused_path(a, p->desc.n_wells)) {
+        if (fused_path(a, u)) {
             NG_CHECK(timed_begin(p, prof, st, &ev));
             NG_CHECK(launch_fused(ctx, a, u, W, p->desc.n_wells, logp, st));
             NG_CHECK(timed_end(p, prof, st, 3, ev));
@@ -1079,12 +1127,12 @@ int ngrtd_plan_kernel_stats(ngrtd_plan* p, double* times_ms, int64_t* counts, in
     return NGRTD_OK;
 }
 
-int ngrtd_surrogate_check(const double* cols, int32_t C, int64_t N, double* coef, double* max_rel_err) {
+int ngrtd_surrogate_check(const double* cols, int32_t C, int64_t N, double dtp, double* coef, double* max_rel_err) {
     if (!cols || C < 1 || C > kMaxChan || N < 2 || !max_rel_err) return NGRTD_EINVAL;
     std::vector<std::vector<double>> cv((size_t)C);
     for (int c = 0; c < C; ++c) cv[c].assign(cols + (size_t)c * N, cols + (size_t)(c + 1) * N);
     std::vector<double> co;
-    *max_rel_err = cheb_build(cv, C, (C + 1) & ~1, co);
+    *max_rel_err = cheb_build(cv, C, (1.0 + dtp) - ((0.0 + 1e-5) + dtp), co);
     if (coef) std::copy(co.begin(), co.end(), coef);
     return NGRTD_OK;
 }

@@ -20,6 +20,7 @@ struct RtdArgs {
     int32_t J_is_log10;     // 1: J = 10**theta[row_J] (ForwardMod :101); 0: J = theta[row_J]
     double thalf_a, thalf_b;// t_half = thalf_a * theta[row_thalf] + thalf_b
     const double* tab;      // channel table [N][CP]
+    double tab0[kMaxChan];  // its row 0 (age 0), as kernel arguments
     int32_t N, C, CP;
     double tp0, dtp;        // age grid: tp_0 = tp0, tp_k = k + dtp (k >= 1)
     int32_t mod[2];         // component models; mod[1] = MOD_NONE for a single RTD
@@ -38,8 +39,10 @@ struct RtdArgs {
     const double* cheb;     // [kChebPieces][kChebN][CP]
 };
 
-// Chebyshev surrogate of Y_c(tau) = sum_{j>=0} A_{c,1+j} exp(-j / tau) (the exponential
-// RTD channel sums): piecewise in u = log(tau), kChebLogPieces pieces of width kChebW from
+// Chebyshev surrogate of Z_c(tau) = s01(tau) sum_{j>=0} A_{c,1+j} exp(-j / tau) (the
+// exponential RTD channel sums times s01 = exp(-(tp_1 - tp_0) / tau)) for every channel c,
+// and of Z_G(tau) = s01(tau) sum_{j=0}^{N-2} exp(-j / tau) (the normaliser), so that
+// conc = (A_{c,0} + Z_c) / (1 + Z_G) with no exp/expm1/division per unit: piecewise in u = log(tau), kChebLogPieces pieces of width kChebW from
 // tau = 1/2 (u0 = log 1/2), then one piece in s = 1/tau over [0, kChebSHi] for the tail up
 // to tau = inf.  kChebN coefficients per piece and channel.  Built and validated per plan
 // on the host (ngrtd.hip cheb_build); tau < 1/2, NaN take the exact matrix-core path.
@@ -50,6 +53,8 @@ constexpr int kChebPieces = kChebLogPieces + 1;
 constexpr double kChebTauLo = 0.5;
 constexpr double kChebU0 = -0.69314718055994530942;   // log(0.5)
 constexpr double kChebSHi = 4.55e-6;               // > 1 / (0.5 e^13)
+// surrogate table row length for C channels: C numerator sums + the normaliser, even
+__host__ __device__ constexpr int cheb_cp(int C) { return (C + 2) & ~1; }
 
 // Row tiles of the exponential-RTD GEMM for C channels: R tiles of 16 rows hold 4R row
 // groups; group g = c + C*m (m < 4R/C) of channel c carries the 4 age segments 4m..4m+3.
@@ -104,6 +109,11 @@ struct UnitArgs {
     // logodds Jacobians folded in (beta_block): slot i reads theta row bt_row[i] = x and
     // contributes x^bt_ia (1-x)^bt_ib to ONE product (integer exponents 0..7) plus
     // bt_fa log x + bt_fb log(1-x) for non-integer exponents; bt_betaln = sum of betaln.
+    // per-well observation data packed for one contiguous LDS copy (logp_fused_kernel):
+    // [ce_obs L*G | ce_lam L*G | ce_hll_sum L | ce_Emin L | rtd_obs L*K | rtd_lam L*K |
+    //  rtd_hll_sum L] (blocks present only when that model block is on)
+    const double* wd_src;
+    int32_t wd_n;
     int32_t bt_n;
     int32_t bt_row[kMaxBeta], bt_ia[kMaxBeta], bt_ib[kMaxBeta];
     double bt_fa[kMaxBeta], bt_fb[kMaxBeta];

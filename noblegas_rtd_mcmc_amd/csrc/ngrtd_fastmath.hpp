@@ -89,7 +89,8 @@ NGRTD_FM double flog(double x) {
     const int i = wrap ? 0 : i64;
     const int e = (int)((hi >> 20) & 0x7FF) - 1023 - (sub ? 54 : 0) + (wrap ? 1 : 0);
     const double m = fm_with_hi(xs, (hi & 0x000FFFFFu) | (wrap ? 0x3FE00000u : 0x3FF00000u));
-    const double f = m - (1.0 + (double)i * 0.015625);
+    const double ci = fm_with_hi(0.0, 0x3FF00000u | ((unsigned)i << 14));   // 1 + i/64, from bits
+    const double f = m - ci;
     const double r = f * NGRTD_FMT[2 * kFmExpN + 3 * i];
     double q = -0.125;
     q = fma(q, r, 1.0 / 7.0);

@@ -442,14 +442,43 @@ __device__ __forceinline__ void ce_model_s0(const UnitArgs& a, double T, double 
 // PyMC3's bound.  A product below 1e-280 (x within ~1e-40 of 0 or 1) redoes the sum
 // term by term so that it cannot underflow.  Differs from the term-by-term sum by a few
 // ulp of the largest log (the logp parity bar is atol 1e-9).
-__device__ __forceinline__ double beta_block(const UnitArgs& a, int64_t u) {
+// theta values of a unit loaded ahead of use (logp_fused_kernel issues these loads before
+// its first barrier so their latency overlaps it): the 6 CE rows, tau1 and the RTD nu
+struct ThetaPre {
+    double ce[6];
+    double tau1, nub;
+};
+
+__device__ __forceinline__ void theta_preload(const UnitArgs& a, int64_t u, ThetaPre& t) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) t.ce[i] = a.ce_on ? a.theta[(int64_t)a.row_ce[i] * a.U + u] : 0.0;
+    t.tau1 = a.rtd_on ? a.theta[(int64_t)a.row_tau1 * a.U + u] : 0.0;
+    t.nub = a.rtd_on ? a.theta[(int64_t)a.row_nu * a.U + u] : 0.0;
+}
+
+// x of Beta slot i (beta slots follow the host order: CE Ae, F, E, b, nu, then RTD nu,
+// then thalf_cfc -- ngrtd.hip add_beta) from the preloaded values when available
+// `full`: compile-time promise (literal true, inlined) that the plan has the CE and RTD
+// blocks, priors and likelihoods and no Jacobians -- the joint workload -- so that every
+// flag test folds away and the unit's work is one straight-line block for the scheduler.
+__device__ __forceinline__ double beta_x(const UnitArgs& a, int64_t u, int i, const ThetaPre* pre, bool full) {
+    const bool ce_on = full || a.ce_on, rtd_on = full || a.rtd_on;
+    if (pre) {
+        if (ce_on && i < 5) return pre->ce[i < 3 ? i : i + 1];
+        if (rtd_on && i == (ce_on ? 5 : 0)) return pre->nub;
+    }
+    return a.theta[(int64_t)a.bt_row[i] * a.U + u];
+}
+
+__device__ __forceinline__ double beta_block(const UnitArgs& a, int64_t u, const ThetaPre* pre = nullptr,
+                                             bool full = false) {
     double pint = 1.0, lsum = 0.0;
     bool inb = true;
     double xs[kMaxBeta];
 #pragma unroll
     for (int i = 0; i < kMaxBeta; ++i) {
         if (i < a.bt_n) {
-            const double x = a.theta[(int64_t)a.bt_row[i] * a.U + u];
+            const double x = beta_x(a, u, i, pre, full);
             xs[i] = x;
             inb &= (x >= 0 && x <= 1);
             pint *= ipow_small(x, a.bt_ia[i]) * ipow_small(1 - x, a.bt_ib[i]);
@@ -473,18 +502,19 @@ __device__ __forceinline__ double beta_block(const UnitArgs& a, int64_t u) {
     return inb ? (lint + lsum) - a.bt_betaln : kNegInf;
 }
 
-__device__ __forceinline__ double unit_logp_theta(const UnitArgs& a, int64_t u, int l) {
-    const bool want_like = a.flags & NGRTD_WANT_LIKE;
-    const bool want_prior = a.flags & NGRTD_WANT_PRIOR;
-    const bool jac = a.flags & NGRTD_WANT_JACOBIAN;
+__device__ __forceinline__ double unit_logp_theta(const UnitArgs& a, int64_t u, int l,
+                                                  const ThetaPre* pre = nullptr, bool full = false) {
+    const bool want_like = full || (a.flags & NGRTD_WANT_LIKE);
+    const bool want_prior = full || (a.flags & NGRTD_WANT_PRIOR);
+    const bool jac = !full && (a.flags & NGRTD_WANT_JACOBIAN);
     double lp = 0.0;
-    if (want_prior) lp += beta_block(a, u);
-    if (a.ce_on) {
+    if (want_prior) lp += beta_block(a, u, pre, full);
+    if (full || a.ce_on) {
         double p[6];
 #pragma unroll
-        for (int i = 0; i < 6; ++i) p[i] = a.theta[(int64_t)a.row_ce[i] * a.U + u];
+        for (int i = 0; i < 6; ++i) p[i] = pre ? pre->ce[i] : a.theta[(int64_t)a.row_ce[i] * a.U + u];
         if (want_prior) lp += normal_logp(p[3], a.m_mu, a.m_tau, a.m_log_tau_2pi);
-        if (want_like || a.ce_out) {
+        if (want_like || (!full && a.ce_out)) {
             // noble_gas_mcmc.py:229-250 parameter mapping, then ce_exc_wrapper (:205-213)
             const double Emin = a.ce_Emin[l];
             const double Ae_log = p[0] * (a.logA_max - a.logA_min) + a.logA_min;
@@ -495,14 +525,14 @@ __device__ __forceinline__ double unit_logp_theta(const UnitArgs& a, int64_t u, 
             const double nu = p[5] * (a.nu_max - a.nu_min) + a.nu_min;
             double mod[kMaxGas];
             ce_model_s0(a, T, lapse_rate_fast(E), exp10_fast(Ae_log), exp10_fast(F_log), mod);
-            if (a.ce_out)
+            if (!full && a.ce_out)
                 for (int j = 0; j < a.G; ++j) a.ce_out[(int64_t)j * a.U + u] = mod[j];
             if (want_like)
                 lp += st_block<kMaxGas>(a.G, a.ce_obs + l * a.G, mod, a.ce_lam + l * a.G, a.ce_hll_sum[l], nu);
         }
     }
-    if (a.rtd_on) {
-        const double tau1 = a.theta[(int64_t)a.row_tau1 * a.U + u];
+    if (full || a.rtd_on) {
+        const double tau1 = pre ? pre->tau1 : a.theta[(int64_t)a.row_tau1 * a.U + u];
         if (want_prior) {
             lp += uniform_logp(tau1, a.tau1_lo, a.tau1_hi, a.tau1_nlw);
             if (jac) lp += jac_interval(tau1, a.tau1_lo, a.tau1_hi);
@@ -534,9 +564,10 @@ __device__ __forceinline__ double unit_logp_theta(const UnitArgs& a, int64_t u, 
 // (NMAX: compile-time bound on K -- the single-launch kernel passes its channel count,
 // K <= C since every tracer owns at least one channel)
 template <int NMAX = kMaxTracer>
-__device__ __forceinline__ double unit_like_rtd(const UnitArgs& a, int64_t u, int l, const double* conc) {
-    if (!a.rtd_on || !(a.flags & NGRTD_WANT_LIKE)) return 0.0;
-    const double nub = a.theta[(int64_t)a.row_nu * a.U + u];
+__device__ __forceinline__ double unit_like_rtd(const UnitArgs& a, int64_t u, int l, const double* conc,
+                                                const ThetaPre* pre = nullptr, bool full = false) {
+    if (!full && (!a.rtd_on || !(a.flags & NGRTD_WANT_LIKE))) return 0.0;
+    const double nub = pre ? pre->nub : a.theta[(int64_t)a.row_nu * a.U + u];
     const double nu = nub * (a.rnu_max - a.rnu_min) + a.rnu_min;
     return st_block<NMAX>(a.K, a.rtd_obs + l * a.K, conc, a.rtd_lam + l * a.K, a.rtd_hll_sum[l], nu);
 }
@@ -717,17 +748,12 @@ __host__ __device__ __forceinline__ void cheb_sums(const double* __restrict__ pc
     for (int c = 0; c < C; ++c) y[c] = fma(x, b1[c], pc[c] - b2[c]);
 }
 
-// Channel sums -> tracer concentrations of unit u (rtd_conc_kernel's combination step)
+// Numerators num_c = A_{c,0} + s01 Y_c and the reciprocal normaliser 1 / (1 + s01 G) ->
+// tracer concentrations of unit u (rtd_conc_kernel's combination step): per tracer
+// (A + J B) / den, the BMM mix and the SF6 factor (run_age_mcmc_utils.py:154-161).
 template <int C>
-__device__ __forceinline__ void mfma_unit_conc(const RtdArgs& a, int64_t u, double bu, const double* yy,
-                                               double* conc) {
-    const int n = a.N - 1;
-    const double s01 = fexp(-bu * ((1.0 + a.dtp) - a.tp0));
-    const double G = (n > 0) ? fexpm1(-bu * (double)n) / fexpm1(-bu) : 0.0;
-    const double rden = 1.0 / (1.0 + s01 * G);     // one division for the K tracers (<= 1 ulp)
-    double num[C];
-#pragma unroll
-    for (int c = 0; c < C; ++c) num[c] = a.tab[c] + s01 * yy[c];
+__device__ __forceinline__ void unit_conc(const RtdArgs& a, int64_t u, const double* num, double rden,
+                                          double* conc) {
     const double fmix = (a.row_f1 >= 0) ? a.theta[(int64_t)a.row_f1 * a.U + u] : 1.0;
     double Jw = 0.0;
     if (a.row_J >= 0) {
@@ -748,6 +774,21 @@ __device__ __forceinline__ void mfma_unit_conc(const RtdArgs& a, int64_t u, doub
         if (a.tr_sf6[t] && a.row_lamsf6 >= 0) cout *= (1 + a.theta[(int64_t)a.row_lamsf6 * a.U + u]);
         conc[t] = cout;
     }
+}
+
+// Exact channel sums Y_c (matrix-core path) -> concentrations: the normaliser
+// 1 + s01 G with G = sum_{j<n} q^j = expm1(-beta n) / expm1(-beta) in closed form.
+template <int C>
+__device__ __forceinline__ void mfma_unit_conc(const RtdArgs& a, int64_t u, double bu, const double* yy,
+                                               double* conc) {
+    const int n = a.N - 1;
+    const double s01 = fexp(-bu * ((1.0 + a.dtp) - a.tp0));
+    const double G = (n > 0) ? fexpm1(-bu * (double)n) / fexpm1(-bu) : 0.0;
+    const double rden = 1.0 / (1.0 + s01 * G);     // one division for the K tracers (<= 1 ulp)
+    double num[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) num[c] = a.tab0[c] + s01 * yy[c];
+    unit_conc<C>(a, u, num, rden, conc);
 }
 
 // lanes with tq = t finish the units of tile t: select that tile's sums
@@ -812,7 +853,7 @@ __global__ void __launch_bounds__(64 * mfma_waves(C)) rtd_exp_mfma_kernel(const 
 }
 
 // The whole batched log-prob in ONE launch (exponential single-component RTD with
-// C <= 5 channels, L <= 512).  A block of 8 waves owns WB = 512 / L walkers x all L wells
+// C <= 5 channels, L <= 512; FULL: the joint CE + RTD plan with priors and likelihoods).  A block of 8 waves owns WB = 512 / L walkers x all L wells
 // (block-local unit i = l * WB + w'); lane `lane` of wave `wave` owns unit
 // i = 64 * wave + lane for all of its work:
 //  1. the theta-only part: CE model + likelihood and all priors (the surrogate table's
@@ -832,11 +873,11 @@ constexpr int kFusedWaves = 8;
 constexpr int kFusedUnits = 64 * kFusedWaves;
 constexpr int kFusedPrefetch = 4;   // double2 per thread: covers kChebPieces*kChebN*6 doubles
 
-template <int C>
+template <int C, bool FULL>
 __global__ void __launch_bounds__(64 * kFusedWaves) logp_fused_kernel(const RtdArgs a, const UnitArgs ua,
                                                                      int32_t WB, double* __restrict__ logp) {
     constexpr int NT = mfma_tiles(C);
-    constexpr int CP = (C + 1) & ~1;
+    constexpr int CP = cheb_cp(C);
     constexpr int TAB2 = kChebPieces * kChebN * CP / 2;   // double2 entries of the surrogate table
     static_assert(NT == 4, "one unit per lane needs 4 tiles per wave");
     static_assert(TAB2 <= kFusedPrefetch * 64 * kFusedWaves, "prefetch covers the table");
@@ -855,7 +896,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves) logp_fused_kernel(const RtdA
     const int nb = gridDim.x;
     const int bl = (nb & 7) == 0 ? ((int)blockIdx.x & 7) * (nb >> 3) + ((int)blockIdx.x >> 3) : (int)blockIdx.x;
     const int64_t w0 = (int64_t)bl * WB;
-    // surrogate table -> registers (written to LDS after the theta-only part)
+    // surrogate table -> registers -> LDS (stored after every prologue load is issued)
     double2 pre[kFusedPrefetch];
     if (a.cheb) {
         const double2* src = reinterpret_cast<const double2*>(a.cheb);
@@ -870,12 +911,23 @@ __global__ void __launch_bounds__(64 * kFusedWaves) logp_fused_kernel(const RtdA
     const int mwl = mi % WB, ml = mi / WB;
     const bool mvalid = ml < L && w0 + mwl < W;
     const int64_t mu = mvalid ? (int64_t)ml * W + w0 + mwl : 0;
-    const double tau = mvalid ? a.theta[(int64_t)a.row_tau[0] * a.U + mu] : 1.0;
+    // per-well observation data -> LDS (read per lane by the likelihood blocks): all loads
+    // issued before any store, so the prologue pays one memory latency
+    double* wd = cheb + kChebPieces * kChebN * CP;
+    constexpr int kWdRegs = 4;
+    double wv[kWdRegs];
+#pragma unroll
+    for (int r = 0; r < kWdRegs; ++r) {
+        const int i = tid + r * 64 * kFusedWaves;
+        wv[r] = i < ua.wd_n ? ua.wd_src[i] : 0.0;
+    }
     fm_lds_init();                                        // fexp/flog tables
-    __syncthreads();
-    NGRTD_PROBE(1);
-    const double th = mvalid ? unit_logp_theta(ua, mu, ml) : 0.0;
-    NGRTD_PROBE(2);
+#pragma unroll
+    for (int r = 0; r < kWdRegs; ++r) {
+        const int i = tid + r * 64 * kFusedWaves;
+        if (i < ua.wd_n) wd[i] = wv[r];
+    }
+    for (int i = tid + kWdRegs * 64 * kFusedWaves; i < ua.wd_n; i += 64 * kFusedWaves) wd[i] = ua.wd_src[i];
     if (a.cheb) {
         double2* dst = reinterpret_cast<double2*>(cheb);
 #pragma unroll
@@ -884,12 +936,50 @@ __global__ void __launch_bounds__(64 * kFusedWaves) logp_fused_kernel(const RtdA
             if (i < TAB2) dst[i] = pre[r];
         }
     }
-    double cx = 0.0;
-    const int cpc = a.cheb ? cheb_piece(tau, cx) : -1;
-    const bool exact = __any(cpc < 0);                    // wave-uniform
+    UnitArgs ul = ua;
+    {
+        const int nce = ua.ce_on ? L * ua.G : 0, nrt = ua.rtd_on ? L * ua.K : 0;
+        double* q = wd;
+        if (ua.ce_on) {
+            ul.ce_obs = q; q += nce;
+            ul.ce_lam = q; q += nce;
+            ul.ce_hll_sum = q; q += L;
+            ul.ce_Emin = q; q += L;
+        }
+        if (ua.rtd_on) {
+            ul.rtd_obs = q; q += nrt;
+            ul.rtd_lam = q; q += nrt;
+            ul.rtd_hll_sum = q;
+        }
+    }
     __syncthreads();
-    double yy[C], bu;
-    if (exact) {
+    NGRTD_PROBE(1);
+    // theta of this lane's unit (after the barrier: the 8.4 MB theta read at c4 is
+    // bandwidth-bound, and the tables' loads before the barrier should not wait behind it)
+    const double tau = mvalid ? a.theta[(int64_t)a.row_tau[0] * a.U + mu] : 1.0;
+    ThetaPre tp;
+    theta_preload(ua, mu, tp);
+    // One straight-line block per unit: the theta-only part, the surrogate channel sums,
+    // the concentrations and the RTD likelihood (independent chains the scheduler can
+    // interleave; with FULL every plan-flag test folds away).  Lanes whose tau the
+    // surrogate does not cover evaluate piece 0 here and are redone exactly below.
+    double cx = 0.0;
+    int cpc = a.cheb ? cheb_piece(tau, cx) : -1;
+    const bool bad = cpc < 0;
+    cpc = bad ? 0 : cpc;
+    const double th = mvalid ? unit_logp_theta(ul, mu, ml, &tp, FULL) : 0.0;
+    double zz[C + 1];
+    cheb_sums<C + 1>(cheb + cpc * (kChebN * CP), CP, cx, zz);   // s01 Y_c (c < C), s01 G
+    double like = 0.0;
+    {
+        double num[C], conc[kMaxTracer];
+#pragma unroll
+        for (int c = 0; c < C; ++c) num[c] = a.tab0[c] + zz[c];
+        unit_conc<C>(a, mu, num, 1.0 / (1.0 + zz[C]), conc);
+        like = mvalid ? unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL) : 0.0;
+    }
+    NGRTD_PROBE(2);
+    if (__any(bad)) {                                     // wave-uniform: exact channel sums
         int64_t uoff[NT];
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
@@ -899,25 +989,19 @@ __global__ void __launch_bounds__(64 * kFusedWaves) logp_fused_kernel(const RtdA
         }
         MfmaWave<C> mw;
         mw.init(a, uoff);
-        NGRTD_PROBE(3);
         mw.steps(a.frag, a.nsteps);
-        NGRTD_PROBE(4);
-        double y[NT][C];
+        double y[NT][C], yy[C], bu;
         mw.finish(a, y);
         mfma_pick_tile<C>(y, mw.beta, yy, bu);   // tile tq holds this lane's unit
-    } else {
-        NGRTD_PROBE(3);
-        bu = 1. / tau;
-        cheb_sums<C>(cheb + cpc * (kChebN * CP), CP, cx, yy);
-        NGRTD_PROBE(4);
+        if (mvalid) {
+            double conc[kMaxTracer];
+            mfma_unit_conc<C>(a, mu, bu, yy, conc);
+            like = unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL);
+        }
     }
+    NGRTD_PROBE(3);
+    NGRTD_PROBE(4);
     NGRTD_PROBE(5);
-    double like = 0.0;
-    if (mvalid) {
-        double conc[kMaxTracer];
-        mfma_unit_conc<C>(a, mu, bu, yy, conc);
-        like = unit_like_rtd<C>(ua, mu, ml, conc);
-    }
     part[mi] = th + like;
     NGRTD_PROBE(6);
     __syncthreads();

@@ -300,3 +300,22 @@ def test_surrogate_vs_exact_over_tau_range():
     ref = om.log_prob(spec, th, walkers=walkers)
     assert close(got[walkers], ref, 1e-12, 1e-9).all(), (got[walkers], ref)
     lp.close()
+
+
+def test_many_wells_single_launch():
+    """L = 300 wells: one walker per block (WB = 1), per-well observation data staged in
+    more than 64 KiB of LDS, vs the oracle."""
+    import oracle.models as om
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+    spec = wl.c4_spec(L=300, N=300)
+    th = wl.sample_prior(spec, 5, np.random.default_rng(31))
+    lp = LogProb(spec, max_walkers=5)
+    lp.ctx.set_profiling(True)
+    lp.kernel_stats(reset=True)
+    got = lp(th, soa=True)
+    assert lp.kernel_stats(reset=True)["fused"][1] == 1
+    lp.ctx.set_profiling(False)
+    ref = om.log_prob(spec, th, walkers=[0, 4])
+    assert close(got[[0, 4]], ref, 1e-12, 1e-9).all(), (got, ref)
+    lp.close()

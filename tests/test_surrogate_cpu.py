@@ -45,13 +45,14 @@ def channels(tracers):
     return np.ascontiguousarray(cols, dtype=np.float64)
 
 
-def check(lib, cols):
+def check(lib, cols, dtp=0.0):
     Cn, N = cols.shape
-    CP = (Cn + 1) & ~1
+    CP = (Cn + 2) & ~1
     coef = np.zeros(PIECES * N_COEF * CP)
     err = C.c_double()
     dp = C.POINTER(C.c_double)
-    assert lib.ngrtd_surrogate_check(cols.ctypes.data_as(dp), Cn, N, coef.ctypes.data_as(dp), C.byref(err)) == 0
+    assert lib.ngrtd_surrogate_check(cols.ctypes.data_as(dp), Cn, N, dtp, coef.ctypes.data_as(dp),
+                                     C.byref(err)) == 0
     return err.value, coef.reshape(PIECES, N_COEF, CP)
 
 
@@ -73,12 +74,42 @@ def test_shipped_series_within_bound(lib, n):
     assert err <= 5e-14, err
     cols = channels(trs)
     j = np.arange(n - 1, dtype=np.float64)
+    d01 = 1.0 - (0.0 + 1e-5)                 # tp_1 - tp_0 (dtp = 0)
     for tau in (0.5, 0.731, 1.0, 7.3, 37.3, 333.3, 1000.0, 2.2e5, 3e6, np.inf):
         q = np.exp(-j / tau)
-        for c in range(cols.shape[0]):
-            ref = np.dot(cols[c, 1:], q)
-            scale = np.dot(np.abs(cols[c, 1:]), q)
-            assert abs(numpy_surrogate(coef, tau, c) - ref) <= 1e-13 * scale, (tau, c)
+        s01 = np.exp(-d01 / tau)
+        for c in range(cols.shape[0] + 1):      # channels, then the normaliser
+            col = cols[c, 1:] if c < cols.shape[0] else np.ones(n - 1)
+            ref = s01 * np.dot(col, q)
+            assert abs(numpy_surrogate(coef, tau, c) - ref) <= 1e-13 * ref, (tau, c)
+
+
+def test_reconstructs_reference_convolution(lib):
+    """(A_0 + Z_c) / (1 + Z_G) from the surrogate equals the reference convolve() of the
+    exponential model (conv_golden.npz fixtures, N = 1200) for the fixture's taus >= 1/2."""
+    import os
+    here = os.path.dirname(os.path.abspath(__file__))
+    z = np.load(os.path.join(here, "golden", "conv_golden.npz"))
+    keys = [k for k in z.files if k.endswith("_exponential_1200_out")]
+    assert keys
+    checked = 0
+    for k in keys:
+        name = k.split("_exponential_")[0]
+        t = workloads.tracer(name, 1200)
+        if t.rad_accum in ("4He", "SF6") or name == "He3":
+            continue                  # J-weighted / 3He channels: covered by the GPU tests
+        cols = channels([t])
+        err, coef = check(lib, cols)
+        assert err <= 5e-14
+        taus = z[k.replace("_out", "_tau")]
+        ref = z[k]
+        for tau, r in zip(taus, ref):
+            if not tau >= 0.5:
+                continue
+            val = (cols[0, 0] + numpy_surrogate(coef, tau, 0)) / (1 + numpy_surrogate(coef, tau, 1))
+            assert abs(val - r) <= 1e-12 * abs(r), (name, tau, val, r)
+            checked += 1
+    assert checked >= 50, checked
 
 
 def test_c4_workload_series_within_bound(lib):

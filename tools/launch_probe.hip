@@ -69,8 +69,13 @@ void run2(const char* name, int blocks, size_t lds, long long cycles, double* d,
            1e3 * ms / reps);
 }
 
-int main() {
+int main(int argc, char** argv) {
     double* d; hipMalloc(&d, 1 << 20); hipMemset(d, 0, 1 << 20);
+    if (argc > 1) {   // the single-launch log-prob kernel's shape: 256 blocks x 512 threads, 35 KB LDS
+        for (long long cyc : {0LL, 2400LL, 12000LL, 24000LL, 36000LL})
+            run<512, 48>("512thr VG48 1 stream", 256, 35 * 1024, cyc, d);
+        return 0;
+    }
     const long long cyc = 48000;   // ~20 us at 2.4 GHz
     run<256, 96>("256thr VG96 1 stream", 512, 57344, cyc, d);
     run2<256, 96>("256thr VG96 streams", 512, 57344, cyc, d, 1);

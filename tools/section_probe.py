@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--wells", type=int, default=64)
     ap.add_argument("--walkers", type=int, default=2048)
     ap.add_argument("--build-only", action="store_true")
+    ap.add_argument("--variant", default="joint", choices=["joint", "rtd_only", "rtd_bare"])
     args = ap.parse_args()
     build()
     if args.build_only:
@@ -50,6 +51,12 @@ def main():
     from noblegas_rtd_mcmc_amd import _lib, workloads
     from noblegas_rtd_mcmc_amd.engine import LogProb
     spec = workloads.c4_spec(L=args.wells)
+    if args.variant != "joint":
+        import dataclasses
+        from noblegas_rtd_mcmc_amd.spec import ModelSpec
+        spec = ModelSpec(n_wells=args.wells, rtd=spec.rtd)
+        if args.variant == "rtd_bare":
+            spec = dataclasses.replace(spec, include_prior=False, include_like=False, roles=[])
     th = workloads.sample_prior(spec, args.walkers, np.random.default_rng(34568))
     lp = LogProb(spec, max_walkers=args.walkers)
     dev = torch.from_numpy(th).cuda()
@@ -77,7 +84,20 @@ def main():
     for grp, sel in (("rtd_first", w < 4), ("ce_first", w >= 4)):
         res[grp] = {n: float(np.median(d[sel, i])) for i, n in enumerate(names)}
         res[grp]["total"] = float(np.median(t[sel, 7] - t[sel, 0]))
-    res["start_spread_cycles"] = int(np.percentile(t[:, 0], 99) - t[:, 0].min())
+    # s_memtime counters are per XCD (block b runs on XCD b % 8): spans within one XCD
+    blk = np.arange(t.shape[0]) // 8
+    spans, starts, ends = [], [], []
+    for x in range(8):
+        sel = (blk % 8) == x
+        if sel.any():
+            t0 = t[sel, 0].min()
+            spans.append(int(t[sel, 7].max() - t0))
+            starts.append(np.percentile(t[sel, 0] - t0, [50, 90, 100]).tolist())
+            ends.append(np.percentile(t[sel, 7] - t0, [10, 50, 100]).tolist())
+    res["xcd_span_cycles"] = spans
+    res["xcd_wave_start_p50_p90_max"] = starts[0]
+    res["xcd_wave_end_p10_p50_max"] = ends[0]
+    del res["span_cycles"]
     print(json.dumps(res, indent=1))
 
 
