@@ -171,7 +171,7 @@ def main():
         kfull = {"fused": "logp_fused_kernel", "rtd": "rtd_exp_mfma_kernel" if info["mfma_rows"] else "rtd_conc_kernel"}[kname]
         # committed PMC summary of the same command (tools/gpu_profile.sh -> tools/profile_summary.py)
         pmc = {}
-        path = os.path.join(REPO, "profiles", PMC_SUMMARY)
+        path = os.environ.get("NGRTD_PMC_SUMMARY") or os.path.join(REPO, "profiles", PMC_SUMMARY)
         if os.path.exists(path):
             with open(path) as f:
                 for k, e in json.load(f).items():
@@ -183,8 +183,8 @@ def main():
             # kernel (SQ_INSTS_VALU_FLOPS_FP64 x 64 lanes, fma = 2) x units
             fpu = pmc.get("fp64_flop_per_unit")
             flops = fpu * U if fpu else None
-            flop_src = "PMC fp64_flop_per_unit %s x %d units (profiles/%s)" % (
-                "%.1f" % fpu if fpu else "n/a", U, PMC_SUMMARY)
+            flop_src = "PMC fp64_flop_per_unit %s x %d units (%s)" % (
+                "%.1f" % fpu if fpu else "n/a", U, os.path.relpath(path, REPO))
         else:
             # exact matrix-core path: one FMA (2 FLOP) per (unit, channel, age >= 1)
             flops = 2.0 * U * C * (N - 1)

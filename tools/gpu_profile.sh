@@ -1,7 +1,9 @@
 #!/bin/bash
-# One GPU session: parity tests, bench, rocprofv3 kernel stats of the bench command, then
-# PMC passes (each group in its own rocprofv3 run, never combined with a trace domain).
-# Outputs under gpurun_out/$TAG/; tools/profile_summary.py condenses them into profiles/.
+# One GPU session: parity tests, PMC passes over a short bench (each counter group in its
+# own rocprofv3 run, never combined with a trace domain), their summary, then the bench
+# (reading that summary for the FP64 FLOPs and HBM traffic of its kernel) and rocprofv3
+# --kernel-trace --stats of the same bench command.  Outputs under gpurun_out/$TAG/;
+# copy with:  python tools/profile_summary.py gpurun_out/$TAG profiles/rNN
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${1:-run}
@@ -12,10 +14,6 @@ step() { echo "== $*" >> $OUT/steps.log; }
 step tests
 timeout -k 10 600 python -m pytest tests -m gpu -q -p no:cacheprovider > $OUT/tests.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> $OUT/steps.log; [ $rc -eq 0 ] || exit $rc
-step bench
-timeout -k 10 300 python bench.py --steps 400 --warmup 40 --cpu-seconds 15 > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed rc=$?" >> $OUT/steps.log; exit 1; }
-step rocprof-stats
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o stats -- python3 bench.py --steps 400 --warmup 40 --no-cpu-baseline > $OUT/prof_bench.json 2> $OUT/prof.err || { echo "rocprof failed rc=$?" >> $OUT/steps.log; exit 1; }
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" \
            "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS" \
@@ -26,6 +24,12 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" \
            "GRBM_GUI_ACTIVE SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT"; do
   i=$((i+1))
   step "pmc$i $grp"
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d $OUT/pmc$i -o pmc$i -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > /dev/null 2> $OUT/pmc$i.err || { echo "pmc$i failed rc=$?" >> $OUT/steps.log; exit 1; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d $OUT/pmc$i -o pmc$i -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > $OUT/pmc_bench.json 2> $OUT/pmc$i.err || { echo "pmc$i failed rc=$?" >> $OUT/steps.log; exit 1; }
 done
+step summary
+python tools/profile_summary.py $OUT $OUT/summ > /dev/null || { echo "summary failed" >> $OUT/steps.log; exit 1; }
+step bench
+NGRTD_PMC_SUMMARY=$OUT/summ_pmc.json timeout -k 10 300 python bench.py --steps 400 --warmup 40 --cpu-seconds 15 > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed rc=$?" >> $OUT/steps.log; exit 1; }
+step rocprof-stats
+NGRTD_PMC_SUMMARY=$OUT/summ_pmc.json timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o stats -- python3 bench.py --steps 400 --warmup 40 --no-cpu-baseline > $OUT/prof_bench.json 2> $OUT/prof.err || { echo "rocprof failed rc=$?" >> $OUT/steps.log; exit 1; }
 step done

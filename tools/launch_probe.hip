@@ -74,6 +74,35 @@ int main(int argc, char** argv) {
     if (argc > 1) {   // the single-launch log-prob kernel's shape: 256 blocks x 512 threads, 35 KB LDS
         for (long long cyc : {0LL, 2400LL, 12000LL, 24000LL, 36000LL})
             run<512, 48>("512thr VG48 1 stream", 256, 35 * 1024, cyc, d);
+        // same 2048 waves in other block shapes / LDS sizes
+        run<1024, 48>("1024thr VG48 1 stream", 128, 35 * 1024, 0, d);
+        run<256, 48>("256thr VG48 1 stream", 512, 35 * 1024, 0, d);
+        run<512, 48>("512thr VG48 nolds", 256, 0, 0, d);
+        run<512, 48>("512thr VG48 1 stream", 128, 35 * 1024, 0, d);
+        run<512, 48>("512thr VG48 1 stream", 64, 35 * 1024, 0, d);
+        run<64, 48>("64thr VG48 1 stream", 2048, 0, 0, d);
+        // the same launches replayed from a hipGraph (1 and 10 launches per graph)
+        for (int per : {1, 10}) {
+            for (long long cyc : {0LL, 24000LL}) {
+                auto k = spin<512, 48>;
+                hipStream_t s; hipStreamCreate(&s);
+                hipGraph_t g; hipGraphExec_t ge;
+                hipStreamBeginCapture(s, hipStreamCaptureModeGlobal);
+                for (int i = 0; i < per; ++i) hipLaunchKernelGGL(k, dim3(256), dim3(512), 35 * 1024, s, d, cyc);
+                hipStreamEndCapture(s, &g);
+                hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+                for (int i = 0; i < 3; ++i) hipGraphLaunch(ge, s);
+                hipStreamSynchronize(s);
+                hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
+                const int reps = 200 / per;
+                hipEventRecord(a, s);
+                for (int i = 0; i < reps; ++i) hipGraphLaunch(ge, s);
+                hipEventRecord(b, s); hipEventSynchronize(b);
+                float ms; hipEventElapsedTime(&ms, a, b);
+                printf("graph of %2d launches             spin %.2f us  per launch %.2f us\n", per, cyc / 2.4e3,
+                       1e3 * ms / (reps * per));
+            }
+        }
         return 0;
     }
     const long long cyc = 48000;   // ~20 us at 2.4 GHz

@@ -26,11 +26,13 @@ def main(src, prefix):
     import glob
     res = summarize(sorted(glob.glob(os.path.join(src, "pmc*"))))
     units = None
-    try:
-        with open(os.path.join(src, "bench.json")) as f:
-            units = json.loads(f.read().strip().splitlines()[-1])["geometry"]["units"]
-    except Exception:
-        pass
+    for name in ("bench.json", "prof_bench.json", "pmc_bench.json"):
+        try:
+            with open(os.path.join(src, name)) as f:
+                units = json.loads(f.read().strip().splitlines()[-1])["geometry"]["units"]
+            break
+        except Exception:
+            pass
     out = {}
     for k, d in res.items():
         if "ngrtd" not in k:
