@@ -221,6 +221,20 @@ int ngrtd_plan_kernel_stats(ngrtd_plan* plan, double* times_ms, int64_t* counts,
  * roofline accounting in bench.py. */
 int ngrtd_plan_info(ngrtd_plan* plan, int64_t W, int64_t* info, int32_t n);
 
+/* Device-resident population DE-MC (the sampler loop of PyMC3 DEMetropolisZ,
+ * run_age_mcmc_utils.py:412-417 / noble_gas_mcmc.py:410-415, as sampler.DEMetropolis runs it
+ * over the whole ensemble): n_steps steps of
+ *   x*_w = x_w + lamb (x_r1 - x_r2) + U(-scaling, scaling),  r1 != r2 != w,
+ *   accept iff logp(x*_w) - logp_w > log u_w  (and logp(x*_w) is not NaN),
+ * random numbers from a counter-based generator keyed by (seed, step0 + s, walker).
+ * theta [P][L][W] and logp [W] are DEVICE pointers, updated in place on the ctx stream;
+ * logp must hold the log-prob of theta on entry (ngrtd_logp).  n_accepted (device
+ * uint64, may be NULL) is incremented by the number of acceptances; accepted (device
+ * int32 [W], may be NULL) receives the last step's decisions.  2 launches per step
+ * (proposal + log-prob with the accept in its per-walker reduction).  W >= 3. */
+int ngrtd_demc_run(ngrtd_plan* plan, double* theta, double* logp, int64_t W, int64_t n_steps, double lamb,
+                   double scaling, uint64_t seed, uint64_t step0, uint64_t* n_accepted, int32_t* accepted);
+
 /* Host-only (no device needed): build the piecewise-Chebyshev surrogate the exponential
  * log-prob kernel uses for its channel sums and validate it against a long-double
  * evaluation of the same sums.  With s = 1/tau and s01 = exp(-(tp_1 - tp_0) s) (tp as in

@@ -81,6 +81,8 @@ PROTOTYPES = {
     "ngrtd_forward": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int32]),
     "ngrtd_plan_kernel_stats": (C.c_int, [C.c_void_p, _dp, _i64p, C.c_int32, C.c_int32]),
     "ngrtd_plan_info": (C.c_int, [C.c_void_p, C.c_int64, _i64p, C.c_int32]),
+    "ngrtd_demc_run": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_double, C.c_double,
+                                 C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p]),
     "ngrtd_surrogate_check": (C.c_int, [_dp, C.c_int32, C.c_int64, C.c_double, _dp, _dp]),
 }
 

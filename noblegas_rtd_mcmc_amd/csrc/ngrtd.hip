@@ -99,6 +99,7 @@ struct ngrtd_plan {
     double tp0 = 1e-5, dtp = 0.0;
     // workspaces
     DevBuf conc, ulogp, theta_stage, out_stage, ce_stage;
+    DevBuf demc_prop[2], demc_lp, demc_acc, demc_cnt;   // ngrtd_demc_run scratch
     RtdArgs rtd{};
     UnitArgs unit{};
     LaunchStats stats;
@@ -415,7 +416,8 @@ static bool fused_path(const RtdArgs& a, const UnitArgs& u) {
            fused_lds(a, u) <= kFusedMaxLds;
 }
 template <int C, bool FULL>
-static void launch_fused_cf(const RtdArgs& a, const UnitArgs& u, int WB, int64_t W, double* logp, hipStream_t st) {
+static void launch_fused_cf(const RtdArgs& a, const UnitArgs& u, int WB, int64_t W, double* logp,
+                            const DemcAccept& da, hipStream_t st) {
     static const bool attr = [] {   // dynamic LDS above 64 KiB (many wells) needs the opt-in
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&logp_fused_kernel<C, FULL>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFusedMaxLds);
@@ -423,25 +425,27 @@ static void launch_fused_cf(const RtdArgs& a, const UnitArgs& u, int WB, int64_t
     }();
     (void)attr;
     hipLaunchKernelGGL((logp_fused_kernel<C, FULL>), dim3((unsigned)cdiv(W, WB)), dim3(64 * kFusedWaves),
-                       fused_lds(a, u), st, a, u, WB, logp);
+                       fused_lds(a, u), st, a, u, WB, logp, da);
 }
 // FULL instance: CE + RTD blocks, priors and likelihoods on, no Jacobians (the joint model)
 template <int C>
-static void launch_fused_c(const RtdArgs& a, const UnitArgs& u, int WB, int64_t W, double* logp, hipStream_t st) {
+static void launch_fused_c(const RtdArgs& a, const UnitArgs& u, int WB, int64_t W, double* logp,
+                           const DemcAccept& da, hipStream_t st) {
     const bool full = u.ce_on && u.rtd_on && (u.flags & NGRTD_WANT_LIKE) && (u.flags & NGRTD_WANT_PRIOR) &&
                       !(u.flags & NGRTD_WANT_JACOBIAN);
-    if (full) launch_fused_cf<C, true>(a, u, WB, W, logp, st);
-    else launch_fused_cf<C, false>(a, u, WB, W, logp, st);
+    if (full) launch_fused_cf<C, true>(a, u, WB, W, logp, da, st);
+    else launch_fused_cf<C, false>(a, u, WB, W, logp, da, st);
 }
 static int launch_fused(ngrtd_ctx* ctx, const RtdArgs& a, const UnitArgs& u, int64_t W, int L, double* logp,
-                        hipStream_t st) {
+                        hipStream_t st, const DemcAccept* dap = nullptr) {
     const int WB = kFusedUnits / L;
+    const DemcAccept da = dap ? *dap : DemcAccept{};
     switch (a.C) {
-    case 1: launch_fused_c<1>(a, u, WB, W, logp, st); break;
-    case 2: launch_fused_c<2>(a, u, WB, W, logp, st); break;
-    case 3: launch_fused_c<3>(a, u, WB, W, logp, st); break;
-    case 4: launch_fused_c<4>(a, u, WB, W, logp, st); break;
-    default: launch_fused_c<5>(a, u, WB, W, logp, st); break;
+    case 1: launch_fused_c<1>(a, u, WB, W, logp, da, st); break;
+    case 2: launch_fused_c<2>(a, u, WB, W, logp, da, st); break;
+    case 3: launch_fused_c<3>(a, u, WB, W, logp, da, st); break;
+    case 4: launch_fused_c<4>(a, u, WB, W, logp, da, st); break;
+    default: launch_fused_c<5>(a, u, WB, W, logp, da, st); break;
     }
     HIP_TRY(ctx, hipGetLastError());
     return NGRTD_OK;
@@ -879,7 +883,7 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
         a.conc = p->conc.d();
         set_frag(a, p->table);
         a.cheb = nullptr;
-        if (a.mod[0] == MOD_EXP && a.mod[1] == MOD_NONE && !any_lamw && p->table.C <= 5) {
+        if (a.mod[0] == MOD_EXP && a.mod[1] == MOD_NONE && !any_lamw && p->table.C <= 5 && p->dtp >= 0.0) {
             NG_CHECK(cheb_prepare(ctx, p->table, (1.0 + p->dtp) - p->tp0));
             if (p->table.cheb_ok) a.cheb = p->table.cheb.d();
         }
@@ -1001,7 +1005,8 @@ static int drain_timings(ngrtd_plan* p) {
 }
 
 // Enqueue the plan's kernels for theta (device) -> logp (device) / forward outputs.
-static int plan_run(ngrtd_plan* p, const double* theta, int64_t W, double* logp, double* ce_out, double* rtd_out) {
+static int plan_run(ngrtd_plan* p, const double* theta, int64_t W, double* logp, double* ce_out, double* rtd_out,
+                    const DemcAccept* dap = nullptr) {
     ngrtd_ctx* ctx = p->ctx;
     const int64_t U = (int64_t)p->desc.n_wells * W;
     const bool prof = ctx->profiling;
@@ -1013,15 +1018,24 @@ static int plan_run(ngrtd_plan* p, const double* theta, int64_t W, double* logp,
     u.ce_out = ce_out;
     if (!logp) u.flags = 0;
     bool fused = false;
-    if (logp && !ce_out && !rtd_out && p->desc.rtd_enabled) {
+    // single launch: the log-prob, or the forward outputs (posterior predictive,
+    // run_age_mcmc.py:251-319: concentrations from the same surrogate / exact paths)
+    if (p->desc.rtd_enabled && ((logp && !ce_out && !rtd_out) || (!logp && (ce_out || rtd_out)))) {
         RtdArgs a = p->rtd;
-        a.theta = theta; a.U = U; a.conc = nullptr;
+        a.theta = theta; a.U = U; a.conc = logp ? nullptr : rtd_out;
         if (fused_path(a, u)) {
             NG_CHECK(timed_begin(p, prof, st, &ev));
-            NG_CHECK(launch_fused(ctx, a, u, W, p->desc.n_wells, logp, st));
+            NG_CHECK(launch_fused(ctx, a, u, W, p->desc.n_wells, logp, st, dap));
             NG_CHECK(timed_end(p, prof, st, 3, ev));
             return NGRTD_OK;
         }
+    }
+    if (dap) {   // accept after the generic kernels: log-prob into logp, then one thread per walker
+        NG_CHECK(plan_run(p, theta, W, logp, nullptr, nullptr));
+        hipLaunchKernelGGL(demc_accept_kernel, dim3((unsigned)cdiv(W, 256)), dim3(256), 0, st, *dap,
+                           (const double*)logp, W);
+        HIP_TRY(ctx, hipGetLastError());
+        return NGRTD_OK;
     }
     if (p->desc.rtd_enabled) {
         RtdArgs a = p->rtd;
@@ -1124,6 +1138,42 @@ int ngrtd_plan_kernel_stats(ngrtd_plan* p, double* times_ms, int64_t* counts, in
         if (counts) counts[i] = p->stats.n[i];
     }
     if (reset) p->stats = LaunchStats{};
+    return NGRTD_OK;
+}
+
+int ngrtd_demc_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64_t n_steps, double lamb,
+                   double scaling, uint64_t seed, uint64_t step0, uint64_t* n_accepted, int32_t* accepted) {
+    if (!p) return NGRTD_ESTATE;
+    ngrtd_ctx* ctx = p->ctx;
+    if (!theta || !logp || W < 3 || W > p->max_w || n_steps < 0)
+        return set_err(ctx, NGRTD_EINVAL, "bad theta/logp/W (3 <= W <= %lld)/n_steps", (long long)p->max_w);
+    if (n_steps == 0) return NGRTD_OK;
+    hipStream_t st = S(ctx);
+    const int64_t R = (int64_t)p->desc.n_params * p->desc.n_wells, E = R * W;
+    for (auto& b : p->demc_prop) HIP_TRY(ctx, b.ensure((size_t)E * sizeof(double)));
+    HIP_TRY(ctx, p->demc_lp.ensure((size_t)W * sizeof(double)));
+    HIP_TRY(ctx, p->demc_acc.ensure((size_t)W * sizeof(int32_t)));
+    unsigned long long* cnt = reinterpret_cast<unsigned long long*>(n_accepted);
+    if (!cnt) {
+        HIP_TRY(ctx, p->demc_cnt.ensure(sizeof(unsigned long long)));
+        cnt = static_cast<unsigned long long*>(p->demc_cnt.p);
+    }
+    int32_t* acc = static_cast<int32_t*>(p->demc_acc.p);
+    double* prev = nullptr;
+    const unsigned pblocks = (unsigned)cdiv(E, 256);
+    for (int64_t s = 0; s < n_steps; ++s) {
+        double* prop = p->demc_prop[s & 1].d();
+        DemcArgs d{theta, prev, prev ? acc : nullptr, prop, W, R, lamb, scaling, seed, step0 + (uint64_t)s};
+        hipLaunchKernelGGL(demc_propose_kernel, dim3(pblocks), dim3(256), 0, st, d);
+        HIP_TRY(ctx, hipGetLastError());
+        const DemcAccept da{logp, acc, cnt, seed, step0 + (uint64_t)s};
+        NG_CHECK(plan_run(p, prop, W, p->demc_lp.d(), nullptr, nullptr, &da));
+        prev = prop;
+    }
+    DemcArgs d{theta, prev, acc, nullptr, W, R, lamb, scaling, seed, step0 + (uint64_t)n_steps};
+    hipLaunchKernelGGL(demc_propose_kernel, dim3(pblocks), dim3(256), 0, st, d);   // commit the last step
+    HIP_TRY(ctx, hipGetLastError());
+    if (accepted) HIP_TRY(ctx, hipMemcpyAsync(accepted, acc, (size_t)W * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
     return NGRTD_OK;
 }
 

@@ -120,4 +120,26 @@ struct UnitArgs {
     double bt_betaln;
 };
 
+// Metropolis accept of a device DE-MC step, done where the proposal's log-prob is formed
+// (the per-walker reduction of logp_fused_kernel, or demc_accept_kernel): the walker's
+// current log-prob lp[w] is replaced by the proposal's when accepted, acc[w] records the
+// decision for the next propose kernel, n_acc counts acceptances.
+struct DemcAccept {
+    double* lp;             // [W] current log-prob (in/out); null: plain log-prob launch
+    int32_t* acc;           // [W] out
+    unsigned long long* n_acc;
+    uint64_t seed, step;
+};
+
+// DE-MC proposal over theta rows [R][W] (demc_propose_kernel)
+struct DemcArgs {
+    double* x;              // [R][W] current state (updated in place with the previous accept)
+    const double* prev;     // [R][W] previous proposal, or null (first step of a run)
+    const int32_t* acc;     // [W] previous decisions, or null
+    double* prop;           // [R][W] new proposal, or null (commit only)
+    int64_t W, R;
+    double lamb, scaling;
+    uint64_t seed, step;
+};
+
 }  // namespace ngrtd

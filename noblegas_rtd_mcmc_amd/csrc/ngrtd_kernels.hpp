@@ -776,6 +776,18 @@ __device__ __forceinline__ void unit_conc(const RtdArgs& a, int64_t u, const dou
     }
 }
 
+// The reference's exponential weights g = (1/tau) exp(-tp/tau) / sum(...) (:184, :270)
+// are NaN for every age when exp overflows for some age (inf / inf), when every weight
+// underflows to 0 (0 / 0), and for tau = 0 or NaN; otherwise finite.  -tp/tau is monotone
+// in tp, so its extremes are at tp_0 and tp_{N-1}.
+__device__ __forceinline__ bool exp_rtd_nan(const RtdArgs& a, double tau) {
+    const double tpN = (a.N > 1) ? (double)(a.N - 1) + a.dtp : a.tp0;
+    const double x0 = (-a.tp0) / tau, xN = (-tpN) / tau;
+    const double xmax = x0 > xN ? x0 : xN;
+    return !(tau == tau) || tau == 0.0 || !(xmax == xmax) || xmax > 709.782712893384 ||
+           xmax < -745.1332191019412;
+}
+
 // Exact channel sums Y_c (matrix-core path) -> concentrations: the normaliser
 // 1 + s01 G with G = sum_{j<n} q^j = expm1(-beta n) / expm1(-beta) in closed form.
 template <int C>
@@ -789,6 +801,9 @@ __device__ __forceinline__ void mfma_unit_conc(const RtdArgs& a, int64_t u, doub
 #pragma unroll
     for (int c = 0; c < C; ++c) num[c] = a.tab0[c] + s01 * yy[c];
     unit_conc<C>(a, u, num, rden, conc);
+    const double tau = a.theta[(int64_t)a.row_tau[0] * a.U + u];
+    if (exp_rtd_nan(a, tau))
+        for (int t = 0; t < a.K; ++t) conc[t] = __builtin_nan("");
 }
 
 // lanes with tq = t finish the units of tile t: select that tile's sums
@@ -869,13 +884,77 @@ __global__ void __launch_bounds__(64 * mfma_waves(C)) rtd_exp_mfma_kernel(const 
 // (g, w') of wave 0 adds wells g, g + 64/WB, ... in order and the 64/WB partials are
 // combined by a fixed xor-shuffle tree; otherwise WB lanes add the L wells in order.
 // Both orders are fixed (deterministic, no atomics).
+// ------------------------------------------------------------- device DE-MC
+// Counter-based RNG: splitmix64 finaliser over (seed, step, stream, index); uniform in
+// (0, 1) exclusive of both ends (so log u < 0 always and a re-read decision is stable).
+__host__ __device__ __forceinline__ uint64_t rng_mix(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__host__ __device__ __forceinline__ uint64_t rng_u64(uint64_t seed, uint64_t step, uint64_t stream, uint64_t i) {
+    return rng_mix(rng_mix(rng_mix(seed ^ (stream << 56)) + step) + i);
+}
+__host__ __device__ __forceinline__ double rng_unit(uint64_t h) {
+    return ((double)(h >> 11) + 0.5) * (1.0 / 9007199254740992.0);
+}
+
+// Metropolis decision of walker w (sampler.DEMetropolis: accept iff lp* - lp > log u and
+// lp* is not NaN), applied to lp[w]; one thread per walker
+__device__ __forceinline__ void demc_decide(const DemcAccept& d, int64_t w, double lp_prop) {
+    const double cur = d.lp[w];
+    const double logu = log(rng_unit(rng_u64(d.seed, d.step, 3, (uint64_t)w)));
+    const bool acc = (lp_prop - cur) > logu && lp_prop == lp_prop;
+    d.acc[w] = acc;
+    if (acc) {
+        d.lp[w] = lp_prop;
+        atomicAdd(d.n_acc, 1ull);     // integer count: order-independent
+    }
+}
+
+__device__ __forceinline__ void walker_out(double* logp, const DemcAccept& d, int64_t w, double tot) {
+    if (logp) logp[w] = tot;
+    if (d.lp) demc_decide(d, w, tot);
+}
+
+__global__ void __launch_bounds__(256) demc_accept_kernel(const DemcAccept d, const double* __restrict__ lp_prop,
+                                                          int64_t W) {
+    const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w < W) demc_decide(d, w, lp_prop[w]);
+}
+
+// One element (row r, walker w) per thread: apply the previous step's decision to the
+// state, then (unless commit-only) draw the new proposal
+//   x* = x + lamb (x_r1 - x_r2) + U(-scaling, scaling)
+// with partners r1 != r2, both != w, drawn as sampler.DEMetropolis draws them.
+__global__ void __launch_bounds__(256) demc_propose_kernel(const DemcArgs d) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= d.R * d.W) return;
+    const int64_t w = e % d.W, row = e - w;
+    auto cur = [&](int64_t v) {   // state of walker v after the previous decision
+        return (d.prev && d.acc[v]) ? d.prev[row + v] : d.x[row + v];
+    };
+    const double xw = cur(w);
+    if (d.prev && d.acc[w]) d.x[e] = xw;
+    if (!d.prop) return;
+    const uint64_t W = (uint64_t)d.W;
+    const int64_t r1 = (int64_t)((w + 1 + rng_u64(d.seed, d.step, 1, (uint64_t)w) % (W - 1)) % W);
+    int64_t r2 = (int64_t)((r1 + 1 + rng_u64(d.seed, d.step, 2, (uint64_t)w) % (W - 2)) % W);
+    if (r2 == w) r2 = (r2 + 1) % d.W;
+    if (r2 == r1) r2 = (r2 + 1) % d.W;
+    const double eps = (2.0 * rng_unit(rng_u64(d.seed, d.step, 4, (uint64_t)e)) - 1.0) * d.scaling;
+    d.prop[e] = xw + d.lamb * (cur(r1) - cur(r2)) + eps;
+}
+
 constexpr int kFusedWaves = 8;
 constexpr int kFusedUnits = 64 * kFusedWaves;
 constexpr int kFusedPrefetch = 4;   // double2 per thread: covers kChebPieces*kChebN*6 doubles
 
 template <int C, bool FULL>
 __global__ void __launch_bounds__(64 * kFusedWaves) logp_fused_kernel(const RtdArgs a, const UnitArgs ua,
-                                                                     int32_t WB, double* __restrict__ logp) {
+                                                                     int32_t WB, double* __restrict__ logp,
+                                                                     const DemcAccept dacc) {
     constexpr int NT = mfma_tiles(C);
     constexpr int CP = cheb_cp(C);
     constexpr int TAB2 = kChebPieces * kChebN * CP / 2;   // double2 entries of the surrogate table
@@ -965,17 +1044,32 @@ __global__ void __launch_bounds__(64 * kFusedWaves) logp_fused_kernel(const RtdA
     // surrogate does not cover evaluate piece 0 here and are redone exactly below.
     double cx = 0.0;
     int cpc = a.cheb ? cheb_piece(tau, cx) : -1;
-    const bool bad = cpc < 0;
-    cpc = bad ? 0 : cpc;
+    // An uncovered tau (< 1/2, NaN) outside the support of the tau1 Uniform prior makes the
+    // unit's log-prob -inf whatever the concentrations are -- unless they are NaN, which
+    // the reference's weights produce exactly when (1/tau) exp(-tp/tau) overflows or
+    // divides by 0 (convolution_integral_utils.py:184, then g / g.sum(), :270): such a
+    // lane needs no channel sums, only that NaN predicate.  DE-MC proposals below the
+    // prior bound are common; they would otherwise send whole waves to the exact path.
+    bool skip = false, cnan = false;
+    if (cpc < 0 && a.cheb && (FULL || (ua.rtd_on && (ua.flags & NGRTD_WANT_PRIOR))) && a.row_tau[0] == ua.row_tau1 &&
+        !(tau >= ua.tau1_lo && tau <= ua.tau1_hi) && !(ua.tau1_lo < kChebTauLo && tau >= ua.tau1_lo)) {
+        skip = true;
+        cnan = exp_rtd_nan(a, tau);
+    }
+    const bool bad = cpc < 0 && !skip;
+    cpc = cpc < 0 ? 0 : cpc;
     const double th = mvalid ? unit_logp_theta(ul, mu, ml, &tp, FULL) : 0.0;
     double zz[C + 1];
     cheb_sums<C + 1>(cheb + cpc * (kChebN * CP), CP, cx, zz);   // s01 Y_c (c < C), s01 G
     double like = 0.0;
+    double conc[kMaxTracer];
     {
-        double num[C], conc[kMaxTracer];
+        double num[C];
 #pragma unroll
         for (int c = 0; c < C; ++c) num[c] = a.tab0[c] + zz[c];
         unit_conc<C>(a, mu, num, 1.0 / (1.0 + zz[C]), conc);
+        if (cnan)
+            for (int t = 0; t < a.K; ++t) conc[t] = __builtin_nan("");
         like = mvalid ? unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL) : 0.0;
     }
     NGRTD_PROBE(2);
@@ -994,14 +1088,16 @@ __global__ void __launch_bounds__(64 * kFusedWaves) logp_fused_kernel(const RtdA
         mw.finish(a, y);
         mfma_pick_tile<C>(y, mw.beta, yy, bu);   // tile tq holds this lane's unit
         if (mvalid) {
-            double conc[kMaxTracer];
             mfma_unit_conc<C>(a, mu, bu, yy, conc);
             like = unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL);
         }
     }
+    if (!FULL && a.conc && mvalid)                        // forward(): model concentrations
+        for (int t = 0; t < a.K; ++t) a.conc[(int64_t)t * a.U + mu] = conc[t];
     NGRTD_PROBE(3);
     NGRTD_PROBE(4);
     NGRTD_PROBE(5);
+    if (!logp && !dacc.lp) return;                        // forward() launch: no log-prob
     part[mi] = th + like;
     NGRTD_PROBE(6);
     __syncthreads();
@@ -1012,12 +1108,12 @@ __global__ void __launch_bounds__(64 * kFusedWaves) logp_fused_kernel(const RtdA
             double tot = 0.0;
             for (int l = g; l < L; l += G) tot += part[l * WB + wl];
             for (int off = WB; off < 64; off <<= 1) tot += __shfl_xor(tot, off);
-            if (g == 0 && w0 + wl < W) logp[w0 + wl] = tot;
+            if (g == 0 && w0 + wl < W) walker_out(logp, dacc, w0 + wl, tot);
         }
     } else if (tid < WB && w0 + tid < W) {
         double tot = part[tid];
         for (int l = 1; l < L; ++l) tot += part[l * WB + tid];
-        logp[w0 + tid] = tot;
+        walker_out(logp, dacc, w0 + tid, tot);
     }
     NGRTD_PROBE(7);
 }

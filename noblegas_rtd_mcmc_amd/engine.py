@@ -170,6 +170,19 @@ class LogProb:
                                               _lib.MEM_HOST), "ngrtd_forward")
         return ce, rt
 
+    def demc(self, theta, logp, n_steps, lamb, scaling, seed, step0=0, n_accepted=None, accepted=None):
+        """n_steps device-resident DE-MC steps (ngrtd_demc_run) on torch CUDA tensors:
+        theta [P][L][W] float64 and logp [W] float64 (its log-prob), updated in place on
+        torch's current stream.  n_accepted: optional CUDA uint64/int64 [1] counter."""
+        W = self._check_dev(theta)
+        if logp.dtype.itemsize != 8 or not logp.is_cuda or logp.numel() != W:
+            raise ValueError("logp must be a CUDA float64 tensor [W]")
+        self.ctx.check(self.lib.ngrtd_demc_run(
+            self.plan, C.c_void_p(theta.data_ptr()), C.c_void_p(logp.data_ptr()), W, int(n_steps), float(lamb),
+            float(scaling), int(seed) & (2 ** 64 - 1), int(step0) & (2 ** 64 - 1),
+            C.c_void_p(n_accepted.data_ptr() if n_accepted is not None else 0),
+            C.c_void_p(accepted.data_ptr() if accepted is not None else 0)), "ngrtd_demc_run")
+
     def kernel_stats(self, reset=False):
         ms = (C.c_double * 4)()
         n = (C.c_int64 * 4)()

@@ -89,14 +89,18 @@ class CEModel:
         nu = t[5] * (c.nu_max - c.nu_min) + c.nu_min
         return {"Ae": Ae, "F": F, "E": E, "b": b, "m": t[3], "T": T, "nu": nu}
 
-    def sample(self, nwalkers=100, tune=500, draws=500, seed=12345, tune_interval=100):
-        """Ensemble DE-MC on the GPU log-prob (replaces mc.sample, :408-415)."""
+    def sample(self, nwalkers=100, tune=500, draws=500, seed=12345, tune_interval=100, sampler="device"):
+        """Ensemble DE-MC on the GPU log-prob (replaces mc.sample, :408-415).  sampler:
+        "device" (ngrtd_demc_run, device-resident) or "torch" (DEMetropolis on torch ops)."""
         import torch
-        from .sampler import DEMetropolis
+        from .sampler import DEMetropolis, DeviceDEMetropolis
         from .workloads import sample_prior
         x0 = sample_prior(self.spec, nwalkers, np.random.default_rng(seed))
         x = torch.from_numpy(x0).to("cuda:%d" % self.device)
-        res = DEMetropolis(lambda th: self.logp(th), tune_interval=tune_interval, seed=seed).run(x, tune, draws)
+        if sampler == "device":
+            res = DeviceDEMetropolis(self.logp, tune_interval=tune_interval, seed=seed).run(x, tune, draws)
+        else:
+            res = DEMetropolis(lambda th: self.logp(th), tune_interval=tune_interval, seed=seed).run(x, tune, draws)
         res["samples"] = res["samples"].cpu().numpy()
         res["logp"] = res["logp"].cpu().numpy()
         return res

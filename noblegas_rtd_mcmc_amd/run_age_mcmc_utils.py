@@ -164,15 +164,19 @@ class conv_mcmc:
             self._lp = LogProb(self.spec(), self.max_walkers, self.device)
         return self._lp
 
-    def sample_mcmc(self, nwalkers=96, tune=10000, draws=10000, seed=123423, tune_interval=1000):
-        """Ensemble DE-MC on the GPU log-prob (replaces mc.sample, :407-429)."""
+    def sample_mcmc(self, nwalkers=96, tune=10000, draws=10000, seed=123423, tune_interval=1000, sampler="device"):
+        """Ensemble DE-MC on the GPU log-prob (replaces mc.sample, :407-429).  sampler:
+        "device" (ngrtd_demc_run, device-resident) or "torch" (DEMetropolis on torch ops)."""
         import torch
-        from .sampler import DEMetropolis
+        from .sampler import DEMetropolis, DeviceDEMetropolis
         from .workloads import sample_prior
         lp = self.build_mcmc_model_joint_sT()
         x0 = sample_prior(lp.spec, nwalkers, np.random.default_rng(seed))
         x = torch.from_numpy(x0).to("cuda:%d" % self.device)
-        res = DEMetropolis(lambda th: lp(th), tune_interval=tune_interval, seed=seed).run(x, tune, draws)
+        if sampler == "device":
+            res = DeviceDEMetropolis(lp, tune_interval=tune_interval, seed=seed).run(x, tune, draws)
+        else:
+            res = DEMetropolis(lambda th: lp(th), tune_interval=tune_interval, seed=seed).run(x, tune, draws)
         res = {k: (v.cpu().numpy() if hasattr(v, "cpu") else v) for k, v in res.items()}
         res["roles"] = list(lp.spec.roles)
         if self.savedir:

@@ -96,3 +96,57 @@ class DEMetropolis:
                 "logp": torch.stack(logps) if logps else lp[None][:0],
                 "accept_rate": float(n_acc_total) / max(1, draws * W),
                 "scaling": scaling, "lamb": lamb}
+
+
+class DeviceDEMetropolis:
+    """The same population DE-MC as DEMetropolis, run device-resident by libngrtd
+    (ngrtd_demc_run: a proposal kernel + the log-prob kernel with the Metropolis accept in
+    its per-walker reduction, 2 launches per step, counter-based random numbers).  The host
+    only intervenes every ``tune_interval`` steps (PyMC3 scaling schedule) and every
+    ``thin`` draws (sample snapshot).  Same result dict as DEMetropolis.run; the random
+    stream differs, so chains match DEMetropolis in distribution, not bit for bit."""
+
+    def __init__(self, logprob, lamb=None, scaling=1e-3, tune_interval=100, seed=123423):
+        self.lp = logprob               # engine.LogProb
+        self.lamb = lamb
+        self.scaling = scaling
+        self.tune_interval = tune_interval
+        self.seed = seed
+
+    def run(self, x0, tune, draws, thin=1, callback=None):
+        x = x0.clone().contiguous()
+        W = x.shape[-1]
+        d = int(x[..., 0].numel())
+        if W < 3:
+            raise ValueError("population DE needs at least 3 walkers")
+        lamb = self.lamb if self.lamb is not None else 2.38 / math.sqrt(2 * d)
+        lp = self.lp(x).clone()
+        cnt = torch.zeros(1, dtype=torch.int64, device=x.device)
+        scaling = self.scaling
+        step = 0
+        # tuning: chunks of tune_interval steps, PyMC3 schedule on the chunk's rate
+        while step < tune:
+            n = min(self.tune_interval, tune - step)
+            cnt.zero_()
+            self.lp.demc(x, lp, n, lamb, scaling, self.seed, step, n_accepted=cnt)
+            step += n
+            if n == self.tune_interval:
+                scaling = pymc3_tune(scaling, float(cnt.item()) / (n * W))
+            if callback is not None:
+                callback(step - 1, x, lp)
+        samples, logps = [], []
+        cnt.zero_()
+        kept = 0
+        while kept * thin < draws:
+            n = min(thin, draws - kept * thin)
+            self.lp.demc(x, lp, n, lamb, scaling, self.seed, step, n_accepted=cnt)
+            step += n
+            samples.append(x.clone())
+            logps.append(lp.clone())
+            kept += 1
+            if callback is not None:
+                callback(step - 1, x, lp)
+        return {"samples": torch.stack(samples) if samples else x[None][:0],
+                "logp": torch.stack(logps) if logps else lp[None][:0],
+                "accept_rate": float(cnt.item()) / max(1, draws * W),
+                "scaling": scaling, "lamb": lamb}

@@ -27,6 +27,9 @@ def gen_g_tp(n, index_last, t_samp, tau, mod_type, eta=None, D=None):
     """convolution_integral_utils.py:155-281 for piston / exponential / exp_pist_flow /
     dispersion, normalised by the discrete sum (:270)."""
     tp = age_grid(n, index_last, t_samp)
+    # the reference receives its parameters as numpy float64 (theano dvector elements,
+    # run_age_mcmc_utils.py:84-85): 1/0 is inf (with a warning), never ZeroDivisionError
+    tau = np.float64(tau)
     with np.errstate(all="ignore"):
         if mod_type == "piston":
             g_tp = np.zeros(len(tp))

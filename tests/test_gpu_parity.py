@@ -319,3 +319,44 @@ def test_many_wells_single_launch():
     ref = om.log_prob(spec, th, walkers=[0, 4])
     assert close(got[[0, 4]], ref, 1e-12, 1e-9).all(), (got, ref)
     lp.close()
+
+
+def test_out_of_support_tau_shortcut():
+    """DE-MC proposals below the tau prior bound: lanes whose tau the surrogate does not
+    cover and the prior excludes skip the channel sums.  Their log-prob must still be the
+    reference's: -inf, or NaN exactly where the reference's weights overflow / divide by
+    zero (tau <= 0 close to 0, NaN).  Checked against the exact path (NGRTD_NO_CHEB=1) and
+    the oracle, bit for bit in the -inf/NaN pattern."""
+    import os
+    import subprocess
+    import sys
+    import oracle.models as om
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+    spec = wl.c4_spec(L=2, N=1200)
+    W = 128
+    th = wl.sample_prior(spec, W, np.random.default_rng(41))
+    # -1.6: exp overflows at old ages (NaN); 1e-9 and 1e-300: every weight underflows (0/0)
+    special = [-5.0, -1.7, -1.6, -1.0e-3, 0.0, -0.0, 1.0e-3, 0.3, np.nan, 0.49999, -1e300, 1e-300, 1e-9, 2e-8]
+    r = spec.roles.index("tau1")
+    for i, v in enumerate(special):
+        th[r, 0, 3 * i] = v               # lanes spread over waves; well 1 stays valid
+    path = "/tmp/ngrtd_oos_%d.npy" % os.getpid()
+    np.save(path, th)
+    lp = LogProb(spec, max_walkers=W)
+    got = lp(th, soa=True)
+    code = ("import numpy as np, sys; sys.path.insert(0, %r); from noblegas_rtd_mcmc_amd import workloads as wl;"
+            "from noblegas_rtd_mcmc_amd.engine import LogProb; spec = wl.c4_spec(L=2, N=1200);"
+            "th = np.load(sys.argv[1]); lp = LogProb(spec, max_walkers=th.shape[2]);"
+            "np.save(sys.argv[1], lp(th, soa=True))" % os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    subprocess.run([sys.executable, "-c", code, path], check=True, timeout=300,
+                   env=dict(os.environ, NGRTD_NO_CHEB="1"))
+    exact = np.load(path)
+    os.remove(path)
+    assert close(got, exact, 1e-12, 1e-9).all(), np.nonzero(~close(got, exact, 1e-12, 1e-9))
+    walkers = [3 * i for i in range(len(special))]
+    ref = om.log_prob(spec, th, walkers=walkers)
+    assert np.array_equal(np.isnan(got[walkers]), np.isnan(ref)), (got[walkers], ref)
+    assert close(got[walkers], ref, 1e-12, 1e-9).all(), (got[walkers], ref)
+    assert np.isnan(got[3 * 2]) and got[0] == -np.inf     # tau = -1.6 overflows, -5 does not
+    lp.close()
