@@ -407,7 +407,7 @@ static void launch_mfma(const RtdArgs& a, const UnitArgs& u, int32_t fuse, hipSt
 // data (ce obs, 1/sd^2, sums of 0.5 log 1/sd^2, E_min; rtd obs, 1/sd^2, sums).
 static size_t fused_lds(const RtdArgs& a, const UnitArgs& u) {
     const size_t wells = (size_t)u.L * ((u.ce_on ? 2 * u.G + 2 : 0) + (u.rtd_on ? 2 * u.K + 1 : 0));
-    return (size_t)(kFusedUnits + kChebPieces * kChebN * cheb_cp(a.C) + wells) * sizeof(double);
+    return (size_t)(kFusedUnits + kFusedUnits / 2 + kChebPieces * kChebN * cheb_cp(a.C) + wells) * sizeof(double);
 }
 constexpr size_t kFusedMaxLds = 150 * 1024;
 static bool fused_path(const RtdArgs& a, const UnitArgs& u) {
@@ -1033,7 +1033,7 @@ static int plan_run(ngrtd_plan* p, const double* theta, int64_t W, double* logp,
     if (dap) {   // accept after the generic kernels: log-prob into logp, then one thread per walker
         NG_CHECK(plan_run(p, theta, W, logp, nullptr, nullptr));
         hipLaunchKernelGGL(demc_accept_kernel, dim3((unsigned)cdiv(W, 256)), dim3(256), 0, st, *dap,
-                           (const double*)logp, W);
+                           (const double*)logp, W, (int64_t)p->desc.n_params * p->desc.n_wells);
         HIP_TRY(ctx, hipGetLastError());
         return NGRTD_OK;
     }
@@ -1150,7 +1150,7 @@ int ngrtd_demc_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64_
     if (n_steps == 0) return NGRTD_OK;
     hipStream_t st = S(ctx);
     const int64_t R = (int64_t)p->desc.n_params * p->desc.n_wells, E = R * W;
-    for (auto& b : p->demc_prop) HIP_TRY(ctx, b.ensure((size_t)E * sizeof(double)));
+    HIP_TRY(ctx, p->demc_prop[0].ensure((size_t)E * sizeof(double)));
     HIP_TRY(ctx, p->demc_lp.ensure((size_t)W * sizeof(double)));
     HIP_TRY(ctx, p->demc_acc.ensure((size_t)W * sizeof(int32_t)));
     unsigned long long* cnt = reinterpret_cast<unsigned long long*>(n_accepted);
@@ -1159,20 +1159,16 @@ int ngrtd_demc_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64_
         cnt = static_cast<unsigned long long*>(p->demc_cnt.p);
     }
     int32_t* acc = static_cast<int32_t*>(p->demc_acc.p);
-    double* prev = nullptr;
-    const unsigned pblocks = (unsigned)cdiv(E, 256);
+    double* prop = p->demc_prop[0].d();
+    const dim3 pgrid((unsigned)cdiv(W, 256), (unsigned)cdiv(R, kDemcRows));
     for (int64_t s = 0; s < n_steps; ++s) {
-        double* prop = p->demc_prop[s & 1].d();
-        DemcArgs d{theta, prev, prev ? acc : nullptr, prop, W, R, lamb, scaling, seed, step0 + (uint64_t)s};
-        hipLaunchKernelGGL(demc_propose_kernel, dim3(pblocks), dim3(256), 0, st, d);
+        const uint64_t key = demc_key(seed, step0 + (uint64_t)s);
+        DemcArgs d{theta, prop, W, R, lamb, scaling, key};
+        hipLaunchKernelGGL(demc_propose_kernel, pgrid, dim3(256), 0, st, d);
         HIP_TRY(ctx, hipGetLastError());
-        const DemcAccept da{logp, acc, cnt, seed, step0 + (uint64_t)s};
+        const DemcAccept da{logp, acc, cnt, theta, prop, p->desc.n_params, key};
         NG_CHECK(plan_run(p, prop, W, p->demc_lp.d(), nullptr, nullptr, &da));
-        prev = prop;
     }
-    DemcArgs d{theta, prev, acc, nullptr, W, R, lamb, scaling, seed, step0 + (uint64_t)n_steps};
-    hipLaunchKernelGGL(demc_propose_kernel, dim3(pblocks), dim3(256), 0, st, d);   // commit the last step
-    HIP_TRY(ctx, hipGetLastError());
     if (accepted) HIP_TRY(ctx, hipMemcpyAsync(accepted, acc, (size_t)W * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
     return NGRTD_OK;
 }

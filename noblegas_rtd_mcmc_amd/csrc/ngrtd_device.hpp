@@ -122,24 +122,25 @@ struct UnitArgs {
 
 // Metropolis accept of a device DE-MC step, done where the proposal's log-prob is formed
 // (the per-walker reduction of logp_fused_kernel, or demc_accept_kernel): the walker's
-// current log-prob lp[w] is replaced by the proposal's when accepted, acc[w] records the
-// decision for the next propose kernel, n_acc counts acceptances.
+// current log-prob lp[w] is replaced by the proposal's when accepted and its theta rows
+// are copied from the proposal, acc[w] records the decision, n_acc counts acceptances.
 struct DemcAccept {
     double* lp;             // [W] current log-prob (in/out); null: plain log-prob launch
     int32_t* acc;           // [W] out
     unsigned long long* n_acc;
-    uint64_t seed, step;
+    double* x;              // [P][L][W] current state, updated for accepted walkers
+    const double* prop;     // [P][L][W] the proposal being evaluated
+    int32_t P;              // parameter rows per (walker, well)
+    uint64_t key;           // per-step random key (demc_key)
 };
 
 // DE-MC proposal over theta rows [R][W] (demc_propose_kernel)
 struct DemcArgs {
-    double* x;              // [R][W] current state (updated in place with the previous accept)
-    const double* prev;     // [R][W] previous proposal, or null (first step of a run)
-    const int32_t* acc;     // [W] previous decisions, or null
-    double* prop;           // [R][W] new proposal, or null (commit only)
+    const double* x;        // [R][W] current state
+    double* prop;           // [R][W] new proposal
     int64_t W, R;
     double lamb, scaling;
-    uint64_t seed, step;
+    uint64_t key;           // per-step random key (demc_key)
 };
 
 }  // namespace ngrtd

@@ -885,66 +885,72 @@ __global__ void __launch_bounds__(64 * mfma_waves(C)) rtd_exp_mfma_kernel(const 
 // combined by a fixed xor-shuffle tree; otherwise WB lanes add the L wells in order.
 // Both orders are fixed (deterministic, no atomics).
 // ------------------------------------------------------------- device DE-MC
-// Counter-based RNG: splitmix64 finaliser over (seed, step, stream, index); uniform in
-// (0, 1) exclusive of both ends (so log u < 0 always and a re-read decision is stable).
+// Counter-based RNG: splitmix64 finaliser.  Per step one key = mix(mix(seed) + step);
+// stream s of the step is mix(key + s) (1: partners, 2: proposal noise, 3: accept), and
+// draw i of a stream is mix(stream + i).  Uniforms lie in (0, 1) exclusive of both ends.
 __host__ __device__ __forceinline__ uint64_t rng_mix(uint64_t z) {
     z += 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
 }
-__host__ __device__ __forceinline__ uint64_t rng_u64(uint64_t seed, uint64_t step, uint64_t stream, uint64_t i) {
-    return rng_mix(rng_mix(rng_mix(seed ^ (stream << 56)) + step) + i);
+__host__ __device__ __forceinline__ uint64_t demc_key(uint64_t seed, uint64_t step) {
+    return rng_mix(rng_mix(seed) + step);
 }
 __host__ __device__ __forceinline__ double rng_unit(uint64_t h) {
     return ((double)(h >> 11) + 0.5) * (1.0 / 9007199254740992.0);
 }
 
 // Metropolis decision of walker w (sampler.DEMetropolis: accept iff lp* - lp > log u and
-// lp* is not NaN), applied to lp[w]; one thread per walker
-__device__ __forceinline__ void demc_decide(const DemcAccept& d, int64_t w, double lp_prop) {
+// lp* is not NaN), applied to lp[w]; one thread per walker.  Returns the decision.
+__device__ __forceinline__ bool demc_decide(const DemcAccept& d, int64_t w, double lp_prop) {
     const double cur = d.lp[w];
-    const double logu = log(rng_unit(rng_u64(d.seed, d.step, 3, (uint64_t)w)));
+    const double logu = log(rng_unit(rng_mix(rng_mix(d.key + 3) + (uint64_t)w)));
     const bool acc = (lp_prop - cur) > logu && lp_prop == lp_prop;
     d.acc[w] = acc;
     if (acc) {
         d.lp[w] = lp_prop;
         atomicAdd(d.n_acc, 1ull);     // integer count: order-independent
     }
+    return acc;
 }
 
-__device__ __forceinline__ void walker_out(double* logp, const DemcAccept& d, int64_t w, double tot) {
-    if (logp) logp[w] = tot;
-    if (d.lp) demc_decide(d, w, tot);
-}
-
+// accept after the generic kernels: one thread per walker decides and copies the
+// walker's P*L proposal rows into the state (coalesced across the walkers of a wave)
 __global__ void __launch_bounds__(256) demc_accept_kernel(const DemcAccept d, const double* __restrict__ lp_prop,
-                                                          int64_t W) {
+                                                          int64_t W, int64_t R) {
     const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (w < W) demc_decide(d, w, lp_prop[w]);
+    if (w >= W) return;
+    if (demc_decide(d, w, lp_prop[w]))
+        for (int64_t r = 0; r < R; ++r) d.x[r * W + w] = d.prop[r * W + w];
 }
 
-// One element (row r, walker w) per thread: apply the previous step's decision to the
-// state, then (unless commit-only) draw the new proposal
-//   x* = x + lamb (x_r1 - x_r2) + U(-scaling, scaling)
-// with partners r1 != r2, both != w, drawn as sampler.DEMetropolis draws them.
+// Proposal x* = x + lamb (x_r1 - x_r2) + U(-scaling, scaling) for walker w over rows
+// [r0, r0 + kDemcRows): partners r1 != r2, both != w, drawn once per thread as
+// sampler.DEMetropolis draws them; walkers on x (coalesced), row chunks on y.
+constexpr int kDemcRows = 8;
 __global__ void __launch_bounds__(256) demc_propose_kernel(const DemcArgs d) {
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= d.R * d.W) return;
-    const int64_t w = e % d.W, row = e - w;
-    auto cur = [&](int64_t v) {   // state of walker v after the previous decision
-        return (d.prev && d.acc[v]) ? d.prev[row + v] : d.x[row + v];
-    };
-    const double xw = cur(w);
-    if (d.prev && d.acc[w]) d.x[e] = xw;
-    if (!d.prop) return;
-    const uint64_t W = (uint64_t)d.W;
-    const int64_t r1 = (int64_t)((w + 1 + rng_u64(d.seed, d.step, 1, (uint64_t)w) % (W - 1)) % W);
-    int64_t r2 = (int64_t)((r1 + 1 + rng_u64(d.seed, d.step, 2, (uint64_t)w) % (W - 2)) % W);
-    if (r2 == w) r2 = (r2 + 1) % d.W;
-    if (r2 == r1) r2 = (r2 + 1) % d.W;
-    const double eps = (2.0 * rng_unit(rng_u64(d.seed, d.step, 4, (uint64_t)e)) - 1.0) * d.scaling;
-    d.prop[e] = xw + d.lamb * (cur(r1) - cur(r2)) + eps;
+    const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= d.W) return;
+    const uint32_t W = (uint32_t)d.W;
+    const uint64_t hp = rng_mix(rng_mix(d.key + 1) + (uint64_t)w);
+    const uint32_t r1 = (uint32_t)((w + 1 + (uint32_t)(hp >> 32) % (W - 1)) % W);
+    uint32_t r2 = (r1 + 1 + (uint32_t)hp % (W - 2)) % W;
+    if (r2 == (uint32_t)w) r2 = (r2 + 1) % W;
+    if (r2 == r1) r2 = (r2 + 1) % W;
+    const uint64_t ke = rng_mix(d.key + 2);
+    const int64_t r0 = (int64_t)blockIdx.y * kDemcRows;
+#pragma unroll 4
+    for (int64_t r = r0; r < r0 + kDemcRows && r < d.R; ++r) {
+        const int64_t row = r * d.W, e = row + w;
+        const double eps = (2.0 * rng_unit(rng_mix(ke + (uint64_t)e)) - 1.0) * d.scaling;
+        d.prop[e] = d.x[e] + d.lamb * (d.x[row + r1] - d.x[row + r2]) + eps;
+    }
+}
+
+__device__ __forceinline__ void walker_out(double* logp, const DemcAccept& d, int64_t w, double tot, int* dec) {
+    if (logp) logp[w] = tot;
+    if (d.lp) *dec = demc_decide(d, w, tot);
 }
 
 constexpr int kFusedWaves = 8;
@@ -962,7 +968,8 @@ __global__ void __launch_bounds__(64 * kFusedWaves) logp_fused_kernel(const RtdA
     static_assert(TAB2 <= kFusedPrefetch * 64 * kFusedWaves, "prefetch covers the table");
     extern __shared__ __attribute__((aligned(16))) double lds[];
     double* part = lds;                                   // [512] per-unit log-prob
-    double* cheb = lds + kFusedUnits;                     // [kChebPieces][kChebN][CP]
+    int* dec = reinterpret_cast<int*>(lds + kFusedUnits);  // [512] DE-MC decisions per walker
+    double* cheb = lds + kFusedUnits + kFusedUnits / 2;   // [kChebPieces][kChebN][CP]
     NGRTD_PROBE(0);
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
@@ -1108,12 +1115,17 @@ __global__ void __launch_bounds__(64 * kFusedWaves) logp_fused_kernel(const RtdA
             double tot = 0.0;
             for (int l = g; l < L; l += G) tot += part[l * WB + wl];
             for (int off = WB; off < 64; off <<= 1) tot += __shfl_xor(tot, off);
-            if (g == 0 && w0 + wl < W) walker_out(logp, dacc, w0 + wl, tot);
+            if (g == 0 && w0 + wl < W) walker_out(logp, dacc, w0 + wl, tot, dec + wl);
         }
     } else if (tid < WB && w0 + tid < W) {
         double tot = part[tid];
         for (int l = 1; l < L; ++l) tot += part[l * WB + tid];
-        walker_out(logp, dacc, w0 + tid, tot);
+        walker_out(logp, dacc, w0 + tid, tot, dec + tid);
+    }
+    if (dacc.lp) {   // DE-MC: accepted walkers take the proposal's theta rows of this unit
+        __syncthreads();
+        if (mvalid && dec[mwl])
+            for (int p = 0; p < dacc.P; ++p) dacc.x[(int64_t)p * a.U + mu] = dacc.prop[(int64_t)p * a.U + mu];
     }
     NGRTD_PROBE(7);
 }

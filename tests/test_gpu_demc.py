@@ -17,8 +17,8 @@ def mix(z):
     return z ^ (z >> 31)
 
 
-def u64(seed, step, stream, i):
-    return mix((mix((mix(seed ^ (stream << 56)) + step) & M64) + i) & M64)
+def key(seed, step):
+    return mix((mix(seed) + step) & M64)
 
 
 def unit(h):
@@ -29,22 +29,25 @@ def numpy_step(x, lp, lp_fn, lamb, scaling, seed, step):
     """One step of ngrtd_demc_run restated (csrc/ngrtd_kernels.hpp demc_propose_kernel,
     demc_decide); x [R][W]."""
     R, W = x.shape
+    k = key(seed, step)
+    k1, k2, k3 = mix((k + 1) & M64), mix((k + 2) & M64), mix((k + 3) & M64)
     prop = np.empty_like(x)
     for w in range(W):
-        r1 = (w + 1 + u64(seed, step, 1, w) % (W - 1)) % W
-        r2 = (r1 + 1 + u64(seed, step, 2, w) % (W - 2)) % W
+        hp = mix((k1 + w) & M64)
+        r1 = (w + 1 + (hp >> 32) % (W - 1)) % W
+        r2 = (r1 + 1 + (hp & 0xFFFFFFFF) % (W - 2)) % W
         if r2 == w:
             r2 = (r2 + 1) % W
         if r2 == r1:
             r2 = (r2 + 1) % W
         for r in range(R):
             e = r * W + w
-            eps = (2.0 * unit(u64(seed, step, 4, e)) - 1.0) * scaling
+            eps = (2.0 * unit(mix((k2 + e) & M64)) - 1.0) * scaling
             prop[r, w] = x[r, w] + lamb * (x[r, r1] - x[r, r2]) + eps
     lpp = lp_fn(prop)
     out_x, out_lp, acc = x.copy(), lp.copy(), np.zeros(W, bool)
     for w in range(W):
-        logu = np.log(unit(u64(seed, step, 3, w)))
+        logu = np.log(unit(mix((k3 + w) & M64)))
         if (lpp[w] - lp[w]) > logu and lpp[w] == lpp[w]:
             acc[w] = True
             out_x[:, w] = prop[:, w]
