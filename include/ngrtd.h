@@ -96,6 +96,46 @@ int ngrtd_ce_forward(ngrtd_ctx* ctx, int32_t what, int32_t p_mode,
                      const double* P, const double* S, int64_t n,
                      const int32_t* gas_ids, int32_t n_gases, double* out, int32_t mem);
 
+/* -------------------------------------- prep ensemble propagation (He, CFC, SF6)
+ * The CE posterior ensemble pushed through to tracer observations
+ * (age_modeling_mcmc.prep.py:247-397), one element per ensemble member.  Inputs are
+ * per-member arrays [n]; outputs are structure-of-arrays.
+ *
+ * ngrtd_he_comps replaces ng_parse(obs_dict, Ae, F, E, T).He_comps(Rterr)
+ * (utils/noble_gas_utils.py:380-422): out[k][n] for k = enum ngrtd_he_out, the
+ * obs_dict_ entries He4_eq, He4_atm, He4_ter, He4_del, He3_tu.  Rterr may be NULL to use
+ * Rterr_const for every member (prep.py:341 passes a constant list).                 */
+enum ngrtd_he_out { NGRTD_HE_EQ = 0, NGRTD_HE_ATM = 1, NGRTD_HE_TER = 2, NGRTD_HE_DEL = 3, NGRTD_HE_TU = 4,
+                    NGRTD_HE_NOUT = 5 };
+int ngrtd_he_comps(ngrtd_ctx* ctx, const double* He4_obs, const double* He3_obs, const double* Ae,
+                   const double* F, const double* E, const double* T, const double* Rterr,
+                   double Rterr_const, int64_t n, double* out, int32_t mem);
+
+/* ngrtd_cfc_corr replaces the methods of cfc_ce_corr(cfc_num, E, T, Ae, F, S) and
+ * sf6_ce_corr(E, T, Ae, F, S) (utils/cfc_utils.py:25-306) for n members and n_species
+ * species (enum ngrtd_cfc_species; NGRTD_SF6 selects the sf6_ce_corr unit factors).
+ *   what = NGRTD_CFC_EQUIL_AIR  equil_air_conc_*(x = C_meas)  :86-106, :229-249
+ *          NGRTD_CFC_EQUIL_AQ   equil_aq_conc_*(x = z_i)      :108-124, :264-278
+ *          NGRTD_CFC_CE_EXC     ce_exc_conc_*(x = z_i), with P = self.P [atm]  :126-142, :280-296
+ *          NGRTD_CFC_SOLUBILITY solubility_cfc / _sf6          :64-84, :208-221
+ *          NGRTD_CFC_VAPOR_PRESSURE_ATM, NGRTD_CFC_LAPSE_RATE_ATM  ([n] outputs)
+ * x and out are [n_species][n].  Ae is self.Ae: the constructor's Ae*1000. [ccSTP/kg] (:30).
+ * S, P, x may be NULL when the entry does not read them (S NULL = 0.0).             */
+#define NGRTD_MAX_CFC 4
+enum ngrtd_cfc_species { NGRTD_CFC11 = 0, NGRTD_CFC12 = 1, NGRTD_CFC113 = 2, NGRTD_SF6 = 3 };
+enum ngrtd_cfc_what {
+    NGRTD_CFC_EQUIL_AIR = 0,
+    NGRTD_CFC_EQUIL_AQ = 1,
+    NGRTD_CFC_CE_EXC = 2,
+    NGRTD_CFC_SOLUBILITY = 3,
+    NGRTD_CFC_VAPOR_PRESSURE_ATM = 4,
+    NGRTD_CFC_LAPSE_RATE_ATM = 5
+};
+int ngrtd_cfc_corr(ngrtd_ctx* ctx, int32_t what, const int32_t* species, int32_t n_species,
+                   const double* E, const double* T, const double* Ae, const double* F,
+                   const double* S, const double* P, const double* x, int64_t n, double* out,
+                   int32_t mem);
+
 /* ----------------------------------------------------------- RTD series
  * The C_t input of tracer_conv_integral(C_t, t_samp) (convolution_integral_utils.py:106):
  *   c_by_age[k]   = np.flip(C_t.to_numpy().ravel())[k]  (age k, :336)

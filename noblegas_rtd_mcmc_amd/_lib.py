@@ -20,6 +20,10 @@ MOD_NONE = -1
 CE_WHAT = {"ce_total": 0, "ce_excess": 1, "equil_dry": 2, "equil": 3, "solubility": 4,
            "vapor_pressure": 5, "pressure": 6}
 P_MODE = {"lapse_rate": 0, "1atm": 1, "given": 2}
+HE_OUT = ("He4_eq", "He4_atm", "He4_ter", "He4_del", "He3_tu")       # enum ngrtd_he_out
+CFC_SPECIES = {11: 0, 12: 1, 113: 2, "SF6": 3}                      # enum ngrtd_cfc_species
+CFC_WHAT = {"equil_air": 0, "equil_aq": 1, "ce_exc": 2, "solubility": 3, "vapor_pressure_atm": 4,
+            "lapse_rate_atm": 5}
 WANT_LIKE, WANT_PRIOR, WANT_JACOBIAN = 1, 2, 4
 
 _dp = C.POINTER(C.c_double)
@@ -67,6 +71,9 @@ PROTOTYPES = {
     "ngrtd_set_profiling": (C.c_int, [C.c_void_p, C.c_int]),
     "ngrtd_ce_forward": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                    C.c_void_p, C.c_void_p, C.c_int64, _i32p, C.c_int32, C.c_void_p, C.c_int32]),
+    "ngrtd_he_comps": (C.c_int, [C.c_void_p] + [C.c_void_p] * 7 + [C.c_double, C.c_int64, C.c_void_p, C.c_int32]),
+    "ngrtd_cfc_corr": (C.c_int, [C.c_void_p, C.c_int32, _i32p, C.c_int32] + [C.c_void_p] * 7
+                       + [C.c_int64, C.c_void_p, C.c_int32]),
     "ngrtd_series_create": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int64, C.c_double, _i32p]),
     "ngrtd_series_destroy": (C.c_int, [C.c_void_p, C.c_int32]),
     "ngrtd_conv": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,

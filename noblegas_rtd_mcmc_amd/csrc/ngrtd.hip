@@ -20,6 +20,7 @@
 
 #include "../../include/ngrtd.h"
 #include "ngrtd_kernels.hpp"
+#include "ngrtd_prep.hpp"
 
 using namespace ngrtd;
 
@@ -588,6 +589,90 @@ int ngrtd_ce_forward(ngrtd_ctx* ctx, int32_t what, int32_t p_mode, const double*
         a.out = ctx->stage[6].d();
     }
     hipLaunchKernelGGL(ce_forward_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, S(ctx), a);
+    HIP_TRY(ctx, hipGetLastError());
+    if (mem != NGRTD_MEM_DEVICE) {
+        HIP_TRY(ctx, hipMemcpyAsync(out, a.out, (size_t)nout * sizeof(double), hipMemcpyDeviceToHost, S(ctx)));
+        HIP_TRY(ctx, hipStreamSynchronize(S(ctx)));
+    }
+    return NGRTD_OK;
+}
+
+// ---------------------------------------------------- prep ensemble propagation
+int ngrtd_he_comps(ngrtd_ctx* ctx, const double* He4_obs, const double* He3_obs, const double* Ae,
+                   const double* F, const double* E, const double* T, const double* Rterr, double Rterr_const,
+                   int64_t n, double* out, int32_t mem) {
+    if (!ctx) return NGRTD_ESTATE;
+    if (n < 0 || !out) return set_err(ctx, NGRTD_EINVAL, "bad n/out");
+    if (!He4_obs || !He3_obs || !Ae || !F || !E || !T)
+        return set_err(ctx, NGRTD_EINVAL, "He4_obs, He3_obs, Ae, F, E, T are required");
+    if (n == 0) return NGRTD_OK;
+    HeCompsArgs a{};
+    a.n = n;
+    a.Rterr_c = Rterr_const;
+    NG_CHECK(stage_in(ctx, 0, He4_obs, n, mem, &a.He4));
+    NG_CHECK(stage_in(ctx, 1, He3_obs, n, mem, &a.He3));
+    NG_CHECK(stage_in(ctx, 2, Ae, n, mem, &a.Ae));
+    NG_CHECK(stage_in(ctx, 3, F, n, mem, &a.F));
+    NG_CHECK(stage_in(ctx, 4, E, n, mem, &a.E));
+    NG_CHECK(stage_in(ctx, 5, T, n, mem, &a.T));
+    NG_CHECK(stage_in(ctx, 6, Rterr, n, mem, &a.Rterr));
+    const int64_t nout = n * NGRTD_HE_NOUT;
+    if (mem == NGRTD_MEM_DEVICE) {
+        a.out = out;
+    } else {
+        HIP_TRY(ctx, ctx->stage[7].ensure((size_t)nout * sizeof(double)));
+        a.out = ctx->stage[7].d();
+    }
+    hipLaunchKernelGGL(he_comps_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, S(ctx), a);
+    HIP_TRY(ctx, hipGetLastError());
+    if (mem != NGRTD_MEM_DEVICE) {
+        HIP_TRY(ctx, hipMemcpyAsync(out, a.out, (size_t)nout * sizeof(double), hipMemcpyDeviceToHost, S(ctx)));
+        HIP_TRY(ctx, hipStreamSynchronize(S(ctx)));
+    }
+    return NGRTD_OK;
+}
+
+int ngrtd_cfc_corr(ngrtd_ctx* ctx, int32_t what, const int32_t* species, int32_t n_species, const double* E,
+                   const double* T, const double* Ae, const double* F, const double* Sal, const double* P,
+                   const double* x, int64_t n, double* out, int32_t mem) {
+    if (!ctx) return NGRTD_ESTATE;
+    if (n < 0 || !out) return set_err(ctx, NGRTD_EINVAL, "bad n/out");
+    if (what < 0 || what > NGRTD_CFC_LAPSE_RATE_ATM) return set_err(ctx, NGRTD_EINVAL, "bad 'what' %d", what);
+    const bool scalar_out = (what == NGRTD_CFC_VAPOR_PRESSURE_ATM || what == NGRTD_CFC_LAPSE_RATE_ATM);
+    if (!scalar_out) {
+        if (n_species < 1 || n_species > NGRTD_MAX_CFC || !species)
+            return set_err(ctx, NGRTD_EINVAL, "n_species must be 1..%d", NGRTD_MAX_CFC);
+        if ((what == NGRTD_CFC_EQUIL_AIR || what == NGRTD_CFC_EQUIL_AQ || what == NGRTD_CFC_CE_EXC) && !x)
+            return set_err(ctx, NGRTD_EINVAL, "x (C_meas / z_i) required");
+        if (what == NGRTD_CFC_CE_EXC && !P) return set_err(ctx, NGRTD_EINVAL, "P (self.P, atm) required for ce_exc");
+    }
+    if (what == NGRTD_CFC_LAPSE_RATE_ATM ? !E : !T) return set_err(ctx, NGRTD_EINVAL, "E / T required");
+    if (!scalar_out && (!E || !Ae || !F)) return set_err(ctx, NGRTD_EINVAL, "E, T, Ae, F are required");
+    if (n == 0) return NGRTD_OK;
+    CfcArgs a{};
+    a.what = what;
+    a.ns = scalar_out ? 1 : n_species;
+    a.n = n;
+    for (int j = 0; j < (scalar_out ? 0 : n_species); ++j) {
+        if (species[j] < 0 || species[j] > NGRTD_SF6) return set_err(ctx, NGRTD_EINVAL, "bad species %d", species[j]);
+        a.sp[j] = species[j];
+    }
+    NG_CHECK(stage_in(ctx, 0, E, n, mem, &a.E));
+    NG_CHECK(stage_in(ctx, 1, T, n, mem, &a.T));
+    NG_CHECK(stage_in(ctx, 2, scalar_out ? nullptr : Ae, n, mem, &a.Ae));
+    NG_CHECK(stage_in(ctx, 3, scalar_out ? nullptr : F, n, mem, &a.F));
+    NG_CHECK(stage_in(ctx, 4, scalar_out ? nullptr : Sal, n, mem, &a.S));
+    NG_CHECK(stage_in(ctx, 5, what == NGRTD_CFC_CE_EXC ? P : nullptr, n, mem, &a.P));
+    const bool reads_x = (what == NGRTD_CFC_EQUIL_AIR || what == NGRTD_CFC_EQUIL_AQ || what == NGRTD_CFC_CE_EXC);
+    NG_CHECK(stage_in(ctx, 6, reads_x ? x : nullptr, n * a.ns, mem, &a.x));
+    const int64_t nout = n * a.ns;
+    if (mem == NGRTD_MEM_DEVICE) {
+        a.out = out;
+    } else {
+        HIP_TRY(ctx, ctx->stage[7].ensure((size_t)nout * sizeof(double)));
+        a.out = ctx->stage[7].d();
+    }
+    hipLaunchKernelGGL(cfc_corr_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, S(ctx), a);
     HIP_TRY(ctx, hipGetLastError());
     if (mem != NGRTD_MEM_DEVICE) {
         HIP_TRY(ctx, hipMemcpyAsync(out, a.out, (size_t)nout * sizeof(double), hipMemcpyDeviceToHost, S(ctx)));

@@ -136,3 +136,48 @@ def F_w(C_i, T, S, E, Ae, F):
     R_atm = {g: C_i_atm[g] / C_i_atm['Ar'] for g in C_i_atm}
     R_smp = {g: C_i[g] / C_i['Ar'] for g in C_i}
     return {'F_' + g: R_smp[g] / R_atm[g] for g in R_atm}
+
+
+def _he_comps_call(He4, He3, Ae, F, E, T, Rterr, device=0):
+    """One ngrtd_he_comps launch over broadcast arrays -> ([5][n] SoA, shape)."""
+    arrs = np.broadcast_arrays(*[np.asarray(x, dtype=np.float64) for x in (He4, He3, Ae, F, E, T, Rterr)])
+    shape = arrs[0].shape
+    flat = [np.ascontiguousarray(a.ravel()) for a in arrs]
+    n = flat[0].size
+    ctx = _lib.Context.get(device)
+    out = np.empty((len(_lib.HE_OUT), n))
+    ptr = [a.ctypes.data_as(C.c_void_p) for a in flat]
+    ctx.check(ctx.lib.ngrtd_he_comps(ctx.h, *ptr, 0.0, n, out.ctypes.data_as(C.c_void_p), _lib.MEM_HOST),
+              "ngrtd_he_comps")
+    return out, shape
+
+
+class ng_parse:
+    """utils/noble_gas_utils.py:380-444 on the GPU.  obs_dict holds one well's
+    observations (keys He4, He3, ...); Ae, F, E, T (and the obs values) may be numpy arrays
+    of ensemble members, evaluated in one launch (age_modeling_mcmc.prep.py:356-382 loops
+    over them one object at a time)."""
+
+    def __init__(self, obs_dict, Ae, F, E, T):
+        self.obs_dict = obs_dict
+        self.Ae = Ae
+        self.F = F
+        self.E = E
+        self.T = T
+        self.obs_dict_ = obs_dict.copy()
+
+    def He_comps(self, Rterr):
+        """:394-422 -- adds He4_eq, He4_atm, He4_ter, He4_del, He3_tu to obs_dict_."""
+        v, shape = _he_comps_call(self.obs_dict['He4'], self.obs_dict['He3'], self.Ae, self.F, self.E, self.T,
+                                  Rterr)
+        for k, name in enumerate(_lib.HE_OUT):
+            self.obs_dict_[name] = _unwrap(v[k], shape)
+
+    def Ne_del(self):
+        """:425-432 -- delta Ne [%] against the wet equilibrium.  (The reference body calls
+        ``ng.noble_gas_fun``, a name its module never defines, so it raises NameError there;
+        this is the computation it spells out.)"""
+        Ne_obs = self.obs_dict_['Ne']
+        ng_ = noble_gas_fun(gases=['Ne'], E=self.E, T=self.T, Ae=self.Ae, F=self.F, P='lapse_rate')
+        Ne_atm = ng_.equil_conc()['Ne']
+        self.obs_dict_['Ne_del'] = (Ne_obs / Ne_atm - 1) * 100

@@ -18,6 +18,8 @@ Fixtures (all float64):
                      N in {1200, 25256} x seeded params + edge cases; gen_g_tp() vectors.
   fwd_golden.npz     ForwardMod compositions (BMM, thalf_cfc, lamsf6, sampled J) built
                      from the reference class per run_age_mcmc_utils.py:81-163.
+  prep_golden.npz    ng_parse.He_comps and cfc_ce_corr / sf6_ce_corr outputs (prep-stage
+                     ensemble propagation) for 2048 seeded members + branch edges.
   logp_golden.npz    per-walker log-probs of small CE / RTD / joint workloads: reference
                      forward models + scipy.stats log-densities.
 """
@@ -380,9 +382,63 @@ def make_logp(conv, ng):
     np.savez_compressed(os.path.join(HERE, "logp_golden.npz"), **out)
 
 
+def make_prep(ng):
+    """ng_parse.He_comps (noble_gas_utils.py:394-422) and cfc_utils.cfc_ce_corr /
+    sf6_ce_corr (cfc_utils.py:25-306), one reference object per member as
+    age_modeling_mcmc.prep.py:247-397 builds them."""
+    sys.path.insert(0, os.path.join(REF, "utils"))
+    import cfc_utils  # noqa: E402
+    rng = np.random.default_rng(2002)
+    n = 2048
+    E = rng.uniform(2500.0, 3400.0, n)
+    T = rng.uniform(-3.0, 20.0, n)
+    Ae = 10 ** rng.uniform(-4, -1, n)
+    F = rng.uniform(0.0, 1.0, n)
+    T[:6] = [0.0, -0.5, 99.0, 99.5, 65.0, 120.0]     # T<0 sentinel, Antoine / Setchenow branches
+    He4 = rng.normal(6.0e-8, 2.0e-8, n)
+    He3 = rng.normal(1.0e-13, 3.0e-14, n)
+    Rterr = 10 ** (rng.beta(2, 2, n) * 2.0 + np.log10(2.e-8) - 1.0)
+    he = np.zeros((5, n))
+    keys = ["He4_eq", "He4_atm", "He4_ter", "He4_del", "He3_tu"]
+    for i in range(n):
+        ngp = ng.ng_parse({"He4": float(He4[i]), "He3": float(He3[i])}, float(Ae[i]), float(F[i]),
+                          float(E[i]), float(T[i]))
+        ngp.He_comps(float(Rterr[i]))
+        he[:, i] = [ngp.obs_dict_[k] for k in keys]
+    S = np.zeros(n)
+    S[1024:1280] = rng.uniform(0.0, 35.0, 256)
+    cmeas = np.stack([rng.lognormal(np.log(2.5), 0.3, n), rng.lognormal(np.log(1.2), 0.3, n),
+                      rng.lognormal(np.log(0.25), 0.3, n)])
+    sf6_meas = rng.lognormal(np.log(1.5), 0.3, n)
+    z_in = np.stack([rng.uniform(200, 300, n), rng.uniform(400, 550, n), rng.uniform(60, 90, n)])
+    sf6_z = rng.uniform(2, 12, n)
+    out = dict(E=E, T=T, Ae=Ae, F=F, He4=He4, He3=He3, Rterr=Rterr, he=he, S=S, cmeas=cmeas,
+               sf6_meas=sf6_meas, z_in=z_in, sf6_z=sf6_z)
+    res = {k: np.zeros((3, n)) for k in ("cfc_air", "cfc_aq", "cfc_exc", "cfc_sol")}
+    res.update({k: np.zeros(n) for k in ("sf6_air", "sf6_aq", "sf6_exc", "sf6_sol", "pv_atm", "p_atm")})
+    for i in range(n):
+        c = cfc_utils.cfc_ce_corr(cfc_num=[11, 12, 113], E=float(E[i]), T=float(T[i]), Ae=float(Ae[i]),
+                                  F=float(F[i]), S=float(S[i]))
+        res["cfc_air"][:, i] = c.equil_air_conc_cfc(cmeas[:, i].copy())    # sets self.P
+        res["cfc_aq"][:, i] = c.equil_aq_conc_cfc(z_in[:, i].copy())
+        res["cfc_exc"][:, i] = c.ce_exc_conc_cfc(z_in[:, i].copy())
+        res["cfc_sol"][:, i] = c.solubility_cfc()
+        res["pv_atm"][i] = c.vapor_pressure_atm()
+        res["p_atm"][i] = c.lapse_rate_atm()
+        s6 = cfc_utils.sf6_ce_corr(E=float(E[i]), T=float(T[i]), Ae=float(Ae[i]), F=float(F[i]), S=float(S[i]))
+        res["sf6_air"][i] = s6.equil_air_conc_sf6(float(sf6_meas[i]))
+        res["sf6_aq"][i] = s6.equil_aq_conc_sf6(float(sf6_z[i]))
+        res["sf6_exc"][i] = s6.ce_exc_conc_sf6(float(sf6_z[i]))
+        res["sf6_sol"][i] = s6.solubility_sf6()
+    out.update(res)
+    np.savez_compressed(os.path.join(HERE, "prep_golden.npz"), **out)
+
+
 def main():
     ng, conv = import_reference()
-    which = sys.argv[1:] or ["ce", "conv", "fwd", "logp"]
+    which = sys.argv[1:] or ["ce", "conv", "fwd", "logp", "prep"]
+    if "prep" in which:
+        make_prep(ng)
     if "ce" in which:
         make_ce(ng)
     if "conv" in which:

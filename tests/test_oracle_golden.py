@@ -145,3 +145,39 @@ def test_series_reference_frame_roundtrip():
     v, i, t = s.reference_frame()
     s2 = Series.from_reference_frame(v, i, t)
     assert np.array_equal(s2.c_by_age, s.c_by_age) and s2.dtp == 3.0
+
+
+def test_prep_he_comps_matches_reference(golden):
+    from oracle import prep as oprep
+    z = golden("prep_golden.npz")
+    r = oprep.he_comps(z["He4"], z["He3"], z["Ae"], z["F"], z["E"], z["T"], z["Rterr"])
+    scale = he_scales(z)
+    for k, name in enumerate(oprep.HE_OUT):
+        assert close(r[name], z["he"][k], atol=RTOL * scale[k]).all(), name
+
+
+def he_scales(z):
+    """He4_ter, He4_del and He3_tu are differences of nearly equal terms
+    (noble_gas_utils.py:405,418): their tolerance is relative to the OPERANDS of the
+    cancelling subtraction, not to the (tiny) result."""
+    He4, He3, Rt = np.abs(z["He4"]), np.abs(z["He3"]), np.abs(z["Rterr"])
+    atm = np.abs(z["he"][1])
+    return np.stack([np.zeros_like(He4), np.zeros_like(He4), He4 + atm, 100 * (He4 + atm) / atm,
+                     4.021e14 * (He3 + (He4 + atm) * 1.384e-6 + (He4 + atm) * Rt)])
+
+
+def test_prep_cfc_sf6_matches_reference(golden):
+    from oracle import prep as oprep
+    z = golden("prep_golden.npz")
+    E, T, Ae, F, S = z["E"], z["T"], z["Ae"], z["F"], z["S"]
+    assert close(oprep.vapor_pressure_atm(T), z["pv_atm"]).all()
+    assert close(oprep.lapse_rate_atm(E), z["p_atm"]).all()
+    for j, sp in enumerate((11, 12, 113)):
+        assert close(oprep.solubility(sp, T, S), z["cfc_sol"][j]).all()
+        assert close(oprep.equil_air_conc(sp, z["cmeas"][j], E, T, Ae, F, S), z["cfc_air"][j]).all()
+        assert close(oprep.equil_aq_conc(sp, z["z_in"][j], E, T, S), z["cfc_aq"][j]).all()
+        assert close(oprep.ce_exc_conc(sp, z["z_in"][j], z["p_atm"], T, Ae, F, S), z["cfc_exc"][j]).all()
+    assert close(oprep.solubility("SF6", T, S), z["sf6_sol"]).all()
+    assert close(oprep.equil_air_conc("SF6", z["sf6_meas"], E, T, Ae, F, S), z["sf6_air"]).all()
+    assert close(oprep.equil_aq_conc("SF6", z["sf6_z"], E, T, S), z["sf6_aq"]).all()
+    assert close(oprep.ce_exc_conc("SF6", z["sf6_z"], z["p_atm"], T, Ae, F, S), z["sf6_exc"]).all()
