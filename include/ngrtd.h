@@ -163,6 +163,24 @@ int ngrtd_conv(ngrtd_ctx* ctx, int32_t series_id, int32_t mod_type, int32_t accu
 int ngrtd_rtd_weights(ngrtd_ctx* ctx, int32_t series_id, int32_t mod_type,
                       double tau, double eta, double D, double* g_out, int32_t mem);
 
+/* Fracture / matrix-diffusion RTD 'frac_inf_diff' (:238-266) for n parameter sets on the
+ * age grid of series_id: the inner integral over 1000 log-spaced advective times per age
+ * (frac_rtd_numba_disp :36-65 with the dispersion advective RTD of tau, D; or
+ * frac_rtd_numba :67-97 when f_tadv_ext != NULL: rows of N values in age order, row
+ * stride ext_stride doubles, 0 = one row shared by every set), then f[0] = 0, the trapz
+ * normalisation, FM_mu and g /= g.sum() (:257-270), then convolve() (:305-340) with
+ * decay / accumulation as ngrtd_conv.  Outputs (each may be NULL, at least one not):
+ *   conc [n]      convolve()
+ *   g_out [n][N]  gen_g_tp()
+ *   fm_mu [n]     the FM_mu attribute (mean travel time, :262-263)
+ * Per-set arrays: tau, D (NULL allowed with f_tadv_ext), bbar, Phi_im (required); t_half
+ * and J as in ngrtd_conv.                                                            */
+int ngrtd_frac_conv(ngrtd_ctx* ctx, int32_t series_id, int32_t accum,
+                    const double* tau, const double* D, const double* bbar, const double* Phi_im,
+                    const double* f_tadv_ext, int64_t ext_stride,
+                    const double* t_half, double t_half_const, const double* J, double J_const,
+                    int64_t n, double* conc, double* g_out, double* fm_mu, int32_t mem);
+
 /* convolve(g_tau=g) (:298-302): dot product with an externally supplied weight vector. */
 int ngrtd_conv_dot(ngrtd_ctx* ctx, int32_t series_id, const double* g, double t_half,
                    int32_t accum, double J, double* out, int32_t mem);

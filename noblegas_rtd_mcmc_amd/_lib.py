@@ -80,6 +80,9 @@ PROTOTYPES = {
                              C.c_void_p, C.c_double, C.c_void_p, C.c_double, C.c_int64, C.c_void_p, C.c_int32]),
     "ngrtd_rtd_weights": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_double, C.c_double, C.c_double,
                                     C.c_void_p, C.c_int32]),
+    "ngrtd_frac_conv": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32] + [C.c_void_p] * 5
+                        + [C.c_int64, C.c_void_p, C.c_double, C.c_void_p, C.c_double, C.c_int64]
+                        + [C.c_void_p] * 3 + [C.c_int32]),
     "ngrtd_conv_dot": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_double, C.c_int32, C.c_double,
                                  C.c_void_p, C.c_int32]),
     "ngrtd_plan_create": (C.c_int, [C.c_void_p, C.POINTER(ModelDesc), C.c_int64, C.POINTER(C.c_void_p)]),

@@ -10,8 +10,10 @@ form of the reference's posterior-predictive and sweep loops (run_age_mcmc.py:25
 age_modeling_mcmc.prep.py:739-778).
 
 Supported models: piston, exponential, exp_pist_flow, dispersion (the hot-path models,
-SURVEY.md §8a-a19).  The matrix-diffusion models 'frac_inf_diff*' are not implemented in
-this version and raise NotImplementedError.
+SURVEY.md §8a-a19) and the fracture / matrix-diffusion model 'frac_inf_diff' (:238-266,
+SURVEY.md §8f rank 3; with the dispersion advective RTD of tau, D or an external one via
+f_tadv_ext; 'frac_inf_diff.mint' (:199-236) is the same integral and prints its mean
+travel time like the reference), which runs through ``ngrtd_frac_conv``.
 """
 import ctypes as C
 import hashlib
@@ -22,6 +24,7 @@ from . import _lib
 from .spec import ACCUM_IDS, MOD_IDS
 
 _series_cache = {}
+_FRAC = ("frac_inf_diff", "frac_inf_diff.mint")
 
 
 def _series_arrays(C_t, rad_accum):
@@ -102,10 +105,56 @@ class tracer_conv_integral:
         return self.lamba
 
     def _check_model(self):
-        if self.mod_type not in MOD_IDS:
-            if isinstance(self.mod_type, str) and self.mod_type.startswith("frac_inf_diff"):
-                raise NotImplementedError("frac_inf_diff models are not implemented (SURVEY.md §8f rank 3)")
+        if self.mod_type not in MOD_IDS and self.mod_type not in _FRAC:
             raise ValueError("unsupported mod_type %r" % (self.mod_type,))
+
+    def _frac(self, sid, n, accum, Jv, want_conc, want_g):
+        """One ngrtd_frac_conv call over the broadcast parameter sets -> (conc, g, FM_mu, shape)."""
+        ctx = _lib.Context.get(self._device)
+        ext = self.f_tadv_ext
+        try:
+            len(ext)            # :249-253: an external advective RTD when f_tadv_ext has a length
+            use_ext = True
+        except TypeError:
+            use_ext = False
+        shapes = [np.shape(self.bbar), np.shape(self.Phi_im), np.shape(self.lamba), np.shape(Jv if Jv is not None else 0)]
+        if use_ext:
+            ext = np.asarray(ext, dtype=np.float64)
+            if ext.shape[-1] != n:
+                raise ValueError("External advective function does not match the length of the tracer input "
+                                 "function (convolution_integral_utils.py:79-80)")
+            shapes.append(ext.shape[:-1])
+        else:
+            shapes += [np.shape(self.tau), np.shape(self.D)]
+        shape = np.broadcast_shapes(*shapes)
+        m = int(np.prod(shape)) if shape else 1
+        if use_ext:
+            if ext.ndim == 1:
+                exts, stride = np.ascontiguousarray(ext), 0
+            else:
+                exts, stride = np.ascontiguousarray(np.broadcast_to(ext, shape + (n,)).reshape(m, n)), n
+        else:
+            exts, stride = None, 0
+        taus = None if use_ext else _arr(self.tau, m)
+        Ds = None if use_ext else _arr(self.D, m)
+        th = self._t_half_arg()
+        per_th = np.ndim(th) > 0
+        per_J = np.ndim(Jv) > 0 if Jv is not None else False
+        conc = np.empty(m) if want_conc else None
+        g = np.empty((m, n)) if want_g else None
+        fm = np.empty(m)
+        p = lambda a: a.ctypes.data_as(C.c_void_p) if a is not None else None  # noqa: E731
+        ctx.check(ctx.lib.ngrtd_frac_conv(ctx.h, sid, accum, p(taus), p(Ds), p(_arr(self.bbar, m)),
+                                          p(_arr(self.Phi_im, m)), p(exts), stride,
+                                          p(_arr(th, m) if per_th else None), 0.0 if per_th else float(th),
+                                          p(_arr(Jv, m) if per_J else None),
+                                          0.0 if (per_J or Jv is None or Jv is False) else float(Jv),
+                                          m, p(conc), p(g), p(fm), _lib.MEM_HOST), "ngrtd_frac_conv")
+        self.FM_mu = float(fm[0]) if shape == () else fm.reshape(shape)
+        if self.mod_type == "frac_inf_diff.mint":
+            for v in np.ravel(self.FM_mu):
+                print("mean travel time is " + '%3.2f' % v)
+        return conc, g, shape
 
     def _t_half_arg(self):
         # the device recomputes lamba from the half-life exactly as thalf_2_lambda does; use
@@ -124,6 +173,12 @@ class tracer_conv_integral:
         ctx = _lib.Context.get(self._device)
         v, i = _series_arrays(self.C_t, self.rad_accum)
         sid, n = _series_id(ctx, v, i, self.t_samp)
+        t = np.arange(0, n).astype(float)
+        t[0] += 1e-5
+        if self.mod_type in _FRAC:
+            self.tau_list = t + np.floor(self.t_samp - i[-1])
+            _, g, shape = self._frac(sid, n, 0, None, False, True)
+            return g[0] if shape == () else g.reshape(shape + (n,))
         g = np.empty(n)
         eta = float(self.eta) if self.eta is not None and self.eta is not False else 0.0
         D = float(self.D) if self.D is not None and self.D is not False else 0.0
@@ -153,6 +208,10 @@ class tracer_conv_integral:
             self.C_i = float(out[0])
             return self.C_i
         self._check_model()
+        if self.mod_type in _FRAC:
+            conc, _, shape = self._frac(sid, n, accum, Jv, True, False)
+            self.C_i = float(conc[0]) if shape == () else conc.reshape(shape)
+            return self.C_i
         tau = np.asarray(self.tau, dtype=np.float64)
         shape = np.broadcast_shapes(tau.shape, np.shape(self.eta if self.eta is not None else 0),
                                     np.shape(self.D if self.D is not None else 0), np.shape(self.lamba),

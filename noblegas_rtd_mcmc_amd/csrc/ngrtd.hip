@@ -21,6 +21,7 @@
 #include "../../include/ngrtd.h"
 #include "ngrtd_kernels.hpp"
 #include "ngrtd_prep.hpp"
+#include "ngrtd_frac.hpp"
 
 using namespace ngrtd;
 
@@ -75,7 +76,7 @@ struct ngrtd_ctx {
     std::map<int, SeriesHost> series;
     // conv-API channel tables keyed by (series, lambda bits, accum, per-set decay)
     std::map<std::tuple<int, uint64_t, int, int>, std::unique_ptr<TableDev>> tables;
-    DevBuf stage[8];
+    DevBuf stage[16];
     std::vector<hipEvent_t> event_pool;   // recycled profiling events
     hipEvent_t take_event() {
         if (!event_pool.empty()) { hipEvent_t e = event_pool.back(); event_pool.pop_back(); return e; }
@@ -819,6 +820,92 @@ int ngrtd_conv_dot(ngrtd_ctx* ctx, int32_t series_id, const double* g, double t_
     HIP_TRY(ctx, hipGetLastError());
     if (mem != NGRTD_MEM_DEVICE) {
         HIP_TRY(ctx, hipMemcpyAsync(out, o, sizeof(double), hipMemcpyDeviceToHost, S(ctx)));
+        HIP_TRY(ctx, hipStreamSynchronize(S(ctx)));
+    }
+    return NGRTD_OK;
+}
+
+// ------------------------------------------------------- frac_inf_diff RTD
+int ngrtd_frac_conv(ngrtd_ctx* ctx, int32_t series_id, int32_t accum, const double* tau, const double* D,
+                    const double* bbar, const double* Phi_im, const double* f_tadv_ext, int64_t ext_stride,
+                    const double* t_half, double t_half_const, const double* J, double J_const, int64_t n,
+                    double* conc, double* g_out, double* fm_mu, int32_t mem) {
+    if (!ctx) return NGRTD_ESTATE;
+    const SeriesHost* s = find_series(ctx, series_id);
+    if (!s) return set_err(ctx, NGRTD_ESTATE, "unknown series %d", series_id);
+    if (n < 0 || accum < 0 || accum > 3) return set_err(ctx, NGRTD_EINVAL, "bad n/accum");
+    if (!bbar || !Phi_im) return set_err(ctx, NGRTD_EINVAL, "bbar and Phi_im are required");
+    if (!f_tadv_ext && (!tau || !D)) return set_err(ctx, NGRTD_EINVAL, "tau and D are required without f_tadv_ext");
+    if (f_tadv_ext && ext_stride != 0 && ext_stride < s->n)
+        return set_err(ctx, NGRTD_EINVAL, "ext_stride must be 0 or >= N");
+    if (!conc && !g_out && !fm_mu) return set_err(ctx, NGRTD_EINVAL, "no output requested");
+    if (s->n < 2) return set_err(ctx, NGRTD_EINVAL, "series too short");
+    if (n == 0) return NGRTD_OK;
+    const int64_t N = s->n;
+    if (n * N > ((int64_t)1 << 40)) return set_err(ctx, NGRTD_EINVAL, "n * N too large");
+    FracArgs a{};
+    a.N = (int32_t)N;
+    a.n = n;
+    a.dtp = s->dtp;
+    a.tp0 = (0.0 + 1e-5) + s->dtp;
+    a.ext_stride = ext_stride;
+    NG_CHECK(stage_in(ctx, 0, f_tadv_ext ? nullptr : tau, n, mem, &a.tau));
+    NG_CHECK(stage_in(ctx, 1, f_tadv_ext ? nullptr : D, n, mem, &a.D));
+    NG_CHECK(stage_in(ctx, 2, bbar, n, mem, &a.bbar));
+    NG_CHECK(stage_in(ctx, 3, Phi_im, n, mem, &a.Phi));
+    NG_CHECK(stage_in(ctx, 4, f_tadv_ext, ext_stride ? (n - 1) * ext_stride + N : N, mem, &a.ext));
+    FracFinish b{};
+    NG_CHECK(stage_in(ctx, 5, t_half, n, mem, &b.t_half));
+    NG_CHECK(stage_in(ctx, 6, J, n, mem, &b.J));
+    // series by age + index (device copy per call, as ngrtd_conv_dot)
+    HIP_TRY(ctx, ctx->stage[7].ensure((size_t)2 * N * sizeof(double)));
+    double* cs = ctx->stage[7].d();
+    HIP_TRY(ctx, hipMemcpyAsync(cs, s->c.data(), N * sizeof(double), hipMemcpyHostToDevice, S(ctx)));
+    HIP_TRY(ctx, hipMemcpyAsync(cs + N, s->idx.data(), N * sizeof(double), hipMemcpyHostToDevice, S(ctx)));
+    // f / g: the caller's device buffer or ctx scratch
+    double* f = (mem == NGRTD_MEM_DEVICE && g_out) ? g_out : nullptr;
+    if (!f) {
+        HIP_TRY(ctx, ctx->stage[8].ensure((size_t)n * N * sizeof(double)));
+        f = ctx->stage[8].d();
+    }
+    double *dconc = nullptr, *dfm = nullptr;
+    if (mem == NGRTD_MEM_DEVICE) {
+        dconc = conc;
+        dfm = fm_mu;
+    } else {
+        HIP_TRY(ctx, ctx->stage[9].ensure((size_t)2 * n * sizeof(double)));
+        dconc = conc ? ctx->stage[9].d() : nullptr;
+        dfm = fm_mu ? ctx->stage[9].d() + n : nullptr;
+    }
+    a.f = f;
+    // one wave per (set, age); chunks of sets keep a launch below 2^30 threads
+    const int64_t chunk = std::max<int64_t>(1, ((int64_t)1 << 30) / (64 * N));
+    for (int64_t p0 = 0; p0 < n; p0 += chunk) {
+        a.p0 = p0;
+        const int64_t waves = std::min(chunk, n - p0) * N;
+        a.waves = waves;
+        hipLaunchKernelGGL(frac_inner_kernel, dim3((unsigned)cdiv(waves, kFracWaves)), dim3(64 * kFracWaves), 0,
+                           S(ctx), a);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    b.c = cs;
+    b.idx = cs + N;
+    b.t_half_c = t_half_const;
+    b.J_c = J_const;
+    b.accum = accum;
+    b.tp0 = a.tp0;
+    b.dtp = a.dtp;
+    b.N = a.N;
+    b.n = n;
+    b.f = f;
+    b.conc = dconc;
+    b.fm = dfm;
+    hipLaunchKernelGGL(frac_finish_kernel, dim3((unsigned)n), dim3(256), 0, S(ctx), b);
+    HIP_TRY(ctx, hipGetLastError());
+    if (mem != NGRTD_MEM_DEVICE) {
+        if (conc) HIP_TRY(ctx, hipMemcpyAsync(conc, dconc, n * sizeof(double), hipMemcpyDeviceToHost, S(ctx)));
+        if (fm_mu) HIP_TRY(ctx, hipMemcpyAsync(fm_mu, dfm, n * sizeof(double), hipMemcpyDeviceToHost, S(ctx)));
+        if (g_out) HIP_TRY(ctx, hipMemcpyAsync(g_out, f, (size_t)n * N * sizeof(double), hipMemcpyDeviceToHost, S(ctx)));
         HIP_TRY(ctx, hipStreamSynchronize(S(ctx)));
     }
     return NGRTD_OK;

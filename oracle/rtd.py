@@ -116,3 +116,53 @@ def forward_mod(tracer, conv_kwgs, par_names, theta):
     if tracer == "SF6" and "lamsf6" in p:
         cout *= (1 + p["lamsf6"])
     return float(cout)
+
+
+# ---------------------------------------------------------------- frac_inf_diff
+def _trapz(y, x):
+    """convolution_integral_utils.py:23-26."""
+    return 0.5 * ((x[1:] - x[:-1]) * (y[1:] + y[:-1])).sum()
+
+
+def frac_kappa(Phi_im):
+    """convolution_integral_utils.py:245-248."""
+    D_o = (2.3e-9) * 60 * 60 * 24 * 365
+    R_im = 1
+    return Phi_im * np.sqrt((D_o * Phi_im ** 2) * R_im)
+
+
+def frac_inner(tp, tau, D, bbar, kappa, f_tadv_ext=None):
+    """frac_rtd_numba_disp (:36-65) / frac_rtd_numba (:67-97): the inner integral per age."""
+    f_t_tran = np.zeros_like(tp)
+    with np.errstate(all="ignore"):
+        for i in range(len(tp)):
+            _tp = tp[i]
+            tadv = np.logspace(-6, np.log10(_tp - 1.e-6), 1000)
+            if f_tadv_ext is None:
+                f_tadv = ((1. / tau) / (np.sqrt(4. * np.pi * D * (tadv / tau)))) * (1. / (tadv / tau)) \
+                    * np.exp(-1. * (((1. - (tadv / tau)) ** 2) / (4. * D * (tadv / tau))))
+            else:
+                f_tadv = np.interp(tadv, tp[:i + 1], f_tadv_ext[:i + 1])
+            t_ret = _tp - tadv
+            Beta_tadv = tadv / bbar
+            f_ret = (kappa * Beta_tadv) / (2 * np.sqrt(np.pi) * t_ret ** (3 / 2)) \
+                * np.exp((-1 * kappa ** 2 * Beta_tadv ** 2) / (4 * t_ret))
+            f_ret = f_ret / _trapz(f_ret[::-1], t_ret[::-1])
+            f_t_tran[i] = _trapz(f_ret * f_tadv, tadv)
+    return f_t_tran
+
+
+def frac_g_tp(n, index_last, t_samp, tau, D, bbar, Phi_im, f_tadv_ext=None):
+    """gen_g_tp() for 'frac_inf_diff' (:238-266, :270) -> (g, FM_mu)."""
+    tp = age_grid(n, index_last, t_samp)
+    f = frac_inner(tp, np.float64(tau), np.float64(D), np.float64(bbar), frac_kappa(np.float64(Phi_im)),
+                   None if f_tadv_ext is None else np.asarray(f_tadv_ext, dtype=np.float64))
+    with np.errstate(all="ignore"):
+        f[0] = 0
+        tp_ = tp.copy()
+        tp_[0] = 0
+        f = f / np.trapezoid(f, tp_)
+        g = f
+        fm = np.trapezoid(g * tp_, tp_) / np.trapezoid(g, tp_)
+        g = g / g.sum()
+    return g, fm

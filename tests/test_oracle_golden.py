@@ -181,3 +181,29 @@ def test_prep_cfc_sf6_matches_reference(golden):
     assert close(oprep.equil_air_conc("SF6", z["sf6_meas"], E, T, Ae, F, S), z["sf6_air"]).all()
     assert close(oprep.equil_aq_conc("SF6", z["sf6_z"], E, T, S), z["sf6_aq"]).all()
     assert close(oprep.ce_exc_conc("SF6", z["sf6_z"], z["p_atm"], T, Ae, F, S), z["sf6_exc"]).all()
+
+
+FRAC_TRACERS = {"CFC12": ("CFC12", False, False, False), "SF6": ("SF6", False, False, False),
+                "H3": ("H3", 12.34, False, False), "He3": ("H3", 12.34, "3He", False),
+                "He4_ter": ("He4_ter", False, "4He", 3.30885e-11)}
+
+
+def test_frac_inf_diff_matches_reference(golden):
+    """oracle frac_g_tp / convolve vs the reference's 'frac_inf_diff' (bitwise: same NumPy ops)."""
+    z = golden("frac_golden.npz")
+    n = 300
+    for i in range(z["tau"].size):
+        g, fm = ortd.frac_g_tp(n, 0, 0, z["tau"][i], z["D"][i], z["bbar"][i], z["Phi"][i])
+        assert close(g, z["g_%d" % n][i]).all() and close(fm, z["fm_%d" % n][i])
+        for tname, (sname, t_half, accum, J) in FRAC_TRACERS.items():
+            s = atmos_series(sname, n)
+            c = s.c_by_age * (0.0 if tname == "He4_ter" else 1.0)
+            lam = ortd.thalf_2_lambda(t_half) if t_half else 0.0
+            v = ortd.convolve(np.flip(c), np.arange(n - 1, -1, -1), 0, None, None, lamba=lam, rad_accum=accum,
+                              J=J, g_tau=g)
+            assert close(v, z["conc_%s_%d" % (tname, n)][i]), (tname, i)
+    for i in range(z["ext"].shape[0]):
+        g, fm = ortd.frac_g_tp(600, 0, 0, None, None, z["bbar"][i], z["Phi"][i], f_tadv_ext=z["ext"][i])
+        # the reference's g_tp attribute after convolve() carries the H3 decay (:315-317)
+        gd = g * np.exp(-ortd.thalf_2_lambda(12.34) * ortd.age_grid(600, 0, 0))
+        assert close(gd, z["ext_g"][i]).all() and close(fm, z["ext_fm"][i])
