@@ -72,6 +72,37 @@ NGRTD_FM double fexp(double x) {
     return (x == x) ? res : x;
 }
 
+// 10^y = e^(y ln10) with y ln10 carried as a double-double (ph + pl) through the argument
+// reduction, so r is exact to ~2^-61 and the result is fexp's table/polynomial evaluation
+// of e^r: < 0.51 ulp (correctly rounded in all but ~1% of cases), against NumPy's
+// np.power(10.0, y) (tests/test_fastmath_cpu.py).  The frac_inf_diff advective grid
+// tadv = logspace(...) needs this accuracy: t_ret = tp - tadv cancels.
+NGRTD_FM double fexp10(double y) {
+    const double LN10 = 2.302585092994046;
+    const double LN10_LO = -2.1707562233822494e-16;      // ln10 - LN10
+    const double L64E = 92.332482616893656;
+    const double L2HI = 6.93147180369123816490e-01 / 64;
+    const double L2LO = 1.90821492927058770002e-10 / 64;
+    const double yc = fmin(fmax(y, -350.0), 350.0);
+    const double ph = yc * LN10;
+    const double pl = fma(yc, LN10, -ph) + yc * LN10_LO;
+    const double kd = rint(ph * L64E);
+    double r = fma(-kd, L2HI, ph);
+    r = fma(-kd, L2LO, r) + pl;
+    double q = 1.0 / 5040.0;
+    q = fma(q, r, 1.0 / 720.0);
+    q = fma(q, r, 1.0 / 120.0);
+    q = fma(q, r, 1.0 / 24.0);
+    q = fma(q, r, 1.0 / 6.0);
+    q = fma(q, r, 0.5);
+    const double p = fma(r * r, q, r);                   // e^r - 1
+    const int k = (int)kd;
+    const int j = k & 63;
+    const double th = NGRTD_FMT[2 * j], tl = NGRTD_FMT[2 * j + 1];
+    const double res = ldexp(th + fma(th, p, tl), k >> 6);
+    return (y == y) ? res : y;
+}
+
 // log x: x = 2^e m, m in [1 - 2^-7, 2 - 2^-7) taken from the bit pattern, c_i = 1 + i/64
 // the nearest table point, r = (m - c_i) / c_i (m - c_i exact, |r| < 2^-7); log x = e ln2 + log c_i +
 // log1p(r), log1p by its Taylor series to r^8/8 (truncation < 2e-20).  <= 1 ulp.

@@ -66,6 +66,8 @@ __device__ __forceinline__ double interp_age(double x, const double* fp, int i, 
 }
 
 __global__ void __launch_bounds__(64 * kFracWaves) frac_inner_kernel(const FracArgs a) {
+    fm_lds_init();                                 // fexp / fexp10 tables (before any exit)
+    __syncthreads();
     const int lane = threadIdx.x & 63;
     const int64_t gw = (int64_t)blockIdx.x * kFracWaves + (threadIdx.x >> 6);
     const int64_t pl = gw / a.N;
@@ -100,17 +102,18 @@ __global__ void __launch_bounds__(64 * kFracWaves) frac_inner_kernel(const FracA
         const double jd = (double)j;
         double y = (step == 0.0) ? (jd / (kFracPts - 1)) * delta + start : jd * step + start;
         if (j == kFracPts - 1) y = stop;
-        const double tadv = pow(10.0, y);
+        // np.power(10.0, y): fexp10 is < 0.51 ulp (t_ret below cancels against tadv)
+        const double tadv = fexp10(y);
         double f_tadv;
         if (ext) {
             f_tadv = interp_age(tadv, ext, i, a.tp0, a.dtp);
         } else {
             const double x = tadv / tau;
-            f_tadv = (inv_tau / (sqrt(c4piD * x))) * (1. / x) * exp(-1. * (((1. - x) * (1. - x)) / (c4D * x)));
+            f_tadv = (inv_tau / (sqrt(c4piD * x))) * (1. / x) * fexp(-1. * (((1. - x) * (1. - x)) / (c4D * x)));
         }
         const double t_ret = tp_i - tadv;
         const double beta = tadv / bbar;
-        const double f_ret = (kappa * beta) / (c2spi * (t_ret * sqrt(t_ret))) * exp((k2 * (beta * beta)) / (4 * t_ret));
+        const double f_ret = (kappa * beta) / (c2spi * (t_ret * sqrt(t_ret))) * fexp((k2 * (beta * beta)) / (4 * t_ret));
         const double fi = f_ret * f_tadv;
         // left neighbour (j - 1): lane - 1 of this k, or lane 63 of the previous k
         double l_t = shfl_up1(t_ret), l_fr = shfl_up1(f_ret), l_ta = shfl_up1(tadv), l_fi = shfl_up1(fi);

@@ -98,3 +98,21 @@ def test_lgamma_half_diff(host_tool):
     assert np.all(np.abs((D1 - D0) - np.log1p(0.5 / big)) <= 8 * np.spacing(D1))   # 2 x 4 ulp of D
     big = big[big >= 1e4]        # next asymptotic term 1/(192 x^3) < 1e-14 here
     assert np.allclose(host_tool("g", big), 0.5 * np.log(big) - 1.0 / (8 * big), rtol=1e-13, atol=0)
+
+
+def test_fexp10_vs_numpy_power(host_tool):
+    """fexp10 against np.power(10.0, y) -- the reference's logspace (convolution_integral_utils.py
+    :48, :83) -- and against 80-bit long double: < 0.51 ulp, and identical to NumPy's result
+    for >= 90 % of arguments (measured 95 %; NumPy's own power is <= 0.67 ulp here)."""
+    rng = np.random.default_rng(3)
+    y = np.concatenate([rng.uniform(-6.0, 4.5, 40000), rng.uniform(-300, 300, 5000), [0.0, 1.0, -6.0, 2.0]])
+    got = host_tool("t", y)
+    ref_np = np.power(10.0, y)
+    assert np.mean(got == ref_np) >= 0.9      # NumPy (SVML here) is itself up to 0.67 ulp off
+    assert np.all(np.abs(got - ref_np) <= np.spacing(np.abs(ref_np)))
+    if np.finfo(np.longdouble).nmant >= 60:
+        ref = np.power(np.longdouble(10), y.astype(np.longdouble))
+        ok = np.abs(ref) > np.finfo(np.float64).tiny
+        assert ulp_err(got[ok], ref[ok]).max() <= 0.51
+    sp = host_tool("t", np.array([np.nan, np.inf, -np.inf, 400.0, -400.0]))
+    assert np.isnan(sp[0]) and sp[1] == np.inf and sp[2] == 0.0 and sp[3] == np.inf and sp[4] == 0.0
