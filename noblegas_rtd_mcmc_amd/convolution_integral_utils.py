@@ -111,6 +111,9 @@ class tracer_conv_integral:
     def _frac(self, sid, n, accum, Jv, want_conc, want_g):
         """One ngrtd_frac_conv call over the broadcast parameter sets -> (conc, g, FM_mu, shape)."""
         ctx = _lib.Context.get(self._device)
+        if self.bbar is None or self.Phi_im is None:
+            # the reference computes kappa = Phi_im*... and tadv / bbar with None: TypeError
+            raise TypeError("frac_inf_diff needs bbar and Phi_im (convolution_integral_utils.py:246-251)")
         ext = self.f_tadv_ext
         try:
             len(ext)            # :249-253: an external advective RTD when f_tadv_ext has a length
@@ -144,8 +147,9 @@ class tracer_conv_integral:
         g = np.empty((m, n)) if want_g else None
         fm = np.empty(m)
         p = lambda a: a.ctypes.data_as(C.c_void_p) if a is not None else None  # noqa: E731
-        ctx.check(ctx.lib.ngrtd_frac_conv(ctx.h, sid, accum, p(taus), p(Ds), p(_arr(self.bbar, m)),
-                                          p(_arr(self.Phi_im, m)), p(exts), stride,
+        bbars = np.ascontiguousarray(np.broadcast_to(np.asarray(self.bbar, dtype=np.float64), (m,)))
+        phis = np.ascontiguousarray(np.broadcast_to(np.asarray(self.Phi_im, dtype=np.float64), (m,)))
+        ctx.check(ctx.lib.ngrtd_frac_conv(ctx.h, sid, accum, p(taus), p(Ds), p(bbars), p(phis), p(exts), stride,
                                           p(_arr(th, m) if per_th else None), 0.0 if per_th else float(th),
                                           p(_arr(Jv, m) if per_J else None),
                                           0.0 if (per_J or Jv is None or Jv is False) else float(Jv),

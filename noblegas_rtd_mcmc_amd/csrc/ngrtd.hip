@@ -409,7 +409,7 @@ static void launch_mfma(const RtdArgs& a, const UnitArgs& u, int32_t fuse, hipSt
 // data (ce obs, 1/sd^2, sums of 0.5 log 1/sd^2, E_min; rtd obs, 1/sd^2, sums).
 static size_t fused_lds(const RtdArgs& a, const UnitArgs& u) {
     const size_t wells = (size_t)u.L * ((u.ce_on ? 2 * u.G + 2 : 0) + (u.rtd_on ? 2 * u.K + 1 : 0));
-    return (size_t)(kFusedUnits + kFusedUnits / 2 + kChebPieces * kChebN * cheb_cp(a.C) + wells) * sizeof(double);
+    return (size_t)(2 * kFusedUnits + kFusedUnits / 2 + kChebPieces * kChebN * cheb_cp(a.C) + wells) * sizeof(double);
 }
 constexpr size_t kFusedMaxLds = 150 * 1024;
 static bool fused_path(const RtdArgs& a, const UnitArgs& u) {
@@ -417,17 +417,32 @@ static bool fused_path(const RtdArgs& a, const UnitArgs& u) {
     return !disabled && mfma_path(a, a.row_thalf >= 0) && a.C <= 5 && u.L >= 1 && u.L <= kFusedUnits &&
            fused_lds(a, u) <= kFusedMaxLds;
 }
-template <int C, bool FULL>
-static void launch_fused_cf(const RtdArgs& a, const UnitArgs& u, int WB, int64_t W, double* logp,
-                            const DemcAccept& da, hipStream_t st) {
+// Waves per unit group (logp_fused_kernel ROLES): 2 = theta-only and RTD blocks in separate
+// waves (default), 1 = one wave runs the whole unit.  NGRTD_FUSED_ROLES overrides (A/B runs).
+static int fused_roles() {
+    static const int r = [] {
+        const char* e = std::getenv("NGRTD_FUSED_ROLES");
+        return (e && std::atoi(e) == 1) ? 1 : 2;
+    }();
+    return r;
+}
+template <int C, bool FULL, int ROLES>
+static void launch_fused_cfr(const RtdArgs& a, const UnitArgs& u, int WB, int64_t W, double* logp,
+                             const DemcAccept& da, hipStream_t st) {
     static const bool attr = [] {   // dynamic LDS above 64 KiB (many wells) needs the opt-in
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&logp_fused_kernel<C, FULL>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&logp_fused_kernel<C, FULL, ROLES>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFusedMaxLds);
         return true;
     }();
     (void)attr;
-    hipLaunchKernelGGL((logp_fused_kernel<C, FULL>), dim3((unsigned)cdiv(W, WB)), dim3(64 * kFusedWaves),
-                       fused_lds(a, u), st, a, u, WB, logp, da);
+    hipLaunchKernelGGL((logp_fused_kernel<C, FULL, ROLES>), dim3((unsigned)cdiv(W, WB)),
+                       dim3(64 * kFusedWaves * ROLES), fused_lds(a, u), st, a, u, WB, logp, da);
+}
+template <int C, bool FULL>
+static void launch_fused_cf(const RtdArgs& a, const UnitArgs& u, int WB, int64_t W, double* logp,
+                            const DemcAccept& da, hipStream_t st) {
+    if (fused_roles() == 2) launch_fused_cfr<C, FULL, 2>(a, u, WB, W, logp, da, st);
+    else launch_fused_cfr<C, FULL, 1>(a, u, WB, W, logp, da, st);
 }
 // FULL instance: CE + RTD blocks, priors and likelihoods on, no Jacobians (the joint model)
 template <int C>

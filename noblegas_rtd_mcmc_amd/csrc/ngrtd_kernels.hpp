@@ -647,9 +647,11 @@ constexpr int kMfmaUnitsPerBlock = 256;
 // column `col` in tile t given by uoff[t]).  init() sets the powers, steps() runs the
 // MFMA recurrence over fragments already staged in LDS (callable chunk after chunk),
 // finish() forms the per-tile channel sums Y_c (identical in the 4 lanes of a column).
-template <int C>
+// NTT: tiles held at once (default all of the wave's tiles; 1 = one tile per pass, 40
+// accumulator VGPRs at C = 5, for callers with a tight register budget).
+template <int C, int NTT = mfma_tiles(C)>
 struct MfmaWave {
-    static constexpr int R = mfma_rows(C), SG = mfma_groups_per_chan(C), NT = mfma_tiles(C);
+    static constexpr int R = mfma_rows(C), SG = mfma_groups_per_chan(C), NT = NTT;
     double beta[NT], q4[NT], pw[NT];
     ngrtd_v4d acc[NT][R];
 
@@ -727,13 +729,44 @@ __host__ __device__ __forceinline__ int cheb_piece(double tau, double& x) {
     return p;
 }
 
-// Clenshaw sums of C channels at x from one piece's coefficients [kChebN][CP]
-template <int C>
-__host__ __device__ __forceinline__ void cheb_sums(const double* __restrict__ pc, int CP, double x, double* y) {
+// Clenshaw sums of C channels at x from one piece's coefficients [kChebN][CP].
+// PIPE (device only): software-pipelined one row ahead, with each row's results pinned
+// ("+v") behind a compiler memory barrier, so at most two rows of coefficients are live
+// in registers (2 C doubles) -- otherwise the scheduler issues all kChebN rows' LDS loads
+// up front (12 C doubles, 144 VGPRs at C = 6), which caps occupancy at 2 waves/SIMD.
+template <int C, bool PIPE = false>
+__host__ __device__ __forceinline__ void cheb_sums(const double* pc, int CP, double x, double* y) {
     const double x2 = x + x;
     double b1[C], b2[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) { b1[c] = 0.0; b2[c] = 0.0; }
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (PIPE) {
+        double cur[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) cur[c] = pc[(kChebN - 1) * CP + c];
+#pragma unroll
+        for (int k = kChebN - 1; k >= 1; --k) {
+            double nxt[C];
+#pragma unroll
+            for (int c = 0; c < C; ++c) nxt[c] = pc[(k - 1) * CP + c];   // row k-1 (row 0 at k = 1)
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const double t = fma(x2, b1[c], cur[c] - b2[c]);
+                b2[c] = b1[c];
+                b1[c] = t;
+            }
+#pragma unroll
+            for (int c = 0; c < C; ++c) asm volatile("" : "+v"(b1[c]));
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int c = 0; c < C; ++c) cur[c] = nxt[c];
+        }
+#pragma unroll
+        for (int c = 0; c < C; ++c) y[c] = fma(x, b1[c], cur[c] - b2[c]);
+        return;
+    }
+#endif
 #pragma unroll
     for (int k = kChebN - 1; k >= 1; --k) {
         const double* row = pc + k * CP;
@@ -953,27 +986,89 @@ __device__ __forceinline__ void walker_out(double* logp, const DemcAccept& d, in
     if (d.lp) *dec = demc_decide(d, w, tot);
 }
 
-constexpr int kFusedWaves = 8;
-constexpr int kFusedUnits = 64 * kFusedWaves;
-constexpr int kFusedPrefetch = 4;   // double2 per thread: covers kChebPieces*kChebN*6 doubles
+// Exact (matrix-core) channel sums for a wave of logp_fused_kernel with an uncovered tau:
+// its 64 units as 4 tiles of 16, then this lane's concentrations and RTD likelihood.
+template <int C, bool FULL, bool SEQ>
+__device__ __forceinline__ void fused_exact(const RtdArgs& a, const UnitArgs& ul, int WB, int64_t w0, int uw,
+                                            bool mvalid, int64_t mu, int ml, double nub, double* conc,
+                                            double& like) {
+    constexpr int NT = mfma_tiles(C);
+    const int col = threadIdx.x & 15;
+    const int L = ul.L;
+    const int64_t W = ul.W;
+    int64_t uoff[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const int i = (uw * NT + t) * 16 + col;
+        const int wl = i % WB, l = i / WB;
+        uoff[t] = (l < L && w0 + wl < W) ? (int64_t)l * W + w0 + wl : 0;
+    }
+    double yy[C], bu;
+    if (SEQ) {   // one 16-unit tile per pass: 1/NT of the accumulators live
+        const int tq = (threadIdx.x & 63) >> 4;
+        bu = 0.0;
+#pragma unroll 1
+        for (int t = 0; t < NT; ++t) {
+            MfmaWave<C, 1> mw;
+            mw.init(a, uoff + t);
+            mw.steps(a.frag, a.nsteps);
+            double y[1][C];
+            mw.finish(a, y);
+            if (t == tq) {
+                bu = mw.beta[0];
+#pragma unroll
+                for (int c = 0; c < C; ++c) yy[c] = y[0][c];
+            }
+        }
+    } else {
+        MfmaWave<C> mw;
+        mw.init(a, uoff);
+        mw.steps(a.frag, a.nsteps);
+        double y[NT][C];
+        mw.finish(a, y);
+        mfma_pick_tile<C>(y, mw.beta, yy, bu);   // tile tq holds this lane's unit
+    }
+    if (mvalid) {
+        ThetaPre tp;
+        tp.nub = nub;
+        mfma_unit_conc<C>(a, mu, bu, yy, conc);
+        like = unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL);
+    }
+}
 
-template <int C, bool FULL>
-__global__ void __launch_bounds__(64 * kFusedWaves) logp_fused_kernel(const RtdArgs a, const UnitArgs ua,
-                                                                     int32_t WB, double* __restrict__ logp,
-                                                                     const DemcAccept dacc) {
+constexpr int kFusedWaves = 8;                 // waves of units per block (512 units)
+constexpr int kFusedUnits = 64 * kFusedWaves;
+constexpr int kFusedPrefetch = 4;   // double2 per thread (512 threads): covers kChebPieces*kChebN*6 doubles
+
+// ROLES = 1: one wave per 64 units runs the whole unit (2 waves/SIMD at c4, 228 VGPRs).
+// ROLES = 2: the block has 2 x 8 waves; waves 0-7 run the theta-only block (priors, CE model,
+// CE likelihood) and waves 8-15 the RTD block (surrogate channel sums, concentrations, RTD
+// likelihood, exact fallback) of the SAME 512 units, and their results meet in LDS in the
+// reference's addition order (th + like).  Role is wave-uniform (no divergence); each role
+// needs fewer registers, so at c4 a SIMD holds 4 waves of two different instruction mixes
+// (transcendental-heavy CE, FMA-chain Clenshaw) that hide each other's latency.
+template <int C, bool FULL, int ROLES>
+__global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(const RtdArgs a, const UnitArgs ua,
+                                                                              int32_t WB, double* __restrict__ logp,
+                                                                              const DemcAccept dacc) {
     constexpr int NT = mfma_tiles(C);
     constexpr int CP = cheb_cp(C);
+    constexpr int NTH = 64 * kFusedWaves * ROLES;           // threads per block
+    constexpr int NPRE = (kFusedPrefetch * 64 * kFusedWaves + NTH - 1) / NTH;
     constexpr int TAB2 = kChebPieces * kChebN * CP / 2;   // double2 entries of the surrogate table
     static_assert(NT == 4, "one unit per lane needs 4 tiles per wave");
-    static_assert(TAB2 <= kFusedPrefetch * 64 * kFusedWaves, "prefetch covers the table");
+    static_assert(TAB2 <= NPRE * NTH, "prefetch covers the table");
     extern __shared__ __attribute__((aligned(16))) double lds[];
     double* part = lds;                                   // [512] per-unit log-prob
-    int* dec = reinterpret_cast<int*>(lds + kFusedUnits);  // [512] DE-MC decisions per walker
-    double* cheb = lds + kFusedUnits + kFusedUnits / 2;   // [kChebPieces][kChebN][CP]
+    double* part2 = lds + kFusedUnits;                    // [512] RTD likelihood (ROLES = 2)
+    int* dec = reinterpret_cast<int*>(lds + 2 * kFusedUnits);   // [512] DE-MC decisions per walker
+    double* cheb = lds + 2 * kFusedUnits + kFusedUnits / 2;   // [kChebPieces][kChebN][CP]
     NGRTD_PROBE(0);
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
-    const int col = lane & 15;
+    const int uw = wave % kFusedWaves;                    // unit wave
+    const bool do_theta = ROLES == 1 || wave < kFusedWaves;
+    const bool do_rtd = ROLES == 1 || wave >= kFusedWaves;
     const int L = ua.L;
     const int64_t W = ua.W;
     // XCD-aware walker blocks: the dispatcher deals block b to XCD b % 8, so consecutive
@@ -983,42 +1078,42 @@ __global__ void __launch_bounds__(64 * kFusedWaves) logp_fused_kernel(const RtdA
     const int bl = (nb & 7) == 0 ? ((int)blockIdx.x & 7) * (nb >> 3) + ((int)blockIdx.x >> 3) : (int)blockIdx.x;
     const int64_t w0 = (int64_t)bl * WB;
     // surrogate table -> registers -> LDS (stored after every prologue load is issued)
-    double2 pre[kFusedPrefetch];
+    double2 pre[NPRE];
     if (a.cheb) {
         const double2* src = reinterpret_cast<const double2*>(a.cheb);
 #pragma unroll
-        for (int r = 0; r < kFusedPrefetch; ++r) {
-            const int i = tid + r * 64 * kFusedWaves;
+        for (int r = 0; r < NPRE; ++r) {
+            const int i = tid + r * NTH;
             pre[r] = i < TAB2 ? src[i] : double2{0.0, 0.0};
         }
     }
     // this lane's unit
-    const int mi = 64 * wave + lane;
+    const int mi = 64 * uw + lane;
     const int mwl = mi % WB, ml = mi / WB;
     const bool mvalid = ml < L && w0 + mwl < W;
     const int64_t mu = mvalid ? (int64_t)ml * W + w0 + mwl : 0;
     // per-well observation data -> LDS (read per lane by the likelihood blocks): all loads
     // issued before any store, so the prologue pays one memory latency
     double* wd = cheb + kChebPieces * kChebN * CP;
-    constexpr int kWdRegs = 4;
+    constexpr int kWdRegs = (4 * 64 * kFusedWaves + NTH - 1) / NTH;
     double wv[kWdRegs];
 #pragma unroll
     for (int r = 0; r < kWdRegs; ++r) {
-        const int i = tid + r * 64 * kFusedWaves;
+        const int i = tid + r * NTH;
         wv[r] = i < ua.wd_n ? ua.wd_src[i] : 0.0;
     }
     fm_lds_init();                                        // fexp/flog tables
 #pragma unroll
     for (int r = 0; r < kWdRegs; ++r) {
-        const int i = tid + r * 64 * kFusedWaves;
+        const int i = tid + r * NTH;
         if (i < ua.wd_n) wd[i] = wv[r];
     }
-    for (int i = tid + kWdRegs * 64 * kFusedWaves; i < ua.wd_n; i += 64 * kFusedWaves) wd[i] = ua.wd_src[i];
+    for (int i = tid + kWdRegs * NTH; i < ua.wd_n; i += NTH) wd[i] = ua.wd_src[i];
     if (a.cheb) {
         double2* dst = reinterpret_cast<double2*>(cheb);
 #pragma unroll
-        for (int r = 0; r < kFusedPrefetch; ++r) {
-            const int i = tid + r * 64 * kFusedWaves;
+        for (int r = 0; r < NPRE; ++r) {
+            const int i = tid + r * NTH;
             if (i < TAB2) dst[i] = pre[r];
         }
     }
@@ -1042,70 +1137,65 @@ __global__ void __launch_bounds__(64 * kFusedWaves) logp_fused_kernel(const RtdA
     NGRTD_PROBE(1);
     // theta of this lane's unit (after the barrier: the 8.4 MB theta read at c4 is
     // bandwidth-bound, and the tables' loads before the barrier should not wait behind it)
-    const double tau = mvalid ? a.theta[(int64_t)a.row_tau[0] * a.U + mu] : 1.0;
-    ThetaPre tp;
-    theta_preload(ua, mu, tp);
-    // One straight-line block per unit: the theta-only part, the surrogate channel sums,
-    // the concentrations and the RTD likelihood (independent chains the scheduler can
-    // interleave; with FULL every plan-flag test folds away).  Lanes whose tau the
-    // surrogate does not cover evaluate piece 0 here and are redone exactly below.
-    double cx = 0.0;
-    int cpc = a.cheb ? cheb_piece(tau, cx) : -1;
-    // An uncovered tau (< 1/2, NaN) outside the support of the tau1 Uniform prior makes the
-    // unit's log-prob -inf whatever the concentrations are -- unless they are NaN, which
-    // the reference's weights produce exactly when (1/tau) exp(-tp/tau) overflows or
-    // divides by 0 (convolution_integral_utils.py:184, then g / g.sum(), :270): such a
-    // lane needs no channel sums, only that NaN predicate.  DE-MC proposals below the
-    // prior bound are common; they would otherwise send whole waves to the exact path.
-    bool skip = false, cnan = false;
-    if (cpc < 0 && a.cheb && (FULL || (ua.rtd_on && (ua.flags & NGRTD_WANT_PRIOR))) && a.row_tau[0] == ua.row_tau1 &&
-        !(tau >= ua.tau1_lo && tau <= ua.tau1_hi) && !(ua.tau1_lo < kChebTauLo && tau >= ua.tau1_lo)) {
-        skip = true;
-        cnan = exp_rtd_nan(a, tau);
+    double th = 0.0, like = 0.0;
+    if (do_theta) {
+        ThetaPre tp;
+        theta_preload(ua, mu, tp);
+        th = mvalid ? unit_logp_theta(ul, mu, ml, &tp, FULL) : 0.0;
     }
-    const bool bad = cpc < 0 && !skip;
-    cpc = cpc < 0 ? 0 : cpc;
-    const double th = mvalid ? unit_logp_theta(ul, mu, ml, &tp, FULL) : 0.0;
-    double zz[C + 1];
-    cheb_sums<C + 1>(cheb + cpc * (kChebN * CP), CP, cx, zz);   // s01 Y_c (c < C), s01 G
-    double like = 0.0;
-    double conc[kMaxTracer];
-    {
-        double num[C];
-#pragma unroll
-        for (int c = 0; c < C; ++c) num[c] = a.tab0[c] + zz[c];
-        unit_conc<C>(a, mu, num, 1.0 / (1.0 + zz[C]), conc);
-        if (cnan)
-            for (int t = 0; t < a.K; ++t) conc[t] = __builtin_nan("");
-        like = mvalid ? unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL) : 0.0;
-    }
-    NGRTD_PROBE(2);
-    if (__any(bad)) {                                     // wave-uniform: exact channel sums
-        int64_t uoff[NT];
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            const int i = (wave * NT + t) * 16 + col;
-            const int wl = i % WB, l = i / WB;
-            uoff[t] = (l < L && w0 + wl < W) ? (int64_t)l * W + w0 + wl : 0;
+    if (do_rtd) {
+        const double tau = mvalid ? a.theta[(int64_t)a.row_tau[0] * a.U + mu] : 1.0;
+        ThetaPre tp;
+        tp.nub = (FULL || ua.rtd_on) ? a.theta[(int64_t)ua.row_nu * a.U + mu] : 0.0;
+        // The surrogate channel sums, the concentrations and the RTD likelihood.  Lanes
+        // whose tau the surrogate does not cover evaluate piece 0 here and are redone
+        // exactly below.
+        double cx = 0.0;
+        int cpc = a.cheb ? cheb_piece(tau, cx) : -1;
+        // An uncovered tau (< 1/2, NaN) outside the support of the tau1 Uniform prior makes the
+        // unit's log-prob -inf whatever the concentrations are -- unless they are NaN, which
+        // the reference's weights produce exactly when (1/tau) exp(-tp/tau) overflows or
+        // divides by 0 (convolution_integral_utils.py:184, then g / g.sum(), :270): such a
+        // lane needs no channel sums, only that NaN predicate.  DE-MC proposals below the
+        // prior bound are common; they would otherwise send whole waves to the exact path.
+        bool skip = false, cnan = false;
+        if (cpc < 0 && a.cheb && (FULL || (ua.rtd_on && (ua.flags & NGRTD_WANT_PRIOR))) &&
+            a.row_tau[0] == ua.row_tau1 && !(tau >= ua.tau1_lo && tau <= ua.tau1_hi) &&
+            !(ua.tau1_lo < kChebTauLo && tau >= ua.tau1_lo)) {
+            skip = true;
+            cnan = exp_rtd_nan(a, tau);
         }
-        MfmaWave<C> mw;
-        mw.init(a, uoff);
-        mw.steps(a.frag, a.nsteps);
-        double y[NT][C], yy[C], bu;
-        mw.finish(a, y);
-        mfma_pick_tile<C>(y, mw.beta, yy, bu);   // tile tq holds this lane's unit
-        if (mvalid) {
-            mfma_unit_conc<C>(a, mu, bu, yy, conc);
-            like = unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL);
+        const bool bad = cpc < 0 && !skip;
+        cpc = cpc < 0 ? 0 : cpc;
+        double zz[C + 1];
+        cheb_sums<C + 1, ROLES == 2>(cheb + cpc * (kChebN * CP), CP, cx, zz);   // s01 Y_c (c < C), s01 G
+        double conc[kMaxTracer];
+        {
+            double num[C];
+#pragma unroll
+            for (int c = 0; c < C; ++c) num[c] = a.tab0[c] + zz[c];
+            unit_conc<C>(a, mu, num, 1.0 / (1.0 + zz[C]), conc);
+            if (cnan)
+                for (int t = 0; t < a.K; ++t) conc[t] = __builtin_nan("");
+            like = mvalid ? unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL) : 0.0;
         }
+        NGRTD_PROBE(2);
+        if (__any(bad)) {                                     // wave-uniform: exact channel sums
+            // ROLES = 2: one tile per pass keeps the exact path inside the 128-VGPR budget
+            fused_exact<C, FULL, ROLES == 2>(a, ul, WB, w0, uw, mvalid, mu, ml, tp.nub, conc, like);
+        }
+        if (!FULL && a.conc && mvalid)                        // forward(): model concentrations
+            for (int t = 0; t < a.K; ++t) a.conc[(int64_t)t * a.U + mu] = conc[t];
     }
-    if (!FULL && a.conc && mvalid)                        // forward(): model concentrations
-        for (int t = 0; t < a.K; ++t) a.conc[(int64_t)t * a.U + mu] = conc[t];
     NGRTD_PROBE(3);
-    NGRTD_PROBE(4);
-    NGRTD_PROBE(5);
     if (!logp && !dacc.lp) return;                        // forward() launch: no log-prob
-    part[mi] = th + like;
+    if (ROLES == 1) {
+        part[mi] = th + like;
+    } else {
+        if (do_rtd) part2[mi] = like;
+        __syncthreads();
+        if (do_theta) part[mi] = th + part2[mi];          // th + like, as ROLES = 1
+    }
     NGRTD_PROBE(6);
     __syncthreads();
     if (WB <= 64 && (WB & (WB - 1)) == 0) {
@@ -1124,7 +1214,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves) logp_fused_kernel(const RtdA
     }
     if (dacc.lp) {   // DE-MC: accepted walkers take the proposal's theta rows of this unit
         __syncthreads();
-        if (mvalid && dec[mwl])
+        if (do_theta && mvalid && dec[mwl])
             for (int p = 0; p < dacc.P; ++p) dacc.x[(int64_t)p * a.U + mu] = dacc.prop[(int64_t)p * a.U + mu];
     }
     NGRTD_PROBE(7);

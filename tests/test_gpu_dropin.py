@@ -81,8 +81,11 @@ def test_tracer_conv_integral(golden, tname):
         got = cm.convolve()      # batched path: all parameter sets in one launch
         assert close(got, ref, 1e-12, 1e-300).all(), key
     cm.update_pars(tau=37.3, mod_type="exponential", t_half=t_half, rad_accum=accum, J=J)
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(TypeError):   # frac_inf_diff without bbar / Phi_im: None arithmetic, as the reference
         cm.update_pars(tau=1.0, mod_type="frac_inf_diff")
+        cm.convolve()
+    with pytest.raises(ValueError):
+        cm.update_pars(tau=1.0, mod_type="frac_inf_diff_typo")
         cm.convolve()
 
 
