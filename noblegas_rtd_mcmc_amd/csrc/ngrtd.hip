@@ -409,7 +409,7 @@ static void launch_mfma(const RtdArgs& a, const UnitArgs& u, int32_t fuse, hipSt
 // data (ce obs, 1/sd^2, sums of 0.5 log 1/sd^2, E_min; rtd obs, 1/sd^2, sums).
 static size_t fused_lds(const RtdArgs& a, const UnitArgs& u) {
     const size_t wells = (size_t)u.L * ((u.ce_on ? 2 * u.G + 2 : 0) + (u.rtd_on ? 2 * u.K + 1 : 0));
-    return (size_t)(2 * kFusedUnits + kFusedUnits / 2 + kChebPieces * kChebN * cheb_cp(a.C) + wells) * sizeof(double);
+    return (size_t)(2 * kFusedUnits + kFusedUnits / 2 + kChebPieces * cheb_lds_stride(a.C) + wells) * sizeof(double);
 }
 constexpr size_t kFusedMaxLds = 150 * 1024;
 static bool fused_path(const RtdArgs& a, const UnitArgs& u) {

@@ -1039,6 +1039,11 @@ __device__ __forceinline__ void fused_exact(const RtdArgs& a, const UnitArgs& ul
 constexpr int kFusedWaves = 8;                 // waves of units per block (512 units)
 constexpr int kFusedUnits = 64 * kFusedWaves;
 constexpr int kFusedPrefetch = 4;   // double2 per thread (512 threads): covers kChebPieces*kChebN*6 doubles
+// LDS stride of one surrogate piece: kChebN*CP doubles + 2 of padding, so that consecutive
+// pieces start 16-B slots an ODD number apart -- lanes gathering different pieces with
+// ds_read_b128 then spread over all 16 slots of a bank row instead of 4 (MI355X_MICROARCH.md
+// §LDS: a b128 lane group conflicts on equal slots).
+__host__ __device__ constexpr int cheb_lds_stride(int C) { return kChebN * cheb_cp(C) + 2; }
 
 // ROLES = 1: one wave per 64 units runs the whole unit (2 waves/SIMD at c4, 228 VGPRs).
 // ROLES = 2: the block has 2 x 8 waves; waves 0-7 run the theta-only block (priors, CE model,
@@ -1056,6 +1061,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     constexpr int NTH = 64 * kFusedWaves * ROLES;           // threads per block
     constexpr int NPRE = (kFusedPrefetch * 64 * kFusedWaves + NTH - 1) / NTH;
     constexpr int TAB2 = kChebPieces * kChebN * CP / 2;   // double2 entries of the surrogate table
+    constexpr int PST = cheb_lds_stride(C);               // LDS doubles per piece (padded)
     static_assert(NT == 4, "one unit per lane needs 4 tiles per wave");
     static_assert(TAB2 <= NPRE * NTH, "prefetch covers the table");
     extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -1094,7 +1100,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     const int64_t mu = mvalid ? (int64_t)ml * W + w0 + mwl : 0;
     // per-well observation data -> LDS (read per lane by the likelihood blocks): all loads
     // issued before any store, so the prologue pays one memory latency
-    double* wd = cheb + kChebPieces * kChebN * CP;
+    double* wd = cheb + kChebPieces * PST;
     constexpr int kWdRegs = (4 * 64 * kFusedWaves + NTH - 1) / NTH;
     double wv[kWdRegs];
 #pragma unroll
@@ -1114,7 +1120,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
 #pragma unroll
         for (int r = 0; r < NPRE; ++r) {
             const int i = tid + r * NTH;
-            if (i < TAB2) dst[i] = pre[r];
+            if (i < TAB2) dst[(i / (kChebN * CP / 2)) * (PST / 2) + i % (kChebN * CP / 2)] = pre[r];
         }
     }
     UnitArgs ul = ua;
@@ -1168,7 +1174,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         const bool bad = cpc < 0 && !skip;
         cpc = cpc < 0 ? 0 : cpc;
         double zz[C + 1];
-        cheb_sums<C + 1, ROLES == 2>(cheb + cpc * (kChebN * CP), CP, cx, zz);   // s01 Y_c (c < C), s01 G
+        cheb_sums<C + 1, ROLES == 2>(cheb + cpc * PST, CP, cx, zz);   // s01 Y_c (c < C), s01 G
         double conc[kMaxTracer];
         {
             double num[C];
