@@ -41,6 +41,7 @@ def parse():
     ap.add_argument("--ages", type=int, default=1200)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-overlap", action="store_true", help="N > 1: all-gather on the compute stream")
     ap.add_argument("--event-every", type=int, default=8,
                     help="bracket the kernels of every k-th timed step with HIP events (kernel roofline)")
     return ap.parse_args()
@@ -94,13 +95,38 @@ def main():
     theta_h = workloads.sample_prior(spec, W, np.random.default_rng(34568 + rank))
     theta = torch.from_numpy(theta_h).to(dev)
     lp = LogProb(spec, max_walkers=W, device=local)
-    out = torch.empty(W, dtype=torch.float64, device=dev)
-    gathered = torch.empty(W * world, dtype=torch.float64, device=dev)
+    # N > 1: the all-gather of step i runs on a communication stream while step i+1's
+    # kernel runs (double-buffered logp / gather buffers); the compute stream reuses a
+    # buffer only after the gather that read it has finished.  --no-overlap serialises.
+    outs = [torch.empty(W, dtype=torch.float64, device=dev) for _ in range(2)]
+    gathered = [torch.empty(W * world, dtype=torch.float64, device=dev) for _ in range(2)]
+    overlap = world > 1 and not args.no_overlap
+    comm = torch.cuda.Stream(device=dev) if overlap else None
+    ready = [torch.cuda.Event() for _ in range(2)]
+    freed = [torch.cuda.Event() for _ in range(2)]
+    issued = [False, False]
+    nstep = [0]
 
     def step():
-        lp(theta, out=out)
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, out)
+        k = nstep[0] % 2
+        nstep[0] += 1
+        o = outs[k]
+        if not overlap:
+            lp(theta, out=o)
+            if world > 1:
+                dist.all_gather_into_tensor(gathered[k], o)
+            return
+        cur = torch.cuda.current_stream(dev)
+        if issued[k]:
+            cur.wait_event(freed[k])              # the gather that read outs[k] is done
+        lp(theta, out=o)
+        ready[k].record(cur)
+        comm.wait_event(ready[k])
+        with torch.cuda.stream(comm):
+            dist.all_gather_into_tensor(gathered[k], o)
+            freed[k].record(comm)
+        issued[k] = True
+    out = outs[0]
 
     for _ in range(args.warmup):
         step()
@@ -209,7 +235,9 @@ def main():
             "config": {"workload": "c4 joint CE+RTD log-prob: %d walkers/GPU x %d wells x (5 gases CE + 5 tracers "
                                    "RTD exponential, N=%d ages)" % (W, args.wells, N),
                        "walkers_per_gpu": W, "wells": args.wells, "gases": 5, "tracers": 5, "ages": N,
-                       "parallelism": "walker blocks per GPU + RCCL all-gather of logp" if world > 1 else "single GPU"},
+                       "parallelism": ("walker blocks per GPU + RCCL all-gather of logp" +
+                                       (" (overlapped with the next step's kernel)" if overlap else ""))
+                                      if world > 1 else "single GPU"},
             "roofline": {"bound": "mfma", "achieved": achieved / 1e12 if achieved else None,
                          "peak": FP64_MFMA_PEAK / 1e12, "unit": "TFLOP/s",
                          "frac": achieved / FP64_MFMA_PEAK if achieved else None, "traffic": traffic,

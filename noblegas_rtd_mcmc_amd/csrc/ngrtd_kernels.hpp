@@ -741,15 +741,19 @@ __host__ __device__ __forceinline__ void cheb_sums(const double* pc, int CP, dou
 #pragma unroll
     for (int c = 0; c < C; ++c) { b1[c] = 0.0; b2[c] = 0.0; }
 #if defined(__HIP_DEVICE_COMPILE__)
-    if (PIPE) {
-        double cur[C];
+    if (PIPE) {   // rows k (cur) and k-1 (nxt) in registers, row k-2 in flight
+        double cur[C], nxt[C];
 #pragma unroll
         for (int c = 0; c < C; ++c) cur[c] = pc[(kChebN - 1) * CP + c];
 #pragma unroll
-        for (int k = kChebN - 1; k >= 1; --k) {
-            double nxt[C];
+        for (int c = 0; c < C; ++c) nxt[c] = pc[(kChebN - 2) * CP + c];
 #pragma unroll
-            for (int c = 0; c < C; ++c) nxt[c] = pc[(k - 1) * CP + c];   // row k-1 (row 0 at k = 1)
+        for (int k = kChebN - 1; k >= 1; --k) {
+            double nn[C];
+            if (k >= 2) {
+#pragma unroll
+                for (int c = 0; c < C; ++c) nn[c] = pc[(k - 2) * CP + c];
+            }
 #pragma unroll
             for (int c = 0; c < C; ++c) {
                 const double t = fma(x2, b1[c], cur[c] - b2[c]);
@@ -760,7 +764,10 @@ __host__ __device__ __forceinline__ void cheb_sums(const double* pc, int CP, dou
             for (int c = 0; c < C; ++c) asm volatile("" : "+v"(b1[c]));
             asm volatile("" ::: "memory");
 #pragma unroll
-            for (int c = 0; c < C; ++c) cur[c] = nxt[c];
+            for (int c = 0; c < C; ++c) {
+                cur[c] = nxt[c];
+                if (k >= 2) nxt[c] = nn[c];
+            }
         }
 #pragma unroll
         for (int c = 0; c < C; ++c) y[c] = fma(x, b1[c], cur[c] - b2[c]);
@@ -1143,15 +1150,17 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     NGRTD_PROBE(1);
     // theta of this lane's unit (after the barrier: the 8.4 MB theta read at c4 is
     // bandwidth-bound, and the tables' loads before the barrier should not wait behind it)
+    // (theta rows are loaded after the barrier: issued before it, with the table loads,
+    // they lengthened the prologue by more than they saved -- tools/section_probe.py)
     double th = 0.0, like = 0.0;
+    ThetaPre tp{};
+    double tau = 1.0;
     if (do_theta) {
-        ThetaPre tp;
         theta_preload(ua, mu, tp);
         th = mvalid ? unit_logp_theta(ul, mu, ml, &tp, FULL) : 0.0;
     }
     if (do_rtd) {
-        const double tau = mvalid ? a.theta[(int64_t)a.row_tau[0] * a.U + mu] : 1.0;
-        ThetaPre tp;
+        tau = mvalid ? a.theta[(int64_t)a.row_tau[0] * a.U + mu] : 1.0;
         tp.nub = (FULL || ua.rtd_on) ? a.theta[(int64_t)ua.row_nu * a.U + mu] : 0.0;
         // The surrogate channel sums, the concentrations and the RTD likelihood.  Lanes
         // whose tau the surrogate does not cover evaluate piece 0 here and are redone

@@ -1,15 +1,14 @@
 #!/usr/bin/env python3
-"""Per-section shader-clock timing of logp_fused_kernel (c4 workload).
+"""Per-section shader-clock timing of logp_fused_kernel (c4 workload, ROLES = 2 layout).
 
 Builds noblegas_rtd_mcmc_amd/libngrtd_probe.so with -DNGRTD_SECTION_PROBE (lane 0 of each
-wave stamps s_memtime at 8 points, ngrtd_kernels.hpp NGRTD_PROBE), runs the c4 log-prob,
-and prints the median cycles per section for the RTD-first waves (0-3) and the CE-first
-waves (4-7) of each block:
+wave stamps s_memtime at the NGRTD_PROBE points of ngrtd_kernels.hpp), runs the c4
+log-prob, and prints the median cycles per section for the theta-role waves (0-7 of each
+block) and the RTD-role waves (8-15):
 
-  0->1 fragment-table LDS copy + barrier     1->2 CE/prior part (CE-first waves)
-  2->3 MFMA init (q powers)                   3->4 MFMA steps
-  4->5 segment recombination + tile pick      5->6 conc + RTD likelihood (+ CE, RTD-first)
-  6->7 barrier + per-walker sum over wells
+  0->1 prologue: table loads, LDS stores, barrier
+  1->3 the role's work (RTD waves: 1->2 surrogate + likelihood, 2->3 exact fallback)
+  3->6 exchange barrier (th + like)          6->7 per-walker sum over wells
 
     python tools/section_probe.py [--wells 64] [--walkers 2048]
 """
@@ -71,33 +70,28 @@ def main():
     ks = lp.kernel_stats(reset=True)
     lib = _lib.load()
     lib.ngrtd_probe_read.argtypes = [C.c_void_p, C.c_int64]
-    blocks = lp.info(args.walkers)
-    nwaves = (args.walkers * args.wells + 511) // 512 * 8
+    nwaves = (args.walkers * args.wells + 511) // 512 * 16
     buf = np.zeros(nwaves * 8, dtype=np.uint64)
     assert lib.ngrtd_probe_read(buf.ctypes.data, buf.size) == 0
     t = buf.reshape(-1, 8).astype(np.int64)
-    d = np.diff(t, axis=1)
-    names = ["lds_copy", "ce_first_theta", "mfma_init", "mfma_steps", "finish_pick", "conc_like(+theta)",
-             "reduce"]
-    res = {"kernel_us_event": ks["fused"][0] * 1e3, "span_cycles": int(t[:, 7].max() - t[:, 0].min())}
-    w = np.arange(t.shape[0]) % 8
-    for grp, sel in (("rtd_first", w < 4), ("ce_first", w >= 4)):
-        res[grp] = {n: float(np.median(d[sel, i])) for i, n in enumerate(names)}
-        res[grp]["total"] = float(np.median(t[sel, 7] - t[sel, 0]))
+    w = np.arange(t.shape[0]) % 16
+    res = {"kernel_us_event": ks["fused"][0] * 1e3}
+    for grp, sel in (("theta_role", w < 8), ("rtd_role", w >= 8)):
+        tt = t[sel]
+        r = {"prologue": tt[:, 1] - tt[:, 0], "work": tt[:, 3] - tt[:, 1], "exchange": tt[:, 6] - tt[:, 3],
+             "reduce": tt[:, 7] - tt[:, 6], "total": tt[:, 7] - tt[:, 0]}
+        if grp == "rtd_role":
+            r["surrogate_like"] = tt[:, 2] - tt[:, 1]
+        res[grp] = {k: float(np.median(v)) for k, v in r.items()}
     # s_memtime counters are per XCD (block b runs on XCD b % 8): spans within one XCD
-    blk = np.arange(t.shape[0]) // 8
-    spans, starts, ends = [], [], []
-    for x in range(8):
-        sel = (blk % 8) == x
-        if sel.any():
-            t0 = t[sel, 0].min()
-            spans.append(int(t[sel, 7].max() - t0))
-            starts.append(np.percentile(t[sel, 0] - t0, [50, 90, 100]).tolist())
-            ends.append(np.percentile(t[sel, 7] - t0, [10, 50, 100]).tolist())
-    res["xcd_span_cycles"] = spans
-    res["xcd_wave_start_p50_p90_max"] = starts[0]
-    res["xcd_wave_end_p10_p50_max"] = ends[0]
-    del res["span_cycles"]
+    blk = np.arange(t.shape[0]) // 16
+    sel = (blk % 8) == 0
+    t0 = t[sel, 0].min()
+    res["xcd0_span_cycles"] = int(t[sel, 7].max() - t0)
+    res["xcd0_wave_start_p50_p90_max"] = np.percentile(t[sel, 0] - t0, [50, 90, 100]).tolist()
+    res["xcd0_theta_end_p10_p50_max"] = np.percentile(t[sel & (w < 8), 3] - t0, [10, 50, 100]).tolist()
+    res["xcd0_rtd_end_p10_p50_max"] = np.percentile(t[sel & (w >= 8), 3] - t0, [10, 50, 100]).tolist()
+    res["xcd0_wave_end_p10_p50_max"] = np.percentile(t[sel, 7] - t0, [10, 50, 100]).tolist()
     print(json.dumps(res, indent=1))
 
 
