@@ -25,17 +25,36 @@ struct HeCompsArgs {
     double* out;           // [NGRTD_HE_NOUT][n]
 };
 
+// noble_gas_fun(gases=['He'], E, T, Ae, F, P='lapse_rate') (:76-113), S = 0.0, then the
+// mass balance of :400-421.  Restated for one pass over the member with the per-unit
+// rewrites of ce_model_s0 (ngrtd_kernels.hpp): table-driven fexp/flog
+// instead of OCML pow/exp (<= 1-2 ulp), ln K in Horner form of 1/x (one division), and
+// K_He = K_Ar / F_He exactly as the reference's chain of ratios
+// (5.24e-6 / (F (5.24e-6/9.31e-3) (9.31e-3 / K_Ar))), so x_He = gamma p_He exp(ln F - ln K_Ar);
+// the Setchenow factor exp(0 * setch) is 1, or NaN when T < 65 and T_k <= 0.  Each rewrite
+// moves a result by a few ulp; He4_ter / He4_del / He3_tu then inherit them relative to
+// their cancelling operands (tests/test_gpu_prep.py).
 NGRTD_HD void he_comps(double He4_obs, double He3_obs, double Ae, double F, double E, double T, double Rterr,
                        double o[NGRTD_HE_NOUT]) {
-    // noble_gas_fun(gases=['He'], E, T, Ae, F, P='lapse_rate') (:76-113), S = 0.0
-    const double P = lapse_rate(E);
-    const double Pv = vapor_pressure(T);
-    const double K = solubility(NGRTD_HE, T, 0.0);
-    const double He4_eq = equil_conc(NGRTD_HE, P, K);                 // equil_conc()['He'], :202-213
-    const double ceq = equil_conc_dry(NGRTD_HE, T, P, Pv, K);
-    const double He4_atm = ce_excess(NGRTD_HE, Ae, F, ceq) + ceq;     // ce_exc(True)['He'], :235-253
-    const double He4_ter = He4_obs - He4_atm;                          // :405
-    const double He4_del = 100 * (He4_ter / He4_atm);                  // :408
+    const double P = lapse_rate_fast(E);
+    double A, B, Cc;
+    if (T <= 99.0) { A = 8.07131; B = 1730.63; Cc = 233.426; }
+    else           { A = 8.14019; B = 1810.94; Cc = 244.485; }
+    const double Pv = fexp10(A - (B / (Cc + T))) * (101325. / 760. / 1.0e9);
+    const double T_k = T + 273.15;
+    const double ix = 1.0 / (.001 * T_k);
+    const double gamma = (T < 65. && !(T_k > 0.0)) ? __builtin_nan("") : 1.0;
+    const GasCoef he = gas_coef(NGRTD_HE), ar = gas_coef(NGRTD_AR);
+    const double lnF = fma(fma(fma(he.A3, ix, he.A2), ix, he.A1), ix, he.A0);
+    const double lnAr = fma(fma(fma(ar.A3, ix, ar.A2), ix, ar.A1), ix, ar.A0);
+    const double e = gamma * fexp(lnF - lnAr);                          // 1 / K_He
+    const double z = he.z;
+    const double He4_eq = ((z * P) * e) * (22414. / 18.);               // equil_conc()['He'], :202-213
+    const double ceq = (T < 0.0) ? -9999.0 : ((z * (P - Pv)) * e) * (22414. / 18.);   // :216-232
+    const double ex = ((1 - F) * Ae * z) * ceq / (ceq + F * Ae * z);     // ce_exc excess, :247-248
+    const double He4_atm = ex + ceq;                                     // ce_exc(True)['He']
+    const double He4_ter = He4_obs - He4_atm;                            // :405
+    const double He4_del = 100 * (He4_ter / He4_atm);                   // :408
     // 3He mass balance, :414-421: Ratm = 1.384e-6, CF = 4.021e14/(1-S) with S = 0
     const double Ratm = 1.384e-6;
     const double CF = 4.021e14 / (1 - 0.0);
@@ -48,6 +67,8 @@ NGRTD_HD void he_comps(double He4_obs, double He3_obs, double Ae, double F, doub
 }
 
 __global__ void __launch_bounds__(256) he_comps_kernel(const HeCompsArgs a) {
+    fm_lds_init();
+    __syncthreads();
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.n) return;
     double o[NGRTD_HE_NOUT];
@@ -57,18 +78,18 @@ __global__ void __launch_bounds__(256) he_comps_kernel(const HeCompsArgs a) {
 }
 
 // ------------------------------------------------------------ CFC / SF6 correction
-// utils/cfc_utils.py: vapor_pressure_atm (:34-51, :181-196), lapse_rate_atm (:53-62,
-// :198-206) -- both in atm.
+// utils/cfc_utils.py: vapor_pressure_atm (:34-51, :181-196) and lapse_rate_atm (:53-62,
+// :198-206), both in atm, through the table-driven fexp10 / fexp / flog (<= 1-2 ulp against
+// libm pow; the parity bar is 1e-12).
 NGRTD_HD double vapor_pressure_atm(double T) {
     double A, B, C;
     if (T <= 99.0) { A = 8.07131; B = 1730.63; C = 233.426; }
     else           { A = 8.14019; B = 1810.94; C = 244.485; }
-    double P = pow(10.0, A - (B / (C + T)));   // mmHg
-    P = P / 760. * 101325;                      // Pa
-    double P_vapor = P / 1.0e9;                 // GPa
-    return P_vapor / 0.000101325;               // atm
+    // mmHg -> Pa -> GPa -> atm (P/760.*101325, /1.0e9, /0.000101325) as ONE multiply by
+    // the folded constant: <= 3 ulp from the reference's three roundings
+    return fexp10(A - (B / (C + T))) * (101325. / 760. / 1.0e9 / 0.000101325);
 }
-NGRTD_HD double lapse_rate_atm(double E) { return pow(1 - .0065 * E / 288.15, 5.2561); }
+NGRTD_HD double lapse_rate_atm(double E) { return fexp(5.2561 * flog(1 - .0065 * E / 288.15)); }
 
 // Bullister solubility coefficients [a1, a2, a3, b1, b2, b3]: cfc_dict (:74) and
 // solubility_sf6 (:214-219); index = enum ngrtd_cfc_species
@@ -80,13 +101,20 @@ NGRTD_HD void cfc_coef(int sp, double c[6]) {
     default:           c[0] = -98.7264000; c[1] = 142.803; c[2] = 38.8746; c[3] = 0.0268696; c[4] = -0.0334407; c[5] = 0.0070843; break;
     }
 }
-// solubility_cfc (:64-84) / solubility_sf6 (:208-221) [mol atm^-1 kg^-1]
-NGRTD_HD double solubility_cfc(int sp, double T, double S) {
+// per-member terms of solubility_cfc (:64-84) / solubility_sf6 (:208-221) shared by the
+// species: 100 / T_k, log(T_k / 100), T_k / 100 (the reference recomputes them per species)
+struct CfcT {
+    double r100, lg, r;
+};
+NGRTD_HD CfcT cfc_t(double T) {
+    const double T_k = T + 273.15;
+    return {100 / T_k, flog(T_k / 100), T_k / 100};
+}
+// K [mol atm^-1 kg^-1]
+NGRTD_HD double solubility_cfc(int sp, const CfcT& t, double S) {
     double c[6];
     cfc_coef(sp, c);
-    const double T_k = T + 273.15;
-    const double r = T_k / 100;
-    return exp(c[0] + c[1] * (100 / T_k) + c[2] * log(T_k / 100) + S * (c[3] + c[4] * r + c[5] * (r * r)));
+    return fexp(c[0] + c[1] * t.r100 + c[2] * t.lg + S * (c[3] + c[4] * t.r + c[5] * (t.r * t.r)));
 }
 
 struct CfcArgs {
@@ -97,25 +125,23 @@ struct CfcArgs {
     double* out;                                 // [ns][n] ([n] for the pressure entries)
 };
 
-// Ae is self.Ae, ccSTP/kg (the constructor's Ae*1000., :30, :176)
-NGRTD_HD double cfc_value(int what, int sp, double E, double T, double Ae, double F, double S, double Pself,
-                          double x) {
+// Ae is self.Ae, ccSTP/kg (the constructor's Ae*1000., :30, :176); P_da / P_vapor per member
+NGRTD_HD double cfc_value(int what, int sp, const CfcT& t, double P_da, double P_vapor, double Ae, double F,
+                          double S, double Pself, double x) {
     const bool sf6 = (sp == NGRTD_SF6);
-    const double Ki = solubility_cfc(sp, T, S);
+    const double Ki = solubility_cfc(sp, t, S);
     if (what == NGRTD_CFC_SOLUBILITY) return Ki;
     if (what == NGRTD_CFC_EQUIL_AIR) {           // equil_air_conc_cfc :86-106 / _sf6 :229-249
-        const double P_da = lapse_rate_atm(E) - vapor_pressure_atm(T);
-        const double molar_volume = 22414.1;
-        const double z = (x + ((x * F * (Ae / molar_volume)) / (Ki * P_da))) / (Ki * P_da + (Ae / molar_volume));
+        const double am = Ae / 22414.1;          // Ae/molar_volume (same value per species)
+        const double KP = Ki * P_da;
+        const double z = (x + ((x * F * am) / KP)) / (KP + am);
         return sf6 ? z * 0.001 : z;
     }
     if (what == NGRTD_CFC_EQUIL_AQ) {            // equil_aq_conc_cfc :108-124 / _sf6 :264-278
-        const double P_da = lapse_rate_atm(E) - vapor_pressure_atm(T);
         const double C = Ki * x * P_da;
         return sf6 ? C / 0.001 : C;
     }
     // ce_exc_conc_cfc :126-142 / _sf6 :280-296 (uses self.P as last set by lapse_rate_atm)
-    const double P_vapor = vapor_pressure_atm(T);
     const double C_eq = Ki * x * (Pself - P_vapor);
     const double Aem = Ae / 22414 / 1e-12;
     const double num = (1 - F) * Aem * (x * 1e-12);
@@ -124,19 +150,25 @@ NGRTD_HD double cfc_value(int what, int sp, double E, double T, double Ae, doubl
 }
 
 __global__ void __launch_bounds__(256) cfc_corr_kernel(const CfcArgs a) {
+    fm_lds_init();
+    __syncthreads();
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.n) return;
     const double E = a.E ? a.E[i] : 0.0;
     const double T = a.T ? a.T[i] : 0.0;
     if (a.what == NGRTD_CFC_LAPSE_RATE_ATM) { a.out[i] = lapse_rate_atm(E); return; }
-    if (a.what == NGRTD_CFC_VAPOR_PRESSURE_ATM) { a.out[i] = vapor_pressure_atm(T); return; }
+    const double P_vapor = vapor_pressure_atm(T);
+    if (a.what == NGRTD_CFC_VAPOR_PRESSURE_ATM) { a.out[i] = P_vapor; return; }
     const double Ae = a.Ae ? a.Ae[i] : 0.0;
     const double F = a.F ? a.F[i] : 0.0;
     const double S = a.S ? a.S[i] : 0.0;
     const double P = a.P ? a.P[i] : 0.0;
+    const bool need_pda = a.what == NGRTD_CFC_EQUIL_AIR || a.what == NGRTD_CFC_EQUIL_AQ;
+    const double P_da = need_pda ? lapse_rate_atm(E) - P_vapor : 0.0;
+    const CfcT t = cfc_t(T);
     for (int j = 0; j < a.ns; ++j) {
         const double x = a.x ? a.x[(int64_t)j * a.n + i] : 0.0;
-        a.out[(int64_t)j * a.n + i] = cfc_value(a.what, a.sp[j], E, T, Ae, F, S, P, x);
+        a.out[(int64_t)j * a.n + i] = cfc_value(a.what, a.sp[j], t, P_da, P_vapor, Ae, F, S, P, x);
     }
 }
 
