@@ -88,6 +88,8 @@ __global__ void __launch_bounds__(64 * kFracWaves) frac_inner_kernel(const FracA
     const double c4piD = 4. * kPi * D;
     const double c4D = 4. * D;
     const double c2spi = 2 * 1.7724538509055159;   // 2*np.sqrt(np.pi)
+    const double kc = kappa / c2spi;
+    const double inv_bbar = 1.0 / bbar;
     // numpy logspace(-6, stop, 1000) = 10 ** linspace(-6, stop, 1000):
     // y_j = j * step + start, y_999 = stop (step = (stop - start) / 999; step == 0 -> j/999*delta)
     const double start = -6.0;
@@ -108,12 +110,18 @@ __global__ void __launch_bounds__(64 * kFracWaves) frac_inner_kernel(const FracA
         if (ext) {
             f_tadv = interp_age(tadv, ext, i, a.tp0, a.dtp);
         } else {
-            const double x = tadv / tau;
-            f_tadv = (inv_tau / (sqrt(c4piD * x))) * (1. / x) * fexp(-1. * (((1. - x) * (1. - x)) / (c4D * x)));
+            // ((1/tau)/sqrt(4 pi D x)) (1/x) exp(-(1-x)^2/(4 D x)), x = tadv/tau: the two
+            // prefactor divisions merged and x by the hoisted 1/tau (a few ulp; 2 divisions)
+            const double x = tadv * inv_tau;
+            f_tadv = (inv_tau / (sqrt(c4piD * x) * x)) * fexp(-1. * (((1. - x) * (1. - x)) / (c4D * x)));
         }
+        // kappa beta / (2 sqrt(pi) t^1.5) exp(-kappa^2 beta^2 / (4 t)), beta = tadv/bbar:
+        // ONE division 1/(t sqrt t) gives both t^-1.5 and 1/t = sqrt(t) / (t sqrt t)
         const double t_ret = tp_i - tadv;
-        const double beta = tadv / bbar;
-        const double f_ret = (kappa * beta) / (c2spi * (t_ret * sqrt(t_ret))) * fexp((k2 * (beta * beta)) / (4 * t_ret));
+        const double beta = tadv * inv_bbar;
+        const double st = sqrt(t_ret);
+        const double it15 = 1.0 / (t_ret * st);
+        const double f_ret = (kc * beta) * it15 * fexp((k2 * (beta * beta)) * (0.25 * (st * it15)));
         const double fi = f_ret * f_tadv;
         // left neighbour (j - 1): lane - 1 of this k, or lane 63 of the previous k
         double l_t = shfl_up1(t_ret), l_fr = shfl_up1(f_ret), l_ta = shfl_up1(tadv), l_fi = shfl_up1(fi);
