@@ -41,8 +41,22 @@ struct FracArgs {
     double* f;                            // [n][N] inner integrals f_t_tran
 };
 
-__device__ __forceinline__ double shfl_up1(double v) { return __shfl_up(v, 1, 64); }
-__device__ __forceinline__ double bcast63(double v) { return __shfl(v, 63, 64); }
+// lane l <- lane l-1 of v, lane 0 <- c: DPP wave_shr:1 (a VALU operand modifier on gfx9-family
+// gfx950, no LDS crossbar), per 32-bit half
+__device__ __forceinline__ double shr1_or(double v, double c) {
+    const unsigned long long vb = __double_as_longlong(v), cb = __double_as_longlong(c);
+    const int lo = __builtin_amdgcn_update_dpp((int)(unsigned)cb, (int)(unsigned)vb, 0x138, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(unsigned)(cb >> 32), (int)(unsigned)(vb >> 32), 0x138, 0xf, 0xf,
+                                               false);
+    return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+// lane 63's value in every lane (v_readlane: VALU -> SGPR, no LDS)
+__device__ __forceinline__ double bcast63(double v) {
+    const unsigned long long vb = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(unsigned)vb, 63);
+    const int hi = __builtin_amdgcn_readlane((int)(unsigned)(vb >> 32), 63);
+    return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
 
 // np.interp(x, tp[:i+1], fp[:i+1]) on the uniform age grid tp_k = k + dtp (tp_0 = tp0):
 // numpy's linear interpolation with its exact-knot and NaN-retry rules.
@@ -124,8 +138,8 @@ __global__ void __launch_bounds__(64 * kFracWaves) frac_inner_kernel(const FracA
         const double f_ret = (kc * beta) * it15 * fexp((k2 * (beta * beta)) * (0.25 * (st * it15)));
         const double fi = f_ret * f_tadv;
         // left neighbour (j - 1): lane - 1 of this k, or lane 63 of the previous k
-        double l_t = shfl_up1(t_ret), l_fr = shfl_up1(f_ret), l_ta = shfl_up1(tadv), l_fi = shfl_up1(fi);
-        if (lane == 0) { l_t = c_t; l_fr = c_fr; l_ta = c_ta; l_fi = c_fi; }
+        const double l_t = shr1_or(t_ret, c_t), l_fr = shr1_or(f_ret, c_fr);
+        const double l_ta = shr1_or(tadv, c_ta), l_fi = shr1_or(fi, c_fi);
         if (j >= 1 && j < kFracPts) {
             s_norm += (l_t - t_ret) * (l_fr + f_ret);      // trapz(f_ret[::-1], t_ret[::-1])
             s_int += (tadv - l_ta) * (fi + l_fi);          // trapz(f_ret * f_tadv, tadv)
