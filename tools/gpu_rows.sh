@@ -22,3 +22,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/p
 step prep-stats
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_prep -o stats -- python3 tools/prep_bench.py > $OUT/prof_prep.json 2> $OUT/prof_prep.err || { echo "prep stats failed" >> $OUT/steps.log; exit 1; }
 step done
+step sampler-sweep
+timeout -k 10 300 python tools/sampler_bench.py > $OUT/sampler_bench.json 2> $OUT/sampler.err || { echo "sampler bench failed" >> $OUT/steps.log; exit 1; }
+timeout -k 10 300 python tools/sweep_bench.py > $OUT/sweep_bench.json 2> $OUT/sweep.err || { echo "sweep bench failed" >> $OUT/steps.log; exit 1; }
+step done2
