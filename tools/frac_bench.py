@@ -27,7 +27,7 @@ def main():
     ap.add_argument("--ages", type=int, default=1200)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--pmc", default=None, help="PMC summary json (FP64 FLOPs of frac_inner_kernel)")
+    ap.add_argument("--pmc-dir", default=None, help="rocprofv3 --pmc output of this tool (SQ_INSTS_VALU_FLOPS_FP64)")
     args = ap.parse_args()
     import torch
     from noblegas_rtd_mcmc_amd import _lib, workloads
@@ -83,14 +83,20 @@ def main():
             "cpu_baseline": {"value": k / t_cpu, "unit": "sets/s", "cores": 1, "kind": "port",
                              "sample": "%d sets, oracle/rtd.py frac_g_tp + convolve (NumPy; numba absent)" % k},
             "max_rel_err_vs_oracle": worst}
-    if args.pmc and os.path.exists(args.pmc):
-        with open(args.pmc) as f:
-            for kname, e in json.load(f).items():
-                if "frac_inner_kernel" in kname and e.get("SQ_INSTS_VALU_FLOPS_FP64"):
-                    # per launch: SQ_INSTS_VALU_FLOPS_FP64 is per-lane-op count / 64 (fma = 2)
-                    flop = e["SQ_INSTS_VALU_FLOPS_FP64"] * 64
-                    line["fp64_flop_per_call"] = flop
-                    line["fp64_tflops"] = flop / (ms * 1e-3) / 1e12
+    if args.pmc_dir and os.path.isdir(args.pmc_dir):
+        sys.path.insert(0, os.path.join(REPO, "tools"))
+        from pmc_summary import summarize
+        for kname, e in summarize([args.pmc_dir]).items():
+            if "frac_inner_kernel" in kname and e.get("SQ_INSTS_VALU_FLOPS_FP64"):
+                # FP64 FLOP of one inner launch: SQ_INSTS_VALU_FLOPS_FP64 x 64 lanes (fma = 2),
+                # the convention of bench.py / DESIGN.md 6; time: this run's per-call time
+                # (the inner kernel is 99.9 % of it, profiles/r01_frac_kernel_stats.csv)
+                flop = e["SQ_INSTS_VALU_FLOPS_FP64"] * 64
+                ach = flop / (ms * 1e-3)
+                line["roofline"] = {"bound": "mfma", "achieved": ach / 1e12, "peak": 78.6, "unit": "TFLOP/s",
+                                    "frac": ach / 78.6e12, "fp64_valu_peak_measured": 38.3,
+                                    "frac_of_fp64_valu_peak": ach / 38.3e12, "flop_per_call": flop,
+                                    "flop_per_point": flop / pts, "kernel": "frac_inner_kernel"}
     print(json.dumps(line), flush=True)
     assert worst <= 1e-12, worst
 
