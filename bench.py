@@ -216,6 +216,7 @@ def main():
             flops = 2.0 * U * C * (N - 1)
             flop_src = "2 * units * channels * (N - 1) (matrix-core Horner)"
         achieved = flops / (kms * 1e-3) if flops else None
+        evals_per_s_kernel = W / (kms * 1e-3)
         # algorithmic HBM bytes of the same launch: every theta row read once + logp out
         hbm_bytes = U * 8.0 * len(spec.roles) + (W * 8.0 if kname == "fused" else U * 8.0 * len(spec.rtd.tracers))
         evals = W * world * args.steps
@@ -245,6 +246,11 @@ def main():
                          "pipe": "FP64 (gfx950 FP64 VALU and MFMA share one pipe; the surrogate path is VALU)",
                          "fp64_valu_peak_measured": FP64_VALU_PEAK / 1e12,
                          "frac_of_fp64_valu_peak": achieved / FP64_VALU_PEAK if achieved else None,
+                         # SURVEY.md §8d froze the REFERENCE algorithm's count (2 exp per age at
+                         # X = 20, 167 FLOP per walker-well-age + 850 CE): informational only --
+                         # the surrogate/Horner rewrite does not execute that work
+                         "survey_8d_flop_per_eval": args.wells * (N * 167.0 + 850.0),
+                         "survey_8d_equivalent_TFLOPs": evals_per_s_kernel * args.wells * (N * 167.0 + 850.0) / 1e12,
                          "hbm": {"algorithmic_bytes": hbm_bytes, "achieved_GBps": hbm_bytes / (kms * 1e-3) / 1e9,
                                  "peak_GBps": HBM_PEAK / 1e9, "frac": hbm_bytes / (kms * 1e-3) / HBM_PEAK}},
             "host_staged_value": host_staged,
