@@ -1183,7 +1183,9 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         const bool bad = cpc < 0 && !skip;
         cpc = cpc < 0 ? 0 : cpc;
         double zz[C + 1];
+        NGRTD_PROBE(4);
         cheb_sums<C + 1, ROLES == 2>(cheb + cpc * PST, CP, cx, zz);   // s01 Y_c (c < C), s01 G
+        NGRTD_PROBE(5);
         double conc[kMaxTracer];
         {
             double num[C];

@@ -82,6 +82,9 @@ def main():
              "reduce": tt[:, 7] - tt[:, 6], "total": tt[:, 7] - tt[:, 0]}
         if grp == "rtd_role":
             r["surrogate_like"] = tt[:, 2] - tt[:, 1]
+            r["theta_load_piece"] = tt[:, 4] - tt[:, 1]
+            r["clenshaw"] = tt[:, 5] - tt[:, 4]
+            r["conc_like"] = tt[:, 2] - tt[:, 5]
         res[grp] = {k: float(np.median(v)) for k, v in r.items()}
     # s_memtime counters are per XCD (block b runs on XCD b % 8): spans within one XCD
     blk = np.arange(t.shape[0]) // 16
