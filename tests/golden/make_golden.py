@@ -486,6 +486,19 @@ def make_frac(conv):
         res[i] = cm.convolve()
         gs[i], fms[i] = cm.g_tp, cm.FM_mu
     out.update(ext=ext, ext_conc=res, ext_g=gs, ext_fm=fms)
+    # sampling date past the last index (dtp = floor(3.7) = 3, :172-173) and the shortest
+    # series the integral is defined on (N = 2)
+    for key, n, tsh in (("shift", 300, 3.7), ("n2", 2, 0.0)):
+        s = atmos_series("H3", n)
+        df = reference_frame(s, n, "H3")
+        res, fms = np.zeros(4), np.zeros(4)
+        for i in range(4):
+            cm = conv.tracer_conv_integral(df.copy(), df.index[-1] + tsh)
+            cm.update_pars(tau=float(tau[i]), mod_type="frac_inf_diff", t_half=12.34, D=float(D[i]),
+                           bbar=float(bbar[i]), Phi_im=float(Phi[i]))
+            res[i] = cm.convolve()
+            fms[i] = cm.FM_mu
+        out[key + "_conc"], out[key + "_fm"] = res, fms
     # one long series (N = 25256, the shipped C_in_dict length)
     n = 25256
     s = atmos_series("CFC12", n)

@@ -151,3 +151,16 @@ def test_frac_device_pointers(golden):
     st = ctx.lib.ngrtd_frac_conv(ctx.h, sid, 0, p(d["tau"]), p(d["D"]), p(d["bbar"]), p(d["Phi"]), None, 0, None,
                                  0.0, None, 0.0, k, None, None, None, _lib.MEM_DEVICE)
     assert st == _lib.NGRTD_EINVAL
+
+
+@pytest.mark.parametrize("key,n,tsh", [("shift", 300, 3.7), ("n2", 2, 0.0)])
+def test_frac_shifted_sampling_date_and_shortest_series(golden, key, n, tsh):
+    """t_samp past the last index (dtp = floor(t_samp - index[-1]) = 3, :172-173) and N = 2."""
+    from noblegas_rtd_mcmc_amd.convolution_integral_utils import tracer_conv_integral
+    z = golden("frac_golden.npz")
+    df = frame("H3", n, "H3")
+    cm = tracer_conv_integral(df, df.index[-1] + tsh)
+    cm.update_pars(tau=z["tau"][:4], mod_type="frac_inf_diff", t_half=12.34, D=z["D"][:4], bbar=z["bbar"][:4],
+                   Phi_im=z["Phi"][:4])
+    got = cm.convolve()
+    assert rel(got, z[key + "_conc"]) <= RT_C and rel(cm.FM_mu, z[key + "_fm"]) <= RT_C
