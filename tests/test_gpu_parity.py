@@ -360,3 +360,27 @@ def test_out_of_support_tau_shortcut():
     assert close(got[walkers], ref, 1e-12, 1e-9).all(), (got[walkers], ref)
     assert np.isnan(got[3 * 2]) and got[0] == -np.inf     # tau = -1.6 overflows, -5 does not
     lp.close()
+
+
+def test_full_instance_exact_fallback_in_support():
+    """The joint (FULL) kernel instance with a tau prior reaching below the surrogate's
+    coverage (U(0.1, 1000)): waves holding an in-support tau < 1/2 redo their 64 units on
+    the exact matrix-core path, one 16-unit tile per pass (ROLES = 2).  Against the oracle."""
+    import dataclasses
+    import oracle.models as om
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+    spec = wl.c4_spec(L=4, N=1200)
+    spec = dataclasses.replace(spec, rtd=dataclasses.replace(spec.rtd, tau1=(0.1, 1000.0)))
+    W = 256
+    th = wl.sample_prior(spec, W, np.random.default_rng(51))
+    r = spec.roles.index("tau1")
+    th[r, :, ::37] = np.random.default_rng(52).uniform(0.1, 0.5, th[r, :, ::37].shape)
+    lp = LogProb(spec, max_walkers=W)
+    assert lp.info(W)["surrogate"] == 1
+    got = lp(th, soa=True)
+    walkers = list(range(0, W, 37)) + [1, 2, 100, 255]
+    ref = om.log_prob(spec, th, walkers=walkers)
+    assert np.isfinite(ref).all()
+    assert close(got[walkers], ref, 1e-12, 1e-9).all(), (got[walkers], ref)
+    lp.close()
