@@ -301,8 +301,10 @@ int ngrtd_demc_run(ngrtd_plan* plan, double* theta, double* logp, int64_t W, int
  *                                                             the decay-folded series, :305-340)
  *   Z_C(tau) = s01 sum_{j=0}^{N-2} exp(-j s)                  (the normaliser g.sum(), :270)
  * cols: [C][N] channel columns (age order); coef (may be NULL): receives
- * [NGRTD_CHEB_PIECES][NGRTD_CHEB_N][(C+2)&~1]; *max_rel_err: max |surrogate - exact| / exact
- * over the validation points.  Plans use the surrogate only when this is <= 5e-14. */
+ * [NGRTD_CHEB_PIECES][NGRTD_CHEB_N][(C+2)&~1], per piece the Chebyshev interpolant in
+ * monomial form (coefficient k of x^k, x the piece's local coordinate in [-1, 1], as the
+ * kernel evaluates it by Horner); *max_rel_err: max |surrogate - exact| / exact over the
+ * validation points.  Plans use the surrogate only when this is <= 5e-14. */
 #define NGRTD_CHEB_N 12
 #define NGRTD_CHEB_PIECES 53
 int ngrtd_surrogate_check(const double* cols, int32_t C, int64_t N, double dtp, double* coef,

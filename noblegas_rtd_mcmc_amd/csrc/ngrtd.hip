@@ -255,7 +255,14 @@ static double cheb_build(const std::vector<std::vector<double>>& cols, int C, do
             if (!(v >= 0.0) || !std::isfinite(v)) return HUGE_VAL;
     const long double PI = 3.14159265358979323846264338327950288L;
     const long double dd = d01;
-    std::vector<long double> f(n);
+    std::vector<long double> f(n), ch(n);
+    // power-basis coefficients of T_j: T_0 = 1, T_1 = x, T_{j+1} = 2x T_j - T_{j-1} (exact)
+    std::vector<std::vector<long double>> Tm(n, std::vector<long double>(n, 0.0L));
+    Tm[0][0] = 1.0L;
+    if (n > 1) Tm[1][1] = 1.0L;
+    for (int j = 2; j < n; ++j)
+        for (int k = 0; k < n; ++k)
+            Tm[j][k] = (k > 0 ? 2.0L * Tm[j - 1][k - 1] : 0.0L) - Tm[j - 2][k];
     for (int p = 0; p < kChebPieces; ++p) {
         for (int c = 0; c <= C; ++c) {
             const std::vector<double>& col = cols[c < C ? c : 0];
@@ -275,7 +282,16 @@ static double cheb_build(const std::vector<std::vector<double>>& cols, int C, do
                 for (int k = 0; k < n; ++k) acc += f[k] * cosl(PI * j * (k + 0.5L) / n);
                 acc *= 2.0L / n;
                 if (j == 0) acc *= 0.5L;
-                coef[((size_t)p * n + j) * CP + c] = (double)acc;
+                ch[j] = acc;
+            }
+            // Chebyshev -> monomial coefficients in the piece's local x (long double): the
+            // kernel evaluates one FMA per coefficient by Horner.  The coefficients decay
+            // like rho^-j with rho ~ 25 (the strip |Im log tau| < pi/2 over half-width 1/8),
+            // far above 1 + sqrt 2, so the monomial form amplifies rounding by ~1.1 only.
+            for (int k = 0; k < n; ++k) {
+                long double m = 0.0L;
+                for (int j = k; j < n; ++j) m += ch[j] * Tm[j][k];
+                coef[((size_t)p * n + k) * CP + c] = (double)m;
             }
         }
     }

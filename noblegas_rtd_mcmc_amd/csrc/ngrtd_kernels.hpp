@@ -729,63 +729,52 @@ __host__ __device__ __forceinline__ int cheb_piece(double tau, double& x) {
     return p;
 }
 
-// Clenshaw sums of C channels at x from one piece's coefficients [kChebN][CP].
-// PIPE (device only): software-pipelined one row ahead, with each row's results pinned
-// ("+v") behind a compiler memory barrier, so at most two rows of coefficients are live
-// in registers (2 C doubles) -- otherwise the scheduler issues all kChebN rows' LDS loads
-// up front (12 C doubles, 144 VGPRs at C = 6), which caps occupancy at 2 waves/SIMD.
+// Surrogate sums of C channels at x from one piece's coefficients [kChebN][CP]: the
+// Chebyshev fit in monomial form (cheb_build), evaluated by Horner -- one FMA per
+// coefficient and channel.
+// PIPE (device only): software-pipelined two rows ahead, with each row's results pinned
+// ("+v") behind a compiler memory barrier, so at most three rows of coefficients are live
+// in registers -- otherwise the scheduler issues all kChebN rows' LDS loads up front
+// (12 C doubles, 144 VGPRs at C = 6), which caps occupancy at 2 waves/SIMD.
 template <int C, bool PIPE = false>
 __host__ __device__ __forceinline__ void cheb_sums(const double* pc, int CP, double x, double* y) {
-    const double x2 = x + x;
-    double b1[C], b2[C];
-#pragma unroll
-    for (int c = 0; c < C; ++c) { b1[c] = 0.0; b2[c] = 0.0; }
 #if defined(__HIP_DEVICE_COMPILE__)
     if (PIPE) {   // rows k (cur) and k-1 (nxt) in registers, row k-2 in flight
-        double cur[C], nxt[C];
+        double b[C], nxt[C];
 #pragma unroll
-        for (int c = 0; c < C; ++c) cur[c] = pc[(kChebN - 1) * CP + c];
+        for (int c = 0; c < C; ++c) b[c] = pc[(kChebN - 1) * CP + c];
 #pragma unroll
         for (int c = 0; c < C; ++c) nxt[c] = pc[(kChebN - 2) * CP + c];
 #pragma unroll
-        for (int k = kChebN - 1; k >= 1; --k) {
+        for (int k = kChebN - 2; k >= 0; --k) {
             double nn[C];
-            if (k >= 2) {
+            if (k >= 1) {
 #pragma unroll
-                for (int c = 0; c < C; ++c) nn[c] = pc[(k - 2) * CP + c];
+                for (int c = 0; c < C; ++c) nn[c] = pc[(k - 1) * CP + c];
             }
 #pragma unroll
-            for (int c = 0; c < C; ++c) {
-                const double t = fma(x2, b1[c], cur[c] - b2[c]);
-                b2[c] = b1[c];
-                b1[c] = t;
-            }
+            for (int c = 0; c < C; ++c) b[c] = fma(b[c], x, nxt[c]);
 #pragma unroll
-            for (int c = 0; c < C; ++c) asm volatile("" : "+v"(b1[c]));
+            for (int c = 0; c < C; ++c) asm volatile("" : "+v"(b[c]));
             asm volatile("" ::: "memory");
+            if (k >= 1) {
 #pragma unroll
-            for (int c = 0; c < C; ++c) {
-                cur[c] = nxt[c];
-                if (k >= 2) nxt[c] = nn[c];
+                for (int c = 0; c < C; ++c) nxt[c] = nn[c];
             }
         }
 #pragma unroll
-        for (int c = 0; c < C; ++c) y[c] = fma(x, b1[c], cur[c] - b2[c]);
+        for (int c = 0; c < C; ++c) y[c] = b[c];
         return;
     }
 #endif
 #pragma unroll
-    for (int k = kChebN - 1; k >= 1; --k) {
+    for (int c = 0; c < C; ++c) y[c] = pc[(kChebN - 1) * CP + c];
+#pragma unroll
+    for (int k = kChebN - 2; k >= 0; --k) {
         const double* row = pc + k * CP;
 #pragma unroll
-        for (int c = 0; c < C; ++c) {
-            const double t = fma(x2, b1[c], row[c] - b2[c]);
-            b2[c] = b1[c];
-            b1[c] = t;
-        }
+        for (int c = 0; c < C; ++c) y[c] = fma(y[c], x, row[c]);
     }
-#pragma unroll
-    for (int c = 0; c < C; ++c) y[c] = fma(x, b1[c], pc[c] - b2[c]);
 }
 
 // Numerators num_c = A_{c,0} + s01 Y_c and the reciprocal normaliser 1 / (1 + s01 G) ->
