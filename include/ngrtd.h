@@ -275,8 +275,9 @@ int ngrtd_plan_kernel_stats(ngrtd_plan* plan, double* times_ms, int64_t* counts,
  * path) or 16-unit tiles per wave (MFMA path), waves per block, blocks, ages per LDS slice
  * (VALU) or per segment (MFMA), channels, N, LDS bytes, units, MFMA row tiles (0 = VALU
  * path), age segments, 4-age MFMA steps, Chebyshev surrogate in use (0/1), the
- * surrogate's validated max relative error in units of 1e-18 (-1: not built).  For the
- * roofline accounting in bench.py. */
+ * surrogate's validated max relative error in units of 1e-18 (-1: not built), and
+ * info[13] = pieces of the Student-t normaliser table (0: exact c0).  For the roofline
+ * accounting in bench.py. */
 int ngrtd_plan_info(ngrtd_plan* plan, int64_t W, int64_t* info, int32_t n);
 
 /* Device-resident population DE-MC (the sampler loop of PyMC3 DEMetropolisZ,
@@ -309,6 +310,24 @@ int ngrtd_demc_run(ngrtd_plan* plan, double* theta, double* logp, int64_t W, int
 #define NGRTD_CHEB_PIECES 53
 int ngrtd_surrogate_check(const double* cols, int32_t C, int64_t N, double dtp, double* coef,
                           double* max_rel_err);
+
+/* Host-only (no device needed): build the piecewise polynomial of the Student-t normaliser
+ *   c0(nu) = lgamma((nu+1)/2) - lgamma(nu/2) - log(pi nu)/2
+ * (PyMC3 3.11.2 StudentT.logp, the likelihoods of run_age_mcmc_utils.py:390/396 and
+ * noble_gas_mcmc.py:266) that a plan evaluates instead of the lgamma difference, over
+ * the binary octaves spanning [nu_lo, nu_hi] (the nu priors' supports): NGRTD_C0_SUB
+ * pieces per octave, from octave *e0 (nu in [2^e0, 2^(e0+1))), piece p covering
+ * nu = 2^(e0 + p/4) (1 + (p%4)/4 + [0, 1/4)); coef (may be NULL, room for
+ * NGRTD_C0_MAX_PIECES * NGRTD_C0_N) receives [n_pieces][NGRTD_C0_N] monomial coefficients
+ * (coefficient k of x^k, x = 8 (m - 1 - (2 (p%4) + 1)/8), m = nu / 2^(e0 + p/4)).
+ * *max_abs_err: max |table - lgammal| over 41 points per piece (HUGE_VAL: no table, e.g.
+ * nu_lo <= 0, non-finite, or more than NGRTD_C0_MAX_PIECES pieces).  Plans use the table
+ * when this is <= 2e-14, else the exact expression. */
+#define NGRTD_C0_N 12
+#define NGRTD_C0_SUB 4
+#define NGRTD_C0_MAX_PIECES 64
+int ngrtd_c0_check(double nu_lo, double nu_hi, double* coef, int32_t* e0, int32_t* n_pieces,
+                   double* max_abs_err);
 
 #ifdef __cplusplus
 }

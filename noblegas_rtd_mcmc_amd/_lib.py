@@ -94,6 +94,7 @@ PROTOTYPES = {
     "ngrtd_demc_run": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_double, C.c_double,
                                  C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p]),
     "ngrtd_surrogate_check": (C.c_int, [_dp, C.c_int32, C.c_int64, C.c_double, _dp, _dp]),
+    "ngrtd_c0_check": (C.c_int, [C.c_double, C.c_double, _dp, _i32p, _i32p, _dp]),
 }
 
 

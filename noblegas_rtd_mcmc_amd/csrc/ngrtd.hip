@@ -339,6 +339,68 @@ static int cheb_prepare(ngrtd_ctx* ctx, TableDev& tab, double d01) {
     return NGRTD_OK;
 }
 
+// Student-t normaliser table (ngrtd_math.hpp c0_piece / c0_poly) over the octaves of
+// [lo, hi]: per piece, the Chebyshev interpolant of c0 at kC0N nodes from lgammal, turned
+// into monomial coefficients in long double, then checked at 40 points per piece (ends
+// included) through the kernel's own c0_piece + c0_poly against lgammal.  Returns the
+// worst absolute error (HUGE_VAL when the range has no table: non-finite, <= 0, or more
+// than kC0MaxPieces pieces).
+constexpr double kC0Tol = 2e-14;
+static long double c0_ref(long double nu) {
+    const long double PI = 3.14159265358979323846264338327950288L;
+    return lgammal(0.5L * (nu + 1.0L)) - lgammal(0.5L * nu) - 0.5L * logl(PI * nu);
+}
+static double c0_build(double lo, double hi, std::vector<double>& tab, int& e0, int& np) {
+    tab.clear();
+    np = 0;
+    if (!(lo > 0.0) || !(hi >= lo) || !std::isfinite(hi) || !std::isnormal(lo)) return HUGE_VAL;
+    int ea, eb;
+    (void)std::frexp(lo, &ea);
+    (void)std::frexp(hi, &eb);
+    e0 = ea - 1;                          // lo in [2^e0, 2^(e0+1))
+    np = (eb - ea + 1) * kC0Sub;
+    if (np > kC0MaxPieces) { np = 0; return HUGE_VAL; }
+    const int n = kC0N;
+    const long double PI = 3.14159265358979323846264338327950288L;
+    std::vector<std::vector<long double>> Tm(n, std::vector<long double>(n, 0.0L));
+    Tm[0][0] = 1.0L;
+    Tm[1][1] = 1.0L;
+    for (int j = 2; j < n; ++j)
+        for (int k = 0; k < n; ++k)
+            Tm[j][k] = (k > 0 ? 2.0L * Tm[j - 1][k - 1] : 0.0L) - Tm[j - 2][k];
+    tab.assign((size_t)np * n, 0.0);
+    std::vector<long double> f(n), ch(n);
+    for (int p = 0; p < np; ++p) {
+        const long double sc = ldexpl(1.0L, e0 + p / kC0Sub), c = 1.125L + 0.25L * (p % kC0Sub);
+        for (int k = 0; k < n; ++k) f[k] = c0_ref(sc * (c + cosl(PI * (k + 0.5L) / n) / 8.0L));
+        for (int j = 0; j < n; ++j) {
+            long double acc = 0.0L;
+            for (int k = 0; k < n; ++k) acc += f[k] * cosl(PI * j * (k + 0.5L) / n);
+            ch[j] = acc * (j == 0 ? 1.0L : 2.0L) / n;
+        }
+        for (int k = 0; k < n; ++k) {
+            long double m = 0.0L;
+            for (int j = k; j < n; ++j) m += ch[j] * Tm[j][k];
+            tab[(size_t)p * n + k] = (double)m;
+        }
+    }
+    double worst = 0.0;
+    const int M = 40;
+    for (int p = 0; p < np; ++p) {
+        const double base = std::ldexp(1.0 + 0.25 * (p % kC0Sub), e0 + p / kC0Sub);
+        const double w = std::ldexp(0.25, e0 + p / kC0Sub);
+        for (int i = 0; i <= M; ++i) {
+            double nu = (i == M) ? std::nextafter(base + w, 0.0) : base + w * i / M;
+            double x = 0.0;
+            const int pp = c0_piece(nu, e0, np, x);
+            if (pp != p) return HUGE_VAL;
+            const double e = (double)fabsl((long double)c0_poly(tab.data() + (size_t)pp * n, x) - c0_ref(nu));
+            if (!(e <= worst)) worst = e;   // NaN -> worst = NaN
+        }
+    }
+    return worst;
+}
+
 static void set_frag(RtdArgs& a, const TableDev& tab) {
     for (int c = 0; c < kMaxChan; ++c)
         a.tab0[c] = (c < tab.C && !tab.cols_host.empty()) ? tab.cols_host[c][0] : 0.0;
@@ -419,13 +481,12 @@ static void launch_mfma(const RtdArgs& a, const UnitArgs& u, int32_t fuse, hipSt
 // Single-launch log-prob (logp_fused_kernel): exponential RTD on the MFMA path with 4
 // tiles per wave (C <= 5), the whole fragment table in LDS next to the 512 per-unit
 // partial sums, and L <= 512 wells.
-// LDS: the 512 per-unit partial sums and the surrogate table (the exact path's fragments
-// are read from global memory: they are needed only by waves with an uncovered tau)
-// LDS: the 512 per-unit partial sums, the surrogate table and the per-well observation
-// data (ce obs, 1/sd^2, sums of 0.5 log 1/sd^2, E_min; rtd obs, 1/sd^2, sums).
+// LDS: the 512 per-unit partial sums, the surrogate table (the exact path's fragments are
+// read from global memory: they are needed only by waves with an uncovered tau) and the
+// packed per-well data (ce obs, 1/sd^2, sums of 0.5 log 1/sd^2, E_min; rtd obs, 1/sd^2,
+// sums; the Student-t normaliser table).
 static size_t fused_lds(const RtdArgs& a, const UnitArgs& u) {
-    const size_t wells = (size_t)u.L * ((u.ce_on ? 2 * u.G + 2 : 0) + (u.rtd_on ? 2 * u.K + 1 : 0));
-    return (size_t)(2 * kFusedUnits + kFusedUnits / 2 + kChebPieces * cheb_lds_stride(a.C) + wells) * sizeof(double);
+    return (size_t)(2 * kFusedUnits + kFusedUnits / 2 + kChebPieces * cheb_lds_stride(a.C) + u.wd_n) * sizeof(double);
 }
 constexpr size_t kFusedMaxLds = 150 * 1024;
 static bool fused_path(const RtdArgs& a, const UnitArgs& u) {
@@ -1158,9 +1219,27 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
             add(p->rtd_lam, 0, LK);
             add(p->rtd_lam, 2 * LK, (size_t)L);
         }
+        // Student-t normaliser table over every nu the priors' supports allow
+        static const bool no_c0 = std::getenv("NGRTD_NO_C0TAB") != nullptr;
+        double lo = HUGE_VAL, hi = -HUGE_VAL;
+        if (d->ce_enabled) { lo = std::min(lo, u.nu_min); hi = std::max(hi, u.nu_max); }
+        if (d->rtd_enabled) { lo = std::min(lo, u.rnu_min); hi = std::max(hi, u.rnu_max); }
+        std::vector<double> c0t;
+        int e0 = 0, np = 0;
+        size_t c0_off = 0;
+        if (!no_c0 && c0_build(lo, hi, c0t, e0, np) <= kC0Tol) {
+            if (wd.size() & 1) wd.push_back(0.0);   // 16-B aligned table rows in LDS
+            c0_off = wd.size();
+            wd.insert(wd.end(), c0t.begin(), c0t.end());
+        } else {
+            np = 0;
+        }
         NG_CHECK(upload(ctx, p->welldata, wd.data(), wd.size()));
         u.wd_src = p->welldata.d();
         u.wd_n = (int32_t)wd.size();
+        u.c0_tab = np > 0 ? p->welldata.d() + c0_off : nullptr;
+        u.c0_e0 = e0;
+        u.c0_np = np;
     }
     HIP_TRY(ctx, p->ulogp.ensure((size_t)Umax * sizeof(double)));
     u.ulogp = p->ulogp.d();
@@ -1386,10 +1465,22 @@ int ngrtd_surrogate_check(const double* cols, int32_t C, int64_t N, double dtp, 
     return NGRTD_OK;
 }
 
+int ngrtd_c0_check(double nu_lo, double nu_hi, double* coef, int32_t* e0, int32_t* n_pieces, double* max_abs_err) {
+    if (!e0 || !n_pieces || !max_abs_err) return NGRTD_EINVAL;
+    std::vector<double> t;
+    int e = 0, np = 0;
+    *max_abs_err = c0_build(nu_lo, nu_hi, t, e, np);
+    *e0 = e;
+    *n_pieces = np;
+    if (coef) std::copy(t.begin(), t.end(), coef);
+    return NGRTD_OK;
+}
+
 int ngrtd_plan_info(ngrtd_plan* p, int64_t W, int64_t* info, int32_t n) {
     if (!p) return NGRTD_ESTATE;
     const int64_t U = (int64_t)p->desc.n_wells * W;
-    int64_t v[13] = {0};
+    int64_t v[14] = {0};
+    v[13] = p->unit.c0_np;
     if (p->desc.rtd_enabled) {
         RtdArgs a = p->rtd;
         v[11] = a.cheb != nullptr;
@@ -1408,7 +1499,7 @@ int ngrtd_plan_info(ngrtd_plan* p, int64_t W, int64_t* info, int32_t n) {
         v[4] = p->table.C; v[5] = p->N;
     }
     v[7] = U;
-    for (int i = 0; i < n && i < 13; ++i) info[i] = v[i];
+    for (int i = 0; i < n && i < 14; ++i) info[i] = v[i];
     return NGRTD_OK;
 }
 

@@ -111,9 +111,13 @@ struct UnitArgs {
     // bt_fa log x + bt_fb log(1-x) for non-integer exponents; bt_betaln = sum of betaln.
     // per-well observation data packed for one contiguous LDS copy (logp_fused_kernel):
     // [ce_obs L*G | ce_lam L*G | ce_hll_sum L | ce_Emin L | rtd_obs L*K | rtd_lam L*K |
-    //  rtd_hll_sum L] (blocks present only when that model block is on)
+    //  rtd_hll_sum L | pad to even | c0 table c0_np*kC0N] (blocks present only when that
+    // model block is on)
     const double* wd_src;
     int32_t wd_n;
+    // Student-t normaliser table (ngrtd_math.hpp c0_piece; null: exact c0 everywhere)
+    const double* c0_tab;
+    int32_t c0_e0, c0_np;
     int32_t bt_n;
     int32_t bt_row[kMaxBeta], bt_ia[kMaxBeta], bt_ib[kMaxBeta];
     double bt_fa[kMaxBeta], bt_fb[kMaxBeta];

@@ -528,7 +528,8 @@ __device__ __forceinline__ double unit_logp_theta(const UnitArgs& a, int64_t u, 
             if (!full && a.ce_out)
                 for (int j = 0; j < a.G; ++j) a.ce_out[(int64_t)j * a.U + u] = mod[j];
             if (want_like)
-                lp += st_block<kMaxGas>(a.G, a.ce_obs + l * a.G, mod, a.ce_lam + l * a.G, a.ce_hll_sum[l], nu);
+                lp += st_block<kMaxGas>(a.G, a.ce_obs + l * a.G, mod, a.ce_lam + l * a.G, a.ce_hll_sum[l], nu,
+                                         C0Tab{a.c0_tab, a.c0_e0, a.c0_np});
         }
     }
     if (full || a.rtd_on) {
@@ -569,7 +570,8 @@ __device__ __forceinline__ double unit_like_rtd(const UnitArgs& a, int64_t u, in
     if (!full && (!a.rtd_on || !(a.flags & NGRTD_WANT_LIKE))) return 0.0;
     const double nub = pre ? pre->nub : a.theta[(int64_t)a.row_nu * a.U + u];
     const double nu = nub * (a.rnu_max - a.rnu_min) + a.rnu_min;
-    return st_block<NMAX>(a.K, a.rtd_obs + l * a.K, conc, a.rtd_lam + l * a.K, a.rtd_hll_sum[l], nu);
+    return st_block<NMAX>(a.K, a.rtd_obs + l * a.K, conc, a.rtd_lam + l * a.K, a.rtd_hll_sum[l], nu,
+                          C0Tab{a.c0_tab, a.c0_e0, a.c0_np});
 }
 
 // full log-prob contribution of one unit (same addition order as the reference's sum)
@@ -1134,6 +1136,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             ul.rtd_lam = q; q += nrt;
             ul.rtd_hll_sum = q;
         }
+        if (ua.c0_tab) ul.c0_tab = wd + (ua.c0_tab - ua.wd_src);
     }
     __syncthreads();
     NGRTD_PROBE(1);

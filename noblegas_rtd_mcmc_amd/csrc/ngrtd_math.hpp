@@ -227,17 +227,59 @@ NGRTD_HD double beta_logp_fast(double x, double a, double b, double betaln_ab, i
 // i.e. 2 logs per block instead of 3 + n, and 2 divisions (1/(y P), 1/nu) instead of n + 3.  log(1 + z) vs log1p(z) differs by < 2^-53 per
 // factor.  Very large z (z >= 1e38, inf, NaN) take a per-observation log path so the
 // product cannot overflow (the T < 0 sentinel -9999 gives z ~ 1e28: still one log).  hll_sum = sum_j 0.5 log lam_j (host precomputed).
-template <int NMAX>
-NGRTD_HD double st_block(int n, const double* obs, const double* mu, const double* lam, double hll_sum,
-                         double nu) {
+// Student-t normaliser c0(nu) = lgamma((nu+1)/2) - lgamma(nu/2) - log(pi nu)/2, exact form
+// (~50 FP64 operations, one division and one log).
+NGRTD_HD double st_c0_exact(double nu, double inu) {
     const double x = nu / 2.0;
     double P, Q;
     shift12(x, P, Q);
     const double y = (x < 1.0e6) ? x + 12.0 : x;
     const double iyP = 1.0 / (y * P);               // one division for 1/y and Q/P
     const double qp = (Q * y) * iyP;
+    return 0.5 * flog(y * qp * qp * (inu * (1.0 / kPi))) + lgamma_half_tail(P * iyP);
+}
+
+// c0(nu) from a per-plan piecewise polynomial (ngrtd.hip c0_build): kC0Sub pieces per
+// binary octave of nu, over the octaves [2^e0, 2^(e0 + np/kC0Sub)) spanned by the nu
+// priors' supports, kC0N monomial coefficients per piece in x = 8 (m - c_j), where m in
+// [1, 2) is nu's significand and c_j = 1 + (2j + 1)/8 the centre of piece j (x in [-1, 1),
+// exact in binary).  c0 is analytic up to its poles at nu = 0, -1, ...; every piece sits at
+// >= 9 half-widths from nu = 0 whatever the octave, so one degree fits every scale.  The
+// host validates the table against lgammal (kC0Tol) and the kernel evaluates 11 FMAs
+// instead of st_c0_exact.  Returns the piece, or -1 for nu outside the table -- NaN, inf,
+// <= 0 and subnormal nu land there through the exponent field alone.
+constexpr int kC0N = 12, kC0Sub = 4, kC0MaxPieces = 64;
+NGRTD_HD int c0_piece(double nu, int e0, int np, double& x) {
+    const unsigned hi = fm_hi(nu);
+    const int j = (int)((hi >> 18) & 3u);
+    const int p = ((int)(hi >> 20) - 1023 - e0) * kC0Sub + j;    // sign bit -> p >= 4096
+    const double m = fm_with_hi(nu, (hi & 0x000FFFFFu) | 0x3FF00000u);
+    x = (m - (1.125 + 0.25 * j)) * 8.0;
+    return (unsigned)p < (unsigned)np ? p : -1;
+}
+NGRTD_HD double c0_poly(const double* t, double x) {
+    double b = t[kC0N - 1];
+#pragma unroll
+    for (int k = kC0N - 2; k >= 0; --k) b = fma(b, x, t[k]);
+    return b;
+}
+// table view: t = [np][kC0N] coefficients (null: exact everywhere)
+struct C0Tab {
+    const double* t;
+    int32_t e0, np;
+};
+
+template <int NMAX>
+NGRTD_HD double st_block(int n, const double* obs, const double* mu, const double* lam, double hll_sum,
+                         double nu, C0Tab c0t = C0Tab{nullptr, 0, 0}) {
     const double inu = 1.0 / nu;
-    const double c0 = 0.5 * flog(y * qp * qp * (inu * (1.0 / kPi))) + lgamma_half_tail(P * iyP);
+    double c0;
+    double cx;
+    const int cp = c0t.t ? c0_piece(nu, c0t.e0, c0t.np, cx) : -1;
+    if (cp >= 0)
+        c0 = c0_poly(c0t.t + cp * kC0N, cx);
+    else
+        c0 = st_c0_exact(nu, inu);
     // unrolled over NMAX constant slots (slots j >= n masked; their loads clamp to n - 1)
     double prod = 1.0;
     bool big = false, ok = nu > 0;

@@ -190,10 +190,10 @@ class LogProb:
         return {"rtd": (ms[0], n[0]), "unit": (ms[1], n[1]), "reduce": (ms[2], n[2]), "fused": (ms[3], n[3])}
 
     def info(self, W):
-        v = (C.c_int64 * 13)()
-        self.ctx.check(self.lib.ngrtd_plan_info(self.plan, int(W), v, 13), "plan_info")
+        v = (C.c_int64 * 14)()
+        self.ctx.check(self.lib.ngrtd_plan_info(self.plan, int(W), v, 14), "plan_info")
         keys = ("R", "NW", "blocks", "slice_ages", "channels", "N", "lds_bytes", "units", "mfma_rows", "S_seg",
-                "nsteps", "surrogate", "surrogate_err_e18")
+                "nsteps", "surrogate", "surrogate_err_e18", "c0_pieces")
         d = dict(zip(keys, list(v)))
         d["surrogate_max_rel_err"] = d.pop("surrogate_err_e18") * 1e-18 if v[12] >= 0 else None
         return d
