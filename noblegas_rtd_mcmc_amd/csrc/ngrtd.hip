@@ -486,11 +486,27 @@ static void launch_mfma(const RtdArgs& a, const UnitArgs& u, int32_t fuse, hipSt
 // packed per-well data (ce obs, 1/sd^2, sums of 0.5 log 1/sd^2, E_min; rtd obs, 1/sd^2,
 // sums; the Student-t normaliser table).
 static size_t fused_lds(const RtdArgs& a, const UnitArgs& u) {
-    return (size_t)(2 * kFusedUnits + kFusedUnits / 2 + kChebPieces * cheb_lds_stride(a.C) + u.wd_n) * sizeof(double);
+    return (size_t)(2 * kFusedUnits + kFusedUnits / 2 + a.cheb_np * cheb_lds_stride(a.C) + u.wd_n) * sizeof(double);
+}
+// Surrogate pieces the fused kernel stages: when the unit's log-prob carries the tau1
+// Uniform prior and the RTD's tau is tau1, only the pieces over the prior's support
+// [tau1_lo, tau1_hi] -- a tau outside it makes the log-prob -inf whatever the channel sums
+// (the kernel's `skip` lanes), so no lane reads another piece.  Else the whole table.
+static void cheb_window(RtdArgs& a, const UnitArgs& u) {
+    a.cheb_p0 = 0;
+    a.cheb_np = a.cheb ? kChebPieces : 0;
+    if (!a.cheb || !u.rtd_on || !(u.flags & NGRTD_WANT_PRIOR) || a.row_tau[0] != u.row_tau1) return;
+    double x;
+    const int pa = cheb_piece(std::max(u.tau1_lo, kChebTauLo), x), pb = cheb_piece(u.tau1_hi, x);
+    if (pa < 0 || pb < pa) return;
+    a.cheb_p0 = pa;
+    a.cheb_np = pb - pa + 1;
 }
 constexpr size_t kFusedMaxLds = 150 * 1024;
-static bool fused_path(const RtdArgs& a, const UnitArgs& u) {
+static bool fused_path(const RtdArgs& a0, const UnitArgs& u) {
     static const bool disabled = std::getenv("NGRTD_NO_FUSED") != nullptr;
+    RtdArgs a = a0;
+    cheb_window(a, u);
     return !disabled && mfma_path(a, a.row_thalf >= 0) && a.C <= 5 && u.L >= 1 && u.L <= kFusedUnits &&
            fused_lds(a, u) <= kFusedMaxLds;
 }
@@ -530,9 +546,11 @@ static void launch_fused_c(const RtdArgs& a, const UnitArgs& u, int WB, int64_t 
     if (full) launch_fused_cf<C, true>(a, u, WB, W, logp, da, st);
     else launch_fused_cf<C, false>(a, u, WB, W, logp, da, st);
 }
-static int launch_fused(ngrtd_ctx* ctx, const RtdArgs& a, const UnitArgs& u, int64_t W, int L, double* logp,
+static int launch_fused(ngrtd_ctx* ctx, const RtdArgs& a0, const UnitArgs& u, int64_t W, int L, double* logp,
                         hipStream_t st, const DemcAccept* dap = nullptr) {
     const int WB = kFusedUnits / L;
+    RtdArgs a = a0;
+    cheb_window(a, u);
     const DemcAccept da = dap ? *dap : DemcAccept{};
     switch (a.C) {
     case 1: launch_fused_c<1>(a, u, WB, W, logp, da, st); break;

@@ -37,6 +37,9 @@ struct RtdArgs {
     int32_t nsteps, S_seg, Lseg;
     // Chebyshev surrogate of the exponential channel sums (logp_fused_kernel), or null
     const double* cheb;     // [kChebPieces][kChebN][CP]
+    // pieces [cheb_p0, cheb_p0 + cheb_np) of it that logp_fused_kernel stages in LDS (the
+    // window covering the tau1 prior's support; launch_fused)
+    int32_t cheb_p0, cheb_np;
 };
 
 // Chebyshev surrogate of Z_c(tau) = s01(tau) sum_{j>=0} A_{c,1+j} exp(-j / tau) (the

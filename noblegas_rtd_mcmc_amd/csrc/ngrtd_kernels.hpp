@@ -1058,10 +1058,11 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     constexpr int CP = cheb_cp(C);
     constexpr int NTH = 64 * kFusedWaves * ROLES;           // threads per block
     constexpr int NPRE = (kFusedPrefetch * 64 * kFusedWaves + NTH - 1) / NTH;
-    constexpr int TAB2 = kChebPieces * kChebN * CP / 2;   // double2 entries of the surrogate table
+    constexpr int TAB2MAX = kChebPieces * kChebN * CP / 2;   // double2 entries of the whole table
+    const int TAB2 = a.cheb_np * (kChebN * CP / 2);       // ... of the staged window
     constexpr int PST = cheb_lds_stride(C);               // LDS doubles per piece (padded)
     static_assert(NT == 4, "one unit per lane needs 4 tiles per wave");
-    static_assert(TAB2 <= NPRE * NTH, "prefetch covers the table");
+    static_assert(TAB2MAX <= NPRE * NTH, "prefetch covers the table");
     extern __shared__ __attribute__((aligned(16))) double lds[];
     double* part = lds;                                   // [512] per-unit log-prob
     double* part2 = lds + kFusedUnits;                    // [512] RTD likelihood (ROLES = 2)
@@ -1084,7 +1085,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     // surrogate table -> registers -> LDS (stored after every prologue load is issued)
     double2 pre[NPRE];
     if (a.cheb) {
-        const double2* src = reinterpret_cast<const double2*>(a.cheb);
+        const double2* src = reinterpret_cast<const double2*>(a.cheb + (size_t)a.cheb_p0 * kChebN * CP);
 #pragma unroll
         for (int r = 0; r < NPRE; ++r) {
             const int i = tid + r * NTH;
@@ -1098,7 +1099,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     const int64_t mu = mvalid ? (int64_t)ml * W + w0 + mwl : 0;
     // per-well observation data -> LDS (read per lane by the likelihood blocks): all loads
     // issued before any store, so the prologue pays one memory latency
-    double* wd = cheb + kChebPieces * PST;
+    double* wd = cheb + a.cheb_np * PST;
     constexpr int kWdRegs = (4 * 64 * kFusedWaves + NTH - 1) / NTH;
     double wv[kWdRegs];
 #pragma unroll
@@ -1107,6 +1108,16 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         wv[r] = i < ua.wd_n ? ua.wd_src[i] : 0.0;
     }
     fm_lds_init();                                        // fexp/flog tables
+    // theta rows of this lane's unit, issued behind the table loads (the LDS stores below
+    // wait only for those) so that their HBM latency overlaps the prologue's barrier
+    // (A/B against loading them after the barrier: 11.87 vs 11.95 us, tools/gpu_ab_libs.sh)
+    ThetaPre tp{};
+    double tau = 1.0;
+    if (do_theta) theta_preload(ua, mu, tp);
+    if (do_rtd) {
+        tau = mvalid ? a.theta[(int64_t)a.row_tau[0] * a.U + mu] : 1.0;
+        tp.nub = (FULL || ua.rtd_on) ? a.theta[(int64_t)ua.row_nu * a.U + mu] : 0.0;
+    }
 #pragma unroll
     for (int r = 0; r < kWdRegs; ++r) {
         const int i = tid + r * NTH;
@@ -1140,25 +1151,15 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     }
     __syncthreads();
     NGRTD_PROBE(1);
-    // theta of this lane's unit (after the barrier: the 8.4 MB theta read at c4 is
-    // bandwidth-bound, and the tables' loads before the barrier should not wait behind it)
-    // (theta rows are loaded after the barrier: issued before it, with the table loads,
-    // they lengthened the prologue by more than they saved -- tools/section_probe.py)
     double th = 0.0, like = 0.0;
-    ThetaPre tp{};
-    double tau = 1.0;
-    if (do_theta) {
-        theta_preload(ua, mu, tp);
-        th = mvalid ? unit_logp_theta(ul, mu, ml, &tp, FULL) : 0.0;
-    }
+    if (do_theta) th = mvalid ? unit_logp_theta(ul, mu, ml, &tp, FULL) : 0.0;
     if (do_rtd) {
-        tau = mvalid ? a.theta[(int64_t)a.row_tau[0] * a.U + mu] : 1.0;
-        tp.nub = (FULL || ua.rtd_on) ? a.theta[(int64_t)ua.row_nu * a.U + mu] : 0.0;
         // The surrogate channel sums, the concentrations and the RTD likelihood.  Lanes
         // whose tau the surrogate does not cover evaluate piece 0 here and are redone
         // exactly below.
         double cx = 0.0;
-        int cpc = a.cheb ? cheb_piece(tau, cx) : -1;
+        int cpc = a.cheb ? cheb_piece(tau, cx) - a.cheb_p0 : -1;
+        cpc = (unsigned)cpc < (unsigned)a.cheb_np ? cpc : -1;   // outside the staged window
         // An uncovered tau (< 1/2, NaN) outside the support of the tau1 Uniform prior makes the
         // unit's log-prob -inf whatever the concentrations are -- unless they are NaN, which
         // the reference's weights produce exactly when (1/tau) exp(-tp/tau) overflows or
