@@ -415,21 +415,33 @@ __device__ __forceinline__ double lnK_horner(const GasCoef& c, double ix) {
 }
 __device__ __forceinline__ void ce_model_s0(const UnitArgs& a, double T, double P, double Ae, double F,
                                             double* mod) {
-    const double Pv = vapor_pressure_fast(T);
     const double T_k = T + 273.15;
-    const double ix = 1.0 / (.001 * T_k);
+    // the Antoine denominator C + T and .001 T_k share one division (batch_recip)
+    double vA, vB, vC;
+    antoine(T, vA, vB, vC);
+    const double dv[2] = {vC + T, .001 * T_k};
+    double rv[2];
+    batch_recip<2>(dv, rv);
+    const double Pv = vapor_pressure_rcp(vA, vB, rv[0]);
+    const double ix = rv[1];
     const double gamma = (T < 65. && !(T_k > 0.0)) ? __builtin_nan("") : 1.0;
     const double dP = P - Pv;
     const double lnAr = lnK_horner(gas_coef(2), ix);
     const double FA = F * Ae, ImFA = (1 - F) * Ae;
     const bool neg = T < 0.0;
+    double ceq[kMaxGas], den[kMaxGas], rd[kMaxGas];
 #pragma unroll
     for (int j = 0; j < kMaxGas; ++j) {
         const double lnK = fma(fma(fma(a.gA3[j], ix, a.gA2[j]), ix, a.gA1[j]), ix, a.gA0[j]);
         const double e = fexp(a.g_he[j] ? lnK - lnAr : -lnK);
-        const double ceq = neg ? -9999.0 : (gamma * (a.gz[j] * dP) * e) * (22414. / 18.);
-        const double ex = (ImFA * a.gz[j]) * ceq / (ceq + FA * a.gz[j]);
-        mod[j] = ex + ceq;
+        ceq[j] = neg ? -9999.0 : (gamma * (a.gz[j] * dP) * e) * (22414. / 18.);
+        den[j] = ceq[j] + FA * a.gz[j];
+    }
+    batch_recip<kMaxGas>(den, rd);                  // the 5 excess-air denominators: one division
+#pragma unroll
+    for (int j = 0; j < kMaxGas; ++j) {
+        const double ex = ((ImFA * a.gz[j]) * ceq[j]) * rd[j];
+        mod[j] = ex + ceq[j];
     }
 }
 
@@ -521,15 +533,18 @@ __device__ __forceinline__ double unit_logp_theta(const UnitArgs& a, int64_t u, 
             const double F_log = p[1] * (a.logF_max - a.logF_min) + a.logF_min;
             const double E = p[2] * (a.E_max - Emin) + Emin;
             const double b = p[4] * (a.b_max - a.b_min) + a.b_min;
-            const double T = (E - b) / p[3];
             const double nu = p[5] * (a.nu_max - a.nu_min) + a.nu_min;
+            const double dm[2] = {p[3], nu};        // 1/m and the Student-t 1/nu: one division
+            double rm[2];
+            batch_recip<2>(dm, rm);
+            const double T = (E - b) * rm[0];
             double mod[kMaxGas];
             ce_model_s0(a, T, lapse_rate_fast(E), exp10_fast(Ae_log), exp10_fast(F_log), mod);
             if (!full && a.ce_out)
                 for (int j = 0; j < a.G; ++j) a.ce_out[(int64_t)j * a.U + u] = mod[j];
             if (want_like)
-                lp += st_block<kMaxGas>(a.G, a.ce_obs + l * a.G, mod, a.ce_lam + l * a.G, a.ce_hll_sum[l], nu,
-                                         C0Tab{a.c0_tab, a.c0_e0, a.c0_np});
+                lp += st_block_inu<kMaxGas>(a.G, a.ce_obs + l * a.G, mod, a.ce_lam + l * a.G, a.ce_hll_sum[l], nu,
+                                             rm[1], C0Tab{a.c0_tab, a.c0_e0, a.c0_np});
         }
     }
     if (full || a.rtd_on) {
@@ -564,14 +579,16 @@ __device__ __forceinline__ double unit_logp_theta(const UnitArgs& a, int64_t u, 
 // Student-t likelihood of the unit's K model concentrations (run_age_mcmc_utils.py:292-296)
 // (NMAX: compile-time bound on K -- the single-launch kernel passes its channel count,
 // K <= C since every tracer owns at least one channel)
+// (inu: 1 / nu when the caller has it from batched reciprocals)
 template <int NMAX = kMaxTracer>
 __device__ __forceinline__ double unit_like_rtd(const UnitArgs& a, int64_t u, int l, const double* conc,
-                                                const ThetaPre* pre = nullptr, bool full = false) {
+                                                const ThetaPre* pre = nullptr, bool full = false,
+                                                const double* inu = nullptr) {
     if (!full && (!a.rtd_on || !(a.flags & NGRTD_WANT_LIKE))) return 0.0;
     const double nub = pre ? pre->nub : a.theta[(int64_t)a.row_nu * a.U + u];
     const double nu = nub * (a.rnu_max - a.rnu_min) + a.rnu_min;
-    return st_block<NMAX>(a.K, a.rtd_obs + l * a.K, conc, a.rtd_lam + l * a.K, a.rtd_hll_sum[l], nu,
-                          C0Tab{a.c0_tab, a.c0_e0, a.c0_np});
+    return st_block_inu<NMAX>(a.K, a.rtd_obs + l * a.K, conc, a.rtd_lam + l * a.K, a.rtd_hll_sum[l], nu,
+                              inu ? *inu : 1.0 / nu, C0Tab{a.c0_tab, a.c0_e0, a.c0_np});
 }
 
 // full log-prob contribution of one unit (same addition order as the reference's sum)
@@ -1184,10 +1201,14 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             double num[C];
 #pragma unroll
             for (int c = 0; c < C; ++c) num[c] = a.tab0[c] + zz[c];
-            unit_conc<C>(a, mu, num, 1.0 / (1.0 + zz[C]), conc);
+            // the normaliser's reciprocal and the Student-t 1/nu: one division
+            const double dr[2] = {1.0 + zz[C], tp.nub * (ua.rnu_max - ua.rnu_min) + ua.rnu_min};
+            double rr[2];
+            batch_recip<2>(dr, rr);
+            unit_conc<C>(a, mu, num, rr[0], conc);
             if (cnan)
                 for (int t = 0; t < a.K; ++t) conc[t] = __builtin_nan("");
-            like = mvalid ? unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL) : 0.0;
+            like = mvalid ? unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL, &rr[1]) : 0.0;
         }
         NGRTD_PROBE(2);
         if (__any(bad)) {                                     // wave-uniform: exact channel sums

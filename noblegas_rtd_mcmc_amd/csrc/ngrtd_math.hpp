@@ -69,6 +69,50 @@ NGRTD_HD double vapor_pressure_fast(double T) {
     return exp10_fast(A - (B / (C + T))) * (101325. / 760. / 1.0e9);
 }
 
+// Antoine coefficients of vapor_pressure() for T (NaN T takes the else branch), and the
+// pressure from them with B / (C + T) given as B * rcp, rcp = 1 / (C + T) (<= 3 ulp).
+NGRTD_HD void antoine(double T, double& A, double& B, double& C) {
+    const bool lo = T <= 99.0;
+    A = lo ? 8.07131 : 8.14019;
+    B = lo ? 1730.63 : 1810.94;
+    C = lo ? 233.426 : 244.485;
+}
+NGRTD_HD double vapor_pressure_rcp(double A, double B, double rcp) {
+    return exp10_fast(A - B * rcp) * (101325. / 760. / 1.0e9);
+}
+
+// r_i = 1 / d_i for i < n with ONE division (the running products, one reciprocal of
+// the last, then back-substitution: 3(n-1) multiplies; each r_i within ~3(n-1)/2 ulp).
+// FP64 division is 11 VALU instructions on gfx950.  When some |d_i| lies outside
+// [2^-200, 2^200] -- zero, inf, NaN, subnormal or extreme values, where products could
+// leave the normal range or IEEE division's special values differ -- every r_i is a plain
+// division instead (a divergent branch that in-range data never takes).
+template <int n>
+NGRTD_HD void batch_recip(const double* d, double* r) {
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+        const unsigned e = (fm_hi(d[i]) >> 20) & 0x7FFu;          // biased exponent
+        ok &= e - (1023u - 200u) <= 400u;
+    }
+    if (ok) {
+        double p[n];
+        p[0] = d[0];
+#pragma unroll
+        for (int i = 1; i < n; ++i) p[i] = p[i - 1] * d[i];
+        double inv = 1.0 / p[n - 1];
+#pragma unroll
+        for (int i = n - 1; i > 0; --i) {
+            r[i] = inv * p[i - 1];
+            inv *= d[i];
+        }
+        r[0] = inv;
+    } else {
+#pragma unroll
+        for (int i = 0; i < n; ++i) r[i] = 1.0 / d[i];
+    }
+}
+
 // Setchenow salting factor of solubility(), :154-159.  With S = 0 this is exp(0*s) = 1
 // unless s is not finite (T_k <= 0), exactly as the reference.
 NGRTD_HD double setchenow_gamma(const GasCoef& c, double T, double S, double T_k) {
@@ -269,10 +313,10 @@ struct C0Tab {
     int32_t e0, np;
 };
 
+// (inu = 1 / nu, from the caller's batched reciprocals)
 template <int NMAX>
-NGRTD_HD double st_block(int n, const double* obs, const double* mu, const double* lam, double hll_sum,
-                         double nu, C0Tab c0t = C0Tab{nullptr, 0, 0}) {
-    const double inu = 1.0 / nu;
+NGRTD_HD double st_block_inu(int n, const double* obs, const double* mu, const double* lam, double hll_sum,
+                             double nu, double inu, C0Tab c0t) {
     double c0;
     double cx;
     const int cp = c0t.t ? c0_piece(nu, c0t.e0, c0t.np, cx) : -1;
@@ -306,6 +350,11 @@ NGRTD_HD double st_block(int n, const double* obs, const double* mu, const doubl
     }
     const double v = (double)n * c0 + hll_sum - (nu + 1.0) / 2.0 * Lg;
     return ok ? v : kNegInf;
+}
+template <int NMAX>
+NGRTD_HD double st_block(int n, const double* obs, const double* mu, const double* lam, double hll_sum,
+                         double nu, C0Tab c0t = C0Tab{nullptr, 0, 0}) {
+    return st_block_inu<NMAX>(n, obs, mu, lam, hll_sum, nu, 1.0 / nu, c0t);
 }
 
 // Beta.logp with precomputed betaln(a, b)
