@@ -116,3 +116,24 @@ def test_fexp10_vs_numpy_power(host_tool):
         assert ulp_err(got[ok], ref[ok]).max() <= 0.51
     sp = host_tool("t", np.array([np.nan, np.inf, -np.inf, 400.0, -400.0]))
     assert np.isnan(sp[0]) and sp[1] == np.inf and sp[2] == 0.0 and sp[3] == np.inf and sp[4] == 0.0
+
+
+def test_lapse_rate_polynomial(host_tool):
+    """lapse_rate_fast (noble_gas_utils.py:103-113, (1 - .0065 E/288.15)**5.2561 * 0.000101325):
+    the degree-9 polynomial on E in [-500, 4500] m and the exp/log form outside, against
+    80-bit long double; NaN propagates."""
+    if np.finfo(np.longdouble).nmant < 60:
+        pytest.skip("long double is not 80-bit here")
+    rng = np.random.default_rng(9)
+    E = np.concatenate([rng.uniform(-500, 4500, 20000), np.linspace(-500, 4500, 2001),
+                        rng.uniform(-3000, -500, 500), rng.uniform(4500, 20000, 500), [-500.0, 4500.0, 2000.0]])
+    got = host_tool("p", E)
+    El = E.astype(np.longdouble)
+    ref = (1 - np.longdouble(".0065") * El / np.longdouble("288.15")) ** np.longdouble("5.2561") \
+        * np.longdouble("0.000101325")
+    rel = np.abs((got.astype(np.longdouble) - ref) / ref).astype(np.float64)
+    poly = (E >= -500) & (E <= 4500)
+    assert rel[poly].max() <= 5e-16, rel[poly].max()
+    # exp(5.2561 log(.)) outside: the argument rounding scales with |5.2561 log(.)|
+    assert rel[~poly].max() <= 4e-15, rel[~poly].max()
+    assert np.isnan(host_tool("p", np.array([np.nan]))[0])
