@@ -1461,10 +1461,20 @@ int ngrtd_demc_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64_
     int32_t* acc = static_cast<int32_t*>(p->demc_acc.p);
     double* prop = p->demc_prop[0].d();
     const dim3 pgrid((unsigned)cdiv(W, 256), (unsigned)cdiv(R, kDemcRows));
+    // rows staged in LDS (demc_propose_rows_kernel): K rows per block within 64 KiB, while
+    // that still leaves a block per CU's worth of blocks (c4: K = 2, 256 blocks)
+    static const bool no_stage = std::getenv("NGRTD_DEMC_NO_STAGE") != nullptr;
+    int K = (int)std::min<int64_t>(8, (64 * 1024 / 8) / W);
+    while (K > 1 && cdiv(R, K) < 256) K /= 2;
+    const bool stage = !no_stage && K >= 1;
     for (int64_t s = 0; s < n_steps; ++s) {
         const uint64_t key = demc_key(seed, step0 + (uint64_t)s);
         DemcArgs d{theta, prop, W, R, lamb, scaling, key};
-        hipLaunchKernelGGL(demc_propose_kernel, pgrid, dim3(256), 0, st, d);
+        if (stage)
+            hipLaunchKernelGGL(demc_propose_rows_kernel, dim3((unsigned)cdiv(R, K)), dim3(kDemcStageThreads),
+                               (size_t)K * W * sizeof(double), st, d, (int32_t)K);
+        else
+            hipLaunchKernelGGL(demc_propose_kernel, pgrid, dim3(256), 0, st, d);
         HIP_TRY(ctx, hipGetLastError());
         const DemcAccept da{logp, acc, cnt, theta, prop, p->desc.n_params, key};
         NG_CHECK(plan_run(p, prop, W, p->demc_lp.d(), nullptr, nullptr, &da));

@@ -977,15 +977,19 @@ __global__ void __launch_bounds__(256) demc_accept_kernel(const DemcAccept d, co
 // [r0, r0 + kDemcRows): partners r1 != r2, both != w, drawn once per thread as
 // sampler.DEMetropolis draws them; walkers on x (coalesced), row chunks on y.
 constexpr int kDemcRows = 8;
+// partners of walker w for the step keyed `key`: r1 != w, r2 != r1, r2 != w
+__device__ __forceinline__ void demc_partners(uint64_t key, uint32_t W, uint32_t w, uint32_t& r1, uint32_t& r2) {
+    const uint64_t hp = rng_mix(rng_mix(key + 1) + (uint64_t)w);
+    r1 = (uint32_t)((w + 1 + (uint32_t)(hp >> 32) % (W - 1)) % W);
+    r2 = (r1 + 1 + (uint32_t)hp % (W - 2)) % W;
+    if (r2 == w) r2 = (r2 + 1) % W;
+    if (r2 == r1) r2 = (r2 + 1) % W;
+}
 __global__ void __launch_bounds__(256) demc_propose_kernel(const DemcArgs d) {
     const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= d.W) return;
-    const uint32_t W = (uint32_t)d.W;
-    const uint64_t hp = rng_mix(rng_mix(d.key + 1) + (uint64_t)w);
-    const uint32_t r1 = (uint32_t)((w + 1 + (uint32_t)(hp >> 32) % (W - 1)) % W);
-    uint32_t r2 = (r1 + 1 + (uint32_t)hp % (W - 2)) % W;
-    if (r2 == (uint32_t)w) r2 = (r2 + 1) % W;
-    if (r2 == r1) r2 = (r2 + 1) % W;
+    uint32_t r1, r2;
+    demc_partners(d.key, (uint32_t)d.W, (uint32_t)w, r1, r2);
     const uint64_t ke = rng_mix(d.key + 2);
     const int64_t r0 = (int64_t)blockIdx.y * kDemcRows;
 #pragma unroll 4
@@ -993,6 +997,32 @@ __global__ void __launch_bounds__(256) demc_propose_kernel(const DemcArgs d) {
         const int64_t row = r * d.W, e = row + w;
         const double eps = (2.0 * rng_unit(rng_mix(ke + (uint64_t)e)) - 1.0) * d.scaling;
         d.prop[e] = d.x[e] + d.lamb * (d.x[row + r1] - d.x[row + r2]) + eps;
+    }
+}
+
+// The same proposal with K whole rows of x staged in LDS per block (coalesced loads and
+// stores; the partner gathers x[row][r1], x[row][r2] -- random within a row -- read LDS
+// instead of 64 scattered cache lines per wave instruction).  Identical arithmetic, so
+// bitwise the same proposals.  Used when K * W doubles fit the block's LDS (demc_run).
+constexpr int kDemcStageThreads = 1024;
+__global__ void __launch_bounds__(kDemcStageThreads) demc_propose_rows_kernel(const DemcArgs d, int32_t K) {
+    extern __shared__ double xs[];                       // [K][W]
+    const int64_t W = d.W;
+    const int64_t r0 = (int64_t)blockIdx.x * K;
+    const int nr = (int)((d.R - r0) < K ? (d.R - r0) : K);
+    const double* src = d.x + r0 * W;
+    for (int64_t i = threadIdx.x; i < nr * W; i += kDemcStageThreads) xs[i] = src[i];
+    __syncthreads();
+    const uint64_t ke = rng_mix(d.key + 2);
+    for (int64_t w = threadIdx.x; w < W; w += kDemcStageThreads) {
+        uint32_t r1, r2;
+        demc_partners(d.key, (uint32_t)W, (uint32_t)w, r1, r2);
+        for (int k = 0; k < nr; ++k) {
+            const double* xr = xs + (int64_t)k * W;
+            const int64_t e = (r0 + k) * W + w;
+            const double eps = (2.0 * rng_unit(rng_mix(ke + (uint64_t)e)) - 1.0) * d.scaling;
+            d.prop[e] = xr[w] + d.lamb * (xr[r1] - xr[r2]) + eps;
+        }
     }
 }
 
