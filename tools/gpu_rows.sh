@@ -26,4 +26,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/p
 step sampler-sweep
 timeout -k 10 300 python tools/sampler_bench.py > $OUT/sampler_bench.json 2> $OUT/sampler.err || { echo "sampler bench failed" >> $OUT/steps.log; exit 1; }
 timeout -k 10 300 python tools/sweep_bench.py > $OUT/sweep_bench.json 2> $OUT/sweep.err || { echo "sweep bench failed" >> $OUT/steps.log; exit 1; }
+step sampler-stats
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_sampler -o stats -- python3 tools/sampler_bench.py > $OUT/prof_sampler.json 2> $OUT/prof_sampler.err || { echo "sampler stats failed" >> $OUT/steps.log; exit 1; }
 step done
