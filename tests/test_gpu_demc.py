@@ -26,8 +26,8 @@ def unit(h):
 
 
 def numpy_step(x, lp, lp_fn, lamb, scaling, seed, step):
-    """One step of ngrtd_demc_run restated (csrc/ngrtd_kernels.hpp demc_propose_kernel,
-    demc_decide); x [R][W]."""
+    """One step of ngrtd_demc_run restated (csrc/ngrtd_kernels.hpp demc_partners,
+    demc_propose_rows_kernel / demc_propose_kernel, demc_decide); x [R][W]."""
     R, W = x.shape
     k = key(seed, step)
     k1, k2, k3 = mix((k + 1) & M64), mix((k + 2) & M64), mix((k + 3) & M64)
@@ -84,6 +84,30 @@ def test_demc_matches_numpy_restatement(kind):
     assert np.array_equal(lpv.cpu().numpy(), rlp)
     assert np.array_equal(acc.cpu().numpy().astype(bool), racc)
     assert int(cnt.item()) == total and 0 < total < 3 * W
+    lp.close()
+
+
+def test_demc_unstaged_proposal_large_w():
+    """W > 8192: a row of theta no longer fits the proposal kernel's LDS staging
+    (demc_propose_rows_kernel), so ngrtd_demc_run takes the gather kernel
+    (demc_propose_kernel); same step, bitwise."""
+    import torch
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+    from noblegas_rtd_mcmc_amd.spec import ModelSpec
+    spec = ModelSpec(n_wells=1, ce=wl.c4_spec(L=1, N=300).ce)
+    W = 8200
+    th0 = wl.sample_prior(spec, W, np.random.default_rng(8))
+    lp = LogProb(spec, max_walkers=W)
+    P, L = th0.shape[0], th0.shape[1]
+    fn = lambda v: lp(np.ascontiguousarray(v.reshape(P, L, W)), soa=True)
+    x = torch.from_numpy(th0).cuda()
+    lpv = lp(x).clone()
+    lamb, scaling, seed = 0.05, 1e-4, 4242
+    lp.demc(x, lpv, 1, lamb, scaling, seed, step0=3)
+    rx, rlp, _ = numpy_step(th0.reshape(P * L, W), fn(th0.reshape(P * L, W)), fn, lamb, scaling, seed, 3)
+    assert np.array_equal(x.cpu().numpy().reshape(P * L, W), rx)
+    assert np.array_equal(lpv.cpu().numpy(), rlp)
     lp.close()
 
 

@@ -225,7 +225,8 @@ def test_mfma_and_valu_paths_agree():
     launch (logp_fused_kernel) and forward() uses rtd_exp_mfma_kernel.  The general VALU
     Horner kernel (NGRTD_NO_MFMA=1), the two-launch MFMA path (NGRTD_NO_FUSED=1) and the
     MFMA kernel with the per-unit epilogue fused (NGRTD_FUSE=1, NGRTD_NO_FUSED=1) must give
-    the same answer."""
+    the same answer, as must the single launch without the surrogate (NGRTD_NO_CHEB=1) or
+    without the Student-t normaliser table (NGRTD_NO_C0TAB=1)."""
     import os
     import subprocess
     import sys
@@ -251,7 +252,8 @@ def test_mfma_and_valu_paths_agree():
             % os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     out = "/tmp/ngrtd_paths_%d.npy" % os.getpid()
     for extra, mfma in (({"NGRTD_NO_MFMA": "1"}, False), ({"NGRTD_NO_FUSED": "1"}, True),
-                        ({"NGRTD_FUSE": "1", "NGRTD_NO_FUSED": "1"}, True), ({"NGRTD_NO_CHEB": "1"}, True)):
+                        ({"NGRTD_FUSE": "1", "NGRTD_NO_FUSED": "1"}, True), ({"NGRTD_NO_CHEB": "1"}, True),
+                        ({"NGRTD_NO_C0TAB": "1"}, True)):
         env = dict(os.environ, **extra)
         subprocess.run([sys.executable, "-c", "MFMA = %s; " % mfma + code, out], check=True, env=env, timeout=300)
         b = np.load(out)
