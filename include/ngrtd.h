@@ -304,10 +304,12 @@ int ngrtd_demc_run(ngrtd_plan* plan, double* theta, double* logp, int64_t W, int
  * cols: [C][N] channel columns (age order); coef (may be NULL): receives
  * [NGRTD_CHEB_PIECES][NGRTD_CHEB_N][(C+2)&~1], per piece the Chebyshev interpolant in
  * monomial form (coefficient k of x^k, x the piece's local coordinate in [-1, 1], as the
- * kernel evaluates it by Horner); *max_rel_err: max |surrogate - exact| / exact over the
+ * kernel evaluates it by Horner).  Pieces 0..75 split the octaves [2^-1, 2^18) of tau in
+ * four: piece 4 (e + 1) + j holds tau = 2^e m (m in [1, 2)) with floor(4 (m - 1)) = j, and
+ * x = 8 (m - 1.125 - j/4); piece 76 is the tail tau >= 2^18 in s = 1/tau, x = 2^19 s - 1; *max_rel_err: max |surrogate - exact| / exact over the
  * validation points.  Plans use the surrogate only when this is <= 5e-14. */
 #define NGRTD_CHEB_N 12
-#define NGRTD_CHEB_PIECES 53
+#define NGRTD_CHEB_PIECES 77
 int ngrtd_surrogate_check(const double* cols, int32_t C, int64_t N, double dtp, double* coef,
                           double* max_rel_err);
 

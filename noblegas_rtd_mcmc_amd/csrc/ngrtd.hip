@@ -269,9 +269,9 @@ static double cheb_build(const std::vector<std::vector<double>>& cols, int C, do
             for (int k = 0; k < n; ++k) {
                 const long double xk = cosl(PI * (k + 0.5L) / n);
                 long double sv;
-                if (p < kChebLogPieces) {
-                    const long double u = (long double)kChebU0 + (p + 0.5L) * kChebW + 0.5L * kChebW * xk;
-                    sv = expl(-u);
+                if (p < kChebBinPieces) {
+                    const int e = kChebOct0 + p / kChebSub, j = p % kChebSub;
+                    sv = 1.0L / ldexpl(1.125L + 0.25L * j + xk / 8.0L, e);
                 } else {
                     sv = 0.5L * (long double)kChebSHi * (1.0L + xk);
                 }
@@ -300,9 +300,10 @@ static double cheb_build(const std::vector<std::vector<double>>& cols, int C, do
     for (int p = 0; p < kChebPieces; ++p) {
         for (int i = 0; i <= M + 1; ++i) {
             double tau;
-            if (p < kChebLogPieces) {
-                const long double t = (i == 0) ? p : (i == M + 1) ? p + 1 - 1e-12L : p + (i - 0.5L) / M;
-                tau = (double)expl((long double)kChebU0 + (long double)kChebW * t);
+            if (p < kChebBinPieces) {
+                const int e = kChebOct0 + p / kChebSub, j = p % kChebSub;
+                const long double t = (i == 0) ? 0.0L : (i == M + 1) ? 1.0L - 1e-12L : (i - 0.5L) / M;
+                tau = (double)ldexpl(1.0L + 0.25L * (j + t), e);
             } else {
                 const long double sv = (long double)kChebSHi * (i / (long double)(M + 1));
                 tau = (sv == 0.0L) ? HUGE_VAL : (double)(1.0L / sv);

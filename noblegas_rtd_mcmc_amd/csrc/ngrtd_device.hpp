@@ -45,17 +45,22 @@ struct RtdArgs {
 // Chebyshev surrogate of Z_c(tau) = s01(tau) sum_{j>=0} A_{c,1+j} exp(-j / tau) (the
 // exponential RTD channel sums times s01 = exp(-(tp_1 - tp_0) / tau)) for every channel c,
 // and of Z_G(tau) = s01(tau) sum_{j=0}^{N-2} exp(-j / tau) (the normaliser), so that
-// conc = (A_{c,0} + Z_c) / (1 + Z_G) with no exp/expm1/division per unit: piecewise in u = log(tau), kChebLogPieces pieces of width kChebW from
-// tau = 1/2 (u0 = log 1/2), then one piece in s = 1/tau over [0, kChebSHi] for the tail up
-// to tau = inf.  kChebN coefficients per piece and channel.  Built and validated per plan
-// on the host (ngrtd.hip cheb_build); tau < 1/2, NaN take the exact matrix-core path.
+// conc = (A_{c,0} + Z_c) / (1 + Z_G) with no exp/expm1/division per unit.  Pieces follow
+// tau's binary representation: kChebSub per octave over the kChebOcts octaves
+// [2^kChebOct0, 2^(kChebOct0 + kChebOcts)); piece (e - kChebOct0) kChebSub + j holds
+// tau = 2^e m whose significand m in [1, 2) has top bits j, in the local x = 8 (m - c_j),
+// c_j = 1 + (2j + 1)/8 (exact in binary: the piece index and x need no log).  Then one
+// piece in s = 1/tau over [0, kChebSHi] for the tail up to tau = inf.  kChebN
+// coefficients per piece and channel.  Built and validated per plan on the host
+// (ngrtd.hip cheb_build); tau < 1/2, NaN take the exact matrix-core path.
 constexpr int kChebN = 12;
-constexpr double kChebW = 0.25;                    // piece width in log(tau) (exact in binary)
-constexpr int kChebLogPieces = 52;                 // u in [u0, u0 + 13]: tau up to 221 206.9
-constexpr int kChebPieces = kChebLogPieces + 1;
+constexpr int kChebSub = 4;
+constexpr int kChebOct0 = -1;                      // tau >= 1/2
+constexpr int kChebOcts = 19;                      // up to 2^18 = 262 144
+constexpr int kChebBinPieces = kChebSub * kChebOcts;
+constexpr int kChebPieces = kChebBinPieces + 1;
 constexpr double kChebTauLo = 0.5;
-constexpr double kChebU0 = -0.69314718055994530942;   // log(0.5)
-constexpr double kChebSHi = 4.55e-6;               // > 1 / (0.5 e^13)
+constexpr double kChebSHi = 0x1p-18;               // the tail: s = 1/tau in [0, 2^-18]
 // surrogate table row length for C channels: C numerator sums + the normaliser, even
 __host__ __device__ constexpr int cheb_cp(int C) { return (C + 2) & ~1; }
 

@@ -734,18 +734,17 @@ struct MfmaWave {
 // or NaN).  Host and device run this same code (the host validates the table with it).
 __host__ __device__ __forceinline__ int cheb_piece(double tau, double& x) {
     if (!(tau >= kChebTauLo)) return -1;
-    const double u = flog(tau);
-    const double t = (u - kChebU0) * (1.0 / kChebW);
-    if (t >= (double)kChebLogPieces) {
+    const unsigned hi = fm_hi(tau);
+    const int e = (int)(hi >> 20) - 1023;          // tau >= 1/2: sign bit clear
+    if (e >= kChebOct0 + kChebOcts) {              // tau >= 2^18, inf
         const double sv = 1.0 / tau;
         x = sv * (2.0 / kChebSHi) - 1.0;
-        return kChebLogPieces;
+        return kChebBinPieces;
     }
-    int p = (int)floor(t);
-    p = p < 0 ? 0 : p;
-    const double mid = kChebU0 + ((double)p + 0.5) * kChebW;
-    x = (u - mid) * (2.0 / kChebW);
-    return p;
+    const int j = (int)((hi >> 18) & 3u);
+    const double m = fm_with_hi(tau, (hi & 0x000FFFFFu) | 0x3FF00000u);
+    x = (m - (1.125 + 0.25 * j)) * 8.0;
+    return (e - kChebOct0) * kChebSub + j;
 }
 
 // Surrogate sums of C channels at x from one piece's coefficients [kChebN][CP]: the
@@ -1083,7 +1082,7 @@ __device__ __forceinline__ void fused_exact(const RtdArgs& a, const UnitArgs& ul
 
 constexpr int kFusedWaves = 8;                 // waves of units per block (512 units)
 constexpr int kFusedUnits = 64 * kFusedWaves;
-constexpr int kFusedPrefetch = 4;   // double2 per thread (512 threads): covers kChebPieces*kChebN*6 doubles
+constexpr int kFusedPrefetch = 6;   // double2 per thread (512 threads): covers kChebPieces*kChebN*6 doubles
 // LDS stride of one surrogate piece: kChebN*CP doubles + 2 of padding, so that consecutive
 // pieces start 16-B slots an ODD number apart -- lanes gathering different pieces with
 // ds_read_b128 then spread over all 16 slots of a bank row instead of 4 (MI355X_MICROARCH.md

@@ -15,8 +15,8 @@ import pytest
 
 from noblegas_rtd_mcmc_amd import workloads
 
-N_COEF, PIECES, WIDTH = 12, 53, 0.25
-U0, S_HI = np.log(0.5), 4.55e-6
+N_COEF, PIECES = 12, 77
+SUB, OCT0, OCTS, S_HI = 4, -1, 19, 2.0 ** -18
 
 
 @pytest.fixture(scope="module")
@@ -57,13 +57,15 @@ def check(lib, cols, dtp=0.0):
 
 
 def numpy_surrogate(coef, tau, c):
-    u = np.log(tau)
-    t = (u - U0) / WIDTH
-    if t >= PIECES - 1:
+    """The kernel's piece lookup (ngrtd_kernels.hpp cheb_piece) and Horner sum, in NumPy."""
+    if tau >= 2.0 ** (OCT0 + OCTS):
         p, x = PIECES - 1, (1.0 / tau) * (2.0 / S_HI) - 1.0
     else:
-        p = max(int(np.floor(t)), 0)
-        x = (u - (U0 + (p + 0.5) * WIDTH)) * (2.0 / WIDTH)
+        m, e = np.frexp(tau)                   # tau = m 2^e, m in [1/2, 1)
+        m, e = 2.0 * m, e - 1
+        j = int((m - 1.0) * 4.0)
+        p = (e - OCT0) * SUB + j
+        x = (m - (1.125 + 0.25 * j)) * 8.0
     return np.polynomial.polynomial.polyval(x, coef[p, :, c])   # monomial form of the Chebyshev fit
 
 
