@@ -89,7 +89,7 @@ NGRTD_HD double vapor_pressure_atm(double T) {
     // the folded constant: <= 3 ulp from the reference's three roundings
     return fexp10(A - (B / (C + T))) * (101325. / 760. / 1.0e9 / 0.000101325);
 }
-NGRTD_HD double lapse_rate_atm(double E) { return fexp(5.2561 * flog(1 - .0065 * E / 288.15)); }
+NGRTD_HD double lapse_rate_atm(double E) { return fexp(5.2561 * flog(1 - E * (.0065 / 288.15))); }
 
 // Bullister solubility coefficients [a1, a2, a3, b1, b2, b3]: cfc_dict (:74) and
 // solubility_sf6 (:214-219); index = enum ngrtd_cfc_species
@@ -108,7 +108,8 @@ struct CfcT {
 };
 NGRTD_HD CfcT cfc_t(double T) {
     const double T_k = T + 273.15;
-    return {100 / T_k, flog(T_k / 100), T_k / 100};
+    const double r = T_k * 0.01;                  // T_k / 100 (<= 1 ulp)
+    return {100 / T_k, flog(r), r};
 }
 // K [mol atm^-1 kg^-1]
 NGRTD_HD double solubility_cfc(int sp, const CfcT& t, double S) {
@@ -126,15 +127,17 @@ struct CfcArgs {
 };
 
 // Ae is self.Ae, ccSTP/kg (the constructor's Ae*1000., :30, :176); P_da / P_vapor per member
+// (am = Ae / 22414.1, Ae over the molar volume: the same per species, formed once per member)
 NGRTD_HD double cfc_value(int what, int sp, const CfcT& t, double P_da, double P_vapor, double Ae, double F,
-                          double S, double Pself, double x) {
+                          double S, double Pself, double x, double am) {
     const bool sf6 = (sp == NGRTD_SF6);
     const double Ki = solubility_cfc(sp, t, S);
     if (what == NGRTD_CFC_SOLUBILITY) return Ki;
     if (what == NGRTD_CFC_EQUIL_AIR) {           // equil_air_conc_cfc :86-106 / _sf6 :229-249
-        const double am = Ae / 22414.1;          // Ae/molar_volume (same value per species)
+        // (x + x F am / KP) / (KP + am) over one denominator: x (KP + F am) / (KP (KP + am)),
+        // one division instead of two (a few ulp; parity bar 1e-12)
         const double KP = Ki * P_da;
-        const double z = (x + ((x * F * am) / KP)) / (KP + am);
+        const double z = (x * (KP + F * am)) / (KP * (KP + am));
         return sf6 ? z * 0.001 : z;
     }
     if (what == NGRTD_CFC_EQUIL_AQ) {            // equil_aq_conc_cfc :108-124 / _sf6 :264-278
@@ -166,9 +169,10 @@ __global__ void __launch_bounds__(256) cfc_corr_kernel(const CfcArgs a) {
     const bool need_pda = a.what == NGRTD_CFC_EQUIL_AIR || a.what == NGRTD_CFC_EQUIL_AQ;
     const double P_da = need_pda ? lapse_rate_atm(E) - P_vapor : 0.0;
     const CfcT t = cfc_t(T);
+    const double am = Ae / 22414.1;
     for (int j = 0; j < a.ns; ++j) {
         const double x = a.x ? a.x[(int64_t)j * a.n + i] : 0.0;
-        a.out[(int64_t)j * a.n + i] = cfc_value(a.what, a.sp[j], t, P_da, P_vapor, Ae, F, S, P, x);
+        a.out[(int64_t)j * a.n + i] = cfc_value(a.what, a.sp[j], t, P_da, P_vapor, Ae, F, S, P, x, am);
     }
 }
 
