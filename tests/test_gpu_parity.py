@@ -200,6 +200,29 @@ def test_c4_full_size_vs_oracle_and_properties():
     lp.close()
 
 
+@pytest.mark.parametrize("config", ["c2", "c3"])
+def test_c2_c3_full_size_vs_oracle_and_properties(config):
+    """c2 (CE only, 2048 x 3 wells x 5 gases, T<0 draws hit the -9999 path) and c3 (RTD only,
+    2048 x 4 tracers, N=1200, sampled J) at full size: sampled walkers vs the oracle,
+    bitwise determinism, device == host path, walker-permutation equivariance."""
+    import torch
+    import oracle.models as om
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+    spec, th = getattr(wl, config)()
+    lp = LogProb(spec, max_walkers=th.shape[2])
+    dev = torch.from_numpy(th).cuda()
+    a = lp(dev).cpu().numpy()
+    assert np.array_equal(a, lp(dev).cpu().numpy())
+    assert np.array_equal(a, lp(th, soa=True))
+    walkers = [0, 1, 63, 64, 777, 1000, 2047]
+    ref = om.log_prob(spec, th, walkers=walkers)
+    assert close(a[walkers], ref, 1e-12, 1e-9).all(), (a[walkers], ref)
+    perm = np.random.default_rng(1).permutation(th.shape[2])
+    assert np.array_equal(lp(np.ascontiguousarray(th[:, :, perm]), soa=True), a[perm])
+    lp.close()
+
+
 def test_edge_walkers():
     """W not a multiple of 64, W = 1, out-of-support walkers (-inf), NaN propagation."""
     import oracle.models as om
