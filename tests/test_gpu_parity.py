@@ -223,6 +223,21 @@ def test_c2_c3_full_size_vs_oracle_and_properties(config):
     lp.close()
 
 
+def test_logp_full_series_length():
+    """Joint log-prob over the shipped C_in_dict length (N = 25 256 ages) vs the oracle."""
+    import oracle.models as om
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+    spec = wl.c4_spec(L=2, N=25256)
+    th = wl.sample_prior(spec, 100, np.random.default_rng(11))
+    lp = LogProb(spec, max_walkers=128)
+    got = lp(th, soa=True)
+    walkers = [0, 1, 50, 63, 64, 99]
+    ref = om.log_prob(spec, th, walkers=walkers)
+    assert close(got[walkers], ref, 1e-12, 1e-9).all(), (got[walkers], ref)
+    lp.close()
+
+
 def test_edge_walkers():
     """W not a multiple of 64, W = 1, out-of-support walkers (-inf), NaN propagation."""
     import oracle.models as om
