@@ -74,10 +74,81 @@ def _arr(x, n):
 class tracer_conv_integral:
     """convolution_integral_utils.py:105-340 (same constructor, attributes and methods)."""
 
+    _g_tp = None
+    _g_lazy = None
+
     def __init__(self, C_t, t_samp, device=0):
         self.C_t = C_t
         self.t_samp = t_samp
         self._device = device
+
+    @property
+    def g_tp(self):
+        """The weights convolve() used times its decay factor (3He: 1 - exp(-lamba tp)),
+        as the reference leaves ``self.g_tp`` after convolve() (:300-316).  Nothing on the
+        log-prob path reads it, so it is materialised on first access: the weights come
+        from the device (ngrtd_rtd_weights / ngrtd_frac_conv), the decay factor is the
+        reference's own NumPy expression."""
+        if self._g_tp is None and self._g_lazy is not None:
+            self._g_tp = self._g_lazy()
+            self._g_lazy = None
+        if self._g_tp is None:
+            raise AttributeError("g_tp is set by convolve() (convolution_integral_utils.py:300)")
+        return self._g_tp
+
+    @g_tp.setter
+    def g_tp(self, value):
+        self._g_tp, self._g_lazy = value, None
+
+    def _decayed(self, g, n, index_last, lamba, rad_accum):
+        """:305-316: g x exp(-lamba tp), or g x (1 - exp(-lamba tp)) for 3He."""
+        tp = np.arange(0, n).astype(float)
+        tp[0] += 1e-5
+        tp += np.floor(self.t_samp - index_last)
+        lam = np.asarray(lamba, dtype=np.float64)
+        if lam.ndim:
+            lam = lam.reshape(lam.shape + (1,))
+        if rad_accum == '3He':
+            return g * (1 - np.exp(-lam * tp))
+        return g * np.exp(-lam * tp)
+
+    def _defer_g_tp(self, n, index_last, g_tau=None):
+        """Record what convolve() used so that g_tp can be built on access."""
+        snap = dict(tau=self.tau, mod_type=self.mod_type, eta=self.eta, D=self.D, lamba=self.lamba,
+                    rad_accum=self.rad_accum, bbar=self.bbar, Phi_im=self.Phi_im, f_tadv_ext=self.f_tadv_ext,
+                    t_half=getattr(self, "_thalf_src", None))
+
+        def build():
+            if g_tau is not None:
+                g = np.asarray(g_tau, dtype=np.float64)
+            else:
+                saved = {k: getattr(self, k, None) for k in snap}
+                saved_src = getattr(self, "_thalf_src", None)
+                try:
+                    for k, v in snap.items():
+                        if k != "t_half":
+                            setattr(self, k, v)
+                    shape = np.broadcast_shapes(*[np.shape(snap[k]) for k in ("tau", "eta", "D")
+                                                  if snap[k] is not None and snap[k] is not False])
+                    if shape == () or self.mod_type in _FRAC:
+                        g = self.gen_g_tp()
+                    else:
+                        taus = np.broadcast_to(np.asarray(snap["tau"], dtype=np.float64), shape)
+                        etas = np.broadcast_to(np.asarray(snap["eta"] if snap["eta"] is not None else 0.0,
+                                                          dtype=np.float64), shape)
+                        Ds = np.broadcast_to(np.asarray(snap["D"] if snap["D"] is not None else 0.0,
+                                                        dtype=np.float64), shape)
+                        g = np.empty(shape + (n,))
+                        for ix in np.ndindex(shape):
+                            self.tau, self.eta, self.D = float(taus[ix]), float(etas[ix]), float(Ds[ix])
+                            g[ix] = self.gen_g_tp()
+                finally:
+                    for k, v in saved.items():
+                        setattr(self, k, v)
+                    self._thalf_src = saved_src
+            return self._decayed(g, n, index_last, snap["lamba"], snap["rad_accum"])
+
+        self._g_tp, self._g_lazy = None, build
 
     def update_pars(self, **kwargs):
         """:111-142 -- missing kwargs reset to None/False exactly like the reference."""
@@ -208,12 +279,13 @@ class tracer_conv_integral:
             ctx.check(ctx.lib.ngrtd_conv_dot(ctx.h, sid, g.ctypes.data_as(C.c_void_p), th, accum,
                                              float(Jv or 0.0), out.ctypes.data_as(C.c_void_p), _lib.MEM_HOST),
                       "ngrtd_conv_dot")
-            self.g_tp = g
+            self._defer_g_tp(n, i[-1], g_tau=g)
             self.C_i = float(out[0])
             return self.C_i
         self._check_model()
         if self.mod_type in _FRAC:
             conc, _, shape = self._frac(sid, n, accum, Jv, True, False)
+            self._defer_g_tp(n, i[-1])
             self.C_i = float(conc[0]) if shape == () else conc.reshape(shape)
             return self.C_i
         tau = np.asarray(self.tau, dtype=np.float64)
@@ -235,5 +307,6 @@ class tracer_conv_integral:
                                      0.0 if per_th else float(th), p(Js),
                                      0.0 if (per_J or Jv is None or Jv is False) else float(Jv),
                                      m, out.ctypes.data_as(C.c_void_p), _lib.MEM_HOST), "ngrtd_conv")
+        self._defer_g_tp(n, i[-1])
         self.C_i = float(out[0]) if shape == () else out.reshape(shape)
         return self.C_i

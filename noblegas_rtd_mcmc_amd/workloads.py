@@ -1,7 +1,9 @@
 """Deterministic builders for the BASELINE.json configurations c1..c5.
 
-All inputs are synthetic or come from the small data tables under ``data/`` (extracted
-from the reference's shipped xlsx/CSV files by tools/make_package_data.py):
+All inputs are synthetic or come from the small data tables under ``data/``, extracted
+from the reference's shipped files by tools/make_package_data.py: the noble-gas obs of
+Field_Data/PLM_noblegas_2021.xlsx, the input series of age_ens_runs_mcmc/C_in_dict.pk
+(bit-exact) and the MAP tracer obs of age_ens_runs_mcmc/map_dict.pk:
 
 * c1  CE plumbing: PLM1, gases Ne/Ar/Kr/Xe, 100 walkers (sampler: 500 steps, seed 12345).
 * c2  CE log-prob: 2048 walkers x 3 wells (PLM1, PLM6, PLM7) x 5 gases.
@@ -27,8 +29,10 @@ def field_data():
 
 
 def atmos_series(name, n=None):
-    """Reference-shaped yearly input series for a tracer, age-first, length n (default
-    the full 25256).  'He3' uses the H3 history (run_age_mcmc.py:217-220)."""
+    """The shipped input series C_in_dict[name] (prep.py:165-219), age-first
+    (= np.flip(C_in_dict[name].values), convolution_integral_utils.py:336), its first n
+    ages (= the last n rows of the DataFrame; default all 25256).  'He3' uses the H3
+    history (run_age_mcmc.py:217-220)."""
     z = np.load(os.path.join(_DATA, "atmos_series.npz"), allow_pickle=False)
     key = "H3" if name == "He3" else name
     N = int(z["N_full"]) if n is None else int(n)
@@ -53,6 +57,11 @@ def tracer(name, n=None, series=None, log10_J=None):
     if name == "H3":
         return Tracer(name, s, t_half=12.34)
     raise ValueError(name)
+
+
+def map_obs(well):
+    """MAP tracer observations map_dict[tracer].loc[well] (run_age_mcmc.py:44, prep.py:453-494)."""
+    return {t: v[well] for t, v in field_data()["map_obs"].items() if well in v}
 
 
 def ce_block(wells, gases, E_min=None, obs=None, sd=None):
@@ -119,7 +128,7 @@ def c2(W=2048):
 def c3(W=2048, N=1200):
     fd = field_data()
     names = ("CFC12", "SF6", "H3", "He4_ter")
-    mu = np.array([[fd["map_obs_PLM1"][t] for t in names]])
+    mu = np.array([[map_obs("PLM1")[t] for t in names]])
     rtd = RTDBlock(tracers=[tracer(t, N) for t in names], obs=mu, sd=0.10 * mu,
                    mod_type1="exponential", par_names=("tau1", "J"))
     spec = ModelSpec(n_wells=1, rtd=rtd)
@@ -141,8 +150,7 @@ def c4_spec(L=64, N=1200, seed=34567, mod_type1="exponential", mod_type2=None, p
         c = s.c_by_age * rng.lognormal(0.0, 0.05, N)   # non-constant everywhere
         trs.append(tracer(t, series=Series(c, s.idx_by_age, 0.0),
                           log10_J=LOG10_J_HE4_DEFAULT if t == "He4_ter" else None))
-    base = dict(fd["map_obs_PLM1"])
-    base["He3"] = 8.0
+    base = map_obs("PLM1")
     rtd_obs = np.array([[base[t] for t in names]] * L) * rng.lognormal(0, 0.1, (L, len(names)))
     rtd = RTDBlock(tracers=trs, obs=rtd_obs, sd=0.10 * rtd_obs, mod_type1=mod_type1,
                    mod_type2=mod_type2, par_names=par_names)

@@ -22,6 +22,11 @@ Fixtures (all float64):
                      ensemble propagation) for 2048 seeded members + branch edges.
   logp_golden.npz    per-walker log-probs of small CE / RTD / joint workloads: reference
                      forward models + scipy.stats log-densities.
+  sf6acc_golden.npz  rad_accum='SF6' (J_sf6) convolutions and the post-convolve g_tp.
+
+Every RTD fixture runs on the shipped input series of age_ens_runs_mcmc/C_in_dict.pk: the
+package's data/atmos_series.npz is checked bit for bit against that pickle (read without
+unpickling, tools/pickle_extract.py) before anything is generated.
 """
 import os
 import sys
@@ -511,9 +516,64 @@ def make_frac(conv):
     np.savez_compressed(os.path.join(HERE, "frac_golden.npz"), **out)
 
 
+def check_shipped_series():
+    """The package's series ARE the shipped C_in_dict.pk series, bit for bit (read without
+    unpickling by tools/pickle_extract.py), so every fixture below runs the reference's
+    code on the reference's own inputs."""
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    from pickle_extract import read_frame_dict
+    from noblegas_rtd_mcmc_amd.workloads import atmos_series
+    frames = read_frame_dict(os.path.join(REF, "age_ens_runs_mcmc", "C_in_dict.pk"))
+    for key, fr in frames.items():
+        v = np.flip(fr["values"][0])
+        got = atmos_series(key).c_by_age
+        if not np.array_equal(got.view(np.int64), v.view(np.int64)):
+            raise SystemExit("package series %s differs from C_in_dict.pk" % key)
+
+
+def make_sf6_accum(conv):
+    """rad_accum='SF6' (zero-order SF6 contamination, convolution_integral_utils.py:329-331):
+    C_t['SF6'] + index * J_sf6, with J_sf6 a numpy float (the reference calls .copy())."""
+    sys.path.insert(0, REPO)
+    from noblegas_rtd_mcmc_amd.workloads import atmos_series
+    rng = np.random.default_rng(2003)
+    out = {}
+    for n in (1200, 25256):
+        s = atmos_series("SF6", n)
+        df = reference_frame(s, n, "SF6")
+        for mod in MODS:
+            tau, eta, D = conv_params(rng, mod, n, 16)
+            Js = rng.uniform(0.0, 0.05, len(tau))
+            res = np.zeros(len(tau))
+            for i in range(len(tau)):
+                cm = conv.tracer_conv_integral(df.copy(), df.copy().index[-1])
+                cm.update_pars(tau=float(tau[i]), mod_type=mod, rad_accum="SF6", J_sf6=np.float64(Js[i]),
+                               eta=float(eta[i]), D=float(D[i]))
+                res[i] = cm.convolve()
+            key = "sf6acc_%s_%d" % (mod, n)
+            out[key + "_tau"], out[key + "_eta"], out[key + "_D"] = tau, eta, D
+            out[key + "_J"], out[key + "_out"] = Js, res
+    # g_tp after convolve() is the DECAYED weight vector (:313-316): H3 exponential
+    s = atmos_series("H3", 1200)
+    df = reference_frame(s, 1200, "H3")
+    gt = []
+    for tau in (3.0, 37.3, 480.0):
+        cm = conv.tracer_conv_integral(df.copy(), df.index[-1])
+        cm.update_pars(tau=tau, mod_type="exponential", t_half=12.34)
+        cm.convolve()
+        gt.append(cm.g_tp.copy())
+    out["gtp_after_conv_tau"] = np.array([3.0, 37.3, 480.0])
+    out["gtp_after_conv"] = np.array(gt)
+    np.savez_compressed(os.path.join(HERE, "sf6acc_golden.npz"), **out)
+
+
 def main():
     ng, conv = import_reference()
-    which = sys.argv[1:] or ["ce", "conv", "fwd", "logp", "prep", "frac"]
+    check_shipped_series()
+    which = sys.argv[1:] or ["ce", "conv", "fwd", "logp", "prep", "frac", "sf6acc"]
+    if "sf6acc" in which:
+        make_sf6_accum(conv)
     if "frac" in which:
         make_frac(conv)
     if "prep" in which:

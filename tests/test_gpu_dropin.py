@@ -101,6 +101,45 @@ def test_gen_g_tp_and_g_tau(golden):
     assert close(cm.convolve(g_tau=z["gext"]), z["gext_out"], 1e-12)
 
 
+@pytest.mark.parametrize("n", [1200, 25256])
+def test_sf6_accumulation(golden, n):
+    """rad_accum='SF6' with a numpy-float J_sf6 (convolution_integral_utils.py:329-331)."""
+    from noblegas_rtd_mcmc_amd.convolution_integral_utils import tracer_conv_integral
+    from noblegas_rtd_mcmc_amd.workloads import atmos_series
+    z = golden("sf6acc_golden.npz")
+    s = atmos_series("SF6", n)
+    df = pd.DataFrame({"SF6": np.flip(s.c_by_age)}, index=np.arange(n - 1, -1, -1))
+    cm = tracer_conv_integral(df, df.index[-1])
+    for mod in MODS:
+        key = "sf6acc_%s_%d" % (mod, n)
+        tau, eta, D, J, ref = (z[key + k] for k in ("_tau", "_eta", "_D", "_J", "_out"))
+        cm.update_pars(tau=float(tau[0]), mod_type=mod, rad_accum="SF6", J_sf6=np.float64(J[0]),
+                       eta=float(eta[0]), D=float(D[0]))
+        assert close(cm.convolve(), ref[0], 1e-12, 1e-300), key
+        cm.update_pars(tau=tau, mod_type=mod, rad_accum="SF6", J_sf6=J, eta=eta, D=D)
+        assert close(cm.convolve(), ref, 1e-12, 1e-300).all(), key
+
+
+def test_g_tp_after_convolve(golden):
+    """convolve() leaves g_tp = weights x decay (:300-316), for parameter arrays too."""
+    from noblegas_rtd_mcmc_amd.convolution_integral_utils import tracer_conv_integral
+    z = golden("sf6acc_golden.npz")
+    df = frame("H3", 1200)
+    cm = tracer_conv_integral(df, df.index[-1])
+    with pytest.raises(AttributeError):
+        cm.g_tp
+    for tau, ref in zip(z["gtp_after_conv_tau"], z["gtp_after_conv"]):
+        cm.update_pars(tau=float(tau), mod_type="exponential", t_half=12.34)
+        cm.convolve()
+        assert close(cm.g_tp, ref, 1e-12, 1e-300).all()
+    cm.update_pars(tau=z["gtp_after_conv_tau"], mod_type="exponential", t_half=12.34)
+    cm.convolve()
+    assert cm.g_tp.shape == (3, 1200) and close(cm.g_tp, z["gtp_after_conv"], 1e-12, 1e-300).all()
+    g = np.full(1200, 1.0 / 1200)
+    cm.convolve(g_tau=g)             # external weights: decayed the same way
+    assert close(cm.g_tp[0], g[0] * np.exp(-np.log(2) / 12.34 * 1e-5), 1e-15)
+
+
 FWD_CASES = [("exp_J_thalf_lamsf6", "exponential", False, ["tau1", "J", "thalf_cfc", "lamsf6"]),
              ("epm", "exp_pist_flow", False, ["tau1", "eta1"]),
              ("bmm_exp_piston", "exponential", "piston", ["tau1", "tau2", "f1", "f2"]),

@@ -54,7 +54,8 @@ def test_workload_shapes():
     spec, th = wl.c1()
     assert th.shape == (6, 1, 100)
     s = wl.atmos_series("H3", 25256)
-    assert s.n == 25256 and s.c_by_age[-1] == 3.3273 and s.c_by_age[0] > 0
+    # C_in_dict.pk H3: 69 recent ages, then the pre-bomb fill (prep.py:168 repeats the first row)
+    assert s.n == 25256 and s.c_by_age[-1] == 3.327329892219456 and s.c_by_age[0] == 5.997188929906611
 
 
 def test_series_from_reference_frames():

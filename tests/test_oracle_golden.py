@@ -207,3 +207,25 @@ def test_frac_inf_diff_matches_reference(golden):
         # the reference's g_tp attribute after convolve() carries the H3 decay (:315-317)
         gd = g * np.exp(-ortd.thalf_2_lambda(12.34) * ortd.age_grid(600, 0, 0))
         assert close(gd, z["ext_g"][i]).all() and close(fm, z["ext_fm"][i])
+
+
+@pytest.mark.parametrize("n", [1200, 25256])
+def test_sf6_accumulation_matches_reference(golden, n):
+    """rad_accum='SF6': C_t['SF6'] + index * J_sf6 (convolution_integral_utils.py:329-331)."""
+    z = golden("sf6acc_golden.npz")
+    s = atmos_series("SF6", n)
+    cv, ci = np.flip(s.c_by_age), np.arange(n - 1, -1, -1)
+    for mod in MODS:
+        key = "sf6acc_%s_%d" % (mod, n)
+        got = [ortd.convolve(cv, ci, ci[-1], t, mod, rad_accum="SF6", J_sf6=j, eta=e, D=d)
+               for t, e, d, j in zip(z[key + "_tau"], z[key + "_eta"], z[key + "_D"], z[key + "_J"])]
+        assert close(got, z[key + "_out"], rtol=1e-12).all(), mod
+
+
+def test_g_tp_after_convolve_is_decayed(golden):
+    """convolve() leaves self.g_tp = weights x decay factor (:313-316)."""
+    z = golden("sf6acc_golden.npz")
+    tp = ortd.age_grid(1200, 0, 0)
+    for tau, ref in zip(z["gtp_after_conv_tau"], z["gtp_after_conv"]):
+        g = ortd.gen_g_tp(1200, 0, 0, tau, "exponential") * np.exp(-ortd.thalf_2_lambda(12.34) * tp)
+        assert close(g, ref, rtol=1e-12, atol=1e-300).all()

@@ -1,26 +1,26 @@
 #!/usr/bin/env python3
-"""Extract the small data tables the engine ships with from the reference's own
-TEXT/XML data files (run once, in the build container, where /root/reference exists).
+"""Extract the small data tables the engine ships with from the reference's own data
+files (run once, in the build container, where /root/reference exists).
 
 Outputs (committed, tiny):
   noblegas_rtd_mcmc_amd/data/plm_field_data.json
       Noble-gas observations of Field_Data/PLM_noblegas_2021.xlsx sheet1 rows 3-7
       (read at ng_interp/noble_gas_mcmc.py:72-78), parsed with zipfile+xml (no
       openpyxl, nothing executed from the file), the percent errors
-      (noble_gas_mcmc.py:107) and the well elevations (noble_gas_mcmc.py:80-82).
+      (noble_gas_mcmc.py:107), the well elevations (noble_gas_mcmc.py:80-82) and the
+      MAP tracer observations of age_ens_runs_mcmc/map_dict.pk (prep.py:453-494),
+      every tracer x well, at full float64 precision.
   noblegas_rtd_mcmc_amd/data/atmos_series.npz
-      Yearly atmospheric input series in the shape of age_ens_runs_mcmc/C_in_dict.pk
-      (age index 25255..0, built by age_modeling_mcmc.prep.py:165-219).  The pickle
-      itself is NOT loaded (pickle-only format, no safe loader); instead the series are
-      rebuilt from the reference's shipped CSV histories:
-        CFC12/SF6/CFC11/CFC113: Input_Series/NOAA_cfc_sf6/cfc_sf6_atmhist_1765-2021.csv
-        H3: Input_Series/Tritium/TritiumInQuadrangeles_Jurgens2018.csv column
-            '39-37,110-105' (the Crested Butte cell used at Gen_atmos_tracers_v3.py:57-60),
-            annual means, 2013-2021 continued by 12.34-yr decay of the 2012 value,
-            pre-1953 fill 3.3273 TU (the constant prefix SURVEY.md §8a-a15 recorded).
-        He4_ter: zeros (run_age_mcmc.py:212 multiplies the series by 0.0).
-      Ages older than the CSV coverage take the constant fill recorded in SURVEY.md
-      §8a-a15 (1e-10 for the CFC/SF6 family).  Stored compactly as (fill, tail).
+      The shipped input series age_ens_runs_mcmc/C_in_dict.pk (written by
+      age_modeling_mcmc.prep.py:165-219; read at run_age_mcmc.py:46), all 6 tracers.
+      Both pickles are read WITHOUT unpickling: tools/pickle_extract.py walks their
+      opcode stream symbolically (nothing is imported or called) and decodes the float64
+      block buffers and int64 indices with numpy.frombuffer.
+      Stored age-first (age k = np.flip(C_in_dict[t].values)[k], the flip that
+      convolution_integral_utils.py:336 applies) and compactly, bit for bit: every series
+      is a constant fill for all ages >= its tail length, so the file holds the fill value
+      and the ages before it.  tests/test_package_data_cpu.py re-extracts the pickle and
+      checks the reconstruction bitwise.
 """
 import json
 import os
@@ -30,11 +30,14 @@ import zipfile
 
 import numpy as np
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from pickle_extract import read_frame_dict  # noqa: E402
+
 REF = os.environ.get("NGRTD_REFERENCE", "/root/reference")
 HERE = os.path.dirname(os.path.abspath(__file__))
 OUT = os.path.join(HERE, "..", "noblegas_rtd_mcmc_amd", "data")
 N_FULL = 25256          # len(C_in_dict[...])
-SAMPLE_YEAR = 2021      # age 0 == 2021 (CSV coverage ends there)
+SAMPLE_YEAR = 2021      # age 0 == 2021 (prep.py:163)
 
 
 def read_xlsx_sheet1(path):
@@ -75,45 +78,35 @@ def field_data():
         "obs": wells,
         "err_percent": {"He": 1.5, "Ne": 1.5, "Ar": 2.5, "Kr": 3.1, "Xe": 15.1},   # noble_gas_mcmc.py:107
         "well_elev": {"PLM1": 2786.889893, "PLM6": 2759.569824, "PLM7": 2782.550049},  # :80-82
-        # MAP tracer observations map_dict[tracer].loc[well] as recorded in SURVEY.md §8d c3
-        # (map_dict.pk is a pickle and is not loaded here).
-        "map_obs_PLM1": {"CFC12": 36.3828, "SF6": 1.24528, "H3": 4.86877, "He4_ter": 8.82174e-9},
+        # MAP tracer observations map_dict[tracer].loc[well] (run_age_mcmc.py:44,128)
+        "map_obs": map_obs(),
+        "map_source": "age_ens_runs_mcmc/map_dict.pk (no-code read, tools/pickle_extract.py)",
     }
 
 
-def series():
-    import csv
-    years, cols = [], {"CFC11": [], "CFC12": [], "CFC113": [], "SF6": []}
-    with open(os.path.join(REF, "Input_Series", "NOAA_cfc_sf6", "cfc_sf6_atmhist_1765-2021.csv")) as f:
-        for rec in csv.DictReader(f):
-            years.append(int(rec["year"]))
-            for k, c in (("CFC11", "cfc11_ppt"), ("CFC12", "cfc12_ppt"), ("CFC113", "cfc113_ppt"), ("SF6", "sf6_ppt")):
-                cols[k].append(float(rec[c]))
-    years = np.array(years)
+def map_obs():
+    """{tracer column: {well: value}} of every DataFrame in map_dict.pk."""
     out = {}
-    for k, v in cols.items():
-        v = np.array(v)
-        ages = SAMPLE_YEAR - years          # 256..0
-        tail = np.zeros(ages.max() + 1)
-        tail[ages] = v
-        tail[tail == 0.0] = 1e-10           # constant-fill convention of C_in_dict
-        out[k] = (1e-10, tail)
-    # tritium: annual means of the Crested Butte quadrangle cell
-    h3 = {}
-    with open(os.path.join(REF, "Input_Series", "Tritium", "TritiumInQuadrangeles_Jurgens2018.csv")) as f:
-        for rec in csv.DictReader(f):
-            y, v = rec["Year"], rec["39-37,110-105"]
-            if y and v:
-                h3.setdefault(int(float(y)), []).append(float(v))
-    yrs = sorted(h3)
-    ann = {y: float(np.mean(h3[y])) for y in yrs}
-    lam = -np.log(0.5) / 12.34
-    for y in range(yrs[-1] + 1, SAMPLE_YEAR + 1):
-        ann[y] = ann[yrs[-1]] * np.exp(-lam * (y - yrs[-1]))
-    first = min(ann)
-    tail = np.array([ann[SAMPLE_YEAR - a] for a in range(SAMPLE_YEAR - first + 1)])
-    out["H3"] = (3.3273, tail)
-    out["He4_ter"] = (0.0, np.zeros(1))
+    for _key, fr in read_frame_dict(os.path.join(REF, "age_ens_runs_mcmc", "map_dict.pk")).items():
+        for j, col in enumerate(fr["columns"]):
+            out[col] = {str(w): float(fr["values"][j][i]) for i, w in enumerate(fr["index"])}
+    return out
+
+
+def series():
+    """{tracer: (fill, tail)} of C_in_dict.pk, age-first, bit-exact."""
+    out = {}
+    for key, fr in read_frame_dict(os.path.join(REF, "age_ens_runs_mcmc", "C_in_dict.pk")).items():
+        if fr["values"].shape[0] != 1:
+            raise ValueError("%s: expected one column, got %r" % (key, fr["columns"]))
+        v = np.flip(fr["values"][0]).copy()            # age 0 first (:336)
+        idx = np.flip(fr["index"])
+        if len(v) != N_FULL or not np.array_equal(idx, np.arange(N_FULL)):
+            raise ValueError("%s: index is not 25255..0" % key)
+        fill = v[-1]
+        diff = np.nonzero(v != fill)[0]
+        k0 = int(diff.max()) + 1 if len(diff) else 0
+        out[key] = (fill, v[:k0], fr["columns"][0])
     return out
 
 
@@ -124,9 +117,10 @@ def main():
     s = series()
     arrays = {"N_full": np.array(N_FULL), "sample_year": np.array(SAMPLE_YEAR),
               "tracers": np.array(sorted(s))}
-    for k, (fill, tail) in s.items():
+    for k, (fill, tail, col) in s.items():
         arrays[k + "_fill"] = np.array(fill)
         arrays[k + "_tail"] = np.asarray(tail, dtype=np.float64)
+        arrays[k + "_column"] = np.array(col)
     np.savez_compressed(os.path.join(OUT, "atmos_series.npz"), **arrays)
     print("wrote", OUT, file=sys.stderr)
 
