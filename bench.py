@@ -1,16 +1,23 @@
 #!/usr/bin/env python3
 """Headline benchmark: joint CE + RTD-convolution log-likelihood evaluations per second.
 
-Workload (BASELINE.json configs[3]), per GPU: 2048 walkers x 64 wells x
-(CE over 5 gases + RTD convolution of 5 tracers over a 1200-year input series,
-exponential RTD) in float64.  One step = one full log-prob of the rank's walker block
-(theta resident in HBM) + an RCCL all-gather of the per-block log-prob vector (N > 1).
-Scaling is weak: every rank owns its own 2048-walker block (c5).
+Workload (BASELINE.json configs[3]): 2048 walkers x 64 wells x (CE over
+5 gases + RTD convolution of 5 tracers over a 1200-year input series, exponential RTD)
+in float64.  One step = one full batched log-prob of the rank's walker block (theta
+resident in HBM) + ONE all-gather of the per-block log-prob vector (N > 1), the loop of
+distributed.LogpStepLoop.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling weak|strong]
+                    [--mod-type1 exponential|exp_pist_flow|piston|dispersion] [--mod-type2 piston|...]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
-Rank 0 prints ONE JSON line; see DESIGN.md 'Measurement' for the roofline accounting.
+--scaling weak (default): every rank owns 2048 walkers of a (2048 N)-walker ensemble.
+--scaling strong (c5): ONE 2048-walker ensemble is sharded, 2048 / N walkers per rank.
+Either way the ensemble is drawn once from the same seed and each rank takes its
+contiguous block (workloads.shard_walkers).  --mod-type1/2 select the other RTD models the
+reference published runs of.
+
+Rank 0 prints ONE JSON line; see DESIGN.md §6 for the roofline accounting.
 """
 import argparse
 import json
@@ -24,11 +31,14 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 METRIC = "log-likelihood evals/sec (CE + RTD-conv), 2048 walkers, 1/2/4/8 MI355X"
-FP64_MFMA_PEAK = 78.6e12     # dense FP64 matrix peak, 256 CU x 4 SIMD x 32 FLOP/clk x 2.4 GHz
-                             # (tools/ubench_fp64.hip measures 78.3: profiles/r01_ubench_fp64.txt)
-FP64_VALU_PEAK = 38.3e12     # v_fma_f64 throughput measured by tools/ubench_fp64.hip (profiles/r01_ubench_fp64.txt)
+FP64_PEAK = 78.6e12          # MI355X FP64 peak (vector and matrix, AMD spec: 256 CU x 128 FLOP/clk x 2.4 GHz)
+FP64_VALU_MEASURED = 38.3e12 # v_fma_f64 throughput measured by tools/ubench_fp64.hip (profiles/r01_ubench_fp64.txt)
+FP64_MFMA_MEASURED = 78.3e12 # v_mfma_f64_16x16x4f64, same microbenchmark
 HBM_PEAK = 8.0e12            # MI355X_MICROARCH.md chip table
-PMC_SUMMARY = "r01_pmc.json"
+PMC_SUMMARIES = ("r02_pmc.json", "r01_pmc.json")   # newest first (tools/gpu_profile.sh)
+
+# the RTD parameters each model adds (run_age_mcmc.py:145-178)
+MODEL_PARS = {"exponential": (), "piston": (), "exp_pist_flow": ("eta",), "dispersion": ("D",)}
 
 
 def parse():
@@ -36,44 +46,105 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--walkers", type=int, default=2048)
+    ap.add_argument("--walkers", type=int, default=2048, help="walkers per GPU (weak) or in total (strong)")
     ap.add_argument("--wells", type=int, default=64)
     ap.add_argument("--ages", type=int, default=1200)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline budget")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak")
+    ap.add_argument("--mod-type1", default="exponential", choices=sorted(MODEL_PARS))
+    ap.add_argument("--mod-type2", default=None, choices=sorted(MODEL_PARS))
+    ap.add_argument("--cpu-seconds", type=float, default=16.0, help="bounded CPU-baseline budget (both variants)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-overlap", action="store_true", help="N > 1: all-gather on the compute stream")
+    ap.add_argument("--no-exact", action="store_true", help="skip the exact-path (no surrogate) line")
     ap.add_argument("--event-every", type=int, default=8,
-                    help="bracket the kernels of every k-th timed step with HIP events (kernel roofline)")
+                    help="bracket the kernels of every k-th timed step with HIP events (multi-kernel / N > 1)")
     return ap.parse_args()
 
 
-def cpu_baseline(spec, theta, budget_s, workers):
-    """The oracle (reference-faithful NumPy per-walker loop) on the host cores, on a
-    bounded sample of walkers of the same workload."""
-    import multiprocessing as mp
-    from oracle import models as om
-    t0 = time.perf_counter()
-    om.log_prob(spec, theta, walkers=[0])                   # one walker: size the sample
-    per = time.perf_counter() - t0
-    n = max(workers, int(budget_s / max(per, 1e-6)) * workers)
-    idx = [i % theta.shape[2] for i in range(n)]
-    chunks = [idx[i::workers] for i in range(workers)]
-    ctx = mp.get_context("fork")
-    t0 = time.perf_counter()
-    with ctx.Pool(workers) as pool:
-        pool.starmap(_cpu_chunk, [(spec, theta, c) for c in chunks])
-    dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "evals/s", "cores": workers, "kind": "port",
-            "sample": "%d walker log-probs of the same workload (oracle/models.py per-walker loop: "
-                      "reference-faithful NumPy CE + convolve per (well, tracer)), %d processes, %.1f s"
-                      % (n, workers, dt)}
+def model_spec(args):
+    from noblegas_rtd_mcmc_amd import workloads
+    pn = ["tau1"]
+    m1, m2 = args.mod_type1, args.mod_type2
+    if m2:
+        pn += ["tau2", "f1"]
+    pn += [p + "1" for p in MODEL_PARS[m1]]
+    if m2:
+        pn += [p + "2" for p in MODEL_PARS[m2]]
+    return workloads.c4_spec(L=args.wells, N=args.ages, mod_type1=m1, mod_type2=m2, par_names=tuple(pn))
 
 
-def _cpu_chunk(spec, theta, walkers):
+# ------------------------------------------------------------------ CPU baseline
+def cpu_share():
+    """CPUs this job may use: the affinity mask, capped by OMP_NUM_THREADS (the GPU box
+    grants a 16-CPU share of a larger machine and says so there; os.cpu_count() reports
+    the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cap = os.environ.get("OMP_NUM_THREADS")
+    if cap and cap.isdigit() and int(cap) > 0:
+        n = min(n, int(cap))
+    return max(1, n)
+
+
+def _cpu_loop_chunk(spec, theta, walkers):
     from oracle import models as om
     return om.log_prob(spec, theta, walkers=walkers)
 
 
+def _cpu_vec_chunk(spec, theta, reps):
+    from oracle.vectorized import log_prob_vec
+    for _ in range(reps):
+        log_prob_vec(spec, theta)
+    return reps
+
+
+def cpu_baseline(spec, theta, budget_s, workers):
+    """The oracle on the host cores, on a bounded sample of the same workload: (1) the
+    reference-faithful per-walker loop (oracle/models.py: NumPy CE + one convolve per
+    (well, tracer), as ForwardMod.perform does), (2) the vectorised NumPy variant
+    (oracle/vectorized.py: all walkers of a well at once).  One process per CPU."""
+    import multiprocessing as mp
+    from oracle import models as om
+    from oracle.vectorized import log_prob_vec
+    os.environ.setdefault("OPENBLAS_NUM_THREADS", "1")
+    ctx = mp.get_context("fork")
+    W = theta.shape[2]
+    # (1) per-walker loop
+    t0 = time.perf_counter()
+    om.log_prob(spec, theta, walkers=[0])
+    per = time.perf_counter() - t0
+    n = max(workers, int(0.5 * budget_s / max(per, 1e-6)) * workers)
+    idx = [i % W for i in range(n)]
+    chunks = [idx[i::workers] for i in range(workers)]
+    t0 = time.perf_counter()
+    with ctx.Pool(workers) as pool:
+        pool.starmap(_cpu_loop_chunk, [(spec, theta, c) for c in chunks])
+    dt_loop = time.perf_counter() - t0
+    loop_rate = n / dt_loop
+    # (2) vectorised: 64-walker slices per call
+    Wc = min(64, W)
+    sl = np.ascontiguousarray(theta[:, :, :Wc])
+    t0 = time.perf_counter()
+    log_prob_vec(spec, sl)
+    per = time.perf_counter() - t0
+    reps = max(1, int(0.5 * budget_s / max(per, 1e-6)))
+    t0 = time.perf_counter()
+    with ctx.Pool(workers) as pool:
+        pool.starmap(_cpu_vec_chunk, [(spec, sl, reps)] * workers)
+    dt_vec = time.perf_counter() - t0
+    vec_rate = workers * reps * Wc / dt_vec
+    return {"value": loop_rate, "unit": "evals/s", "cores": workers, "kind": "port",
+            "sample": ("%d walker log-probs of the same workload through the reference-faithful per-walker "
+                       "loop (oracle/models.py: NumPy CE + one convolve per (well, tracer)), %d processes, "
+                       "%.1f s.  The oracle skips the reference's per-call DataFrame copies and object "
+                       "construction (ForwardMod.perform, run_age_mcmc_utils.py:94), so it is faster than the "
+                       "reference itself" % (n, workers, dt_loop)),
+            "variants": {"per_walker_loop": loop_rate,
+                         "vectorised_numpy": vec_rate,
+                         "vectorised_sample": "%d calls of %d walkers (oracle/vectorized.py), %d processes, %.1f s"
+                                              % (reps * workers, Wc, workers, dt_vec)},
+            "cpu_count_machine": os.cpu_count()}
+
+
+# ------------------------------------------------------------------ main
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -82,6 +153,7 @@ def main():
     import torch
     import torch.distributed as dist
     from noblegas_rtd_mcmc_amd import workloads
+    from noblegas_rtd_mcmc_amd.distributed import LogpStepLoop
     from noblegas_rtd_mcmc_amd.engine import LogProb
 
     torch.cuda.set_device(local)
@@ -89,51 +161,30 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    W = args.walkers
-    spec = workloads.c4_spec(L=args.wells, N=args.ages)
-    # this rank's walker block of the global ensemble (weak scaling: W per GPU)
-    theta_h = workloads.sample_prior(spec, W, np.random.default_rng(34568 + rank))
+    W_total = args.walkers * world if args.scaling == "weak" else args.walkers
+    spec = model_spec(args)
+    # ONE ensemble for the whole job (same seed at every N); each rank takes its block
+    lo, hi = workloads.shard_walkers(W_total, rank, world)
+    theta_full = workloads.sample_prior(spec, W_total, np.random.default_rng(34568))
+    theta_h = np.ascontiguousarray(theta_full[:, :, lo:hi])
+    del theta_full
+    Wb = hi - lo
     theta = torch.from_numpy(theta_h).to(dev)
-    lp = LogProb(spec, max_walkers=W, device=local)
-    # N > 1: the all-gather of step i runs on a communication stream while step i+1's
-    # kernel runs (double-buffered logp / gather buffers); the compute stream reuses a
-    # buffer only after the gather that read it has finished.  --no-overlap serialises.
-    outs = [torch.empty(W, dtype=torch.float64, device=dev) for _ in range(2)]
-    gathered = [torch.empty(W * world, dtype=torch.float64, device=dev) for _ in range(2)]
-    overlap = world > 1 and not args.no_overlap
-    comm = torch.cuda.Stream(device=dev) if overlap else None
-    ready = [torch.cuda.Event() for _ in range(2)]
-    freed = [torch.cuda.Event() for _ in range(2)]
-    issued = [False, False]
-    nstep = [0]
-
-    def step():
-        k = nstep[0] % 2
-        nstep[0] += 1
-        o = outs[k]
-        if not overlap:
-            lp(theta, out=o)
-            if world > 1:
-                dist.all_gather_into_tensor(gathered[k], o)
-            return
-        cur = torch.cuda.current_stream(dev)
-        if issued[k]:
-            cur.wait_event(freed[k])              # the gather that read outs[k] is done
-        lp(theta, out=o)
-        ready[k].record(cur)
-        comm.wait_event(ready[k])
-        with torch.cuda.stream(comm):
-            dist.all_gather_into_tensor(gathered[k], o)
-            freed[k].record(comm)
-        issued[k] = True
-    out = outs[0]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    lp = LogProb(spec, max_walkers=Wb, device=local)     # plan: tables, surrogate fit + validation, c0 table
+    torch.cuda.synchronize()
+    plan_build_ms = (time.perf_counter() - t0) * 1e3
+    loop = LogpStepLoop(None, W_total, dev)
+    fast = lp.bind(theta, loop.out)
+    loop.evaluate = lambda out: fast()
 
     for _ in range(args.warmup):
-        step()
+        loop.step()
     # which kernels does one step launch? (one profiled step after the warm-up)
     lp.ctx.set_profiling(True)
     lp.kernel_stats(reset=True)
-    step()
+    loop.step()
     lp.ctx.set_profiling(False)
     kinds = {k for k, v in lp.kernel_stats(reset=True).items() if v[1]}
     single_kernel = kinds == {"fused"}
@@ -143,21 +194,22 @@ def main():
     torch.cuda.synchronize()
     # timed region.  Kernel time for the roofline, measured live with HIP events on the
     # launch stream (torch's current stream, which the plan enqueues on):
-    #  * N = 1: one event pair around the whole region; every launch in it is the
-    #    single-launch log-prob kernel, so region / steps is its average duration
-    #    (back-to-back, as rocprofv3 --kernel-trace sees it);
-    #  * N > 1: the all-gather shares the stream, so the kernels of every k-th step are
-    #    bracketed by their own event pair (read back after the region, no host syncs).
+    #  * N = 1 and one kernel per step: one event pair around the whole region, so
+    #    region / steps is that kernel's average duration back to back (as rocprofv3
+    #    --kernel-trace sees it);
+    #  * otherwise the kernels of every k-th step get their own event pairs (read back
+    #    after the region, no host syncs inside it).
     lp.kernel_stats(reset=True)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
+    per_step_events = world > 1 or not single_kernel
     t0 = time.perf_counter()
     ev0.record()
     for i in range(args.steps):
-        sample = (world > 1 or not single_kernel) and i % args.event_every == 0
+        sample = per_step_events and i % args.event_every == 0
         if sample:
             lp.ctx.set_profiling(True)
-        step()
+        loop.step()
         if sample:
             lp.ctx.set_profiling(False)
     ev1.record()
@@ -166,105 +218,152 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    ks = lp.kernel_stats(reset=True)
-    if world == 1 and single_kernel:
-        ks = dict(ks)
+    ks = dict(lp.kernel_stats(reset=True))
+    if not per_step_events:
         ks["fused"] = (ev0.elapsed_time(ev1), args.steps)
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    assert torch.isfinite(out).any()
-    # PCIe-inclusive rate: theta handed over as host memory (staged H2D per call, results
-    # copied back) -- reported beside `value`, never as it (DESIGN.md 'Measurement')
-    host_staged = None
-    if rank == 0:
-        hs = max(5, args.steps // 20)
-        lp(theta_h, soa=True)
-        t1 = time.perf_counter()
-        for _ in range(hs):
-            lp(theta_h, soa=True)
-        host_staged = W * hs / (time.perf_counter() - t1)
+    assert torch.isfinite(loop.ensemble()).any()
 
     if rank == 0:
-        info = lp.info(W)
-        U = spec.n_wells * W
-        C = info["channels"]
-        N = spec.rtd.n_ages
-        # dominant kernel: the single-launch log-prob kernel when the plan uses it
-        kname = "fused" if ks["fused"][1] else "rtd"
-        kms = ks[kname][0] / max(ks[kname][1], 1)
-        kfull = {"fused": "logp_fused_kernel", "rtd": "rtd_exp_mfma_kernel" if info["mfma_rows"] else "rtd_conc_kernel"}[kname]
-        # committed PMC summary of the same command (tools/gpu_profile.sh -> tools/profile_summary.py)
-        pmc = {}
-        path = os.environ.get("NGRTD_PMC_SUMMARY") or os.path.join(REPO, "profiles", PMC_SUMMARY)
+        line = report(args, spec, lp, ks, dt, world, W_total, Wb, plan_build_ms, theta, theta_h)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def pmc_summary(kfull):
+    """Committed PMC summary of the same command (tools/gpu_profile.sh -> tools/profile_summary.py)."""
+    for name in PMC_SUMMARIES:
+        path = os.environ.get("NGRTD_PMC_SUMMARY") or os.path.join(REPO, "profiles", name)
         if os.path.exists(path):
             with open(path) as f:
                 for k, e in json.load(f).items():
                     if kfull in k:
-                        pmc = e
-        traffic = pmc.get("hbm_bytes_per_launch")   # FETCH_SIZE x 2 (calibrated) + WRITE_SIZE
-        if info.get("surrogate"):
-            # FP64 work of the launch: PMC-counted FP64 FLOPs per (walker, well) unit of this
-            # kernel (SQ_INSTS_VALU_FLOPS_FP64 x 64 lanes, fma = 2) x units
-            fpu = pmc.get("fp64_flop_per_unit")
-            flops = fpu * U if fpu else None
-            flop_src = "PMC fp64_flop_per_unit %s x %d units (%s)" % (
-                "%.1f" % fpu if fpu else "n/a", U, os.path.relpath(path, REPO))
-        else:
-            # exact matrix-core path: one FMA (2 FLOP) per (unit, channel, age >= 1)
-            flops = 2.0 * U * C * (N - 1)
-            flop_src = "2 * units * channels * (N - 1) (matrix-core Horner)"
-        achieved = flops / (kms * 1e-3) if flops else None
-        evals_per_s_kernel = W / (kms * 1e-3)
-        # algorithmic HBM bytes of the same launch: every theta row read once + logp out
-        hbm_bytes = U * 8.0 * len(spec.roles) + (W * 8.0 if kname == "fused" else U * 8.0 * len(spec.rtd.tracers))
-        evals = W * world * args.steps
-        line = {
-            "metric": METRIC,
-            "value": evals / dt,
-            "unit": "evals/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": dt * 1e3 / args.steps,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic",
-            "config": {"workload": "c4 joint CE+RTD log-prob: %d walkers/GPU x %d wells x (5 gases CE + 5 tracers "
-                                   "RTD exponential, N=%d ages)" % (W, args.wells, N),
-                       "walkers_per_gpu": W, "wells": args.wells, "gases": 5, "tracers": 5, "ages": N,
-                       "parallelism": ("walker blocks per GPU + RCCL all-gather of logp" +
-                                       (" (overlapped with the next step's kernel)" if overlap else ""))
-                                      if world > 1 else "single GPU"},
-            "roofline": {"bound": "mfma", "achieved": achieved / 1e12 if achieved else None,
-                         "peak": FP64_MFMA_PEAK / 1e12, "unit": "TFLOP/s",
-                         "frac": achieved / FP64_MFMA_PEAK if achieved else None, "traffic": traffic,
-                         "kernel": kfull, "kernel_ms": kms, "flop_per_launch": flops, "flop_source": flop_src,
-                         "pipe": "FP64 (gfx950 FP64 VALU and MFMA share one pipe; the surrogate path is VALU)",
-                         "fp64_valu_peak_measured": FP64_VALU_PEAK / 1e12,
-                         "frac_of_fp64_valu_peak": achieved / FP64_VALU_PEAK if achieved else None,
-                         # SURVEY.md §8d froze the REFERENCE algorithm's count (2 exp per age at
-                         # X = 20, 167 FLOP per walker-well-age + 850 CE): informational only --
-                         # the surrogate/Horner rewrite does not execute that work
-                         "survey_8d_flop_per_eval": args.wells * (N * 167.0 + 850.0),
-                         "survey_8d_equivalent_TFLOPs": evals_per_s_kernel * args.wells * (N * 167.0 + 850.0) / 1e12,
-                         "hbm": {"algorithmic_bytes": hbm_bytes, "achieved_GBps": hbm_bytes / (kms * 1e-3) / 1e9,
-                                 "peak_GBps": HBM_PEAK / 1e9, "frac": hbm_bytes / (kms * 1e-3) / HBM_PEAK}},
-            "host_staged_value": host_staged,
-            "kernels_ms": {k: v[0] / max(v[1], 1) for k, v in ks.items()},
-            "geometry": info,
-        }
-        if not args.no_cpu_baseline and world == 1:
-            workers = min(16, os.cpu_count() or 1)
-            line["cpu_baseline"] = cpu_baseline(spec, theta_h, args.cpu_seconds, workers)
-        else:
-            line["cpu_baseline"] = None
-        print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+                        return e, os.path.relpath(path, REPO)
+    return {}, None
+
+
+def report(args, spec, lp, ks, dt, world, W_total, Wb, plan_build_ms, theta, theta_h):
+    import torch
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+    info = lp.info(Wb)
+    U = spec.n_wells * Wb
+    C = info["channels"]
+    N = spec.rtd.n_ages
+    kname = "fused" if ks["fused"][1] else "rtd"
+    kms = ks[kname][0] / max(ks[kname][1], 1)
+    kfull = {"fused": "logp_fused_kernel", "rtd": "rtd_exp_mfma_kernel" if info["mfma_rows"] else "rtd_conc_kernel"}[kname]
+    pmc, pmc_path = pmc_summary(kfull)
+    traffic = pmc.get("hbm_bytes_per_launch")        # FETCH_SIZE x 2 (calibrated) + WRITE_SIZE
+    exp_single = spec.rtd.mod_type1 == "exponential" and not spec.rtd.mod_type2
+    if info.get("surrogate") and pmc.get("fp64_flop_per_unit"):
+        # FP64 work of the launch: PMC-counted FP64 FLOPs per (walker, well) unit of this
+        # kernel (SQ_INSTS_VALU_FLOPS_FP64 x 64 lanes, fma = 2) x units (DESIGN.md §6)
+        fpu = pmc["fp64_flop_per_unit"]
+        flops = fpu * U
+        flop_src = "PMC fp64_flop_per_unit %.1f x %d units (%s)" % (fpu, U, pmc_path)
+        bound = "fp64_valu"
+    else:
+        # exact path: one FMA (2 FLOP) per (unit, channel, age >= 1) per geometric component
+        ncomp = sum(1 for m in (spec.rtd.mod_type1, spec.rtd.mod_type2) if m in ("exponential", "exp_pist_flow"))
+        flops = 2.0 * U * C * (N - 1) * max(ncomp, 1)
+        flop_src = "algorithmic: 2 x units x channels x (N - 1) x %d geometric component(s)" % max(ncomp, 1)
+        bound = "fp64_mfma" if info["mfma_rows"] else "fp64_valu"
+    achieved = flops / (kms * 1e-3)
+    hbm_bytes = U * 8.0 * len(spec.roles) + (Wb * 8.0 if kname == "fused" else U * 8.0 * len(spec.rtd.tracers))
+    evals = W_total * args.steps
+    model = spec.rtd.mod_type1 + ("-" + spec.rtd.mod_type2 if spec.rtd.mod_type2 else "")
+    line = {
+        "metric": METRIC,
+        "value": evals / dt,
+        "unit": "evals/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": args.scaling,
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded c4 ensemble; series = shipped C_in_dict.pk x lognormal noise)",
+        "config": {"workload": "c4 joint CE+RTD log-prob: %d walkers (%d/GPU) x %d wells x (5 gases CE + 5 tracers "
+                               "RTD %s, N=%d ages)" % (W_total, Wb, args.wells, model, N),
+                   "walkers_total": W_total, "walkers_per_gpu": Wb, "wells": args.wells, "gases": 5, "tracers": 5,
+                   "ages": N, "rtd_model": model,
+                   "rtd_sums": ("piecewise-Chebyshev surrogate of the exponential channel sums, fitted and "
+                                "validated per plan (max rel err %.2g <= 5e-14); uncovered tau take the exact "
+                                "matrix-core path" % info["surrogate_max_rel_err"]) if info.get("surrogate")
+                               else "exact (no surrogate)",
+                   "parallelism": ("%d walker blocks + RCCL all-gather of logp (%s scaling)" % (world, args.scaling))
+                                  if world > 1 else "single GPU"},
+        "roofline": {"bound": bound, "achieved": achieved / 1e12, "peak": FP64_PEAK / 1e12, "unit": "TFLOP/s",
+                     "frac": achieved / FP64_PEAK, "traffic": traffic, "kernel": kfull, "kernel_ms": kms,
+                     "flop_per_launch": flops, "flop_source": flop_src,
+                     "peak_source": "MI355X FP64 spec (vector = matrix = 78.6 TFLOP/s)",
+                     "frac_of_measured_fp64_valu": achieved / FP64_VALU_MEASURED if bound == "fp64_valu" else None,
+                     "hbm": {"algorithmic_bytes": hbm_bytes, "achieved_GBps": hbm_bytes / (kms * 1e-3) / 1e9,
+                             "peak_GBps": HBM_PEAK / 1e9, "frac": hbm_bytes / (kms * 1e-3) / HBM_PEAK}},
+        "plan_build_ms": plan_build_ms,
+        "kernels_ms": {k: v[0] / max(v[1], 1) for k, v in ks.items()},
+        "geometry": info,
+    }
+    if world == 1 and exp_single and info.get("surrogate") and not args.no_exact:
+        line.update(exact_line(args, spec, theta, Wb, C, N))
+    # PCIe-inclusive rate: theta handed over as host memory (staged H2D per call, results
+    # copied back) -- reported beside `value`, never as it (DESIGN.md §6)
+    hs = max(5, args.steps // 20)
+    lp(theta_h, soa=True)
+    t1 = time.perf_counter()
+    for _ in range(hs):
+        lp(theta_h, soa=True)
+    line["host_staged_value"] = Wb * hs / (time.perf_counter() - t1)
+    torch.cuda.synchronize()
+    if not args.no_cpu_baseline and world == 1:
+        line["cpu_baseline"] = cpu_baseline(spec, theta_h, args.cpu_seconds, cpu_share())
+    else:
+        line["cpu_baseline"] = None
+    return line
+
+
+def exact_line(args, spec, theta, Wb, C, N):
+    """The same step with the surrogate switched off (NGRTD_EXACT_RTD): every unit sums
+    its channels over all N ages on the matrix cores."""
+    import dataclasses
+    import torch
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+    sx = dataclasses.replace(spec, exact_rtd=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    lx = LogProb(sx, max_walkers=Wb, device=theta.device.index)
+    torch.cuda.synchronize()
+    build_ms = (time.perf_counter() - t0) * 1e3
+    out = torch.empty(Wb, dtype=torch.float64, device=theta.device)
+    run = lx.bind(theta, out)
+    for _ in range(max(3, args.warmup // 4)):
+        run()
+    n = max(10, args.steps // 4)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(n):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / n
+    U = spec.n_wells * Wb
+    flops = 2.0 * U * C * (N - 1)
+    info = lx.info(Wb)
+    lx.close()
+    return {"exact_value": Wb / (ms * 1e-3),
+            "exact_roofline": {"bound": "fp64_mfma", "achieved": flops / (ms * 1e-3) / 1e12,
+                               "peak": FP64_PEAK / 1e12, "unit": "TFLOP/s",
+                               "frac": flops / (ms * 1e-3) / FP64_PEAK, "kernel": "logp_fused_kernel (exact)",
+                               "kernel_ms": ms, "flop_per_launch": flops,
+                               "flop_source": "algorithmic: 2 x units x channels x (N - 1), v_mfma_f64_16x16x4 Horner",
+                               "surrogate": info.get("surrogate"), "plan_build_ms": build_ms}}
 
 
 if __name__ == "__main__":

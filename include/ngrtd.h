@@ -220,7 +220,10 @@ typedef struct {
     int32_t is_sf6;         /* cout *= (1 + lamsf6) when the lamsf6 role is present (:160-161) */
 } ngrtd_tracer_desc;
 
-enum ngrtd_flags { NGRTD_WANT_LIKE = 1, NGRTD_WANT_PRIOR = 2, NGRTD_WANT_JACOBIAN = 4 };
+/* NGRTD_EXACT_RTD: never use the plan-time surrogate of the exponential channel sums;
+ * every unit evaluates them exactly (matrix-core Horner over all N ages).  For A/B and
+ * for the exact-path rate bench.py reports beside the headline. */
+enum ngrtd_flags { NGRTD_WANT_LIKE = 1, NGRTD_WANT_PRIOR = 2, NGRTD_WANT_JACOBIAN = 4, NGRTD_EXACT_RTD = 8 };
 
 typedef struct {
     int32_t n_wells;                        /* L */

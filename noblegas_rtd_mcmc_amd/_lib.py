@@ -24,7 +24,7 @@ HE_OUT = ("He4_eq", "He4_atm", "He4_ter", "He4_del", "He3_tu")       # enum ngrt
 CFC_SPECIES = {11: 0, 12: 1, 113: 2, "SF6": 3}                      # enum ngrtd_cfc_species
 CFC_WHAT = {"equil_air": 0, "equil_aq": 1, "ce_exc": 2, "solubility": 3, "vapor_pressure_atm": 4,
             "lapse_rate_atm": 5}
-WANT_LIKE, WANT_PRIOR, WANT_JACOBIAN = 1, 2, 4
+WANT_LIKE, WANT_PRIOR, WANT_JACOBIAN, EXACT_RTD = 1, 2, 4, 8
 
 _dp = C.POINTER(C.c_double)
 _i32p = C.POINTER(C.c_int32)
@@ -167,8 +167,15 @@ class Context:
             msg = self.lib.ngrtd_last_error(self.h)
             raise NgrtdError("%s failed (status %d): %s" % (what, status, msg.decode() if msg else ""))
 
+    _stream = None
+
     def set_stream(self, stream_handle):
-        self.check(self.lib.ngrtd_set_stream(self.h, C.c_void_p(int(stream_handle))), "ngrtd_set_stream")
+        """Enqueue on this hipStream_t from now on (skipped when it is already the ctx stream)."""
+        h = int(stream_handle)
+        if h == self._stream:
+            return
+        self.check(self.lib.ngrtd_set_stream(self.h, C.c_void_p(h)), "ngrtd_set_stream")
+        self._stream = h
 
     def synchronize(self):
         self.check(self.lib.ngrtd_synchronize(self.h), "ngrtd_synchronize")

@@ -1166,7 +1166,8 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
         a.conc = p->conc.d();
         set_frag(a, p->table);
         a.cheb = nullptr;
-        if (a.mod[0] == MOD_EXP && a.mod[1] == MOD_NONE && !any_lamw && p->table.C <= 5 && p->dtp >= 0.0) {
+        if (a.mod[0] == MOD_EXP && a.mod[1] == MOD_NONE && !any_lamw && p->table.C <= 5 && p->dtp >= 0.0 &&
+            !(d->flags & NGRTD_EXACT_RTD)) {
             NG_CHECK(cheb_prepare(ctx, p->table, (1.0 + p->dtp) - p->tp0));
             if (p->table.cheb_ok) a.cheb = p->table.cheb.d();
         }

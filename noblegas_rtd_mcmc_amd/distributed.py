@@ -22,6 +22,46 @@ from .sampler import pymc3_tune
 from .workloads import shard_walkers
 
 
+class LogpStepLoop:
+    """The per-step work of ``bench.py`` on one rank (and of any caller that shards a
+    walker ensemble): the batched log-prob of the rank's walker block, then -- world > 1
+    -- ONE all-gather of the per-block log-prob vectors into the ensemble vector.
+
+    ``evaluate(out)`` writes the block's log-probs into ``out`` (a contiguous prefix of a
+    block buffer padded to the largest block, so uneven shards gather with one collective).
+    Both the block buffer and the gathered vector are allocated once.  ``step()`` returns
+    the gathered [per * world] vector; ``ensemble()`` the unpadded [W_total] view.
+
+    The same function runs under torchrun (RCCL) and in the world-size-2 gloo tests
+    (tests/test_distributed_cpu.py), so the bench's multi-GPU step has no untested branch.
+    """
+
+    def __init__(self, evaluate, W_total, device, dtype=torch.float64, group=None):
+        self.evaluate = evaluate
+        self.group = group
+        self.W_total = int(W_total)
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.lo, self.hi = shard_walkers(self.W_total, self.rank, self.world)
+        self.per = (self.W_total + self.world - 1) // self.world
+        self.buf = torch.full((self.per,), float("nan"), dtype=dtype, device=device)
+        self.out = self.buf[: self.hi - self.lo]
+        self.gathered = (torch.empty(self.per * self.world, dtype=dtype, device=device)
+                         if self.world > 1 else self.buf)
+
+    def step(self):
+        self.evaluate(self.out)
+        if self.world > 1:
+            dist.all_gather_into_tensor(self.gathered, self.buf, group=self.group)
+        return self.gathered
+
+    def ensemble(self):
+        if self.world == 1:
+            return self.out
+        return torch.cat([self.gathered[r * self.per: r * self.per + (lambda s: s[1] - s[0])(
+            shard_walkers(self.W_total, r, self.world))] for r in range(self.world)])
+
+
 class ShardedLogProb:
     """Evaluate a rank's walker block and all-gather the ensemble log-prob."""
 

@@ -41,7 +41,7 @@ class LogProb:
         for i in range(_lib.ROLE_COUNT):
             d.role_index[i] = ri[i]
         d.flags = ((_lib.WANT_LIKE if spec.include_like else 0) | (_lib.WANT_PRIOR if spec.include_prior else 0)
-                   | (_lib.WANT_JACOBIAN if spec.jacobian else 0))
+                   | (_lib.WANT_JACOBIAN if spec.jacobian else 0) | (_lib.EXACT_RTD if spec.exact_rtd else 0))
         if spec.ce is not None:
             c = spec.ce
             d.ce_enabled = 1
@@ -144,6 +144,25 @@ class LogProb:
         self.ctx.check(self.lib.ngrtd_logp(self.plan, t.ctypes.data_as(C.c_void_p), W,
                                            res.ctypes.data_as(C.c_void_p), _lib.MEM_HOST), "ngrtd_logp")
         return res
+
+    def bind(self, theta, out):
+        """Fast path for repeated log-probs of the same device buffers: returns a no-argument
+        callable that enqueues ngrtd_logp(theta -> out) on torch's current stream of the
+        moment of binding (checked once here, not per call)."""
+        W = self._check_dev(theta)
+        if out.dtype != theta.dtype or not out.is_cuda or not out.is_contiguous() or out.numel() != W:
+            raise ValueError("out must be a contiguous CUDA float64 tensor [W]")
+        f = self.lib.ngrtd_logp
+        args = (self.plan, C.c_void_p(theta.data_ptr()), C.c_int64(W), C.c_void_p(out.data_ptr()),
+                C.c_int32(_lib.MEM_DEVICE))
+        keep = (theta, out)
+
+        def run():
+            st = f(*args)
+            if st:
+                self.ctx.check(st, "ngrtd_logp")
+            return keep[1]
+        return run
 
     def forward(self, theta, soa=False):
         """Model outputs: (ce [G][L][W] or None, rtd [K][L][W] or None)."""

@@ -199,6 +199,7 @@ class ModelSpec:
     include_prior: bool = True
     include_like: bool = True
     jacobian: bool = False             # add PyMC3 transform log|J| (parity unpinned)
+    exact_rtd: bool = False            # no channel-sum surrogate: exact sums on the matrix cores
     roles: List[str] = field(default_factory=list)
 
     def __post_init__(self):

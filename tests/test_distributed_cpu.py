@@ -80,3 +80,47 @@ def test_shard_walkers_partition():
             spans = [shard_walkers(W, r, G) for r in range(G)]
             assert spans[0][0] == 0 and spans[-1][1] == W
             assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+
+
+def _step_loop_worker(rank, world, port, W_total, outdir):
+    """bench.py's per-step function (distributed.LogpStepLoop) on gloo: each rank's block
+    of ONE seeded ensemble, evaluated into the padded block buffer, then one all-gather."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle.models as om
+        from noblegas_rtd_mcmc_amd import workloads as wl
+        from noblegas_rtd_mcmc_amd.distributed import LogpStepLoop
+        spec = _spec()
+        full = wl.sample_prior(spec, W_total, np.random.default_rng(34568))
+        loop = LogpStepLoop(None, W_total, "cpu")
+        blk = np.ascontiguousarray(full[:, :, loop.lo:loop.hi])
+
+        def evaluate(out):
+            out.copy_(torch.from_numpy(om.log_prob(spec, blk)))
+        loop.evaluate = evaluate
+        g1 = loop.step().clone()
+        g2 = loop.step().clone()
+        np.savez(os.path.join(outdir, "s%d.npz" % rank), ens=loop.ensemble().numpy(), g1=g1.numpy(),
+                 g2=g2.numpy(), lo=loop.lo, hi=loop.hi, per=loop.per)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("W_total", [9, 16])
+def test_bench_step_loop_gloo(tmp_path, W_total):
+    """Strong (one ensemble split over the ranks, uneven when W is odd) and weak (W per
+    rank: W_total = 2 W) sharding both run this function; the gathered ensemble vector on
+    every rank equals the single-process log-prob of the whole ensemble."""
+    import oracle.models as om
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    port = _free_port()
+    mp.start_processes(_step_loop_worker, args=(2, port, W_total, str(tmp_path)), nprocs=2, start_method="spawn")
+    r0, r1 = (np.load(tmp_path / ("s%d.npz" % r)) for r in (0, 1))
+    spec = _spec()
+    ref = om.log_prob(spec, wl.sample_prior(spec, W_total, np.random.default_rng(34568)))
+    assert np.array_equal(r0["ens"], ref) and np.array_equal(r1["ens"], ref)
+    assert np.array_equal(r0["g1"], r1["g1"], equal_nan=True) and np.array_equal(r0["g1"], r0["g2"], equal_nan=True)
+    assert int(r0["hi"]) == int(r1["lo"]) and int(r1["hi"]) == W_total
+    if W_total % 2:                      # the short last block is NaN-padded in the gather
+        assert np.isnan(r0["g1"][-1])

@@ -229,3 +229,29 @@ def test_g_tp_after_convolve_is_decayed(golden):
     for tau, ref in zip(z["gtp_after_conv_tau"], z["gtp_after_conv"]):
         g = ortd.gen_g_tp(1200, 0, 0, tau, "exponential") * np.exp(-ortd.thalf_2_lambda(12.34) * tp)
         assert close(g, ref, rtol=1e-12, atol=1e-300).all()
+
+
+@pytest.mark.parametrize("which", ["c2", "c3", "c4", "bmm_epm_piston", "bmm_exp_disp"])
+def test_vectorized_oracle_matches_per_walker_loop(which):
+    """The vectorised CPU baseline (oracle/vectorized.py) is the same arithmetic as the
+    reference-faithful per-walker loop, up to the dot product's summation order."""
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    from oracle.vectorized import log_prob_vec
+    if which == "c2":
+        spec, th = wl.c2(W=24)
+    elif which == "c3":
+        spec, th = wl.c3(W=24)
+    elif which == "c4":
+        spec = wl.c4_spec(L=3, N=300)
+        th = wl.sample_prior(spec, 24, np.random.default_rng(3))
+    elif which == "bmm_epm_piston":
+        spec = wl.c4_spec(L=2, N=300, mod_type1="exp_pist_flow", mod_type2="piston",
+                          par_names=("tau1", "tau2", "f1", "eta1", "thalf_cfc", "lamsf6"))
+        th = wl.sample_prior(spec, 24, np.random.default_rng(4))
+    else:
+        spec = wl.c4_spec(L=2, N=300, mod_type1="exponential", mod_type2="dispersion",
+                          par_names=("tau1", "tau2", "f1", "D2", "J"))
+        th = wl.sample_prior(spec, 24, np.random.default_rng(5))
+    ref = omod.log_prob(spec, th)
+    got = log_prob_vec(spec, th)
+    assert close(got, ref, rtol=1e-12, atol=1e-9).all(), (got, ref)
