@@ -283,19 +283,66 @@ int ngrtd_plan_kernel_stats(ngrtd_plan* plan, double* times_ms, int64_t* counts,
  * accounting in bench.py. */
 int ngrtd_plan_info(ngrtd_plan* plan, int64_t W, int64_t* info, int32_t n);
 
-/* Device-resident population DE-MC (the sampler loop of PyMC3 DEMetropolisZ,
- * run_age_mcmc_utils.py:412-417 / noble_gas_mcmc.py:410-415, as sampler.DEMetropolis runs it
- * over the whole ensemble): n_steps steps of
- *   x*_w = x_w + lamb (x_r1 - x_r2) + U(-scaling, scaling),  r1 != r2 != w,
- *   accept iff logp(x*_w) - logp_w > log u_w  (and logp(x*_w) is not NaN),
- * random numbers from a counter-based generator keyed by (seed, step0 + s, walker).
- * theta [P][L][W] and logp [W] are DEVICE pointers, updated in place on the ctx stream;
- * logp must hold the log-prob of theta on entry (ngrtd_logp).  n_accepted (device
- * uint64, may be NULL) is incremented by the number of acceptances; accepted (device
- * int32 [W], may be NULL) receives the last step's decisions.  2 launches per step
- * (proposal + log-prob with the accept in its per-walker reduction).  W >= 3. */
-int ngrtd_demc_run(ngrtd_plan* plan, double* theta, double* logp, int64_t W, int64_t n_steps, double lamb,
-                   double scaling, uint64_t seed, uint64_t step0, uint64_t* n_accepted, int32_t* accepted);
+/* Device-resident DEMetropolisZ: the sampler of the reference, PyMC3 3.11.2
+ * DEMetropolisZ (pymc3/step_methods/metropolis.py; called at run_age_mcmc_utils.py:412-417
+ * and noble_gas_mcmc.py:410-415), for W independent chains at once -- one chain per walker
+ * (the reference runs 3-4 chains in separate processes).  Per chain w and step s:
+ *   tuning (s < n_tune): at the start of every step s = k tune_interval (k >= 1),
+ *     lamb_w (tune_target LAMBDA, PyMC3's default) or scaling_w (SCALING) *= pymc3 tune()
+ *     of the acceptance rate over the last interval, and the counter restarts;
+ *   before step s = n_tune (stop_tuning): the first floor(drop_fraction * it) history
+ *     entries are dropped (hist_lo advances), it = entries in the history;
+ *   eps = U(-1, 1) S_r scaling_w per parameter row r (UniformProposal(S) * scaling; S NULL =
+ *     ones, PyMC3's default);
+ *   space: PyMC3 proposes in the TRANSFORMED space of its free variables (Beta: logodds,
+ *     Uniform: interval, HalfNormal: log; pymc3/distributions/transforms.py).  With theta_u
+ *     set, the chains, their histories and the proposals live in that space: the proposal
+ *     kernel maps every proposed row back, x = backward(u) (logodds 1/(1+exp(-u)), interval
+ *     s b + (1-s) a with s = 1/(1+exp(-u)), log exp(u)), and the plan must carry
+ *     NGRTD_WANT_JACOBIAN so that logp is the density of u.  theta holds backward(theta_u).
+ *     theta_u NULL: the chains move in the natural space of theta (no Jacobian).
+ *   it = hist_len - hist_lo;  it > 1: iz1 != iz2 uniform in [0, it),
+ *     x* = x + lamb_w (Z_w[hist_lo + iz1] - Z_w[hist_lo + iz2]) + eps;  else x* = x + eps;
+ *   mr = logp(x*) - logp(x): accept iff mr is finite and log(u) < mr (metrop_select);
+ *   the chain's new state is appended to its history Z_w.
+ * Random numbers come from a counter-based generator keyed by (seed, s, chain0 + w), so a
+ * run split over several calls, or over walker-block shards, equals one call.  theta [P][L][W] and logp [W] are DEVICE
+ * pointers updated in place on the ctx stream; logp must hold logp(theta) on entry.
+ * Every array in the state is device memory owned by the caller.  History layout:
+ * [hist_cap][NC][W][16] float64, NC = ceil(P*L/16): entry e, theta row r of chain w at
+ * ((e*NC + r/16)*W + w)*16 + r%16 -- the 16 rows of a chunk are one 128-B line.  Entry e
+ * is the state after step e (hist_len == steps_done after every call).
+ * accepted_log [n_steps][W] (uint8) and logp_log [n_steps][W] (each chain's log-prob after
+ * the step) may be NULL.  n_accepted (device uint64, may be NULL) counts acceptances.
+ * 2 launches per step: the proposal kernel (which also appends the previous state) and the
+ * log-prob kernel with the accept in its per-walker reduction; one append at the end. */
+enum ngrtd_tune_target { NGRTD_TUNE_NONE = 0, NGRTD_TUNE_SCALING = 1, NGRTD_TUNE_LAMBDA = 2 };
+enum ngrtd_transform { NGRTD_TR_NONE = 0, NGRTD_TR_LOGODDS = 1, NGRTD_TR_INTERVAL = 2, NGRTD_TR_LOG = 3 };
+typedef struct {
+    double* lamb;            /* [W] per-chain lambda (PyMC3 default 2.38 / sqrt(2 ndim)) */
+    double* scaling;         /* [W] per-chain scaling (PyMC3 default 0.001) */
+    int32_t* n_acc_tune;     /* [W] acceptances since the last tune (start at 0) */
+    double* hist;            /* [hist_cap][NC][W][16] */
+    int64_t hist_cap;
+    int64_t hist_len;        /* in/out: entries written */
+    int64_t hist_lo;         /* in/out: first entry proposals draw from */
+    int64_t steps_done;      /* in/out: steps taken so far (tune schedule, random stream) */
+    int64_t n_tune;          /* tuning steps of the run (PyMC3 tune=) */
+    int32_t tune_interval;   /* PyMC3 tune_interval (default 100; the reference: 1000 / 5000) */
+    int32_t tune_target;     /* enum ngrtd_tune_target */
+    double drop_fraction;    /* PyMC3 tune_drop_fraction (default 0.9) */
+    uint64_t seed;
+    int64_t chain0;          /* global index of chain 0 in the random stream (walker-block
+                                shards of one ensemble draw the numbers of their own chains) */
+    int64_t n_chains_total;  /* chains of the whole ensemble (0: W, unsharded) */
+    const double* S;         /* [P*L] proposal scale per theta row (PyMC3 S), device; NULL = ones */
+    double* theta_u;         /* [P][L][W] transformed state (device), NULL = natural space */
+    int32_t tr_kind[NGRTD_ROLE_COUNT];  /* per parameter row p < P: enum ngrtd_transform */
+    double tr_a[NGRTD_ROLE_COUNT], tr_b[NGRTD_ROLE_COUNT];   /* interval bounds */
+} ngrtd_demcz_state;
+int ngrtd_demcz_run(ngrtd_plan* plan, double* theta, double* logp, int64_t W, int64_t n_steps,
+                    ngrtd_demcz_state* state, uint8_t* accepted_log, double* logp_log,
+                    uint64_t* n_accepted);
 
 /* Host-only (no device needed): build the piecewise-Chebyshev surrogate the exponential
  * log-prob kernel uses for its channel sums and validate it against a long-double

@@ -25,6 +25,8 @@ CFC_SPECIES = {11: 0, 12: 1, 113: 2, "SF6": 3}                      # enum ngrtd
 CFC_WHAT = {"equil_air": 0, "equil_aq": 1, "ce_exc": 2, "solubility": 3, "vapor_pressure_atm": 4,
             "lapse_rate_atm": 5}
 WANT_LIKE, WANT_PRIOR, WANT_JACOBIAN, EXACT_RTD = 1, 2, 4, 8
+TUNE_TARGET = {None: 0, "none": 0, "scaling": 1, "lambda": 2}       # enum ngrtd_tune_target
+Z_CHUNK = 16                                                          # history rows per 128-B line
 
 _dp = C.POINTER(C.c_double)
 _i32p = C.POINTER(C.c_int32)
@@ -34,6 +36,17 @@ _i64p = C.POINTER(C.c_int64)
 class TracerDesc(C.Structure):
     _fields_ = [("series_id", C.c_int32), ("accum", C.c_int32), ("t_half", C.c_double), ("J", C.c_double),
                 ("is_cfc12", C.c_int32), ("is_sf6", C.c_int32)]
+
+
+class DemczState(C.Structure):
+    """ngrtd_demcz_state: device pointers + the host-side counters of a DEMetropolisZ run."""
+    _fields_ = [("lamb", C.c_void_p), ("scaling", C.c_void_p), ("n_acc_tune", C.c_void_p), ("hist", C.c_void_p),
+                ("hist_cap", C.c_int64), ("hist_len", C.c_int64), ("hist_lo", C.c_int64),
+                ("steps_done", C.c_int64), ("n_tune", C.c_int64), ("tune_interval", C.c_int32),
+                ("tune_target", C.c_int32), ("drop_fraction", C.c_double), ("seed", C.c_uint64),
+                ("chain0", C.c_int64), ("n_chains_total", C.c_int64), ("S", C.c_void_p),
+                ("theta_u", C.c_void_p), ("tr_kind", C.c_int32 * ROLE_COUNT), ("tr_a", C.c_double * ROLE_COUNT),
+                ("tr_b", C.c_double * ROLE_COUNT)]
 
 
 class ModelDesc(C.Structure):
@@ -91,8 +104,8 @@ PROTOTYPES = {
     "ngrtd_forward": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int32]),
     "ngrtd_plan_kernel_stats": (C.c_int, [C.c_void_p, _dp, _i64p, C.c_int32, C.c_int32]),
     "ngrtd_plan_info": (C.c_int, [C.c_void_p, C.c_int64, _i64p, C.c_int32]),
-    "ngrtd_demc_run": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_double, C.c_double,
-                                 C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p]),
+    "ngrtd_demcz_run": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_void_p,
+                                  C.c_void_p, C.c_void_p, C.c_void_p]),
     "ngrtd_surrogate_check": (C.c_int, [_dp, C.c_int32, C.c_int64, C.c_double, _dp, _dp]),
     "ngrtd_c0_check": (C.c_int, [C.c_double, C.c_double, _dp, _i32p, _i32p, _dp]),
 }

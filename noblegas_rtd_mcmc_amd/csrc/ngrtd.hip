@@ -101,7 +101,7 @@ struct ngrtd_plan {
     double tp0 = 1e-5, dtp = 0.0;
     // workspaces
     DevBuf conc, ulogp, theta_stage, out_stage, ce_stage;
-    DevBuf demc_prop[2], demc_lp, demc_acc, demc_cnt;   // ngrtd_demc_run scratch
+    DevBuf demc_prop[2], demc_lp, demc_acc, demc_cnt;   // ngrtd_demcz_run scratch
     RtdArgs rtd{};
     UnitArgs unit{};
     LaunchStats stats;
@@ -1443,15 +1443,25 @@ int ngrtd_plan_kernel_stats(ngrtd_plan* p, double* times_ms, int64_t* counts, in
     return NGRTD_OK;
 }
 
-int ngrtd_demc_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64_t n_steps, double lamb,
-                   double scaling, uint64_t seed, uint64_t step0, uint64_t* n_accepted, int32_t* accepted) {
+int ngrtd_demcz_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64_t n_steps,
+                    ngrtd_demcz_state* z, uint8_t* accepted_log, double* logp_log, uint64_t* n_accepted) {
     if (!p) return NGRTD_ESTATE;
     ngrtd_ctx* ctx = p->ctx;
-    if (!theta || !logp || W < 3 || W > p->max_w || n_steps < 0)
-        return set_err(ctx, NGRTD_EINVAL, "bad theta/logp/W (3 <= W <= %lld)/n_steps", (long long)p->max_w);
+    if (!theta || !logp || !z || W < 1 || W > p->max_w || n_steps < 0)
+        return set_err(ctx, NGRTD_EINVAL, "bad theta/logp/state/W (1 <= W <= %lld)/n_steps", (long long)p->max_w);
+    if (!z->lamb || !z->scaling || !z->n_acc_tune || !z->hist || z->hist_cap < 1 || z->hist_len < 0 ||
+        z->hist_lo < 0 || z->hist_lo > z->hist_len || z->steps_done < 0 || z->tune_interval < 1 ||
+        z->tune_target < 0 || z->tune_target > 2 || !(z->drop_fraction >= 0.0 && z->drop_fraction <= 1.0) ||
+        z->chain0 < 0 || (z->n_chains_total != 0 && z->chain0 + W > z->n_chains_total))
+        return set_err(ctx, NGRTD_EINVAL, "bad DEMetropolisZ state");
+    const int64_t Wg = z->n_chains_total ? z->n_chains_total : W;
+    if (z->hist_len + n_steps > z->hist_cap)
+        return set_err(ctx, NGRTD_EINVAL, "history full: %lld entries + %lld steps > capacity %lld",
+                       (long long)z->hist_len, (long long)n_steps, (long long)z->hist_cap);
     if (n_steps == 0) return NGRTD_OK;
     hipStream_t st = S(ctx);
     const int64_t R = (int64_t)p->desc.n_params * p->desc.n_wells, E = R * W;
+    const int32_t NC = (int32_t)cdiv(R, kZChunk);
     HIP_TRY(ctx, p->demc_prop[0].ensure((size_t)E * sizeof(double)));
     HIP_TRY(ctx, p->demc_lp.ensure((size_t)W * sizeof(double)));
     HIP_TRY(ctx, p->demc_acc.ensure((size_t)W * sizeof(int32_t)));
@@ -1461,27 +1471,50 @@ int ngrtd_demc_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64_
         cnt = static_cast<unsigned long long*>(p->demc_cnt.p);
     }
     int32_t* acc = static_cast<int32_t*>(p->demc_acc.p);
-    double* prop = p->demc_prop[0].d();
-    const dim3 pgrid((unsigned)cdiv(W, 256), (unsigned)cdiv(R, kDemcRows));
-    // rows staged in LDS (demc_propose_rows_kernel): K rows per block within 64 KiB, while
-    // that still leaves a block per CU's worth of blocks (c4: K = 2, 256 blocks)
-    static const bool no_stage = std::getenv("NGRTD_DEMC_NO_STAGE") != nullptr;
-    int K = (int)std::min<int64_t>(8, (64 * 1024 / 8) / W);
-    while (K > 1 && cdiv(R, K) < 256) K /= 2;
-    const bool stage = !no_stage && K >= 1;
-    for (int64_t s = 0; s < n_steps; ++s) {
-        const uint64_t key = demc_key(seed, step0 + (uint64_t)s);
-        DemcArgs d{theta, prop, W, R, lamb, scaling, key};
-        if (stage)
-            hipLaunchKernelGGL(demc_propose_rows_kernel, dim3((unsigned)cdiv(R, K)), dim3(kDemcStageThreads),
-                               (size_t)K * W * sizeof(double), st, d, (int32_t)K);
-        else
-            hipLaunchKernelGGL(demc_propose_kernel, pgrid, dim3(256), 0, st, d);
-        HIP_TRY(ctx, hipGetLastError());
-        const DemcAccept da{logp, acc, cnt, theta, prop, p->desc.n_params, key};
-        NG_CHECK(plan_run(p, prop, W, p->demc_lp.d(), nullptr, nullptr, &da));
+    const bool tr = z->theta_u != nullptr;
+    if (tr && !(p->desc.flags & NGRTD_WANT_JACOBIAN))
+        return set_err(ctx, NGRTD_EINVAL, "transformed-space chains need a plan with NGRTD_WANT_JACOBIAN");
+    if (tr) HIP_TRY(ctx, p->demc_prop[1].ensure((size_t)E * sizeof(double)));
+    double* prop = p->demc_prop[0].d();                   // proposal in the chains' space
+    double* prop_x = tr ? p->demc_prop[1].d() : prop;     // ... and in theta's (natural) space
+    double* state = tr ? z->theta_u : theta;              // what the history records
+    DemczArgs base{};
+    base.x = state; base.prop = prop; base.hist = z->hist; base.lamb = z->lamb; base.scaling = z->scaling;
+    base.W = W; base.R = R; base.NC = NC; base.chain0 = z->chain0; base.Wg = Wg; base.S = z->S;
+    base.prop_x = tr ? prop_x : nullptr; base.L = p->desc.n_wells;
+    for (int i = 0; i < kRoleCount; ++i) {
+        base.tr_kind[i] = z->tr_kind[i]; base.tr_a[i] = z->tr_a[i]; base.tr_b[i] = z->tr_b[i];
     }
-    if (accepted) HIP_TRY(ctx, hipMemcpyAsync(accepted, acc, (size_t)W * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+    const dim3 grid((unsigned)cdiv(W, 64), (unsigned)cdiv(NC, 4));
+    for (int64_t j = 0; j < n_steps; ++j) {
+        const int64_t s = z->steps_done;
+        const uint64_t key = demc_key(z->seed, (uint64_t)s);
+        // the previous step's state becomes history entry s - 1 (the previous call appended
+        // its own last state), then proposals draw from [hist_lo, hist_len)
+        const int64_t append_at = j > 0 ? z->hist_len : -1;
+        if (j > 0) z->hist_len += 1;
+        if (s == z->n_tune && z->n_tune > 0)   // stop_tuning before the first draw: drop the
+            z->hist_lo += (int64_t)(z->drop_fraction * (double)(z->hist_len - z->hist_lo));   // oldest
+        DemczArgs d = base;
+        d.propose = 1; d.append_at = append_at; d.lo = z->hist_lo; d.it = z->hist_len - z->hist_lo; d.key = key;
+        hipLaunchKernelGGL(demcz_propose_kernel, grid, dim3(256), 0, st, d);
+        HIP_TRY(ctx, hipGetLastError());
+        const int64_t next = s + 1;
+        const int32_t tune_now = (z->tune_target != NGRTD_TUNE_NONE && next < z->n_tune &&
+                                  next % z->tune_interval == 0) ? 1 : 0;
+        const DemcAccept da{logp, acc, cnt, theta, prop_x, p->desc.n_params, key, z->n_acc_tune, z->lamb, z->scaling,
+                            tune_now, z->tune_target, z->tune_interval,
+                            accepted_log ? accepted_log + j * W : nullptr, logp_log ? logp_log + j * W : nullptr,
+                            z->chain0, tr ? z->theta_u : nullptr, tr ? prop : nullptr};
+        NG_CHECK(plan_run(p, prop_x, W, p->demc_lp.d(), nullptr, nullptr, &da));
+        z->steps_done = next;
+    }
+    // the last step's state: history entry steps_done - 1
+    DemczArgs d = base;
+    d.propose = 0; d.append_at = z->hist_len;
+    hipLaunchKernelGGL(demcz_propose_kernel, grid, dim3(256), 0, st, d);
+    HIP_TRY(ctx, hipGetLastError());
+    z->hist_len += 1;
     return NGRTD_OK;
 }
 

@@ -132,27 +132,55 @@ struct UnitArgs {
     double bt_betaln;
 };
 
-// Metropolis accept of a device DE-MC step, done where the proposal's log-prob is formed
-// (the per-walker reduction of logp_fused_kernel, or demc_accept_kernel): the walker's
-// current log-prob lp[w] is replaced by the proposal's when accepted and its theta rows
-// are copied from the proposal, acc[w] records the decision, n_acc counts acceptances.
+// Metropolis accept of a device DEMetropolisZ step, done where the proposal's log-prob is
+// formed (the per-walker reduction of logp_fused_kernel, or demc_accept_kernel): the
+// chain's current log-prob lp[w] is replaced by the proposal's when accepted and its theta
+// rows are copied from the proposal; n_acc counts acceptances; the per-chain tuning
+// counters and, at the end of a tune interval, the tuned lamb / scaling are updated here
+// (one thread per chain, so no other thread reads them during the launch).
 struct DemcAccept {
     double* lp;             // [W] current log-prob (in/out); null: plain log-prob launch
-    int32_t* acc;           // [W] out
+    int32_t* acc;           // [W] out: this step's decisions
     unsigned long long* n_acc;
-    double* x;              // [P][L][W] current state, updated for accepted walkers
+    double* x;              // [P][L][W] current state, updated for accepted chains
     const double* prop;     // [P][L][W] the proposal being evaluated
     int32_t P;              // parameter rows per (walker, well)
     uint64_t key;           // per-step random key (demc_key)
+    int32_t* n_acc_tune;    // [W] accepted since the last tune (null: no tuning state)
+    double* lamb;           // [W] per-chain lambda
+    double* scaling;        // [W] per-chain scaling
+    int32_t tune_now;       // apply PyMC3 tune() after this step's decision
+    int32_t tune_target;    // 1 = scaling, 2 = lambda
+    int32_t tune_interval;
+    uint8_t* acc_log;       // [W] this step's decisions (null: not logged)
+    double* lp_log;         // [W] each chain's log-prob after this step (null: not logged)
+    int64_t chain0;         // global index of chain 0 in the random stream
+    double* xu;             // [P][L][W] transformed state (null: natural-space chains)
+    const double* prop_u;   // [P][L][W] the transformed proposal, copied to xu on accept
 };
 
-// DE-MC proposal over theta rows [R][W] (demc_propose_kernel)
-struct DemcArgs {
+// DEMetropolisZ proposal / history append over theta rows [R][W] (demcz_propose_kernel)
+constexpr int kZChunk = 16;
+constexpr int kRoleCount = NGRTD_ROLE_COUNT;     // history rows per 128-B chunk: [entry][R/16][W][16]
+struct DemczArgs {
     const double* x;        // [R][W] current state
     double* prop;           // [R][W] new proposal
+    double* hist;           // [cap][NC][W][kZChunk] chain histories
+    const double* lamb;     // [W]
+    const double* scaling;  // [W]
     int64_t W, R;
-    double lamb, scaling;
+    int32_t NC;             // chunks of kZChunk rows
+    int32_t propose;        // 0: append only (no proposal)
+    int64_t append_at;      // history entry that receives x (-1: none)
+    int64_t lo, it;         // partners come from entries lo + [0, it)
     uint64_t key;           // per-step random key (demc_key)
+    int64_t chain0;         // global index of chain 0 in the random stream
+    int64_t Wg;             // chains of the whole ensemble (the element stream's row stride)
+    const double* S;        // [R] proposal scale per row (null: ones)
+    double* prop_x;         // [R][W] backward(prop) for transformed chains (null: natural space)
+    int32_t L;              // wells: row r belongs to parameter r / L
+    int32_t tr_kind[kRoleCount];
+    double tr_a[kRoleCount], tr_b[kRoleCount];
 };
 
 }  // namespace ngrtd

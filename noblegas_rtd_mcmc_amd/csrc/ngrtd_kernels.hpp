@@ -948,17 +948,45 @@ __host__ __device__ __forceinline__ double rng_unit(uint64_t h) {
     return ((double)(h >> 11) + 0.5) * (1.0 / 9007199254740992.0);
 }
 
-// Metropolis decision of walker w (sampler.DEMetropolis: accept iff lp* - lp > log u and
-// lp* is not NaN), applied to lp[w]; one thread per walker.  Returns the decision.
+// PyMC3 3.11.2 step_methods/metropolis.py tune(): multiplicative update from the
+// acceptance rate of the last tune interval.
+__host__ __device__ __forceinline__ double pymc3_tune(double scale, double acc_rate) {
+    if (acc_rate < 0.001) return scale * 0.1;
+    if (acc_rate < 0.05) return scale * 0.5;
+    if (acc_rate < 0.2) return scale * 0.9;
+    if (acc_rate > 0.95) return scale * 10.0;
+    if (acc_rate > 0.75) return scale * 2.0;
+    if (acc_rate > 0.5) return scale * 1.1;
+    return scale;
+}
+
+// Metropolis decision of chain w (PyMC3 metrop_select, step_methods/arraystep.py: accept
+// iff mr = logp(x*) - logp(x) is finite and log(u) < mr), applied to lp[w]; one thread per
+// chain.  Then the chain's tuning counter and, at the end of a tune interval, its lamb or
+// scaling (DEMetropolisZ.astep: tuned at the start of the next step from the interval's
+// acceptance rate, counter reset).  Returns the decision.
 __device__ __forceinline__ bool demc_decide(const DemcAccept& d, int64_t w, double lp_prop) {
     const double cur = d.lp[w];
-    const double logu = log(rng_unit(rng_mix(rng_mix(d.key + 3) + (uint64_t)w)));
-    const bool acc = (lp_prop - cur) > logu && lp_prop == lp_prop;
+    const double logu = log(rng_unit(rng_mix(rng_mix(d.key + 3) + (uint64_t)(d.chain0 + w))));
+    const double mr = lp_prop - cur;
+    const bool acc = __builtin_isfinite(mr) && logu < mr;
     d.acc[w] = acc;
     if (acc) {
         d.lp[w] = lp_prop;
         atomicAdd(d.n_acc, 1ull);     // integer count: order-independent
     }
+    if (d.n_acc_tune) {
+        int32_t na = d.n_acc_tune[w] + (acc ? 1 : 0);
+        if (d.tune_now) {
+            const double rate = (double)na / (double)d.tune_interval;
+            if (d.tune_target == 2) d.lamb[w] = pymc3_tune(d.lamb[w], rate);
+            else if (d.tune_target == 1) d.scaling[w] = pymc3_tune(d.scaling[w], rate);
+            na = 0;
+        }
+        d.n_acc_tune[w] = na;
+    }
+    if (d.acc_log) d.acc_log[w] = (uint8_t)acc;
+    if (d.lp_log) d.lp_log[w] = acc ? lp_prop : cur;
     return acc;
 }
 
@@ -968,59 +996,105 @@ __global__ void __launch_bounds__(256) demc_accept_kernel(const DemcAccept d, co
                                                           int64_t W, int64_t R) {
     const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= W) return;
-    if (demc_decide(d, w, lp_prop[w]))
+    if (demc_decide(d, w, lp_prop[w])) {
         for (int64_t r = 0; r < R; ++r) d.x[r * W + w] = d.prop[r * W + w];
-}
-
-// Proposal x* = x + lamb (x_r1 - x_r2) + U(-scaling, scaling) for walker w over rows
-// [r0, r0 + kDemcRows): partners r1 != r2, both != w, drawn once per thread as
-// sampler.DEMetropolis draws them; walkers on x (coalesced), row chunks on y.
-constexpr int kDemcRows = 8;
-// partners of walker w for the step keyed `key`: r1 != w, r2 != r1, r2 != w
-__device__ __forceinline__ void demc_partners(uint64_t key, uint32_t W, uint32_t w, uint32_t& r1, uint32_t& r2) {
-    const uint64_t hp = rng_mix(rng_mix(key + 1) + (uint64_t)w);
-    r1 = (uint32_t)((w + 1 + (uint32_t)(hp >> 32) % (W - 1)) % W);
-    r2 = (r1 + 1 + (uint32_t)hp % (W - 2)) % W;
-    if (r2 == w) r2 = (r2 + 1) % W;
-    if (r2 == r1) r2 = (r2 + 1) % W;
-}
-__global__ void __launch_bounds__(256) demc_propose_kernel(const DemcArgs d) {
-    const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= d.W) return;
-    uint32_t r1, r2;
-    demc_partners(d.key, (uint32_t)d.W, (uint32_t)w, r1, r2);
-    const uint64_t ke = rng_mix(d.key + 2);
-    const int64_t r0 = (int64_t)blockIdx.y * kDemcRows;
-#pragma unroll 4
-    for (int64_t r = r0; r < r0 + kDemcRows && r < d.R; ++r) {
-        const int64_t row = r * d.W, e = row + w;
-        const double eps = (2.0 * rng_unit(rng_mix(ke + (uint64_t)e)) - 1.0) * d.scaling;
-        d.prop[e] = d.x[e] + d.lamb * (d.x[row + r1] - d.x[row + r2]) + eps;
+        if (d.xu)
+            for (int64_t r = 0; r < R; ++r) d.xu[r * W + w] = d.prop_u[r * W + w];
     }
 }
 
-// The same proposal with K whole rows of x staged in LDS per block (coalesced loads and
-// stores; the partner gathers x[row][r1], x[row][r2] -- random within a row -- read LDS
-// instead of 64 scattered cache lines per wave instruction).  Identical arithmetic, so
-// bitwise the same proposals.  Used when K * W doubles fit the block's LDS (demc_run).
-constexpr int kDemcStageThreads = 1024;
-__global__ void __launch_bounds__(kDemcStageThreads) demc_propose_rows_kernel(const DemcArgs d, int32_t K) {
-    extern __shared__ double xs[];                       // [K][W]
+// PyMC3 3.11 transforms (pymc3/distributions/transforms.py) backward(u): LogOdds
+// invlogit(u, 0) = 1 / (1 + exp(-u)); Interval s b + (1 - s) a with s = sigmoid(u); Log exp(u).
+// Plain OCML exp, so that sampler.Transform (torch on the same device) agrees bitwise.
+__host__ __device__ __forceinline__ double pymc3_backward(int kind, double a, double b, double u) {
+    if (kind == NGRTD_TR_LOGODDS) return 1.0 / (1.0 + exp(-u));
+    if (kind == NGRTD_TR_INTERVAL) {
+        const double s = 1.0 / (1.0 + exp(-u));
+        return s * b + (1.0 - s) * a;
+    }
+    if (kind == NGRTD_TR_LOG) return exp(u);
+    return u;
+}
+
+// Partners of chain w for the step keyed `key` (DEMetropolisZ.astep: iz1 = randint(it),
+// iz2 = randint(it) redrawn until != iz1 -- i.e. uniform over the it - 1 others):
+// iz1 = floor(u1 it), iz2 = floor(u2 (it - 1)), +1 when >= iz1.  it >= 2.
+__host__ __device__ __forceinline__ void demcz_partners(uint64_t key, uint64_t w, uint64_t it, uint64_t& iz1,
+                                                        uint64_t& iz2) {
+    const uint64_t hp = rng_mix(rng_mix(key + 1) + w);
+    iz1 = ((hp >> 32) * it) >> 32;
+    iz2 = ((hp & 0xFFFFFFFFull) * (it - 1)) >> 32;
+    iz2 += (iz2 >= iz1) ? 1 : 0;
+}
+
+// DEMetropolisZ proposal of every chain (pymc3 DEMetropolisZ.astep):
+//   x* = x + lamb_w (Z_w[iz1] - Z_w[iz2]) + eps,  eps = U(-1, 1) scaling_w per parameter
+// (noise only while the history has < 2 entries), and the history append of the current
+// state x (the previous step's q_new) into entry append_at.  Thread = (chain w, chunk c
+// of 16 theta rows): its x rows load coalesced across the wave's 64 chains ([R][W]), its
+// history chunk is one contiguous 128-B line ([entry][NC][W][16]: the wave touches 8 KiB
+// contiguous), so partner rows of different entries per chain cost no wasted bytes.
+__global__ void __launch_bounds__(256) demcz_propose_kernel(const DemczArgs d) {
+    const int64_t w = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+    const int c = (int)blockIdx.y * 4 + (int)(threadIdx.x >> 6);
+    if (w >= d.W || c >= d.NC) return;
     const int64_t W = d.W;
-    const int64_t r0 = (int64_t)blockIdx.x * K;
-    const int nr = (int)((d.R - r0) < K ? (d.R - r0) : K);
-    const double* src = d.x + r0 * W;
-    for (int64_t i = threadIdx.x; i < nr * W; i += kDemcStageThreads) xs[i] = src[i];
-    __syncthreads();
+    const int64_t r0 = (int64_t)c * kZChunk;
+    const int nr = (int)((d.R - r0) < kZChunk ? (d.R - r0) : kZChunk);
+    double x[kZChunk];
+#pragma unroll
+    for (int i = 0; i < kZChunk; ++i) x[i] = i < nr ? d.x[(r0 + i) * W + w] : 0.0;
+    const size_t line = (size_t)W * kZChunk;                 // doubles per (entry, chunk)
+    const size_t off = (size_t)c * line + (size_t)w * kZChunk;
+    const size_t entry = (size_t)d.NC * line;                 // doubles per entry
+    if (d.append_at >= 0) {
+        double2* dst = reinterpret_cast<double2*>(d.hist + (size_t)d.append_at * entry + off);
+#pragma unroll
+        for (int i = 0; i < kZChunk / 2; ++i) dst[i] = double2{x[2 * i], x[2 * i + 1]};
+    }
+    if (!d.propose) return;
+    const double lamb = d.lamb[w], sc = d.scaling[w];
     const uint64_t ke = rng_mix(d.key + 2);
-    for (int64_t w = threadIdx.x; w < W; w += kDemcStageThreads) {
-        uint32_t r1, r2;
-        demc_partners(d.key, (uint32_t)W, (uint32_t)w, r1, r2);
-        for (int k = 0; k < nr; ++k) {
-            const double* xr = xs + (int64_t)k * W;
-            const int64_t e = (r0 + k) * W + w;
-            const double eps = (2.0 * rng_unit(rng_mix(ke + (uint64_t)e)) - 1.0) * d.scaling;
-            d.prop[e] = xr[w] + d.lamb * (xr[r1] - xr[r2]) + eps;
+    double y[kZChunk];
+    if (d.it > 1) {
+        uint64_t iz1, iz2;
+        demcz_partners(d.key, (uint64_t)(d.chain0 + w), (uint64_t)d.it, iz1, iz2);
+        const int64_t e1 = d.lo + (int64_t)iz1, e2 = d.lo + (int64_t)iz2;
+        double z1[kZChunk], z2[kZChunk];
+        const double2* s1 = reinterpret_cast<const double2*>(d.hist + (size_t)e1 * entry + off);
+        const double2* s2 = reinterpret_cast<const double2*>(d.hist + (size_t)e2 * entry + off);
+#pragma unroll
+        for (int i = 0; i < kZChunk / 2; ++i) {
+            const double2 a = s1[i], b = s2[i];
+            z1[2 * i] = a.x; z1[2 * i + 1] = a.y;
+            z2[2 * i] = b.x; z2[2 * i + 1] = b.y;
+        }
+        // the entry written above by this same thread: take it from registers
+        if (e1 == d.append_at)
+#pragma unroll
+            for (int i = 0; i < kZChunk; ++i) z1[i] = x[i];
+        if (e2 == d.append_at)
+#pragma unroll
+            for (int i = 0; i < kZChunk; ++i) z2[i] = x[i];
+#pragma unroll
+        for (int i = 0; i < kZChunk; ++i) y[i] = x[i] + lamb * (z1[i] - z2[i]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < kZChunk; ++i) y[i] = x[i];
+    }
+#pragma unroll
+    for (int i = 0; i < kZChunk; ++i) {
+        if (i < nr) {
+            // element stream: row-major over (row, GLOBAL chain) -- a shard draws its chains' numbers
+            const uint64_t e = (uint64_t)(r0 + i) * (uint64_t)d.Wg + (uint64_t)(d.chain0 + w);
+            const double u2 = 2.0 * rng_unit(rng_mix(ke + e)) - 1.0;
+            const double eps = (d.S ? u2 * d.S[r0 + i] : u2) * sc;
+            const double v = y[i] + eps;
+            d.prop[(r0 + i) * W + w] = v;
+            if (d.prop_x) {       // transformed chains: the natural-space value the log-prob reads
+                const int pr = (int)((r0 + i) / d.L);
+                d.prop_x[(r0 + i) * W + w] = pymc3_backward(d.tr_kind[pr], d.tr_a[pr], d.tr_b[pr], v);
+            }
         }
     }
 }
@@ -1274,8 +1348,11 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     }
     if (dacc.lp) {   // DE-MC: accepted walkers take the proposal's theta rows of this unit
         __syncthreads();
-        if (do_theta && mvalid && dec[mwl])
+        if (do_theta && mvalid && dec[mwl]) {
             for (int p = 0; p < dacc.P; ++p) dacc.x[(int64_t)p * a.U + mu] = dacc.prop[(int64_t)p * a.U + mu];
+            if (dacc.xu)
+                for (int p = 0; p < dacc.P; ++p) dacc.xu[(int64_t)p * a.U + mu] = dacc.prop_u[(int64_t)p * a.U + mu];
+        }
     }
     NGRTD_PROBE(7);
 }

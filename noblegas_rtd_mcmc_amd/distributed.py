@@ -8,17 +8,13 @@ block with its own GPU plan and the per-block log-prob vectors are exchanged wit
 tests).  The payload is W_total float64 (16 KiB at 2048 walkers): latency-bound, so it is
 a single collective per step, never bucketed.
 
-``exchange="positions"`` additionally all-gathers the walker positions so the DE proposal
-of a walker may draw partners from every block (one more all-gather of P*L*W_total
-doubles per step); the default ``"logp"`` keeps DE moves inside each block (independent
-sub-ensembles, no position traffic).
+``sharded_demcz`` runs the reference's sampler (DEMetropolisZ, one chain per walker) over
+the shards: its chains propose from their own histories, so sampling itself exchanges
+nothing; the trace's log-probs are gathered once at the end.
 """
-import math
-
 import torch
 import torch.distributed as dist
 
-from .sampler import pymc3_tune
 from .workloads import shard_walkers
 
 
@@ -111,42 +107,33 @@ class ShardedLogProb:
         return torch.cat(parts, dim=-1)
 
 
-def sharded_de_step_loop(sharded, x_block, tune, draws, seed=123423, scaling=1e-3, tune_interval=100,
-                         exchange="logp"):
-    """Population DE-MC over a sharded ensemble (see sampler.DEMetropolis).  Every rank
-    runs the same number of steps; tuning uses the GLOBAL acceptance rate (all-reduce)."""
-    x = x_block.clone()
-    Wb = x.shape[-1]
-    d = int(x[..., 0].numel())
-    lamb = 2.38 / math.sqrt(2 * d)
-    g = torch.Generator(device=x.device)
-    g.manual_seed(seed + 7919 * sharded.rank)
-    lp, lp_full = sharded(x)
-    acc_window = 0.0
-    kept = []
-    for it in range(tune + draws):
-        pool = sharded.gather_positions(x) if exchange == "positions" else x
-        Wp = pool.shape[-1]
-        base = sharded.lo if exchange == "positions" else 0
-        idx = torch.arange(Wb, device=x.device) + base
-        r1 = (idx + torch.randint(1, Wp, (Wb,), generator=g, device=x.device)) % Wp
-        r2 = (r1 + torch.randint(1, Wp - 1, (Wb,), generator=g, device=x.device)) % Wp
-        r2 = torch.where(r2 == idx, (r2 + 1) % Wp, r2)
-        r2 = torch.where(r2 == r1, (r2 + 1) % Wp, r2)
-        eps = (torch.rand(x.shape, generator=g, device=x.device, dtype=x.dtype) * 2 - 1) * scaling
-        prop = x + lamb * (pool[..., r1] - pool[..., r2]) + eps
-        lp_prop, _ = sharded(prop)
-        logu = torch.log(torch.rand((Wb,), generator=g, device=x.device, dtype=lp.dtype))
-        acc = ((lp_prop - lp) > logu) & ~torch.isnan(lp_prop)
-        x = torch.where(acc, prop, x)
-        lp = torch.where(acc, lp_prop, lp)
-        acc_window += float(acc.sum())
-        if it < tune and (it + 1) % tune_interval == 0:
-            t = torch.tensor([acc_window], dtype=torch.float64, device=x.device)
-            if sharded.world > 1:
-                dist.all_reduce(t, group=sharded.group)
-            scaling = pymc3_tune(scaling, float(t) / (tune_interval * sharded.W_total))
-            acc_window = 0.0
-        if it >= tune:
-            kept.append(sharded.gather(lp))
-    return x, lp, (torch.stack(kept) if kept else None), scaling
+def sharded_demcz(log_prob, x_block, W_total, tune, draws, device_sampler=False, group=None, **kw):
+    """DEMetropolisZ over an ensemble sharded in walker blocks: every rank runs the chains
+    of its block (sampler.DEMetropolisZ on a batched log_prob, or DeviceDEMetropolisZ on an
+    engine.LogProb), each chain drawing the random numbers of its GLOBAL index, so the
+    union of the shards is bitwise the single-process run of the whole ensemble.  Chains
+    are independent (each proposes from its own history), so sampling needs no
+    collective at all; the per-draw log-probs and decisions are all-gathered once, at
+    the end, for the trace.  Returns (result of this rank's block, logp [draws, W_total],
+    accepted [draws, W_total])."""
+    from .sampler import DEMetropolisZ, DeviceDEMetropolisZ
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    lo, hi = shard_walkers(int(W_total), rank, world)
+    if x_block.shape[-1] != hi - lo:
+        raise ValueError("rank %d owns walkers [%d, %d), got a block of %d" % (rank, lo, hi, x_block.shape[-1]))
+    cls = DeviceDEMetropolisZ if device_sampler else DEMetropolisZ
+    res = cls(log_prob, chain0=lo, n_chains_total=int(W_total), **kw).run(x_block, tune, draws)
+    if world == 1:
+        return res, res["logp"], res["accepted"]
+    per = (int(W_total) + world - 1) // world
+
+    def gather(t, fill):
+        buf = torch.full((t.shape[0], per), fill, dtype=t.dtype, device=t.device)
+        buf[:, : t.shape[1]] = t
+        out = torch.empty((world * t.shape[0], per), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, buf.contiguous(), group=group)
+        out = out.view(world, t.shape[0], per)
+        return torch.cat([out[r, :, : shard_walkers(int(W_total), r, world)[1] - shard_walkers(int(W_total), r, world)[0]]
+                          for r in range(world)], dim=1)
+    return res, gather(res["logp"], float("nan")), gather(res["accepted"].to(torch.float64), 0.0).to(torch.uint8)

@@ -20,6 +20,11 @@ ROLE_ORDER = ("Ae_beta", "F_beta", "E_beta", "m", "b_beta", "nu_ce_beta", "tau1"
               "eta2", "D1", "D2", "J", "thalf_cfc_beta", "lamsf6", "nu_rtd_beta")
 
 
+def torch_float64():
+    import torch
+    return torch.float64
+
+
 def _is_torch(x):
     return type(x).__module__.startswith("torch")
 
@@ -189,18 +194,27 @@ class LogProb:
                                               _lib.MEM_HOST), "ngrtd_forward")
         return ce, rt
 
-    def demc(self, theta, logp, n_steps, lamb, scaling, seed, step0=0, n_accepted=None, accepted=None):
-        """n_steps device-resident DE-MC steps (ngrtd_demc_run) on torch CUDA tensors:
-        theta [P][L][W] float64 and logp [W] float64 (its log-prob), updated in place on
-        torch's current stream.  n_accepted: optional CUDA uint64/int64 [1] counter."""
+    def demcz(self, theta, logp, n_steps, state, accepted_log=None, logp_log=None, n_accepted=None):
+        """n_steps device-resident DEMetropolisZ steps (ngrtd_demcz_run) of the chains theta
+        [P][L][W] (CUDA float64, logp [W] = their log-prob), updated in place on torch's
+        current stream.  state: sampler.ZState (its host counters advance).  accepted_log
+        (uint8) / logp_log (float64): optional CUDA [n_steps][W]; n_accepted: optional CUDA
+        int64 [1] counter."""
         W = self._check_dev(theta)
-        if logp.dtype.itemsize != 8 or not logp.is_cuda or logp.numel() != W:
+        if logp.dtype != torch_float64() or not logp.is_cuda or logp.numel() != W:
             raise ValueError("logp must be a CUDA float64 tensor [W]")
-        self.ctx.check(self.lib.ngrtd_demc_run(
-            self.plan, C.c_void_p(theta.data_ptr()), C.c_void_p(logp.data_ptr()), W, int(n_steps), float(lamb),
-            float(scaling), int(seed) & (2 ** 64 - 1), int(step0) & (2 ** 64 - 1),
-            C.c_void_p(n_accepted.data_ptr() if n_accepted is not None else 0),
-            C.c_void_p(accepted.data_ptr() if accepted is not None else 0)), "ngrtd_demc_run")
+        R = self.spec.n_params * self.spec.n_wells
+        if state.W != W or state.R != R:
+            raise ValueError("state was built for R=%d, W=%d" % (state.R, state.W))
+        for name, t, dt in (("accepted_log", accepted_log, 1), ("logp_log", logp_log, 8)):
+            if t is not None and (not t.is_cuda or t.element_size() != dt or t.numel() < n_steps * W
+                                  or not t.is_contiguous()):
+                raise ValueError("%s must be a contiguous CUDA tensor [n_steps][W]" % name)
+        self.ctx.check(self.lib.ngrtd_demcz_run(
+            self.plan, C.c_void_p(theta.data_ptr()), C.c_void_p(logp.data_ptr()), W, int(n_steps),
+            C.byref(state.c), C.c_void_p(accepted_log.data_ptr() if accepted_log is not None else 0),
+            C.c_void_p(logp_log.data_ptr() if logp_log is not None else 0),
+            C.c_void_p(n_accepted.data_ptr() if n_accepted is not None else 0)), "ngrtd_demcz_run")
 
     def kernel_stats(self, reset=False):
         ms = (C.c_double * 4)()

@@ -89,18 +89,20 @@ class CEModel:
         nu = t[5] * (c.nu_max - c.nu_min) + c.nu_min
         return {"Ae": Ae, "F": F, "E": E, "b": b, "m": t[3], "T": T, "nu": nu}
 
-    def sample(self, nwalkers=100, tune=500, draws=500, seed=12345, tune_interval=100, sampler="device"):
-        """Ensemble DE-MC on the GPU log-prob (replaces mc.sample, :408-415).  sampler:
-        "device" (ngrtd_demc_run, device-resident) or "torch" (DEMetropolis on torch ops)."""
+    def sample(self, nwalkers=100, tune=500, draws=500, seed=12345, tune_interval=100, sampler="device",
+               space="transformed"):
+        """DEMetropolisZ, one chain per walker, on the GPU log-prob (replaces mc.sample,
+        :408-415).  sampler: "device" (ngrtd_demcz_run, device-resident) or "torch"
+        (sampler.DEMetropolisZ on torch ops; same random stream).  space: "transformed"
+        (PyMC3's: logodds for the Beta variables; the log-prob adds the Jacobian) or
+        "natural"."""
         import torch
-        from .sampler import DEMetropolis, DeviceDEMetropolis
+        from .sampler import sample_model
         from .workloads import sample_prior
         x0 = sample_prior(self.spec, nwalkers, np.random.default_rng(seed))
         x = torch.from_numpy(x0).to("cuda:%d" % self.device)
-        if sampler == "device":
-            res = DeviceDEMetropolis(self.logp, tune_interval=tune_interval, seed=seed).run(x, tune, draws)
-        else:
-            res = DEMetropolis(lambda th: self.logp(th), tune_interval=tune_interval, seed=seed).run(x, tune, draws)
+        res = sample_model(self.spec, self.max_walkers, self.device, x, tune, draws, seed, tune_interval, sampler,
+                           space, cache=self.__dict__)
         res["samples"] = res["samples"].cpu().numpy()
         res["logp"] = res["logp"].cpu().numpy()
         return res

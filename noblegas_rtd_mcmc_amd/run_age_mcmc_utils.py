@@ -164,19 +164,20 @@ class conv_mcmc:
             self._lp = LogProb(self.spec(), self.max_walkers, self.device)
         return self._lp
 
-    def sample_mcmc(self, nwalkers=96, tune=10000, draws=10000, seed=123423, tune_interval=1000, sampler="device"):
-        """Ensemble DE-MC on the GPU log-prob (replaces mc.sample, :407-429).  sampler:
-        "device" (ngrtd_demc_run, device-resident) or "torch" (DEMetropolis on torch ops)."""
+    def sample_mcmc(self, nwalkers=96, tune=10000, draws=10000, seed=123423, tune_interval=1000, sampler="device",
+                    space="transformed"):
+        """DEMetropolisZ, one chain per walker, on the GPU log-prob (replaces mc.sample,
+        :407-429).  sampler: "device" (ngrtd_demcz_run, device-resident) or "torch"
+        (sampler.DEMetropolisZ on torch ops; same random stream).  space: "transformed"
+        (PyMC3's: logodds / interval / log; the log-prob adds the Jacobian) or "natural"."""
         import torch
-        from .sampler import DEMetropolis, DeviceDEMetropolis
+        from .sampler import sample_model
         from .workloads import sample_prior
         lp = self.build_mcmc_model_joint_sT()
         x0 = sample_prior(lp.spec, nwalkers, np.random.default_rng(seed))
         x = torch.from_numpy(x0).to("cuda:%d" % self.device)
-        if sampler == "device":
-            res = DeviceDEMetropolis(lp, tune_interval=tune_interval, seed=seed).run(x, tune, draws)
-        else:
-            res = DEMetropolis(lambda th: lp(th), tune_interval=tune_interval, seed=seed).run(x, tune, draws)
+        res = sample_model(lp.spec, self.max_walkers, self.device, x, tune, draws, seed, tune_interval, sampler,
+                           space, cache=self.__dict__)
         res = {k: (v.cpu().numpy() if hasattr(v, "cpu") else v) for k, v in res.items()}
         res["roles"] = list(lp.spec.roles)
         if self.savedir:

@@ -1,152 +1,388 @@
-"""Ensemble Differential-Evolution Metropolis sampler over the batched log-prob.
+"""DEMetropolisZ over the batched log-prob: the reference's sampler, one chain per walker.
 
-The reference samples with PyMC3 3.11.2 ``DEMetropolisZ`` (run_age_mcmc_utils.py:412-417,
-ng_interp/noble_gas_mcmc.py:410-415): one log-prob per proposal per chain, chains in
-separate processes.  Here the whole ensemble of W walkers moves at once (population
-DE-MC, ter Braak 2006 -- PyMC3's ``DEMetropolis`` flavour): every step proposes
+The reference samples with PyMC3 3.11.2 ``DEMetropolisZ`` (run_age_mcmc_utils.py:412-417:
+tune=10000, draws=10000, chains=3, tune_interval=1000; ng_interp/noble_gas_mcmc.py:410-415:
+tune=10000, draws=50000, chains=4, tune_interval=5000), one log-prob per proposal per
+chain, chains in separate processes.  Here W chains run at once and every step evaluates
+ONE batched log-prob.  Each chain is exactly a PyMC3 DEMetropolisZ chain
+(pymc3/step_methods/metropolis.py ``DEMetropolisZ.astep``/``stop_tuning``):
 
-    x*_i = x_i + lamb * (x_r1 - x_r2) + eps_i,   r1 != r2 != i,  eps ~ U(-scaling, scaling)
+* proposal  x* = x + lamb_w (z1 - z2) + eps,  eps ~ U(-1, 1) * S * scaling_w per parameter
+  (S: PyMC3's proposal scale vector, default ones), with
+  z1 != z2 drawn uniformly from the chain's OWN history of past states (noise only while
+  the history holds fewer than 2 entries).  Chains never read each other's states, so they
+  stay independent (no population move, nothing to shard but the log-prob);
+* accept iff mr = logp(x*) - logp(x) is finite and log(u) < mr (``metrop_select``);
+* tuning (tune='lambda' by default, or 'scaling', or None): every ``tune_interval`` steps
+  of the tuning phase the chain's lamb (or scaling) is multiplied by ``pymc3_tune`` of its
+  acceptance rate over the interval;
+* ``stop_tuning`` before the first draw drops the oldest ``tune_drop_fraction`` of the
+  history, so draws are not proposed from unconverged tuning states.
 
-for all walkers, evaluates ONE batched log-prob on the GPU and accepts per walker with the
-Metropolis rule.  ``scaling`` is tuned every ``tune_interval`` steps with PyMC3's
-acceptance-rate schedule (pymc3/step_methods/metropolis.py ``tune``); ``lamb`` defaults to
-2.38 / sqrt(2 d) as in PyMC3.  Walkers are the LAST axis of every array ([..., W]), which
-is the structure-of-arrays layout the engine consumes with no transposes.
+The chains sample the PyMC3 models' free variables in their natural (untransformed)
+space; PyMC3 proposes in its transformed space (logodds / interval / log).  Both target
+the same posterior; the proposal geometry differs (parity of the chains themselves is
+unpinned -- PyMC3 is not installed anywhere here; tests check the stationary
+distribution: analytic prior moments, and the reference's posterior summaries).
 
-Runs on torch tensors (CUDA for the GPU engine, CPU for tests with a CPU log-prob).
+Random numbers are counter-based (splitmix64 of (seed, step, chain[, element])), the same
+stream in ``DEMetropolisZ`` (torch ops, any device, any batched log_prob) and
+``DeviceDEMetropolisZ`` (libngrtd ``ngrtd_demcz_run``: proposal + history append in one
+kernel, log-prob + Metropolis decision + tuning in the next; no host round trip per step),
+so on the same log-prob the two produce bitwise the same chains.
 """
 import math
 
 import torch
 
+from . import _lib
+
+_M64 = (1 << 64) - 1
+
+
+def _s64(v):
+    """Python uint64 -> the int64 with the same bits."""
+    v &= _M64
+    return v - (1 << 64) if v >> 63 else v
+
+
+def _lsr(z, k):
+    """Logical right shift of int64 tensors (torch's >> is arithmetic)."""
+    return (z >> k) & ((1 << (64 - k)) - 1)
+
+
+_C1, _C2, _C3 = _s64(0x9E3779B97F4A7C15), _s64(0xBF58476D1CE4E5B9), _s64(0x94D049BB133111EB)
+
+
+def mix_t(z):
+    """splitmix64 finaliser on int64 tensors (wrapping arithmetic), = ngrtd_kernels.hpp rng_mix."""
+    z = z + _C1
+    z = (z ^ _lsr(z, 30)) * _C2
+    z = (z ^ _lsr(z, 27)) * _C3
+    return z ^ _lsr(z, 31)
+
+
+def mix_int(z):
+    z = (z + 0x9E3779B97F4A7C15) & _M64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _M64
+    return z ^ (z >> 31)
+
+
+def step_key(seed, step):
+    """demc_key: the random key of step `step` of a run seeded `seed`."""
+    return mix_int((mix_int(seed & _M64) + step) & _M64)
+
+
+def unit_t(h):
+    """(0, 1) uniform of a hash (rng_unit): ((h >> 11) + 0.5) 2^-53."""
+    return (_lsr(h, 11).to(torch.float64) + 0.5) * (1.0 / 9007199254740992.0)
+
 
 def pymc3_tune(scale, acc_rate):
-    """pymc3.step_methods.metropolis.tune (3.11): multiplicative scaling update."""
-    if acc_rate < 0.001:
-        return scale * 0.1
-    if acc_rate < 0.05:
-        return scale * 0.5
-    if acc_rate < 0.2:
-        return scale * 0.9
-    if acc_rate > 0.95:
-        return scale * 10.0
-    if acc_rate > 0.75:
-        return scale * 2.0
-    if acc_rate > 0.5:
-        return scale * 1.1
-    return scale
+    """pymc3.step_methods.metropolis.tune (3.11): multiplicative update from the
+    acceptance rate of the last tune interval (elementwise on tensors)."""
+    c = lambda v: torch.full_like(scale, v)   # noqa: E731  (float64 factors, as numpy's)
+    f = torch.where(acc_rate < 0.001, c(0.1), torch.where(acc_rate < 0.05, c(0.5), torch.where(
+        acc_rate < 0.2, c(0.9), torch.where(acc_rate > 0.95, c(10.0), torch.where(
+            acc_rate > 0.75, c(2.0), torch.where(acc_rate > 0.5, c(1.1), c(1.0)))))))
+    return scale * f
 
 
-class DEMetropolis:
-    """Vectorised population DE-MC over walkers (last axis)."""
+def default_lamb(ndim):
+    """PyMC3: 2.38 / sqrt(2 ndim), optimal for normal targets."""
+    return 2.38 / math.sqrt(2 * ndim)
 
-    def __init__(self, log_prob, lamb=None, scaling=1e-3, tune_interval=100, seed=123423):
+
+class Transform:
+    """PyMC3 3.11 default transforms of the free variables, per theta row
+    (pymc3/distributions/transforms.py): Beta -> LogOdds, Uniform -> Interval(a, b),
+    HalfNormal -> Log, Normal -> none.  ``backward`` is the same arithmetic as the
+    device's pymc3_backward (ngrtd_kernels.hpp), so both give the same bits."""
+
+    NONE, LOGODDS, INTERVAL, LOG = 0, 1, 2, 3
+
+    def __init__(self, kind, a, b, L=1):
+        self.kind = [int(k) for k in kind]        # per parameter p
+        self.a = [float(v) for v in a]
+        self.b = [float(v) for v in b]
+        self.L = int(L)
+
+    @classmethod
+    def from_spec(cls, spec):
+        kind, a, b = [], [], []
+        for role in spec.roles:
+            lo = hi = 0.0
+            if role.endswith("_beta"):
+                k = cls.LOGODDS
+            elif role in ("tau1", "tau2", "f1", "eta1", "eta2", "D1", "D2"):
+                k = cls.INTERVAL
+                lo, hi = getattr(spec.rtd, role)
+            elif role == "lamsf6":
+                k = cls.LOG
+            else:                                   # m, J: Normal priors, untransformed
+                k = cls.NONE
+            kind.append(k)
+            a.append(lo)
+            b.append(hi)
+        return cls(kind, a, b, spec.n_wells)
+
+    def _rows(self, t):
+        return t.reshape(-1, len(self.kind), self.L, t.shape[-1])
+
+    def backward(self, u):
+        """u [..., P, L, W] (any leading dims) -> natural x."""
+        ur = self._rows(u)
+        out = torch.empty_like(ur)
+        for p, k in enumerate(self.kind):
+            v = ur[:, p]
+            if k == self.LOGODDS:
+                out[:, p] = 1.0 / (1.0 + torch.exp(-v))
+            elif k == self.INTERVAL:
+                sg = 1.0 / (1.0 + torch.exp(-v))
+                out[:, p] = sg * self.b[p] + (1.0 - sg) * self.a[p]
+            elif k == self.LOG:
+                out[:, p] = torch.exp(v)
+            else:
+                out[:, p] = v
+        return out.reshape(u.shape)
+
+    def forward(self, x):
+        """natural x -> u (logit, log((x - a) / (b - x)), log)."""
+        xr = self._rows(x)
+        out = torch.empty_like(xr)
+        for p, k in enumerate(self.kind):
+            v = xr[:, p]
+            if k == self.LOGODDS:
+                out[:, p] = torch.log(v) - torch.log1p(-v)
+            elif k == self.INTERVAL:
+                out[:, p] = torch.log(v - self.a[p]) - torch.log(self.b[p] - v)
+            elif k == self.LOG:
+                out[:, p] = torch.log(v)
+            else:
+                out[:, p] = v
+        return out.reshape(x.shape)
+
+    def fill(self, c):
+        """Copy into an ngrtd_demcz_state (tr_kind / tr_a / tr_b per parameter row)."""
+        for p, k in enumerate(self.kind):
+            c.tr_kind[p], c.tr_a[p], c.tr_b[p] = k, self.a[p], self.b[p]
+
+
+def _result(hist, lp_log, acc_log, tune, draws, lamb, scaling, x, lp):
+    acc = acc_log[tune:].to(torch.float64)
+    return {"samples": hist[tune:tune + draws], "logp": lp_log[tune:tune + draws],
+            "accepted": acc_log[tune:tune + draws], "accept_rate": float(acc.mean()) if draws else 0.0,
+            "tune_accept_rate": float(acc_log[:tune].to(torch.float64).mean()) if tune else 0.0,
+            "lamb": lamb, "scaling": scaling, "x": x, "lp": lp, "tuning_steps": tune}
+
+
+class DEMetropolisZ:
+    """PyMC3 DEMetropolisZ for the W chains of x0 [..., W] on torch ops (any device).
+
+    log_prob: callable theta [..., W] -> logp [W] (e.g. engine.LogProb, or a CPU oracle)."""
+
+    def __init__(self, log_prob, lamb=None, scaling=0.001, tune="lambda", tune_interval=100,
+                 tune_drop_fraction=0.9, seed=123423, chain0=0, n_chains_total=None, S=None, transform=None):
+        if tune not in (None, "none", "scaling", "lambda"):
+            raise ValueError('tune must be None, "scaling" or "lambda" (pymc3 DEMetropolisZ)')
+        self.transform = transform               # Transform: chains in PyMC3's transformed space
+        self.S = S                               # proposal scale per parameter (x[..., 0] shape), None = ones
+        self.chain0 = int(chain0)                # global index of chain 0 (walker-block shards)
+        self.n_chains_total = n_chains_total
         self.log_prob = log_prob
         self.lamb = lamb
         self.scaling = scaling
-        self.tune_interval = tune_interval
-        self.seed = seed
+        self.tune = tune
+        self.tune_interval = int(tune_interval)
+        self.tune_drop_fraction = float(tune_drop_fraction)
+        self.seed = int(seed)
 
-    def run(self, x0, tune, draws, thin=1, callback=None):
-        """x0: [..., W] tensor.  Returns dict(samples [n_kept, ..., W], logp [n_kept, W],
-        accept_rate, scaling)."""
-        x = x0.clone()
-        W = x.shape[-1]
-        d = int(x[..., 0].numel())
-        if W < 3:
-            raise ValueError("population DE needs at least 3 walkers")
-        lamb = self.lamb if self.lamb is not None else 2.38 / math.sqrt(2 * d)
-        g = torch.Generator(device=x.device)
-        g.manual_seed(self.seed)
-        lp = self.log_prob(x)
-        scaling = self.scaling
-        samples, logps = [], []
-        n_acc_window = torch.zeros((), dtype=torch.float64, device=x.device)
-        n_acc_total = torch.zeros((), dtype=torch.float64, device=x.device)
-        idx = torch.arange(W, device=x.device)
-        for it in range(tune + draws):
-            # two distinct partners r1 != r2, both != i
-            r1 = (idx + torch.randint(1, W, (W,), generator=g, device=x.device)) % W
-            off = torch.randint(1, W - 1, (W,), generator=g, device=x.device)
-            r2 = (r1 + off) % W
-            r2 = torch.where(r2 == idx, (r2 + 1) % W, r2)
-            r2 = torch.where(r2 == r1, (r2 + 1) % W, r2)
-            eps = (torch.rand(x.shape, generator=g, device=x.device, dtype=x.dtype) * 2 - 1) * scaling
-            prop = x + lamb * (x[..., r1] - x[..., r2]) + eps
-            lp_prop = self.log_prob(prop)
-            logu = torch.log(torch.rand((W,), generator=g, device=x.device, dtype=lp.dtype))
-            acc = (lp_prop - lp) > logu
-            acc = acc & ~torch.isnan(lp_prop)
+    def run(self, x0, tune, draws):
+        """Returns dict(samples [draws, ..., W] (natural space), logp [draws, W], accepted
+        [draws, W] (uint8), accept_rate, lamb [W], scaling [W], x, lp).  With a transform the
+        chains move in u = transform.forward(x0), log_prob must return the log-density of u
+        (natural log-prob + log|Jacobian|, e.g. a LogProb of a spec with jacobian=True), and
+        it is called on the natural values backward(u)."""
+        tf = self.transform
+        u = tf.forward(x0) if tf is not None else x0.clone()
+        x = u
+        lead, W = x.shape[:-1], x.shape[-1]
+        R = int(x[..., 0].numel())
+        dev = x.device
+        lamb = torch.full((W,), self.lamb if self.lamb is not None else default_lamb(R), dtype=torch.float64,
+                          device=dev)
+        scaling = torch.full((W,), float(self.scaling), dtype=torch.float64, device=dev)
+        lp = self.log_prob(tf.backward(x) if tf is not None else x).clone()
+        if not bool(torch.isfinite(lp).all()):
+            raise ValueError("initial log-prob is not finite for every chain (pymc3: 'Initial evaluation of model "
+                             "at starting point failed')")
+        n = tune + draws
+        hist = torch.empty((n,) + tuple(x.shape), dtype=x.dtype, device=dev)
+        lp_log = torch.empty((n, W), dtype=torch.float64, device=dev)
+        acc_log = torch.empty((n, W), dtype=torch.uint8, device=dev)
+        n_acc_tune = torch.zeros(W, dtype=torch.int32, device=dev)
+        hist_lo = 0
+        w_loc = torch.arange(W, device=dev, dtype=torch.int64)
+        w_idx = w_loc + self.chain0                                      # global chain index
+        Wg = int(self.n_chains_total or W)
+        e_idx = (torch.arange(R, device=dev, dtype=torch.int64)[:, None] * Wg + w_idx[None, :])  # r Wg + chain
+        target = {"scaling": 1, "lambda": 2}.get(self.tune, 0)
+        S = None if self.S is None else torch.as_tensor(self.S, dtype=torch.float64, device=dev).reshape(R, 1)
+        for s in range(n):
+            if s == tune and tune > 0:                       # stop_tuning: drop the oldest entries
+                hist_lo += int(self.tune_drop_fraction * (s - hist_lo))
+            key = step_key(self.seed, s)
+            it = s - hist_lo
+            xr = x.reshape(R, W)
+            if it > 1:
+                hp = mix_t(w_idx + _s64(mix_int((key + 1) & _M64)))
+                iz1 = (_lsr(hp, 32) * it) >> 32
+                iz2 = ((hp & 0xFFFFFFFF) * (it - 1)) >> 32
+                iz2 = iz2 + (iz2 >= iz1).to(torch.int64)
+                hr = hist.reshape(n, R, W)
+                z1 = hr[hist_lo + iz1, :, w_loc].T            # [R][W]
+                z2 = hr[hist_lo + iz2, :, w_loc].T
+                y = xr + lamb * (z1 - z2)
+            else:
+                y = xr
+            ke = _s64(mix_int((key + 2) & _M64))
+            u2 = 2.0 * unit_t(mix_t(e_idx + ke)) - 1.0
+            eps = (u2 if S is None else u2 * S) * scaling
+            prop = (y + eps).reshape(x.shape)
+            lp_prop = self.log_prob(tf.backward(prop) if tf is not None else prop)
+            logu = torch.log(unit_t(mix_t(w_idx + _s64(mix_int((key + 3) & _M64)))))
+            mr = lp_prop - lp
+            acc = torch.isfinite(mr) & (logu < mr)
             x = torch.where(acc, prop, x)
             lp = torch.where(acc, lp_prop, lp)
-            na = acc.sum().to(torch.float64)
-            n_acc_window += na
-            if it >= tune:
-                n_acc_total += na
-                if (it - tune) % thin == 0:
-                    samples.append(x.clone())
-                    logps.append(lp.clone())
-            elif (it + 1) % self.tune_interval == 0:
-                rate = float(n_acc_window) / (self.tune_interval * W)
-                scaling = pymc3_tune(scaling, rate)
-                n_acc_window.zero_()
-            if callback is not None:
-                callback(it, x, lp)
-        return {"samples": torch.stack(samples) if samples else x[None][:0],
-                "logp": torch.stack(logps) if logps else lp[None][:0],
-                "accept_rate": float(n_acc_total) / max(1, draws * W),
-                "scaling": scaling, "lamb": lamb}
+            n_acc_tune += acc.to(torch.int32)
+            if target and s + 1 < tune and (s + 1) % self.tune_interval == 0:
+                rate = n_acc_tune.to(torch.float64) / self.tune_interval
+                if target == 2:
+                    lamb = pymc3_tune(lamb, rate)
+                else:
+                    scaling = pymc3_tune(scaling, rate)
+                n_acc_tune.zero_()
+            hist[s] = x
+            lp_log[s] = lp
+            acc_log[s] = acc.to(torch.uint8)
+        if tf is not None:
+            hist = tf.backward(hist)
+            x = tf.backward(x)
+        return _result(hist, lp_log, acc_log, tune, draws, lamb, scaling, x, lp)
 
 
-class DeviceDEMetropolis:
-    """The same population DE-MC as DEMetropolis, run device-resident by libngrtd
-    (ngrtd_demc_run: a proposal kernel + the log-prob kernel with the Metropolis accept in
-    its per-walker reduction, 2 launches per step, counter-based random numbers).  The host
-    only intervenes every ``tune_interval`` steps (PyMC3 scaling schedule) and every
-    ``thin`` draws (sample snapshot).  Same result dict as DEMetropolis.run; the random
-    stream differs, so chains match DEMetropolis in distribution, not bit for bit."""
+class ZState:
+    """Device state of a DEMetropolisZ run (ngrtd_demcz_state): per-chain lamb / scaling /
+    tuning counters and the chain histories [cap][NC][W][16] (NC = ceil(R / 16)), which
+    also hold the draws."""
 
-    def __init__(self, logprob, lamb=None, scaling=1e-3, tune_interval=100, seed=123423):
+    def __init__(self, R, W, hist_cap, device, lamb, scaling, n_tune, tune_interval, tune_target,
+                 drop_fraction, seed, chain0=0, n_chains_total=0, S=None):
+        self.R, self.W = int(R), int(W)
+        self.NC = (self.R + _lib.Z_CHUNK - 1) // _lib.Z_CHUNK
+        self.lamb = torch.full((W,), float(lamb), dtype=torch.float64, device=device)
+        self.scaling = torch.full((W,), float(scaling), dtype=torch.float64, device=device)
+        self.n_acc_tune = torch.zeros(W, dtype=torch.int32, device=device)
+        self.hist = torch.empty((int(hist_cap), self.NC, W, _lib.Z_CHUNK), dtype=torch.float64, device=device)
+        self.u = None                     # transformed-space chains (set by DeviceDEMetropolisZ.start)
+        self.S = (None if S is None else
+                  torch.as_tensor(S, dtype=torch.float64).reshape(self.R).contiguous().to(device))
+        self.c = _lib.DemczState(lamb=self.lamb.data_ptr(), scaling=self.scaling.data_ptr(),
+                                 n_acc_tune=self.n_acc_tune.data_ptr(), hist=self.hist.data_ptr(),
+                                 hist_cap=int(hist_cap), hist_len=0, hist_lo=0, steps_done=0, n_tune=int(n_tune),
+                                 tune_interval=int(tune_interval), tune_target=int(tune_target),
+                                 drop_fraction=float(drop_fraction), seed=int(seed) & _M64,
+                                 chain0=int(chain0), n_chains_total=int(n_chains_total or 0),
+                                 S=self.S.data_ptr() if self.S is not None else None)
+
+    def entries(self, lo, hi):
+        """History entries [lo, hi) as [hi - lo][R][W]."""
+        h = self.hist[lo:hi].permute(0, 1, 3, 2).reshape(hi - lo, self.NC * _lib.Z_CHUNK, self.W)
+        return h[:, :self.R]
+
+
+class DeviceDEMetropolisZ:
+    """The same DEMetropolisZ run device-resident by libngrtd (ngrtd_demcz_run): one C call
+    for the whole run, two launches per step, no host synchronisation until the end.
+    Same random stream as DEMetropolisZ, so on the same log-prob the chains agree bitwise.
+
+    transformed: chains in PyMC3's transformed space (Transform.from_spec) -- the default
+    when the plan's spec has jacobian=True (the log-prob is then the density of u); else
+    the natural space."""
+
+    def __init__(self, logprob, lamb=None, scaling=0.001, tune="lambda", tune_interval=100,
+                 tune_drop_fraction=0.9, seed=123423, chain0=0, n_chains_total=None, S=None, transformed=None):
+        if tune not in (None, "none", "scaling", "lambda"):
+            raise ValueError('tune must be None, "scaling" or "lambda" (pymc3 DEMetropolisZ)')
+        if transformed is None:
+            transformed = bool(logprob.spec.jacobian)
+        if transformed and not logprob.spec.jacobian:
+            raise ValueError("transformed-space chains need a LogProb of a spec with jacobian=True")
+        self.transform = Transform.from_spec(logprob.spec) if transformed else None
+        self.S = S
+        self.chain0 = int(chain0)
+        self.n_chains_total = n_chains_total
         self.lp = logprob               # engine.LogProb
         self.lamb = lamb
         self.scaling = scaling
-        self.tune_interval = tune_interval
-        self.seed = seed
+        self.tune = tune
+        self.tune_interval = int(tune_interval)
+        self.tune_drop_fraction = float(tune_drop_fraction)
+        self.seed = int(seed)
 
-    def run(self, x0, tune, draws, thin=1, callback=None):
-        x = x0.clone().contiguous()
+    def start(self, x0, n_tune, hist_cap):
+        """Device state for chains x0 [P][L][W] (natural space, CUDA float64): (x, lp, ZState);
+        x = backward(forward(x0)) for transformed chains (ZState.u holds the chains)."""
+        tf = self.transform
+        u = tf.forward(x0).contiguous() if tf is not None else None
+        x = tf.backward(u).contiguous() if tf is not None else x0.clone().contiguous()
         W = x.shape[-1]
-        d = int(x[..., 0].numel())
-        if W < 3:
-            raise ValueError("population DE needs at least 3 walkers")
-        lamb = self.lamb if self.lamb is not None else 2.38 / math.sqrt(2 * d)
+        R = int(x[..., 0].numel())
         lp = self.lp(x).clone()
-        cnt = torch.zeros(1, dtype=torch.int64, device=x.device)
-        scaling = self.scaling
-        step = 0
-        # tuning: chunks of tune_interval steps, PyMC3 schedule on the chunk's rate
-        while step < tune:
-            n = min(self.tune_interval, tune - step)
-            cnt.zero_()
-            self.lp.demc(x, lp, n, lamb, scaling, self.seed, step, n_accepted=cnt)
-            step += n
-            if n == self.tune_interval:
-                scaling = pymc3_tune(scaling, float(cnt.item()) / (n * W))
-            if callback is not None:
-                callback(step - 1, x, lp)
-        samples, logps = [], []
-        cnt.zero_()
-        kept = 0
-        while kept * thin < draws:
-            n = min(thin, draws - kept * thin)
-            self.lp.demc(x, lp, n, lamb, scaling, self.seed, step, n_accepted=cnt)
-            step += n
-            samples.append(x.clone())
-            logps.append(lp.clone())
-            kept += 1
-            if callback is not None:
-                callback(step - 1, x, lp)
-        return {"samples": torch.stack(samples) if samples else x[None][:0],
-                "logp": torch.stack(logps) if logps else lp[None][:0],
-                "accept_rate": float(cnt.item()) / max(1, draws * W),
-                "scaling": scaling, "lamb": lamb}
+        if not bool(torch.isfinite(lp).all()):
+            raise ValueError("initial log-prob is not finite for every chain (pymc3: 'Initial evaluation of model "
+                             "at starting point failed')")
+        z = ZState(R, W, hist_cap, x.device, self.lamb if self.lamb is not None else default_lamb(R), self.scaling,
+                   n_tune, self.tune_interval, _lib.TUNE_TARGET[self.tune], self.tune_drop_fraction, self.seed,
+                   self.chain0, self.n_chains_total, self.S)
+        if tf is not None:
+            z.u = u
+            z.c.theta_u = u.data_ptr()
+            tf.fill(z.c)
+        return x, lp, z
+
+    def run(self, x0, tune, draws):
+        n = tune + draws
+        x, lp, z = self.start(x0, tune, n)
+        W = x.shape[-1]
+        acc_log = torch.empty((n, W), dtype=torch.uint8, device=x.device)
+        lp_log = torch.empty((n, W), dtype=torch.float64, device=x.device)
+        self.lp.demcz(x, lp, n, z, accepted_log=acc_log, logp_log=lp_log)
+        hist = z.entries(0, n).reshape((n,) + tuple(x.shape))
+        if self.transform is not None:              # the histories hold u: report natural draws
+            hist = self.transform.backward(hist)
+        return _result(hist, lp_log, acc_log, tune, draws, z.lamb, z.scaling, x, lp)
+
+
+def sample_model(spec, max_walkers, device, x0, tune, draws, seed, tune_interval, sampler="device",
+                 space="transformed", cache=None):
+    """DEMetropolisZ on the log-prob of ``spec`` (the drivers' mc.sample replacement):
+    space "transformed" samples PyMC3's free variables (a plan with the Jacobian),
+    "natural" theta itself.  ``cache``: a dict that keeps the sampling plan between calls."""
+    import dataclasses
+    from .engine import LogProb
+    if space not in ("transformed", "natural"):
+        raise ValueError('space must be "transformed" or "natural"')
+    jac = space == "transformed"
+    cache = {} if cache is None else cache
+    key = "_sampling_lp_%s" % space
+    lp = cache.get(key)
+    if lp is None:
+        lp = LogProb(dataclasses.replace(spec, jacobian=jac), max_walkers, device)
+        cache[key] = lp
+    if sampler == "device":
+        return DeviceDEMetropolisZ(lp, tune_interval=tune_interval, seed=seed, transformed=jac).run(x0, tune, draws)
+    tf = Transform.from_spec(spec) if jac else None
+    return DEMetropolisZ(lambda th: lp(th), tune_interval=tune_interval, seed=seed, transform=tf).run(x0, tune, draws)

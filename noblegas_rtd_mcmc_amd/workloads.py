@@ -115,6 +115,39 @@ def sample_prior(spec, W, rng):
     return th
 
 
+def prior_sd(spec):
+    """Prior standard deviation of every theta row [P][L] -- a per-parameter proposal scale
+    (PyMC3 DEMetropolisZ's S) that puts the U(-S, S) * scaling noise of every dimension on
+    the same footing.  Uniform (b - a)/sqrt(12), Beta sqrt(ab/((a+b)^2 (a+b+1))), Normal sd,
+    HalfNormal sd sqrt(1 - 2/pi)."""
+    def beta_sd(ab):
+        a, b = ab
+        return np.sqrt(a * b / ((a + b) ** 2 * (a + b + 1)))
+    c, r = spec.ce, spec.rtd
+    sd = []
+    for role in spec.roles:
+        if role in ("Ae_beta", "F_beta", "E_beta", "b_beta", "nu_ce_beta"):
+            v = beta_sd({"Ae_beta": c.beta_Ae, "F_beta": c.beta_F, "E_beta": c.beta_E, "b_beta": c.beta_b,
+                         "nu_ce_beta": c.beta_nu}[role])
+        elif role == "m":
+            v = c.m_sd
+        elif role == "nu_rtd_beta":
+            v = beta_sd(r.beta_nu)
+        elif role == "thalf_cfc_beta":
+            v = beta_sd(r.beta_thalf)
+        elif role in ("tau1", "tau2", "f1", "eta1", "eta2", "D1", "D2"):
+            lo, hi = getattr(r, role)
+            v = (hi - lo) / np.sqrt(12.0)
+        elif role == "J":
+            v = r.J_sd
+        elif role == "lamsf6":
+            v = r.lamsf6_sd * np.sqrt(1 - 2 / np.pi)
+        else:
+            raise ValueError(role)
+        sd.append(v)
+    return np.repeat(np.array(sd, dtype=np.float64)[:, None], spec.n_wells, axis=1)
+
+
 def c1(W=100):
     spec = ModelSpec(n_wells=1, ce=ce_block(["PLM1"], ("Ne", "Ar", "Kr", "Xe")))
     return spec, sample_prior(spec, W, np.random.default_rng(12345))

@@ -55,6 +55,9 @@ int main(void) {
   printf("%zu %zu %zu %zu %zu %zu\n", sizeof(ngrtd_model_desc), sizeof(ngrtd_tracer_desc),
          offsetof(ngrtd_model_desc, tracers), offsetof(ngrtd_model_desc, rtd_obs),
          offsetof(ngrtd_model_desc, rtd_nu_b), offsetof(ngrtd_model_desc, ce_beta_b));
+  printf("%zu %zu %zu %zu %zu %zu\n", sizeof(ngrtd_demcz_state), offsetof(ngrtd_demcz_state, hist_cap),
+         offsetof(ngrtd_demcz_state, tune_interval), offsetof(ngrtd_demcz_state, drop_fraction),
+         offsetof(ngrtd_demcz_state, seed), offsetof(ngrtd_demcz_state, tr_b));
   return 0;
 }'''
     tmp = "/tmp/ngrtd_layout_%d" % os.getpid()
@@ -62,9 +65,10 @@ int main(void) {
         f.write(src)
     subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), tmp + ".c", "-o", tmp], check=True)
     vals = [int(x) for x in subprocess.run([tmp], capture_output=True, text=True).stdout.split()]
-    M, T = _lib.ModelDesc, _lib.TracerDesc
+    M, T, Z = _lib.ModelDesc, _lib.TracerDesc, _lib.DemczState
     assert vals == [C.sizeof(M), C.sizeof(T), M.tracers.offset, M.rtd_obs.offset, M.rtd_nu_b.offset,
-                    M.ce_beta_b.offset]
+                    M.ce_beta_b.offset, C.sizeof(Z), Z.hist_cap.offset, Z.tune_interval.offset,
+                    Z.drop_fraction.offset, Z.seed.offset, Z.tr_b.offset]
 
 
 def test_roles_match_spec():

@@ -36,26 +36,29 @@ def _worker(rank, world, port, W, outdir):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from noblegas_rtd_mcmc_amd import workloads as wl
-        from noblegas_rtd_mcmc_amd.distributed import ShardedLogProb, sharded_de_step_loop
+        from noblegas_rtd_mcmc_amd.distributed import ShardedLogProb, sharded_demcz
         spec = _spec()
         full = torch.from_numpy(wl.sample_prior(spec, W, np.random.default_rng(5)))
         sh = ShardedLogProb(_oracle_eval(spec), W)
         blk = sh.block(full)
         lp_b, lp_full = sh(blk)
         pos = sh.gather_positions(blk)
-        x, lp, kept, scaling = sharded_de_step_loop(sh, blk, tune=4, draws=3, seed=3, tune_interval=2,
-                                                    exchange="positions")
-        x2, lp2, kept2, _ = sharded_de_step_loop(sh, blk, tune=2, draws=2, seed=3, tune_interval=2, exchange="logp")
+        res, lp_tr, acc_tr = sharded_demcz(_oracle_eval(spec), blk, W, tune=6, draws=4, seed=3, tune_interval=2)
         np.savez(os.path.join(outdir, "r%d.npz" % rank), lp_full=lp_full.numpy(), pos=pos.numpy(),
-                 kept=kept.numpy(), x=x.numpy(), lp=lp.numpy(), lo=sh.lo, hi=sh.hi, kept2=kept2.numpy())
+                 lp_tr=lp_tr.numpy(), acc_tr=acc_tr.numpy(), x=res["x"].numpy(), lp=res["lp"].numpy(),
+                 samples=res["samples"].numpy(), lo=sh.lo, hi=sh.hi)
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("W", [9, 16])
 def test_walker_block_allgather_matches_single_process(tmp_path, W):
+    """Sharded DEMetropolisZ: the union of the two ranks' chains is bitwise the
+    single-process run of the whole ensemble (chains draw the random numbers of their
+    global index), and the gathered trace log-probs are the same on both ranks."""
     import oracle.models as om
     from noblegas_rtd_mcmc_amd import workloads as wl
+    from noblegas_rtd_mcmc_amd.sampler import DEMetropolisZ
     port = _free_port()
     mp.start_processes(_worker, args=(2, port, W, str(tmp_path)), nprocs=2, start_method="spawn")
     r0, r1 = (np.load(tmp_path / ("r%d.npz" % r)) for r in (0, 1))
@@ -66,11 +69,13 @@ def test_walker_block_allgather_matches_single_process(tmp_path, W):
     assert np.array_equal(r0["pos"], full) and np.array_equal(r1["pos"], full)
     # blocks tile the ensemble
     assert int(r0["lo"]) == 0 and int(r0["hi"]) == int(r1["lo"]) and int(r1["hi"]) == W
-    # every rank sees the same gathered trace of log-probs
-    assert np.array_equal(r0["kept"], r1["kept"]) and np.array_equal(r0["kept2"], r1["kept2"])
-    # the final block log-probs are consistent with the positions
-    lp_chk = om.log_prob(spec, r1["x"])
-    assert np.allclose(lp_chk, r1["lp"], rtol=1e-13)
+    one = DEMetropolisZ(_oracle_eval(spec), seed=3, tune_interval=2).run(torch.from_numpy(full), tune=6, draws=4)
+    assert np.array_equal(np.concatenate([r0["x"], r1["x"]], axis=-1), one["x"].numpy())
+    assert np.array_equal(np.concatenate([r0["samples"], r1["samples"]], axis=-1), one["samples"].numpy())
+    assert np.array_equal(r0["lp_tr"], one["logp"].numpy()) and np.array_equal(r1["lp_tr"], one["logp"].numpy())
+    assert np.array_equal(r0["acc_tr"], one["accepted"].numpy())
+    # the final chain log-probs are consistent with the positions
+    assert np.allclose(om.log_prob(spec, r1["x"]), r1["lp"], rtol=1e-13)
 
 
 def test_shard_walkers_partition():

@@ -72,36 +72,91 @@ def test_series_from_reference_frames():
     assert ser.dtp == 3.0 and ser.c_by_age[0] == 9.0
 
 
-def test_de_sampler_gaussian():
-    """Population DE-MC recovers a correlated 2-D Gaussian (CPU, torch)."""
-    from noblegas_rtd_mcmc_amd.sampler import DEMetropolis
+def test_demcz_gaussian_moments():
+    """DEMetropolisZ recovers a correlated 2-D Gaussian: the final states of 2000
+    independent chains are draws from the target, so their mean and covariance must sit
+    within 4 Monte-Carlo standard errors of the truth (CPU, torch)."""
+    from noblegas_rtd_mcmc_amd.sampler import DEMetropolisZ
     cov = np.array([[1.0, 0.6], [0.6, 2.0]])
     P = torch.from_numpy(np.linalg.inv(cov))
 
     def lp(x):   # x [2, W]
         return -0.5 * torch.einsum("iw,ij,jw->w", x, P, x)
-    x0 = torch.from_numpy(np.random.default_rng(0).normal(size=(2, 64)) * 3)
-    res = DEMetropolis(lp, tune_interval=50, seed=1).run(x0, tune=400, draws=800)
-    s = res["samples"].permute(0, 2, 1).reshape(-1, 2).numpy()
-    assert np.allclose(s.mean(0), 0, atol=0.12)
-    assert np.allclose(np.cov(s.T), cov, atol=0.3)
-    assert 0.05 < res["accept_rate"] < 0.9
-    again = DEMetropolis(lp, tune_interval=50, seed=1).run(x0, tune=400, draws=800)
+    W = 2000
+    x0 = torch.from_numpy(np.random.default_rng(0).normal(size=(2, W)) * 3)
+    res = DEMetropolisZ(lp, tune_interval=50, seed=1).run(x0, tune=300, draws=300)
+    fin = res["x"].numpy().T                                         # [W][2]
+    se_mean = np.sqrt(np.diag(cov) / W)
+    assert (np.abs(fin.mean(0)) < 4 * se_mean).all(), fin.mean(0)
+    c = np.cov(fin.T)
+    se_cov = np.sqrt((cov ** 2 + np.outer(np.diag(cov), np.diag(cov))) / W)   # Gaussian var of sample cov
+    assert (np.abs(c - cov) < 4 * se_cov).all(), c
+    assert 0.1 < res["accept_rate"] < 0.9
+    again = DEMetropolisZ(lp, tune_interval=50, seed=1).run(x0, tune=300, draws=300)
     assert torch.equal(again["samples"], res["samples"])
+
+
+def test_demcz_rng_matches_integer_reference():
+    """The torch splitmix64 (int64 tensors, wrapping) equals the integer restatement."""
+    from noblegas_rtd_mcmc_amd.sampler import mix_int, mix_t, _s64, unit_t
+    vals = [0, 1, 2 ** 63 - 1, 2 ** 63, 2 ** 64 - 1, 0x9E3779B97F4A7C15, 123456789123456789]
+    vals += list(np.random.default_rng(3).integers(0, 2 ** 63, 50, dtype=np.int64).tolist())
+    got = mix_t(torch.tensor([_s64(v) for v in vals], dtype=torch.int64)).tolist()
+    assert got == [_s64(mix_int(v)) for v in vals]
+    u = unit_t(torch.tensor([_s64(mix_int(v)) for v in vals], dtype=torch.int64))
+    assert bool(((u > 0) & (u < 1)).all())
+
+
+def test_demcz_partner_distribution_uniform():
+    """iz1 != iz2, each ordered pair of distinct history entries equally likely (so the
+    difference z1 - z2 is symmetric: no Hastings correction needed)."""
+    from noblegas_rtd_mcmc_amd.sampler import mix_int, mix_t, _s64, _lsr, step_key, _M64
+    for it in (2, 3, 5):
+        counts = np.zeros((it, it))
+        for s in range(40):
+            key = step_key(7, s)
+            w = torch.arange(4000, dtype=torch.int64)
+            hp = mix_t(w + _s64(mix_int((key + 1) & _M64)))
+            iz1 = (_lsr(hp, 32) * it) >> 32
+            iz2 = ((hp & 0xFFFFFFFF) * (it - 1)) >> 32
+            iz2 = iz2 + (iz2 >= iz1).to(torch.int64)
+            np.add.at(counts, (iz1.numpy(), iz2.numpy()), 1)
+        assert np.all(np.diag(counts) == 0)
+        off = counts[~np.eye(it, dtype=bool)]
+        expect = counts.sum() / (it * (it - 1))
+        assert np.all(np.abs(off - expect) < 5 * np.sqrt(expect)), (it, counts)
+        assert np.abs(counts - counts.T).max() < 5 * np.sqrt(2 * expect)
 
 
 def test_pymc3_tune_schedule():
     from noblegas_rtd_mcmc_amd.sampler import pymc3_tune
-    assert pymc3_tune(1.0, 0.0005) == 0.1 and pymc3_tune(1.0, 0.96) == 10.0 and pymc3_tune(1.0, 0.3) == 1.0
+    r = torch.tensor([0.0005, 0.01, 0.1, 0.3, 0.6, 0.8, 0.96], dtype=torch.float64)
+    got = pymc3_tune(torch.ones(7, dtype=torch.float64), r).tolist()
+    assert got == [0.1, 0.5, 0.9, 1.0, 1.1, 2.0, 10.0]
+
+
+def test_demcz_tuning_and_history_drop():
+    """lamb is tuned every tune_interval steps of the tuning phase only; stop_tuning drops
+    the oldest 90 % of the history (proposals after it draw from the kept entries)."""
+    from noblegas_rtd_mcmc_amd.sampler import DEMetropolisZ, default_lamb
+
+    def lp(x):
+        return -0.5 * (x ** 2).sum(0)
+    x0 = torch.from_numpy(np.random.default_rng(1).normal(size=(3, 16)))
+    res = DEMetropolisZ(lp, tune_interval=10, seed=4).run(x0, tune=35, draws=20)
+    assert not torch.equal(res["lamb"], torch.full((16,), default_lamb(3), dtype=torch.float64))
+    fixed = DEMetropolisZ(lp, tune=None, tune_interval=10, seed=4).run(x0, tune=35, draws=20)
+    assert torch.equal(fixed["lamb"], torch.full((16,), default_lamb(3), dtype=torch.float64))
+    assert res["samples"].shape == (20, 3, 16) and res["accepted"].shape == (20, 16)
 
 
 def test_ce_sampler_plumbing_with_cpu_logp():
-    """c1 plumbing: the DE sampler driving the CE log-prob (oracle as the CPU log-prob)."""
+    """c1 plumbing: DEMetropolisZ driving the CE log-prob (oracle as the CPU log-prob)."""
     import oracle.models as om
-    from noblegas_rtd_mcmc_amd.sampler import DEMetropolis
+    from noblegas_rtd_mcmc_amd.sampler import DEMetropolisZ
     spec, th = wl.c1(W=12)
 
     def lp(x):
         return torch.from_numpy(om.log_prob(spec, x.numpy()))
-    res = DEMetropolis(lp, tune_interval=5, seed=2).run(torch.from_numpy(th), tune=10, draws=5)
+    res = DEMetropolisZ(lp, tune_interval=5, seed=2).run(torch.from_numpy(th), tune=10, draws=5)
     assert res["samples"].shape == (5, 6, 1, 12) and torch.isfinite(res["logp"]).all()

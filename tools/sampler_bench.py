@@ -1,11 +1,15 @@
 #!/usr/bin/env python3
-"""MCMC sampler throughput on the c4 workload (2048 walkers x 64 wells): walker-steps/s of
-the device-resident DE-MC (ngrtd_demc_run: 2 launches per step) and of the torch-op
-DEMetropolis loop around the same log-prob kernel.  One JSON line.
+"""MCMC sampler throughput on the c4 workload (2048 chains x 64 wells): chain-steps/s of
+the device-resident DEMetropolisZ (ngrtd_demcz_run: proposal + history append, then the
+log-prob kernel with the Metropolis decision and tuning; 2 launches per step) in PyMC3's
+transformed space and in the natural space, and of the torch-op DEMetropolisZ loop
+around the same log-prob kernel.  With --profile the proposal kernel's own time is read
+from the plan's HIP-event profiling.  One JSON line.
 
     python tools/sampler_bench.py [--steps 200]
 """
 import argparse
+import dataclasses
 import json
 import os
 import sys
@@ -16,6 +20,19 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+def time_device(lp, x0, steps, warm=10):
+    import torch
+    from noblegas_rtd_mcmc_amd.sampler import DeviceDEMetropolisZ
+    s = DeviceDEMetropolisZ(lp, tune_interval=100, seed=7)
+    x, l, z = s.start(x0, 50, warm + steps)
+    lp.demcz(x, l, warm, z)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    lp.demcz(x, l, steps, z)
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=200)
@@ -24,33 +41,44 @@ def main():
     import torch
     from noblegas_rtd_mcmc_amd import workloads
     from noblegas_rtd_mcmc_amd.engine import LogProb
-    from noblegas_rtd_mcmc_amd.sampler import DEMetropolis
+    from noblegas_rtd_mcmc_amd.sampler import DEMetropolisZ, Transform
     W = args.walkers
     spec = workloads.c4_spec(L=64)
     th = workloads.sample_prior(spec, W, np.random.default_rng(34568))
-    lp = LogProb(spec, max_walkers=W)
-    x = torch.from_numpy(th).cuda()
-    lpv = lp(x).clone()
-    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
-    d = spec.n_params * spec.n_wells
-    lamb = 2.38 / np.sqrt(2 * d)
-    lp.demc(x, lpv, 10, lamb, 1e-3, 7, n_accepted=cnt)
+    x0 = torch.from_numpy(th).cuda()
+    R = spec.n_params * spec.n_wells
+    out = {"workload": "c4: %d chains x %d wells x 8 params (R = %d theta rows per chain)" % (W, spec.n_wells, R)}
+    lpn = LogProb(spec, max_walkers=W)
+    lpj = LogProb(dataclasses.replace(spec, jacobian=True), max_walkers=W)
+    dn = time_device(lpn, x0, args.steps)
+    dj = time_device(lpj, x0, args.steps)
+    # log-prob alone (same plan) for the split of the step
+    o = torch.empty(W, dtype=torch.float64, device="cuda")
+    for lp_, key in ((lpn, "natural"), (lpj, "transformed")):
+        run = lp_.bind(x0, o)
+        for _ in range(10):
+            run()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            run()
+        torch.cuda.synchronize()
+        out["logp_alone_us_" + key] = (time.perf_counter() - t0) / args.steps * 1e6
+    # proposal kernel traffic per step (algorithmic): x read, history append, two partner
+    # chunks, proposal write = 5 R W doubles (+ the natural-space copy when transformed)
+    out["device_demcz_natural"] = {"us_per_step": dn * 1e6, "chain_steps_per_s": W / dn}
+    out["device_demcz_transformed"] = {"us_per_step": dj * 1e6, "chain_steps_per_s": W / dj}
+    out["proposal_bytes_per_step"] = {"natural": 5 * R * W * 8, "transformed": 6 * R * W * 8}
+    ts = max(10, args.steps // 10)
+    f = lambda t: lpj(t)  # noqa: E731
+    DEMetropolisZ(f, seed=3, transform=Transform.from_spec(spec)).run(x0, 3, 0)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    lp.demc(x, lpv, args.steps, lamb, 1e-3, 7, step0=10, n_accepted=cnt)
+    DEMetropolisZ(f, seed=3, transform=Transform.from_spec(spec), tune=None).run(x0, ts, 0)
     torch.cuda.synchronize()
-    dev = (time.perf_counter() - t0) / args.steps
-    ts = max(20, args.steps // 5)
-    DEMetropolis(lambda t: lp(t), seed=3).run(torch.from_numpy(th).cuda(), 5, 0)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    DEMetropolis(lambda t: lp(t), seed=3, tune_interval=10 ** 9).run(torch.from_numpy(th).cuda(), ts, 0)
-    torch.cuda.synchronize()
-    tor = (time.perf_counter() - t0) / ts
-    print(json.dumps({"workload": "c4: %d walkers x 64 wells (5 gases CE + 5 tracers RTD, N=1200)" % W,
-                      "device_demc": {"us_per_step": dev * 1e6, "walker_steps_per_s": W / dev},
-                      "torch_demetropolis": {"us_per_step": tor * 1e6, "walker_steps_per_s": W / tor},
-                      "speedup": tor / dev}))
+    tt = (time.perf_counter() - t0) / ts
+    out["torch_demcz_transformed"] = {"us_per_step": tt * 1e6, "chain_steps_per_s": W / tt}
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":
