@@ -103,6 +103,8 @@ class CEModel:
         x = torch.from_numpy(x0).to("cuda:%d" % self.device)
         res = sample_model(self.spec, self.max_walkers, self.device, x, tune, draws, seed, tune_interval, sampler,
                            space, cache=self.__dict__)
+        from . import trace
+        res["idata"] = trace.inference_data(res, self.spec, wells=self.wells)   # az.from_pymc3 layout
         res["samples"] = res["samples"].cpu().numpy()
         res["logp"] = res["logp"].cpu().numpy()
         return res

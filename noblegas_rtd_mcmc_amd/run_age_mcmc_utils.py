@@ -7,7 +7,8 @@
 * ``conv_mcmc(well, tracer, obs_kwgs, conv_kwgs, prior_kwgs, savedir, savenum)`` --
   :189-462.  ``build_mcmc_model_joint_sT()`` returns the batched log-prob (ModelSpec
   compiled on the GPU) of the same priors / obs statistics / StudentT likelihood;
-  ``sample_mcmc()`` runs the ensemble DE-MC sampler instead of PyMC3.
+  ``sample_mcmc()`` runs DEMetropolisZ (one chain per walker) on the GPU instead of PyMC3
+  and saves the trace in ArviZ's group layout (trace.py).
 """
 import copy
 import os
@@ -120,7 +121,8 @@ class conv_mcmc:
         self._lp = None
         tl = '.'.join(self.tracer)
         mt = '{}-{}'.format(self.mod_type1, self.mod_type2) if self.mod_type2 else self.mod_type1
-        self.trace_name = os.path.join(savedir, '{}.{}.{}.{}.npz'.format(well, tl, mt, savenum))
+        # :255 -- a directory of per-group netCDF-3 files here (trace.to_netcdf)
+        self.trace_name = os.path.join(savedir, '{}.{}.{}.{}.netcdf'.format(well, tl, mt, savenum))
 
     def frombeta(self, betaval, low, high):
         return betaval * (high - low) + low
@@ -178,11 +180,14 @@ class conv_mcmc:
         x = torch.from_numpy(x0).to("cuda:%d" % self.device)
         res = sample_model(lp.spec, self.max_walkers, self.device, x, tune, draws, seed, tune_interval, sampler,
                            space, cache=self.__dict__)
+        from . import trace
+        idata = trace.inference_data(res, lp.spec, wells=[self.well])
         res = {k: (v.cpu().numpy() if hasattr(v, "cpu") else v) for k, v in res.items()}
         res["roles"] = list(lp.spec.roles)
+        res["idata"] = idata
         if self.savedir:
-            os.makedirs(self.savedir, exist_ok=True)
-            np.savez(self.trace_name, samples=res["samples"], logp=res["logp"], roles=np.array(res["roles"]))
+            # az.to_netcdf(idata, self.trace_name) (:425): same groups / names / attrs
+            trace.to_netcdf(idata, self.trace_name)
         self.idata = res
         return res
 

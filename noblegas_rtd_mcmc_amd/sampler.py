@@ -382,7 +382,14 @@ def sample_model(spec, max_walkers, device, x0, tune, draws, seed, tune_interval
     if lp is None:
         lp = LogProb(dataclasses.replace(spec, jacobian=jac), max_walkers, device)
         cache[key] = lp
+    import time
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
     if sampler == "device":
-        return DeviceDEMetropolisZ(lp, tune_interval=tune_interval, seed=seed, transformed=jac).run(x0, tune, draws)
-    tf = Transform.from_spec(spec) if jac else None
-    return DEMetropolisZ(lambda th: lp(th), tune_interval=tune_interval, seed=seed, transform=tf).run(x0, tune, draws)
+        res = DeviceDEMetropolisZ(lp, tune_interval=tune_interval, seed=seed, transformed=jac).run(x0, tune, draws)
+    else:
+        tf = Transform.from_spec(spec) if jac else None
+        res = DEMetropolisZ(lambda th: lp(th), tune_interval=tune_interval, seed=seed, transform=tf).run(x0, tune, draws)
+    torch.cuda.synchronize()
+    res["sampling_time"] = time.perf_counter() - t0          # PyMC3's trace attribute, seconds
+    return res

@@ -185,6 +185,32 @@ def test_conv_mcmc_logp_matches_oracle():
     assert close(lp(th, soa=True), om.log_prob(lp.spec, th), 1e-12, 1e-9).all()
 
 
+def test_conv_mcmc_sample_writes_arviz_trace(tmp_path):
+    """sample_mcmc on the GPU writes the trace like az.to_netcdf (:425): posterior per
+    PyMC3 variable, sample_stats, tuning_steps / sampling_time attributes."""
+    from noblegas_rtd_mcmc_amd import trace
+    from noblegas_rtd_mcmc_amd.run_age_mcmc_utils import conv_mcmc
+    rng = np.random.default_rng(9)
+    tracers = ["CFC12", "SF6", "H3", "He4_ter"]
+    okw = {t: {"obs_df": pd.Series(rng.lognormal(0, 0.1, 50) * v), "obs_perr": 0.05}
+           for t, v in zip(tracers, (36.4, 1.25, 4.9, 8.8e-9))}
+    ckw = {"mod_type1": "exponential", "mod_type2": False}
+    for t in tracers:
+        ckw[t] = {"C_t": frame(t, 1200)}
+        if t == "He4_ter":
+            ckw[t]["rad_accum"] = "4He"
+        if t == "H3":
+            ckw[t]["t_half"] = 12.34
+    pkw = {"tau1_low": 1.0, "tau1_high": 1000.0, "J_mu": -10.42, "J_sd": 0.33, "par_names": ["tau1", "J"]}
+    m = conv_mcmc("PLM1", tracers, okw, ckw, pkw, str(tmp_path), 1)
+    res = m.sample_mcmc(nwalkers=12, tune=60, draws=30, tune_interval=20)
+    back = trace.from_netcdf(m.trace_name)
+    assert m.trace_name.endswith("PLM1.CFC12.SF6.H3.He4_ter.exponential.1.netcdf")
+    assert back["posterior"]["tau1"][1].shape == (12, 30) and "nu" in back["posterior"]
+    assert back["attrs"]["tuning_steps"] == 60 and back["attrs"]["sampling_time"] > 0
+    assert np.array_equal(back["sample_stats"]["lp"][1], res["logp"].T)
+
+
 def test_c1_sampler_recovers_reference_posterior():
     """c1: CE model of PLM1 (Ne, Ar, Kr, Xe), 100 chains of DEMetropolisZ on the GPU
     log-prob, in PyMC3's transformed space.  The pooled posterior means must land near the

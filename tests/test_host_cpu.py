@@ -160,3 +160,36 @@ def test_ce_sampler_plumbing_with_cpu_logp():
         return torch.from_numpy(om.log_prob(spec, x.numpy()))
     res = DEMetropolisZ(lp, tune_interval=5, seed=2).run(torch.from_numpy(th), tune=10, draws=5)
     assert res["samples"].shape == (5, 6, 1, 12) and torch.isfinite(res["logp"]).all()
+
+
+def test_trace_layout_roundtrip(tmp_path):
+    """ArviZ-layout trace (trace.py): posterior per PyMC3 variable name with (chain, draw)
+    dims, deterministics, sample_stats, tuning_steps / sampling_time attrs; netCDF-3 per
+    group, read back through scipy."""
+    from noblegas_rtd_mcmc_amd import trace
+    spec = wl.c4_spec(L=1, N=50, mod_type1="exponential", mod_type2="piston",
+                      par_names=("tau1", "tau2", "f1", "thalf_cfc", "lamsf6"))
+    from noblegas_rtd_mcmc_amd.spec import ModelSpec
+    spec = ModelSpec(n_wells=1, rtd=spec.rtd)
+    D, W = 7, 5
+    rng = np.random.default_rng(0)
+    s = np.stack([wl.sample_prior(spec, W, rng) for _ in range(D)])          # [D, P, 1, W]
+    res = {"samples": torch.from_numpy(s), "logp": torch.from_numpy(rng.normal(size=(D, W))),
+           "accepted": torch.from_numpy(rng.integers(0, 2, (D, W)).astype(np.uint8)),
+           "lamb": torch.full((W,), 0.5, dtype=torch.float64), "scaling": torch.full((W,), 1e-3, dtype=torch.float64),
+           "tuning_steps": 10000, "sampling_time": 12.5}
+    idata = trace.inference_data(res, spec)
+    p = idata["posterior"]
+    for name in ("tau1", "tau2", "f1", "f2", "tau", "nu_", "nu", "thalf_cfc_", "thalf_cfc", "lamsf6"):
+        assert p[name][0] == ("chain", "draw") and p[name][1].shape == (W, D), name
+    i = spec.roles.index("tau1")
+    assert np.array_equal(p["tau1"][1], s[:, i, 0, :].T)
+    f1 = s[:, spec.roles.index("f1"), 0, :].T
+    assert np.allclose(p["tau"][1], f1 * p["tau1"][1] + (1 - f1) * p["tau2"][1])
+    out = trace.to_netcdf(idata, str(tmp_path / "PLM1.CFC12.exponential-piston.0.netcdf"))
+    back = trace.from_netcdf(out)
+    assert back["attrs"]["tuning_steps"] == 10000 and back["attrs"]["sampling_time"] == 12.5
+    for g in ("posterior", "sample_stats"):
+        for k, (dims, arr) in idata[g].items():
+            assert back[g][k][0] == dims and np.array_equal(back[g][k][1], arr), (g, k)
+    assert np.array_equal(back["coords"]["chain"], np.arange(W))
