@@ -508,8 +508,13 @@ static bool fused_path(const RtdArgs& a0, const UnitArgs& u) {
     static const bool disabled = std::getenv("NGRTD_NO_FUSED") != nullptr;
     RtdArgs a = a0;
     cheb_window(a, u);
-    return !disabled && mfma_path(a, a.row_thalf >= 0) && a.C <= 5 && u.L >= 1 && u.L <= kFusedUnits &&
-           fused_lds(a, u) <= kFusedMaxLds;
+    // exponential first component on the matrix-core / surrogate path, optionally mixed
+    // with a piston second component (BMM exponential-piston, one lookup per unit)
+    RtdArgs a1 = a;
+    a1.mod[1] = MOD_NONE;
+    const bool mods = a.mod[0] == MOD_EXP && (a.mod[1] == MOD_NONE || a.mod[1] == MOD_PISTON);
+    return !disabled && mods && mfma_path(a1, a.row_thalf >= 0) && a.C <= 5 && u.L >= 1 &&
+           u.L <= kFusedUnits && fused_lds(a, u) <= kFusedMaxLds;
 }
 // Waves per unit group (logp_fused_kernel ROLES): 2 = theta-only and RTD blocks in separate
 // waves (default), 1 = one wave runs the whole unit.  NGRTD_FUSED_ROLES overrides (A/B runs).
@@ -520,23 +525,24 @@ static int fused_roles() {
     }();
     return r;
 }
-template <int C, bool FULL, int ROLES>
+template <int C, bool FULL, int ROLES, int MIX>
 static void launch_fused_cfr(const RtdArgs& a, const UnitArgs& u, int WB, int64_t W, double* logp,
                              const DemcAccept& da, hipStream_t st) {
     static const bool attr = [] {   // dynamic LDS above 64 KiB (many wells) needs the opt-in
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&logp_fused_kernel<C, FULL, ROLES>),
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&logp_fused_kernel<C, FULL, ROLES, MIX>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFusedMaxLds);
         return true;
     }();
     (void)attr;
-    hipLaunchKernelGGL((logp_fused_kernel<C, FULL, ROLES>), dim3((unsigned)cdiv(W, WB)),
+    hipLaunchKernelGGL((logp_fused_kernel<C, FULL, ROLES, MIX>), dim3((unsigned)cdiv(W, WB)),
                        dim3(64 * kFusedWaves * ROLES), fused_lds(a, u), st, a, u, WB, logp, da);
 }
 template <int C, bool FULL>
 static void launch_fused_cf(const RtdArgs& a, const UnitArgs& u, int WB, int64_t W, double* logp,
                             const DemcAccept& da, hipStream_t st) {
-    if (fused_roles() == 2) launch_fused_cfr<C, FULL, 2>(a, u, WB, W, logp, da, st);
-    else launch_fused_cfr<C, FULL, 1>(a, u, WB, W, logp, da, st);
+    if (a.mod[1] == MOD_PISTON) launch_fused_cfr<C, FULL, 2, 1>(a, u, WB, W, logp, da, st);
+    else if (fused_roles() == 2) launch_fused_cfr<C, FULL, 2, 0>(a, u, WB, W, logp, da, st);
+    else launch_fused_cfr<C, FULL, 1, 0>(a, u, WB, W, logp, da, st);
 }
 // FULL instance: CE + RTD blocks, priors and likelihoods on, no Jacobians (the joint model)
 template <int C>
@@ -1166,7 +1172,8 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
         a.conc = p->conc.d();
         set_frag(a, p->table);
         a.cheb = nullptr;
-        if (a.mod[0] == MOD_EXP && a.mod[1] == MOD_NONE && !any_lamw && p->table.C <= 5 && p->dtp >= 0.0 &&
+        if (a.mod[0] == MOD_EXP && (a.mod[1] == MOD_NONE || a.mod[1] == MOD_PISTON) && !any_lamw &&
+            p->table.C <= 5 && p->dtp >= 0.0 &&
             !(d->flags & NGRTD_EXACT_RTD)) {
             NG_CHECK(cheb_prepare(ctx, p->table, (1.0 + p->dtp) - p->tp0));
             if (p->table.cheb_ok) a.cheb = p->table.cheb.d();

@@ -798,9 +798,12 @@ __host__ __device__ __forceinline__ void cheb_sums(const double* pc, int CP, dou
 // Numerators num_c = A_{c,0} + s01 Y_c and the reciprocal normaliser 1 / (1 + s01 G) ->
 // tracer concentrations of unit u (rtd_conc_kernel's combination step): per tracer
 // (A + J B) / den, the BMM mix and the SF6 factor (run_age_mcmc_utils.py:154-161).
+// num2: the second BMM component's numerators when it is a piston (its normaliser is
+// g.sum() = 1, convolution_integral_utils.py:178-181, 270): cout = f1 cout1 + f2 cout2 with
+// f2 = 1 - f1 (the Deterministic of run_age_mcmc_utils.py:304).
 template <int C>
 __device__ __forceinline__ void unit_conc(const RtdArgs& a, int64_t u, const double* num, double rden,
-                                          double* conc) {
+                                          double* conc, const double* num2 = nullptr) {
     const double fmix = (a.row_f1 >= 0) ? a.theta[(int64_t)a.row_f1 * a.U + u] : 1.0;
     double Jw = 0.0;
     if (a.row_J >= 0) {
@@ -808,19 +811,36 @@ __device__ __forceinline__ void unit_conc(const RtdArgs& a, int64_t u, const dou
         Jw = a.J_is_log10 ? exp10(jv) : jv;
     }
     for (int t = 0; t < a.K; ++t) {
-        double sA = 0.0, sB = 0.0;
+        double sA = 0.0, sB = 0.0, sA2 = 0.0, sB2 = 0.0;
         bool hasB = false;
 #pragma unroll
         for (int c = 0; c < C; ++c) {
             if (a.chan_tracer[c] != t) continue;
-            if (a.chan_isB[c]) { sB = num[c]; hasB = true; }
-            else sA = num[c];
+            if (a.chan_isB[c]) { sB = num[c]; hasB = true; if (num2) sB2 = num2[c]; }
+            else { sA = num[c]; if (num2) sA2 = num2[c]; }
         }
-        const double cc = hasB ? (sA + ((a.row_J >= 0) ? Jw : a.tr_J[t]) * sB) * rden : sA * rden;
-        double cout = fmix * cc + 0.0 * 0.0;   // f1*cout1 + f2*cout2, run_age_mcmc_utils.py:154
+        const double J = (a.row_J >= 0) ? Jw : a.tr_J[t];
+        const double cc = hasB ? (sA + J * sB) * rden : sA * rden;
+        double cout;
+        if (num2) {
+            const double cc2 = hasB ? (sA2 + J * sB2) : sA2;
+            cout = fmix * cc + (1 - fmix) * cc2;
+        } else {
+            cout = fmix * cc + 0.0 * 0.0;   // f1*cout1 + f2*cout2, run_age_mcmc_utils.py:154
+        }
         if (a.tr_sf6[t] && a.row_lamsf6 >= 0) cout *= (1 + a.theta[(int64_t)a.row_lamsf6 * a.U + u]);
         conc[t] = cout;
     }
+}
+
+// Piston second component (BMM, convolution_integral_utils.py:178-181): the channel-table
+// row at the FIRST argmin |tp - tau2| -- a lookup, no age loop.
+template <int C>
+__device__ __forceinline__ void piston_num(const RtdArgs& a, int64_t u, double* num2) {
+    const double tau2 = a.theta[(int64_t)a.row_tau[1] * a.U + u];
+    const int ix = piston_index(tau2, a.tp0, a.dtp, a.N);
+#pragma unroll
+    for (int c = 0; c < C; ++c) num2[c] = a.tab[(int64_t)ix * a.CP + c];
 }
 
 // The reference's exponential weights g = (1/tau) exp(-tp/tau) / sum(...) (:184, :270)
@@ -839,7 +859,7 @@ __device__ __forceinline__ bool exp_rtd_nan(const RtdArgs& a, double tau) {
 // 1 + s01 G with G = sum_{j<n} q^j = expm1(-beta n) / expm1(-beta) in closed form.
 template <int C>
 __device__ __forceinline__ void mfma_unit_conc(const RtdArgs& a, int64_t u, double bu, const double* yy,
-                                               double* conc) {
+                                               double* conc, const double* num2 = nullptr) {
     const int n = a.N - 1;
     const double s01 = fexp(-bu * ((1.0 + a.dtp) - a.tp0));
     const double G = (n > 0) ? fexpm1(-bu * (double)n) / fexpm1(-bu) : 0.0;
@@ -1106,7 +1126,7 @@ __device__ __forceinline__ void walker_out(double* logp, const DemcAccept& d, in
 
 // Exact (matrix-core) channel sums for a wave of logp_fused_kernel with an uncovered tau:
 // its 64 units as 4 tiles of 16, then this lane's concentrations and RTD likelihood.
-template <int C, bool FULL, bool SEQ>
+template <int C, bool FULL, bool SEQ, int MIX>
 __device__ __forceinline__ void fused_exact(const RtdArgs& a, const UnitArgs& ul, int WB, int64_t w0, int uw,
                                             bool mvalid, int64_t mu, int ml, double nub, double* conc,
                                             double& like) {
@@ -1149,7 +1169,9 @@ __device__ __forceinline__ void fused_exact(const RtdArgs& a, const UnitArgs& ul
     if (mvalid) {
         ThetaPre tp;
         tp.nub = nub;
-        mfma_unit_conc<C>(a, mu, bu, yy, conc);
+        double num2[C];
+        if (MIX) piston_num<C>(a, mu, num2);
+        mfma_unit_conc<C>(a, mu, bu, yy, conc, MIX ? num2 : nullptr);
         like = unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL);
     }
 }
@@ -1170,7 +1192,9 @@ __host__ __device__ constexpr int cheb_lds_stride(int C) { return kChebN * cheb_
 // reference's addition order (th + like).  Role is wave-uniform (no divergence); each role
 // needs fewer registers, so at c4 a SIMD holds 4 waves of two different instruction mixes
 // (transcendental-heavy CE, FMA-chain Clenshaw) that hide each other's latency.
-template <int C, bool FULL, int ROLES>
+// MIX = 1: BMM with a piston second component (tau2, f1 roles): its concentrations are a
+// channel-table lookup, mixed f1 c1 + (1 - f1) c2 (run_age_mcmc_utils.py:126-161).
+template <int C, bool FULL, int ROLES, int MIX>
 __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(const RtdArgs a, const UnitArgs ua,
                                                                               int32_t WB, double* __restrict__ logp,
                                                                               const DemcAccept dacc) {
@@ -1308,7 +1332,9 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             const double dr[2] = {1.0 + zz[C], tp.nub * (ua.rnu_max - ua.rnu_min) + ua.rnu_min};
             double rr[2];
             batch_recip<2>(dr, rr);
-            unit_conc<C>(a, mu, num, rr[0], conc);
+            double num2[C];
+            if (MIX) piston_num<C>(a, mu, num2);
+            unit_conc<C>(a, mu, num, rr[0], conc, MIX ? num2 : nullptr);
             if (cnan)
                 for (int t = 0; t < a.K; ++t) conc[t] = __builtin_nan("");
             like = mvalid ? unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL, &rr[1]) : 0.0;
@@ -1316,7 +1342,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         NGRTD_PROBE(2);
         if (__any(bad)) {                                     // wave-uniform: exact channel sums
             // ROLES = 2: one tile per pass keeps the exact path inside the 128-VGPR budget
-            fused_exact<C, FULL, ROLES == 2>(a, ul, WB, w0, uw, mvalid, mu, ml, tp.nub, conc, like);
+            fused_exact<C, FULL, ROLES == 2, MIX>(a, ul, WB, w0, uw, mvalid, mu, ml, tp.nub, conc, like);
         }
         if (!FULL && a.conc && mvalid)                        // forward(): model concentrations
             for (int t = 0; t < a.K; ++t) a.conc[(int64_t)t * a.U + mu] = conc[t];

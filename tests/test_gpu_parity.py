@@ -172,6 +172,49 @@ def test_logp_golden(golden, prefix):
     lp.close()
 
 
+def many_walkers(W, seed=4):
+    """>= 256 walkers: the first 128, every block / wave boundary (511/512, 1023/1024,
+    2047, ...) and random others."""
+    sel = set(range(min(W, 128)))
+    for b in (64, 511, 512, 1023, 1024, 1535, 1536, 2047):
+        if b < W:
+            sel.add(b)
+    rest = np.random.default_rng(seed).permutation(W)
+    for w in rest:
+        if len(sel) >= 264:
+            break
+        sel.add(int(w))
+    return sorted(sel)
+
+
+def log_prob_vec(spec, th):
+    from oracle.vectorized import log_prob_vec as f
+    return f(spec, th)
+
+
+@pytest.mark.parametrize("model", ["exp_pist_flow", "exponential-piston", "exp_pist_flow-piston"])
+def test_published_models_c4_shape_vs_oracle(model):
+    """The RTD models of the reference's published runs at the c4
+    shape (2048 walkers x 64 wells x (5 gases + 5 tracers), N = 1200) vs the oracle on
+    264 walkers, plus determinism and device == host."""
+    import torch
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+    m1, _, m2 = model.partition("-")
+    pn = ["tau1"] + (["tau2", "f1"] if m2 else []) + (["eta1"] if m1 == "exp_pist_flow" else [])
+    spec = wl.c4_spec(L=64, N=1200, mod_type1=m1, mod_type2=m2 or None, par_names=tuple(pn))
+    th = wl.sample_prior(spec, 2048, np.random.default_rng(34568))
+    lp = LogProb(spec, max_walkers=2048)
+    dev = torch.from_numpy(th).cuda()
+    a = lp(dev).cpu().numpy()
+    assert np.array_equal(a, lp(dev).cpu().numpy()) and np.array_equal(a, lp(th, soa=True))
+    sel = many_walkers(2048, seed=5)
+    refv = log_prob_vec(spec, np.ascontiguousarray(th[:, :, sel]))
+    ok = close(a[sel], refv, 1e-12, 1e-9)
+    assert ok.all(), (np.array(sel)[~ok], a[sel][~ok], refv[~ok])
+    lp.close()
+
+
 def test_c4_full_size_vs_oracle_and_properties():
     """c4 at full size (2048 x 64 x (5 gases + 5 tracers)): sampled walkers vs the oracle,
     bitwise determinism, device == host path, walker-permutation equivariance."""
@@ -190,6 +233,11 @@ def test_c4_full_size_vs_oracle_and_properties():
     walkers = [0, 1, 63, 64, 1000, 2047]
     ref = om.log_prob(spec, th, walkers=walkers)
     assert close(a[walkers], ref, 1e-12, 1e-9).all(), (a[walkers], ref)
+    # 264 walkers across every block / wave boundary through the vectorised oracle
+    sel = many_walkers(th.shape[2])
+    refv = log_prob_vec(spec, np.ascontiguousarray(th[:, :, sel]))
+    ok = close(a[sel], refv, 1e-12, 1e-9)
+    assert ok.all(), (np.array(sel)[~ok], a[sel][~ok], refv[~ok])
     perm = np.random.default_rng(0).permutation(th.shape[2])
     p = lp(np.ascontiguousarray(th[:, :, perm]), soa=True)
     assert np.array_equal(p, a[perm])
@@ -218,6 +266,10 @@ def test_c2_c3_full_size_vs_oracle_and_properties(config):
     walkers = [0, 1, 63, 64, 777, 1000, 2047]
     ref = om.log_prob(spec, th, walkers=walkers)
     assert close(a[walkers], ref, 1e-12, 1e-9).all(), (a[walkers], ref)
+    sel = many_walkers(th.shape[2])
+    refv = log_prob_vec(spec, np.ascontiguousarray(th[:, :, sel]))
+    ok = close(a[sel], refv, 1e-12, 1e-9)
+    assert ok.all(), (np.array(sel)[~ok], a[sel][~ok], refv[~ok])
     perm = np.random.default_rng(1).permutation(th.shape[2])
     assert np.array_equal(lp(np.ascontiguousarray(th[:, :, perm]), soa=True), a[perm])
     lp.close()
