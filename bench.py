@@ -293,10 +293,14 @@ def report(args, spec, lp, ks, dt, world, W_total, Wb, plan_build_ms, theta, the
                                "RTD %s, N=%d ages)" % (W_total, Wb, args.wells, model, N),
                    "walkers_total": W_total, "walkers_per_gpu": Wb, "wells": args.wells, "gases": 5, "tracers": 5,
                    "ages": N, "rtd_model": model,
-                   "rtd_sums": ("piecewise-Chebyshev surrogate of the exponential channel sums, fitted and "
-                                "validated per plan (max rel err %.2g <= 5e-14); uncovered tau take the exact "
-                                "matrix-core path" % info["surrogate_max_rel_err"]) if info.get("surrogate")
-                               else "exact (no surrogate)",
+                   "rtd_sums": {1: "piecewise-Chebyshev surrogate of the exponential channel sums, fitted and "
+                                   "validated per plan (max rel err %.2g <= 5e-14); uncovered tau take the exact "
+                                   "matrix-core path",
+                                2: "exp_pist_flow: exact Horner head of <= 32 ages + piecewise-Chebyshev surrogates "
+                                   "of the block tails, fitted and validated per plan (max rel err %.2g <= 5e-14); "
+                                   "uncovered tau/eta sum their tails exactly"}.get(
+                                       info.get("surrogate"), "exact (no surrogate%s)") % (
+                                       info["surrogate_max_rel_err"] if info.get("surrogate") else ""),
                    "parallelism": ("%d walker blocks + RCCL all-gather of logp (%s scaling)" % (world, args.scaling))
                                   if world > 1 else "single GPU"},
         "roofline": {"bound": bound, "achieved": achieved / 1e12, "peak": FP64_PEAK / 1e12, "unit": "TFLOP/s",

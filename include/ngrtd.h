@@ -277,7 +277,7 @@ int ngrtd_plan_kernel_stats(ngrtd_plan* plan, double* times_ms, int64_t* counts,
 /* Launch geometry the plan chose for its RTD kernel: info[0..12] = units per lane (VALU
  * path) or 16-unit tiles per wave (MFMA path), waves per block, blocks, ages per LDS slice
  * (VALU) or per segment (MFMA), channels, N, LDS bytes, units, MFMA row tiles (0 = VALU
- * path), age segments, 4-age MFMA steps, Chebyshev surrogate in use (0/1), the
+ * path), age segments, 4-age MFMA steps, Chebyshev surrogate in use (0 none, 1 exponential channel sums, 2 exp_pist_flow block tails), the
  * surrogate's validated max relative error in units of 1e-18 (-1: not built), and
  * info[13] = pieces of the Student-t normaliser table (0: exact c0).  For the roofline
  * accounting in bench.py. */

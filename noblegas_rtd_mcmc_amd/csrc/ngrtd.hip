@@ -17,6 +17,7 @@
 #include <string>
 #include <tuple>
 #include <vector>
+#include <thread>
 
 #include "../../include/ngrtd.h"
 #include "ngrtd_kernels.hpp"
@@ -53,6 +54,10 @@ struct TableDev {
     DevBuf cheb;            // Chebyshev surrogate of the exponential channel sums (cheb_build)
     bool cheb_ok = false;
     double cheb_err = -1.0; // max relative error measured by the validation (-1: not built)
+    DevBuf epm;             // exp_pist_flow block-tail surrogates (epm_prepare)
+    bool epm_ok = false;
+    double epm_err = -1.0;
+    int epm_nb = 0, epm_p0 = 0, epm_np = 0;
     std::vector<std::vector<double>> cols_host;   // channel columns (kept for cheb_build)
     int S_seg = 1, Lseg = 0, nsteps = 0;
     int C = 0, CP = 0;
@@ -247,7 +252,8 @@ static long double cheb_exact(const std::vector<double>& A, long double s, long 
 // Returns the max relative error.  Channels with negative or non-finite entries are not
 // expanded (HUGE_VAL): for non-negative columns the error is relative to |value|.
 // d01 = tp_1 - tp_0 as the kernel forms it: (1 + dtp) - (1e-5 + dtp).
-static double cheb_build(const std::vector<std::vector<double>>& cols, int C, double d01, std::vector<double>& coef) {
+static double cheb_build(const std::vector<std::vector<double>>& cols, int C, double d01, std::vector<double>& coef,
+                         int p_lo = 0, int p_hi = kChebPieces) {
     const int n = kChebN, CP = cheb_cp(C);
     coef.assign((size_t)kChebPieces * n * CP, 0.0);
     for (int c = 0; c < C; ++c)
@@ -263,7 +269,7 @@ static double cheb_build(const std::vector<std::vector<double>>& cols, int C, do
     for (int j = 2; j < n; ++j)
         for (int k = 0; k < n; ++k)
             Tm[j][k] = (k > 0 ? 2.0L * Tm[j - 1][k - 1] : 0.0L) - Tm[j - 2][k];
-    for (int p = 0; p < kChebPieces; ++p) {
+    for (int p = p_lo; p < p_hi; ++p) {
         for (int c = 0; c <= C; ++c) {
             const std::vector<double>& col = cols[c < C ? c : 0];
             for (int k = 0; k < n; ++k) {
@@ -297,7 +303,7 @@ static double cheb_build(const std::vector<std::vector<double>>& cols, int C, do
     }
     double worst = 0.0;
     const int M = 24;
-    for (int p = 0; p < kChebPieces; ++p) {
+    for (int p = p_lo; p < p_hi; ++p) {
         for (int i = 0; i <= M + 1; ++i) {
             double tau;
             if (p < kChebBinPieces) {
@@ -337,6 +343,52 @@ static int cheb_prepare(ngrtd_ctx* ctx, TableDev& tab, double d01) {
     HIP_TRY(ctx, tab.cheb.ensure(coef.size() * sizeof(double)));
     HIP_TRY(ctx, hipMemcpy(tab.cheb.p, coef.data(), coef.size() * sizeof(double), hipMemcpyHostToDevice));
     tab.cheb_ok = true;
+    return NGRTD_OK;
+}
+
+// exp_pist_flow block-tail surrogates: for b = 1.. while b S < N, the columns
+// A_c[b S - 1 ...] (so that the surrogate's sum_{j>=0} cols[1 + j] e^{-j/tau'} is
+// T_b = sum_{k >= b S} A_{c,k} e^{-(k - b S)/tau'}), with s01 = 1 (d01 = 0), fitted and
+// validated over the pieces [p_lo, p_hi) only, one thread per table.  Used only if every
+// table validates to kChebTol (else the plan keeps the multi-kernel EPM path).
+static int epm_prepare(ngrtd_ctx* ctx, TableDev& tab, int N, int p_lo, int p_hi) {
+    tab.epm_ok = false;
+    const int C = tab.C, CP = cheb_cp(C), S = kEpmBlock;
+    if (C < 1 || C > 5 || tab.cols_host.empty() || N <= S + 1 || p_lo < 0 || p_hi > kChebPieces || p_hi <= p_lo)
+        return NGRTD_OK;
+    const int nb = (N - 1) / S;                    // b S < N for b = 1..nb
+    std::vector<std::vector<double>> coefs((size_t)nb);
+    std::vector<double> errs((size_t)nb, HUGE_VAL);
+    auto work = [&](int b0, int stride) {
+        for (int b = b0; b <= nb; b += stride) {
+            std::vector<std::vector<double>> cols((size_t)C);
+            for (int c = 0; c < C; ++c)
+                cols[c].assign(tab.cols_host[c].begin() + ((size_t)b * S - 1), tab.cols_host[c].end());
+            errs[b - 1] = cheb_build(cols, C, 0.0, coefs[b - 1], p_lo, p_hi);
+        }
+    };
+    const int nt = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt && t <= nb; ++t) th.emplace_back(work, 1 + t, nt);
+    work(1, nt);
+    for (auto& t : th) t.join();
+    double worst = 0.0;
+    for (double e : errs)
+        if (!(e <= worst)) worst = e;
+    tab.epm_err = worst;
+    if (!(worst <= kChebTol)) return NGRTD_OK;
+    const int np = p_hi - p_lo;
+    const size_t per = (size_t)kChebN * CP;
+    std::vector<double> h((size_t)nb * np * per);
+    for (int b = 0; b < nb; ++b)
+        std::copy(coefs[b].begin() + (size_t)p_lo * per, coefs[b].begin() + (size_t)p_hi * per,
+                  h.begin() + (size_t)b * np * per);
+    HIP_TRY(ctx, tab.epm.ensure(h.size() * sizeof(double)));
+    HIP_TRY(ctx, hipMemcpy(tab.epm.p, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
+    tab.epm_ok = true;
+    tab.epm_nb = nb;
+    tab.epm_p0 = p_lo;
+    tab.epm_np = np;
     return NGRTD_OK;
 }
 
@@ -487,7 +539,9 @@ static void launch_mfma(const RtdArgs& a, const UnitArgs& u, int32_t fuse, hipSt
 // packed per-well data (ce obs, 1/sd^2, sums of 0.5 log 1/sd^2, E_min; rtd obs, 1/sd^2,
 // sums; the Student-t normaliser table).
 static size_t fused_lds(const RtdArgs& a, const UnitArgs& u) {
-    return (size_t)(2 * kFusedUnits + kFusedUnits / 2 + a.cheb_np * cheb_lds_stride(a.C) + u.wd_n) * sizeof(double);
+    const size_t epm_tab = a.mod[0] == MOD_EPM ? (size_t)a.N * a.CP : 0;   // EPM: the channel table
+    return (size_t)(2 * kFusedUnits + kFusedUnits / 2 + a.cheb_np * cheb_lds_stride(a.C) + epm_tab + u.wd_n) *
+           sizeof(double);
 }
 // Surrogate pieces the fused kernel stages: when the unit's log-prob carries the tau1
 // Uniform prior and the RTD's tau is tau1, only the pieces over the prior's support
@@ -510,9 +564,12 @@ static bool fused_path(const RtdArgs& a0, const UnitArgs& u) {
     cheb_window(a, u);
     // exponential first component on the matrix-core / surrogate path, optionally mixed
     // with a piston second component (BMM exponential-piston, one lookup per unit)
+    // or an exp_pist_flow first component with validated block-tail surrogates
     RtdArgs a1 = a;
     a1.mod[1] = MOD_NONE;
-    const bool mods = a.mod[0] == MOD_EXP && (a.mod[1] == MOD_NONE || a.mod[1] == MOD_PISTON);
+    a1.mod[0] = MOD_EXP;
+    const bool mod2 = a.mod[1] == MOD_NONE || a.mod[1] == MOD_PISTON;
+    const bool mods = mod2 && (a.mod[0] == MOD_EXP || (a.mod[0] == MOD_EPM && a.epm != nullptr));
     return !disabled && mods && mfma_path(a1, a.row_thalf >= 0) && a.C <= 5 && u.L >= 1 &&
            u.L <= kFusedUnits && fused_lds(a, u) <= kFusedMaxLds;
 }
@@ -540,9 +597,15 @@ static void launch_fused_cfr(const RtdArgs& a, const UnitArgs& u, int WB, int64_
 template <int C, bool FULL>
 static void launch_fused_cf(const RtdArgs& a, const UnitArgs& u, int WB, int64_t W, double* logp,
                             const DemcAccept& da, hipStream_t st) {
-    if (a.mod[1] == MOD_PISTON) launch_fused_cfr<C, FULL, 2, 1>(a, u, WB, W, logp, da, st);
-    else if (fused_roles() == 2) launch_fused_cfr<C, FULL, 2, 0>(a, u, WB, W, logp, da, st);
-    else launch_fused_cfr<C, FULL, 1, 0>(a, u, WB, W, logp, da, st);
+    const int mix = (a.mod[1] == MOD_PISTON ? 1 : 0) | (a.mod[0] == MOD_EPM ? 2 : 0);
+    switch (mix) {
+    case 1: launch_fused_cfr<C, FULL, 2, 1>(a, u, WB, W, logp, da, st); break;
+    case 2: launch_fused_cfr<C, FULL, 2, 2>(a, u, WB, W, logp, da, st); break;
+    case 3: launch_fused_cfr<C, FULL, 2, 3>(a, u, WB, W, logp, da, st); break;
+    default:
+        if (fused_roles() == 2) launch_fused_cfr<C, FULL, 2, 0>(a, u, WB, W, logp, da, st);
+        else launch_fused_cfr<C, FULL, 1, 0>(a, u, WB, W, logp, da, st);
+    }
 }
 // FULL instance: CE + RTD blocks, priors and likelihoods on, no Jacobians (the joint model)
 template <int C>
@@ -1178,6 +1241,24 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
             NG_CHECK(cheb_prepare(ctx, p->table, (1.0 + p->dtp) - p->tp0));
             if (p->table.cheb_ok) a.cheb = p->table.cheb.d();
         }
+        a.epm = nullptr;
+        a.epm_nb = a.epm_p0 = a.epm_np = 0;
+        if (a.mod[0] == MOD_EPM && (a.mod[1] == MOD_NONE || a.mod[1] == MOD_PISTON) && !any_lamw &&
+            p->table.C <= 5 && p->dtp >= 0.0 && !(d->flags & NGRTD_EXACT_RTD) && ri[NGRTD_ROLE_ETA1] >= 0) {
+            // block-tail surrogates over the tau' = tau / eta range the priors allow (lanes
+            // outside it sum their tails exactly)
+            static const bool disabled = std::getenv("NGRTD_NO_CHEB") != nullptr;
+            double x;
+            const double lo = std::max(kChebTauLo, d->tau1_lo / d->eta1_hi), hi = d->tau1_hi / d->eta1_lo;
+            const int pa = cheb_piece(lo, x), pb = cheb_piece(hi, x);
+            if (!disabled && pa >= 0 && pb >= pa) {
+                NG_CHECK(epm_prepare(ctx, p->table, p->N, pa, pb + 1));
+                if (p->table.epm_ok) {
+                    a.epm = p->table.epm.d();
+                    a.epm_nb = p->table.epm_nb; a.epm_p0 = p->table.epm_p0; a.epm_np = p->table.epm_np;
+                }
+            }
+        }
         u.rtd_on = 1; u.K = K;
         u.rtd_obs = p->rtd_obs.d(); u.rtd_sd = p->rtd_sd.d(); u.conc = p->conc.d();
         u.row_tau1 = ri[NGRTD_ROLE_TAU1]; u.row_nu = ri[NGRTD_ROLE_NU_RTD_BETA]; u.row_tau2 = ri[NGRTD_ROLE_TAU2];
@@ -1553,9 +1634,9 @@ int ngrtd_plan_info(ngrtd_plan* p, int64_t W, int64_t* info, int32_t n) {
     v[13] = p->unit.c0_np;
     if (p->desc.rtd_enabled) {
         RtdArgs a = p->rtd;
-        v[11] = a.cheb != nullptr;
-        v[12] = (p->table.cheb_err >= 0 && p->table.cheb_err < 1.0) ? (int64_t)llround(p->table.cheb_err * 1e18)
-                                                                    : -1;
+        v[11] = a.cheb != nullptr ? 1 : (a.epm != nullptr ? 2 : 0);
+        const double err = a.epm != nullptr ? p->table.epm_err : p->table.cheb_err;
+        v[12] = (err >= 0 && err < 1.0) ? (int64_t)llround(err * 1e18) : -1;
         a.U = U;
         const bool lamw = a.row_thalf >= 0;
         if (mfma_path(a, lamw)) {

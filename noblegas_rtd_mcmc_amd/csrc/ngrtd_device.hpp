@@ -40,7 +40,20 @@ struct RtdArgs {
     // pieces [cheb_p0, cheb_p0 + cheb_np) of it that logp_fused_kernel stages in LDS (the
     // window covering the tau1 prior's support; launch_fused)
     int32_t cheb_p0, cheb_np;
+    // exp_pist_flow block tails (logp_fused_kernel EPM mode, ngrtd.hip epm_prepare): table
+    // b = 1..epm_nb holds pieces [epm_p0, epm_p0 + epm_np) of the surrogate of
+    //   T_b(tau') = sum_{k >= b S} A_{c,k} exp(-(k - b S) / tau'),  S = kEpmBlock,
+    // laid out [b - 1][piece - epm_p0][kChebN][CP]; null when the plan has none
+    const double* epm;
+    int32_t epm_nb, epm_p0, epm_np;
 };
+
+// exp_pist_flow (convolution_integral_utils.py:186-190) on the yearly grid: the unmasked
+// weights are exp(-beta tp_k), beta = eta / tau, from the first index m with
+// tp_m >= tau (1 - 1/eta); the channel sums Y = sum_{k >= m} A_k q^(k - m), q = exp(-beta),
+// split at the block boundary B = (m / S + 1) S into a head of < S + 1 ages (Horner over the
+// LDS-staged channel table) and q^(B - m) T_{B/S}(1 / beta) from the block-tail surrogates.
+constexpr int kEpmBlock = 32;
 
 // Chebyshev surrogate of Z_c(tau) = s01(tau) sum_{j>=0} A_{c,1+j} exp(-j / tau) (the
 // exponential RTD channel sums times s01 = exp(-(tp_1 - tp_0) / tau)) for every channel c,

@@ -1176,6 +1176,94 @@ __device__ __forceinline__ void fused_exact(const RtdArgs& a, const UnitArgs& ul
     }
 }
 
+// exp_pist_flow channel sums of one unit (numerators num_c and normaliser den, as
+// rtd_conc_kernel's EPM finalise: conc = (A + J B) / den):
+//   f = first unmasked age (epm_first, the exact mask of :189), m = max(f, 1),
+//   Y_c = sum_{k >= m} A_{c,k} q^(k - m), q = exp(-beta), beta = eta / tau
+//       = head (ages [m, min(B, N)), Horner over the LDS table, B = (m / S + 1) S)
+//         + q^(B - m) T_{B/S}(1 / beta)        (block-tail surrogate, validated per plan)
+//   f >= 1: num = Y, den = G = sum_{j < N - m} q^j;  f = 0: num = A_0 + s01 Y, den = 1 + s01 G.
+// Lanes whose tau' = 1 / beta the surrogate does not cover (or NaN) sum their tail exactly;
+// the loop is wave-uniform and runs only when some lane needs it.
+template <int C>
+__device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, bool mvalid, double tau, double eta,
+                                         double* num, double& den) {
+    constexpr int CP = cheb_cp(C), S = kEpmBlock;
+    const int N = a.N;
+    const double beta = eta / tau;
+    const int f = epm_first(tau * (1 - (1 / eta)), a.tp0, a.dtp, N);
+    const int m = f > 1 ? f : 1;
+    const int blk = m / S + 1, B = blk * S;
+    const double q = fexp(-beta);
+    double y[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) y[c] = 0.0;
+    const int kt = (B < N ? B : N) - 1;
+#pragma unroll 4
+    for (int i = 0; i < S; ++i) {                      // head, top-down Horner (predicated)
+        const int k = kt - i;
+        const bool on = k >= m;
+        const double* row = tabl + (on ? k : 0) * CP;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const double t = fma(y[c], q, row[c]);
+            y[c] = on ? t : y[c];
+        }
+    }
+    const bool tail = B < N;
+    double ex = 0.0;
+    const double taup = 1.0 / beta;
+    int pc = (tail && a.epm) ? cheb_piece(taup, ex) - a.epm_p0 : -1;
+    pc = (unsigned)pc < (unsigned)a.epm_np ? pc : -1;
+    const bool bad = mvalid && tail && pc < 0;
+    double tl[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) tl[c] = 0.0;
+    if (tail) {
+        const double* pt = a.epm + ((size_t)(blk - 1) * a.epm_np + (pc < 0 ? 0 : pc)) * (size_t)(kChebN * CP);
+        cheb_sums<C>(pt, CP, ex, tl);
+    }
+    if (__any(bad)) {                                   // exact tails of the uncovered lanes
+        int bmin = bad ? B : N;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const int o = __shfl_xor(bmin, off, 64);
+            bmin = o < bmin ? o : bmin;
+        }
+        double te[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) te[c] = 0.0;
+        for (int k = N - 1; k >= bmin; --k) {
+            const bool on = bad && k >= B;
+            const double* row = tabl + k * CP;
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const double t = fma(te[c], q, row[c]);
+                te[c] = on ? t : te[c];
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < C; ++c) tl[c] = bad ? te[c] : tl[c];
+    }
+    if (tail) {
+        const double qB = fexp(-beta * (double)(B - m));
+#pragma unroll
+        for (int c = 0; c < C; ++c) y[c] = fma(qB, tl[c], y[c]);
+    }
+    const int n = N - m;
+    const double G = (n > 0) ? fexpm1(-beta * (double)n) / fexpm1(-beta) : 0.0;
+    if (f == 0) {
+        const double s01 = fexp(-beta * ((1.0 + a.dtp) - a.tp0));
+#pragma unroll
+        for (int c = 0; c < C; ++c) num[c] = a.tab0[c] + s01 * y[c];
+        den = 1.0 + s01 * G;
+    } else {
+#pragma unroll
+        for (int c = 0; c < C; ++c) num[c] = y[c];
+        den = G;
+    }
+}
+
 constexpr int kFusedWaves = 8;                 // waves of units per block (512 units)
 constexpr int kFusedUnits = 64 * kFusedWaves;
 constexpr int kFusedPrefetch = 6;   // double2 per thread (512 threads): covers kChebPieces*kChebN*6 doubles
@@ -1192,8 +1280,12 @@ __host__ __device__ constexpr int cheb_lds_stride(int C) { return kChebN * cheb_
 // reference's addition order (th + like).  Role is wave-uniform (no divergence); each role
 // needs fewer registers, so at c4 a SIMD holds 4 waves of two different instruction mixes
 // (transcendental-heavy CE, FMA-chain Clenshaw) that hide each other's latency.
-// MIX = 1: BMM with a piston second component (tau2, f1 roles): its concentrations are a
+// MIX bit 0: BMM with a piston second component (tau2, f1 roles): its concentrations are a
 // channel-table lookup, mixed f1 c1 + (1 - f1) c2 (run_age_mcmc_utils.py:126-161).
+// MIX bit 1: the first component is exp_pist_flow (eta1 role) instead of exponential: the
+// channel table is staged in LDS, every unit sums a head of <= kEpmBlock ages by Horner and
+// reads the block-tail surrogate a.epm at tau' = 1 / beta (epm_sums); lanes whose tau' the
+// surrogate does not cover sum their tail exactly (Horner over the LDS table).
 template <int C, bool FULL, int ROLES, int MIX>
 __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(const RtdArgs a, const UnitArgs ua,
                                                                               int32_t WB, double* __restrict__ logp,
@@ -1243,7 +1335,9 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     const int64_t mu = mvalid ? (int64_t)ml * W + w0 + mwl : 0;
     // per-well observation data -> LDS (read per lane by the likelihood blocks): all loads
     // issued before any store, so the prologue pays one memory latency
-    double* wd = cheb + a.cheb_np * PST;
+    constexpr bool EPM = (MIX & 2) != 0;
+    double* tabl = cheb + a.cheb_np * PST;                // EPM: the channel table [N][CP]
+    double* wd = tabl + (EPM ? a.N * CP : 0);
     constexpr int kWdRegs = (4 * 64 * kFusedWaves + NTH - 1) / NTH;
     double wv[kWdRegs];
 #pragma unroll
@@ -1256,11 +1350,17 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     // wait only for those) so that their HBM latency overlaps the prologue's barrier
     // (A/B against loading them after the barrier: 11.87 vs 11.95 us, tools/gpu_ab_libs.sh)
     ThetaPre tp{};
-    double tau = 1.0;
+    double tau = 1.0, eta = 1.0;
     if (do_theta) theta_preload(ua, mu, tp);
     if (do_rtd) {
         tau = mvalid ? a.theta[(int64_t)a.row_tau[0] * a.U + mu] : 1.0;
+        if (EPM) eta = mvalid ? a.theta[(int64_t)a.row_eta[0] * a.U + mu] : 1.0;
         tp.nub = (FULL || ua.rtd_on) ? a.theta[(int64_t)ua.row_nu * a.U + mu] : 0.0;
+    }
+    if (EPM) {   // channel table -> LDS (rows of CP doubles, CP even: 16-B copies)
+        const double2* src = reinterpret_cast<const double2*>(a.tab);
+        double2* dst = reinterpret_cast<double2*>(tabl);
+        for (int i = tid; i < a.N * CP / 2; i += NTH) dst[i] = src[i];
     }
 #pragma unroll
     for (int r = 0; r < kWdRegs; ++r) {
@@ -1297,7 +1397,22 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     NGRTD_PROBE(1);
     double th = 0.0, like = 0.0;
     if (do_theta) th = mvalid ? unit_logp_theta(ul, mu, ml, &tp, FULL) : 0.0;
-    if (do_rtd) {
+    if (EPM && do_rtd) {
+        double conc[kMaxTracer];
+        {
+            double num[C], den;
+            epm_sums<C>(a, tabl, mvalid, tau, eta, num, den);
+            const double dr[2] = {den, tp.nub * (ua.rnu_max - ua.rnu_min) + ua.rnu_min};
+            double rr[2];
+            batch_recip<2>(dr, rr);
+            double num2[C];
+            if (MIX & 1) piston_num<C>(a, mu, num2);
+            unit_conc<C>(a, mu, num, rr[0], conc, (MIX & 1) ? num2 : nullptr);
+            like = mvalid ? unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL, &rr[1]) : 0.0;
+        }
+        if (!FULL && a.conc && mvalid)                        // forward(): model concentrations
+            for (int t = 0; t < a.K; ++t) a.conc[(int64_t)t * a.U + mu] = conc[t];
+    } else if (do_rtd) {
         // The surrogate channel sums, the concentrations and the RTD likelihood.  Lanes
         // whose tau the surrogate does not cover evaluate piece 0 here and are redone
         // exactly below.
