@@ -1243,14 +1243,18 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
         }
         a.epm = nullptr;
         a.epm_nb = a.epm_p0 = a.epm_np = 0;
+        {
+            const char* e = std::getenv("NGRTD_EPM_DIAG");     // timing diagnostics only
+            a.epm_diag = e ? std::atoi(e) : 0;
+        }
         if (a.mod[0] == MOD_EPM && (a.mod[1] == MOD_NONE || a.mod[1] == MOD_PISTON) && !any_lamw &&
             p->table.C <= 5 && p->dtp >= 0.0 && !(d->flags & NGRTD_EXACT_RTD) && ri[NGRTD_ROLE_ETA1] >= 0) {
-            // block-tail surrogates over the tau' = tau / eta range the priors allow (lanes
-            // outside it sum their tails exactly)
+            // block-tail surrogates over every tau' = tau / eta >= 1/2 (down to the priors'
+            // lower end when it is higher); lanes below sum their short tails exactly
             static const bool disabled = std::getenv("NGRTD_NO_CHEB") != nullptr;
             double x;
-            const double lo = std::max(kChebTauLo, d->tau1_lo / d->eta1_hi), hi = d->tau1_hi / d->eta1_lo;
-            const int pa = cheb_piece(lo, x), pb = cheb_piece(hi, x);
+            const double lo = std::max(kChebTauLo, d->tau1_lo / d->eta1_hi);
+            const int pa = cheb_piece(lo, x), pb = kChebPieces - 1;
             if (!disabled && pa >= 0 && pb >= pa) {
                 NG_CHECK(epm_prepare(ctx, p->table, p->N, pa, pb + 1));
                 if (p->table.epm_ok) {

@@ -46,6 +46,8 @@ struct RtdArgs {
     // laid out [b - 1][piece - epm_p0][kChebN][CP]; null when the plan has none
     const double* epm;
     int32_t epm_nb, epm_p0, epm_np;
+    int32_t epm_diag;       // timing diagnostics only (NGRTD_EPM_DIAG, tools/epm_probe.py): bit 0 skips
+                            // the head, bit 1 the tail surrogate, bit 2 the exact tails (wrong results)
 };
 
 // exp_pist_flow (convolution_integral_utils.py:186-190) on the yearly grid: the unmasked

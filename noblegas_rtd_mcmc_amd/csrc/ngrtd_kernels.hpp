@@ -1199,8 +1199,9 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
 #pragma unroll
     for (int c = 0; c < C; ++c) y[c] = 0.0;
     const int kt = (B < N ? B : N) - 1;
-#pragma unroll 4
-    for (int i = 0; i < S; ++i) {                      // head, top-down Horner (predicated)
+    const int nhead = (a.epm_diag & 1) ? 0 : S;
+#pragma unroll 8
+    for (int i = 0; i < nhead; ++i) {                  // head, top-down Horner (predicated)
         const int k = kt - i;
         const bool on = k >= m;
         const double* row = tabl + (on ? k : 0) * CP;
@@ -1219,22 +1220,29 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
     double tl[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) tl[c] = 0.0;
-    if (tail) {
+    if (tail && !(a.epm_diag & 2)) {
         const double* pt = a.epm + ((size_t)(blk - 1) * a.epm_np + (pc < 0 ? 0 : pc)) * (size_t)(kChebN * CP);
         cheb_sums<C>(pt, CP, ex, tl);
     }
-    if (__any(bad)) {                                   // exact tails of the uncovered lanes
-        int bmin = bad ? B : N;
+    if (__any(bad) && !(a.epm_diag & 4)) {              // exact tails of the uncovered lanes
+        // tau' < 1/2 (q < e^-2): the tail's terms fall below 2e-56 of its first after 64
+        // ages, so it is summed over [B, B + 64) only; other uncovered tau' (NaN, <= 0, beyond
+        // the table) over the whole series.  The loop runs the wave's union of those ranges.
+        const bool shortq = taup > 0.0 && taup < kChebTauLo;
+        const int kend = shortq ? ((B + 63) < (N - 1) ? (B + 63) : (N - 1)) : (N - 1);
+        int bmin = bad ? B : N, kmax = bad ? kend : -1;
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) {
-            const int o = __shfl_xor(bmin, off, 64);
+            const int o = __shfl_xor(bmin, off, 64), o2 = __shfl_xor(kmax, off, 64);
             bmin = o < bmin ? o : bmin;
+            kmax = o2 > kmax ? o2 : kmax;
         }
         double te[C];
 #pragma unroll
         for (int c = 0; c < C; ++c) te[c] = 0.0;
-        for (int k = N - 1; k >= bmin; --k) {
-            const bool on = bad && k >= B;
+#pragma unroll 8
+        for (int k = kmax; k >= bmin; --k) {
+            const bool on = bad && k >= B && k <= kend;
             const double* row = tabl + k * CP;
 #pragma unroll
             for (int c = 0; c < C; ++c) {

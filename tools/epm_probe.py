@@ -48,6 +48,16 @@ def main():
             t2[i] = 3.0 + (t2[i] - 1.0) * 0.0   # all units the same tau: uniform head/tail rows
             out["epm_uniform_tau_us"] = timeit(lp, t2)
         lp.close()
+    # NGRTD_EPM_DIAG (read at plan creation): skip the head (1), the tail surrogate (2), the
+    # exact tails (4) -- wrong results, timing only
+    spec = wl.c4_spec(L=64, N=1200, mod_type1="exp_pist_flow", par_names=("tau1", "eta1"))
+    th = wl.sample_prior(spec, 2048, np.random.default_rng(34568))
+    for d in (1, 2, 4, 3, 7):
+        os.environ["NGRTD_EPM_DIAG"] = str(d)
+        lp = LogProb(spec, max_walkers=2048)
+        out["epm_diag%d_us" % d] = timeit(lp, th)
+        lp.close()
+    os.environ.pop("NGRTD_EPM_DIAG")
     print(json.dumps(out))
 
 
