@@ -309,9 +309,9 @@ int ngrtd_plan_info(ngrtd_plan* plan, int64_t W, int64_t* info, int32_t n);
  * run split over several calls, or over walker-block shards, equals one call.  theta [P][L][W] and logp [W] are DEVICE
  * pointers updated in place on the ctx stream; logp must hold logp(theta) on entry.
  * Every array in the state is device memory owned by the caller.  History layout:
- * [hist_cap][NC][W][16] float64, NC = ceil(P*L/16): entry e, theta row r of chain w at
- * ((e*NC + r/16)*W + w)*16 + r%16 -- the 16 rows of a chunk are one 128-B line.  Entry e
- * is the state after step e (hist_len == steps_done after every call).
+ * [hist_cap][W][P*L] float64 (chain-major): entry e, theta row r of chain w at
+ * (e*W + w)*P*L + r -- a chain's state is one contiguous run.  Entry e is the state after
+ * step e (hist_len == steps_done after every call).
  * accepted_log [n_steps][W] (uint8) and logp_log [n_steps][W] (each chain's log-prob after
  * the step) may be NULL.  n_accepted (device uint64, may be NULL) counts acceptances.
  * 2 launches per step: the proposal kernel (which also appends the previous state) and the
@@ -322,7 +322,7 @@ typedef struct {
     double* lamb;            /* [W] per-chain lambda (PyMC3 default 2.38 / sqrt(2 ndim)) */
     double* scaling;         /* [W] per-chain scaling (PyMC3 default 0.001) */
     int32_t* n_acc_tune;     /* [W] acceptances since the last tune (start at 0) */
-    double* hist;            /* [hist_cap][NC][W][16] */
+    double* hist;            /* [hist_cap][W][P*L] */
     int64_t hist_cap;
     int64_t hist_len;        /* in/out: entries written */
     int64_t hist_lo;         /* in/out: first entry proposals draw from */

@@ -26,7 +26,6 @@ CFC_WHAT = {"equil_air": 0, "equil_aq": 1, "ce_exc": 2, "solubility": 3, "vapor_
             "lapse_rate_atm": 5}
 WANT_LIKE, WANT_PRIOR, WANT_JACOBIAN, EXACT_RTD = 1, 2, 4, 8
 TUNE_TARGET = {None: 0, "none": 0, "scaling": 1, "lambda": 2}       # enum ngrtd_tune_target
-Z_CHUNK = 16                                                          # history rows per 128-B line
 
 _dp = C.POINTER(C.c_double)
 _i32p = C.POINTER(C.c_int32)

@@ -607,13 +607,16 @@ static void launch_fused_cf(const RtdArgs& a, const UnitArgs& u, int WB, int64_t
         else launch_fused_cfr<C, FULL, 1, 0>(a, u, WB, W, logp, da, st);
     }
 }
-// FULL instance: CE + RTD blocks, priors and likelihoods on, no Jacobians (the joint model)
+// FULL instances: CE + RTD blocks, priors and likelihoods on (the joint model), without or
+// -- single-component RTD -- with the transform Jacobians (the transformed-space sampler)
 template <int C>
 static void launch_fused_c(const RtdArgs& a, const UnitArgs& u, int WB, int64_t W, double* logp,
                            const DemcAccept& da, hipStream_t st) {
-    const bool full = u.ce_on && u.rtd_on && (u.flags & NGRTD_WANT_LIKE) && (u.flags & NGRTD_WANT_PRIOR) &&
-                      !(u.flags & NGRTD_WANT_JACOBIAN);
-    if (full) launch_fused_cf<C, true>(a, u, WB, W, logp, da, st);
+    const bool joint = u.ce_on && u.rtd_on && (u.flags & NGRTD_WANT_LIKE) && (u.flags & NGRTD_WANT_PRIOR);
+    const bool jac = (u.flags & NGRTD_WANT_JACOBIAN) != 0;
+    if (joint && !jac) launch_fused_cf<C, true>(a, u, WB, W, logp, da, st);
+    else if (joint && a.mod[1] == MOD_NONE && a.mod[0] == MOD_EXP) launch_fused_cfr<C, true, 2, 4>(a, u, WB, W, logp, da, st);
+    else if (joint && a.mod[1] == MOD_NONE && a.mod[0] == MOD_EPM) launch_fused_cfr<C, true, 2, 6>(a, u, WB, W, logp, da, st);
     else launch_fused_cf<C, false>(a, u, WB, W, logp, da, st);
 }
 static int launch_fused(ngrtd_ctx* ctx, const RtdArgs& a0, const UnitArgs& u, int64_t W, int L, double* logp,
@@ -1553,7 +1556,6 @@ int ngrtd_demcz_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64
     if (n_steps == 0) return NGRTD_OK;
     hipStream_t st = S(ctx);
     const int64_t R = (int64_t)p->desc.n_params * p->desc.n_wells, E = R * W;
-    const int32_t NC = (int32_t)cdiv(R, kZChunk);
     HIP_TRY(ctx, p->demc_prop[0].ensure((size_t)E * sizeof(double)));
     HIP_TRY(ctx, p->demc_lp.ensure((size_t)W * sizeof(double)));
     HIP_TRY(ctx, p->demc_acc.ensure((size_t)W * sizeof(int32_t)));
@@ -1572,12 +1574,12 @@ int ngrtd_demcz_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64
     double* state = tr ? z->theta_u : theta;              // what the history records
     DemczArgs base{};
     base.x = state; base.prop = prop; base.hist = z->hist; base.lamb = z->lamb; base.scaling = z->scaling;
-    base.W = W; base.R = R; base.NC = NC; base.chain0 = z->chain0; base.Wg = Wg; base.S = z->S;
+    base.W = W; base.R = R; base.chain0 = z->chain0; base.Wg = Wg; base.S = z->S;
     base.prop_x = tr ? prop_x : nullptr; base.L = p->desc.n_wells;
     for (int i = 0; i < kRoleCount; ++i) {
         base.tr_kind[i] = z->tr_kind[i]; base.tr_a[i] = z->tr_a[i]; base.tr_b[i] = z->tr_b[i];
     }
-    const dim3 grid((unsigned)cdiv(W, 64), (unsigned)cdiv(NC, 4));
+    const dim3 grid((unsigned)cdiv(W, kZTileW), (unsigned)cdiv(R, kZTileR));
     for (int64_t j = 0; j < n_steps; ++j) {
         const int64_t s = z->steps_done;
         const uint64_t key = demc_key(z->seed, (uint64_t)s);
@@ -1589,7 +1591,7 @@ int ngrtd_demcz_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64
             z->hist_lo += (int64_t)(z->drop_fraction * (double)(z->hist_len - z->hist_lo));   // oldest
         DemczArgs d = base;
         d.propose = 1; d.append_at = append_at; d.lo = z->hist_lo; d.it = z->hist_len - z->hist_lo; d.key = key;
-        hipLaunchKernelGGL(demcz_propose_kernel, grid, dim3(256), 0, st, d);
+        hipLaunchKernelGGL(demcz_propose_kernel, grid, dim3(kZThreads), 0, st, d);
         HIP_TRY(ctx, hipGetLastError());
         const int64_t next = s + 1;
         const int32_t tune_now = (z->tune_target != NGRTD_TUNE_NONE && next < z->n_tune &&
@@ -1604,7 +1606,7 @@ int ngrtd_demcz_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64
     // the last step's state: history entry steps_done - 1
     DemczArgs d = base;
     d.propose = 0; d.append_at = z->hist_len;
-    hipLaunchKernelGGL(demcz_propose_kernel, grid, dim3(256), 0, st, d);
+    hipLaunchKernelGGL(demcz_propose_kernel, grid, dim3(kZThreads), 0, st, d);
     HIP_TRY(ctx, hipGetLastError());
     z->hist_len += 1;
     return NGRTD_OK;

@@ -175,16 +175,14 @@ struct DemcAccept {
 };
 
 // DEMetropolisZ proposal / history append over theta rows [R][W] (demcz_propose_kernel)
-constexpr int kZChunk = 16;
-constexpr int kRoleCount = NGRTD_ROLE_COUNT;     // history rows per 128-B chunk: [entry][R/16][W][16]
+constexpr int kRoleCount = NGRTD_ROLE_COUNT;
 struct DemczArgs {
     const double* x;        // [R][W] current state
     double* prop;           // [R][W] new proposal
-    double* hist;           // [cap][NC][W][kZChunk] chain histories
+    double* hist;           // [cap][W][R] chain histories (chain-major)
     const double* lamb;     // [W]
     const double* scaling;  // [W]
     int64_t W, R;
-    int32_t NC;             // chunks of kZChunk rows
     int32_t propose;        // 0: append only (no proposal)
     int64_t append_at;      // history entry that receives x (-1: none)
     int64_t lo, it;         // partners come from entries lo + [0, it)

@@ -514,11 +514,14 @@ __device__ __forceinline__ double beta_block(const UnitArgs& a, int64_t u, const
     return inb ? (lint + lsum) - a.bt_betaln : kNegInf;
 }
 
+// full_jac: compile-time promise (with full) that the plan also carries the PyMC3
+// transform Jacobians -- the transformed-space sampler's log-prob (sampler.py)
 __device__ __forceinline__ double unit_logp_theta(const UnitArgs& a, int64_t u, int l,
-                                                  const ThetaPre* pre = nullptr, bool full = false) {
+                                                  const ThetaPre* pre = nullptr, bool full = false,
+                                                  bool full_jac = false) {
     const bool want_like = full || (a.flags & NGRTD_WANT_LIKE);
     const bool want_prior = full || (a.flags & NGRTD_WANT_PRIOR);
-    const bool jac = !full && (a.flags & NGRTD_WANT_JACOBIAN);
+    const bool jac = full ? full_jac : (a.flags & NGRTD_WANT_JACOBIAN) != 0;
     double lp = 0.0;
     if (want_prior) lp += beta_block(a, u, pre, full);
     if (full || a.ce_on) {
@@ -1048,73 +1051,110 @@ __host__ __device__ __forceinline__ void demcz_partners(uint64_t key, uint64_t w
 }
 
 // DEMetropolisZ proposal of every chain (pymc3 DEMetropolisZ.astep):
-//   x* = x + lamb_w (Z_w[iz1] - Z_w[iz2]) + eps,  eps = U(-1, 1) scaling_w per parameter
-// (noise only while the history has < 2 entries), and the history append of the current
-// state x (the previous step's q_new) into entry append_at.  Thread = (chain w, chunk c
-// of 16 theta rows): its x rows load coalesced across the wave's 64 chains ([R][W]), its
-// history chunk is one contiguous 128-B line ([entry][NC][W][16]: the wave touches 8 KiB
-// contiguous), so partner rows of different entries per chain cost no wasted bytes.
-__global__ void __launch_bounds__(256) demcz_propose_kernel(const DemczArgs d) {
-    const int64_t w = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
-    const int c = (int)blockIdx.y * 4 + (int)(threadIdx.x >> 6);
-    if (w >= d.W || c >= d.NC) return;
-    const int64_t W = d.W;
-    const int64_t r0 = (int64_t)c * kZChunk;
-    const int nr = (int)((d.R - r0) < kZChunk ? (d.R - r0) : kZChunk);
-    double x[kZChunk];
-#pragma unroll
-    for (int i = 0; i < kZChunk; ++i) x[i] = i < nr ? d.x[(r0 + i) * W + w] : 0.0;
-    const size_t line = (size_t)W * kZChunk;                 // doubles per (entry, chunk)
-    const size_t off = (size_t)c * line + (size_t)w * kZChunk;
-    const size_t entry = (size_t)d.NC * line;                 // doubles per entry
-    if (d.append_at >= 0) {
-        double2* dst = reinterpret_cast<double2*>(d.hist + (size_t)d.append_at * entry + off);
-#pragma unroll
-        for (int i = 0; i < kZChunk / 2; ++i) dst[i] = double2{x[2 * i], x[2 * i + 1]};
-    }
-    if (!d.propose) return;
-    const double lamb = d.lamb[w], sc = d.scaling[w];
-    const uint64_t ke = rng_mix(d.key + 2);
-    double y[kZChunk];
-    if (d.it > 1) {
+//   x* = x + lamb_w (Z_w[iz1] - Z_w[iz2]) + eps,  eps = U(-1, 1) S_r scaling_w per row
+// (noise only while the history has < 2 entries), the history append of the current state
+// x (the previous step's q_new) into entry append_at, and -- transformed chains -- the
+// natural-space copy backward(x*) the log-prob reads.
+// Layouts: theta / proposals are [R][W] (walkers contiguous: what the log-prob kernel
+// reads coalesced); the history is CHAIN-major, entry e of chain w at (e W + w) R: a
+// partner state is one contiguous R * 8-byte run (4 KiB at c4), so the two random
+// partner reads per chain hit whole DRAM pages instead of R scattered lines.  A block
+// owns a tile of kZTileW chains x kZTileR rows and transposes through LDS: x rows are read
+// (and proposals written) 128 B per row, history rows 1 KiB per chain.
+constexpr int kZTileW = 16, kZTileR = 128, kZThreads = 256;
+constexpr int kZPer = kZTileW * kZTileR / kZThreads;   // tile elements per thread (8)
+__global__ void __launch_bounds__(kZThreads) demcz_propose_kernel(const DemczArgs d) {
+    __shared__ double xs[kZTileW][kZTileR + 1];       // chain-major tiles (+1: no bank conflicts)
+    __shared__ double ps[kZTileW][kZTileR + 1];
+    __shared__ double px[kZTileW][kZTileR + 1];
+    const int64_t W = d.W, R = d.R;
+    const int64_t w0 = (int64_t)blockIdx.x * kZTileW, r0 = (int64_t)blockIdx.y * kZTileR;
+    const int nw = (int)((W - w0) < kZTileW ? (W - w0) : kZTileW);
+    const int nr = (int)((R - r0) < kZTileR ? (R - r0) : kZTileR);
+    const int t = threadIdx.x;
+    // chain-major mapping: thread -> (chain j, rows i0 + 16 k); row-major: (row t / 16 + 16 k, chain t % 16)
+    const int j = t / kZTileW, i0 = t % kZTileW;
+    const int jr = t % kZTileW, ir = t / kZTileW;
+    const bool jv = j < nw;
+    const int64_t w = w0 + j;
+    const size_t entry = (size_t)W * R;
+    // ONE memory round trip: the partner indices need only the random key, so the x tile
+    // (row-major) and both partner runs (chain-major) are loaded together
+    const bool de = d.propose && d.it > 1;
+    int64_t e1 = -1, e2 = -1;
+    if (de && jv) {
         uint64_t iz1, iz2;
         demcz_partners(d.key, (uint64_t)(d.chain0 + w), (uint64_t)d.it, iz1, iz2);
-        const int64_t e1 = d.lo + (int64_t)iz1, e2 = d.lo + (int64_t)iz2;
-        double z1[kZChunk], z2[kZChunk];
-        const double2* s1 = reinterpret_cast<const double2*>(d.hist + (size_t)e1 * entry + off);
-        const double2* s2 = reinterpret_cast<const double2*>(d.hist + (size_t)e2 * entry + off);
+        e1 = d.lo + (int64_t)iz1;
+        e2 = d.lo + (int64_t)iz2;
+    }
+    double xr[kZPer], z1v[kZPer], z2v[kZPer];
 #pragma unroll
-        for (int i = 0; i < kZChunk / 2; ++i) {
-            const double2 a = s1[i], b = s2[i];
-            z1[2 * i] = a.x; z1[2 * i + 1] = a.y;
-            z2[2 * i] = b.x; z2[2 * i + 1] = b.y;
+    for (int k = 0; k < kZPer; ++k) {
+        const int i = ir + kZTileW * k;
+        xr[k] = (i < nr && jr < nw) ? d.x[(r0 + i) * W + w0 + jr] : 0.0;
+    }
+    if (de && jv) {
+        const double* z1 = d.hist + (size_t)e1 * entry + (size_t)w * R + r0;
+        const double* z2 = d.hist + (size_t)e2 * entry + (size_t)w * R + r0;
+#pragma unroll
+        for (int k = 0; k < kZPer; ++k) {
+            const int i = i0 + kZTileW * k;
+            z1v[k] = i < nr ? z1[i] : 0.0;
+            z2v[k] = i < nr ? z2[i] : 0.0;
         }
-        // the entry written above by this same thread: take it from registers
-        if (e1 == d.append_at)
-#pragma unroll
-            for (int i = 0; i < kZChunk; ++i) z1[i] = x[i];
-        if (e2 == d.append_at)
-#pragma unroll
-            for (int i = 0; i < kZChunk; ++i) z2[i] = x[i];
-#pragma unroll
-        for (int i = 0; i < kZChunk; ++i) y[i] = x[i] + lamb * (z1[i] - z2[i]);
-    } else {
-#pragma unroll
-        for (int i = 0; i < kZChunk; ++i) y[i] = x[i];
     }
 #pragma unroll
-    for (int i = 0; i < kZChunk; ++i) {
-        if (i < nr) {
+    for (int k = 0; k < kZPer; ++k) {
+        const int i = ir + kZTileW * k;
+        if (i < nr && jr < nw) xs[jr][i] = xr[k];
+    }
+    __syncthreads();
+    // history append (contiguous R-runs per chain)
+    if (d.append_at >= 0 && jv) {
+        double* dst = d.hist + (size_t)d.append_at * entry + (size_t)w * R + r0;
+#pragma unroll
+        for (int k = 0; k < kZPer; ++k) {
+            const int i = i0 + kZTileW * k;
+            if (i < nr) dst[i] = xs[j][i];
+        }
+    }
+    if (!d.propose) return;
+    if (jv) {
+        const double lamb = d.lamb[w], sc = d.scaling[w];
+        const uint64_t ke = rng_mix(d.key + 2);
+        // an entry appended by this block in this launch: its values are x itself
+        const bool c1 = e1 == d.append_at, c2 = e2 == d.append_at;
+#pragma unroll
+        for (int k = 0; k < kZPer; ++k) {
+            const int i = i0 + kZTileW * k;
+            if (i >= nr) continue;
+            const double x = xs[j][i];
+            double y = x;
+            if (de) {
+                const double a1 = c1 ? x : z1v[k], a2 = c2 ? x : z2v[k];
+                y = x + lamb * (a1 - a2);
+            }
             // element stream: row-major over (row, GLOBAL chain) -- a shard draws its chains' numbers
             const uint64_t e = (uint64_t)(r0 + i) * (uint64_t)d.Wg + (uint64_t)(d.chain0 + w);
             const double u2 = 2.0 * rng_unit(rng_mix(ke + e)) - 1.0;
             const double eps = (d.S ? u2 * d.S[r0 + i] : u2) * sc;
-            const double v = y[i] + eps;
-            d.prop[(r0 + i) * W + w] = v;
+            const double v = y + eps;
+            ps[j][i] = v;
             if (d.prop_x) {       // transformed chains: the natural-space value the log-prob reads
                 const int pr = (int)((r0 + i) / d.L);
-                d.prop_x[(r0 + i) * W + w] = pymc3_backward(d.tr_kind[pr], d.tr_a[pr], d.tr_b[pr], v);
+                px[j][i] = pymc3_backward(d.tr_kind[pr], d.tr_a[pr], d.tr_b[pr], v);
             }
+        }
+    }
+    __syncthreads();
+    // proposals back to [R][W], 128 B per row
+#pragma unroll
+    for (int k = 0; k < kZPer; ++k) {
+        const int i = ir + kZTileW * k;
+        if (i < nr && jr < nw) {
+            d.prop[(r0 + i) * W + w0 + jr] = ps[jr][i];
+            if (d.prop_x) d.prop_x[(r0 + i) * W + w0 + jr] = px[jr][i];
         }
     }
 }
@@ -1170,8 +1210,8 @@ __device__ __forceinline__ void fused_exact(const RtdArgs& a, const UnitArgs& ul
         ThetaPre tp;
         tp.nub = nub;
         double num2[C];
-        if (MIX) piston_num<C>(a, mu, num2);
-        mfma_unit_conc<C>(a, mu, bu, yy, conc, MIX ? num2 : nullptr);
+        if (MIX & 1) piston_num<C>(a, mu, num2);
+        mfma_unit_conc<C>(a, mu, bu, yy, conc, (MIX & 1) ? num2 : nullptr);
         like = unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL);
     }
 }
@@ -1290,6 +1330,7 @@ __host__ __device__ constexpr int cheb_lds_stride(int C) { return kChebN * cheb_
 // (transcendental-heavy CE, FMA-chain Clenshaw) that hide each other's latency.
 // MIX bit 0: BMM with a piston second component (tau2, f1 roles): its concentrations are a
 // channel-table lookup, mixed f1 c1 + (1 - f1) c2 (run_age_mcmc_utils.py:126-161).
+// MIX bit 2 (FULL only): the plan carries the transform Jacobians (NGRTD_WANT_JACOBIAN).
 // MIX bit 1: the first component is exp_pist_flow (eta1 role) instead of exponential: the
 // channel table is staged in LDS, every unit sums a head of <= kEpmBlock ages by Horner and
 // reads the block-tail surrogate a.epm at tau' = 1 / beta (epm_sums); lanes whose tau' the
@@ -1404,7 +1445,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     __syncthreads();
     NGRTD_PROBE(1);
     double th = 0.0, like = 0.0;
-    if (do_theta) th = mvalid ? unit_logp_theta(ul, mu, ml, &tp, FULL) : 0.0;
+    if (do_theta) th = mvalid ? unit_logp_theta(ul, mu, ml, &tp, FULL, (MIX & 4) != 0) : 0.0;
     if (EPM && do_rtd) {
         double conc[kMaxTracer];
         {
@@ -1456,8 +1497,8 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             double rr[2];
             batch_recip<2>(dr, rr);
             double num2[C];
-            if (MIX) piston_num<C>(a, mu, num2);
-            unit_conc<C>(a, mu, num, rr[0], conc, MIX ? num2 : nullptr);
+            if (MIX & 1) piston_num<C>(a, mu, num2);
+            unit_conc<C>(a, mu, num, rr[0], conc, (MIX & 1) ? num2 : nullptr);
             if (cnan)
                 for (int t = 0; t < a.K; ++t) conc[t] = __builtin_nan("");
             like = mvalid ? unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL, &rr[1]) : 0.0;

@@ -275,17 +275,16 @@ class DEMetropolisZ:
 
 class ZState:
     """Device state of a DEMetropolisZ run (ngrtd_demcz_state): per-chain lamb / scaling /
-    tuning counters and the chain histories [cap][NC][W][16] (NC = ceil(R / 16)), which
-    also hold the draws."""
+    tuning counters and the chain histories [cap][W][R] (chain-major: a chain's state is one
+    contiguous run), which also hold the draws."""
 
     def __init__(self, R, W, hist_cap, device, lamb, scaling, n_tune, tune_interval, tune_target,
                  drop_fraction, seed, chain0=0, n_chains_total=0, S=None):
         self.R, self.W = int(R), int(W)
-        self.NC = (self.R + _lib.Z_CHUNK - 1) // _lib.Z_CHUNK
         self.lamb = torch.full((W,), float(lamb), dtype=torch.float64, device=device)
         self.scaling = torch.full((W,), float(scaling), dtype=torch.float64, device=device)
         self.n_acc_tune = torch.zeros(W, dtype=torch.int32, device=device)
-        self.hist = torch.empty((int(hist_cap), self.NC, W, _lib.Z_CHUNK), dtype=torch.float64, device=device)
+        self.hist = torch.empty((int(hist_cap), W, self.R), dtype=torch.float64, device=device)
         self.u = None                     # transformed-space chains (set by DeviceDEMetropolisZ.start)
         self.S = (None if S is None else
                   torch.as_tensor(S, dtype=torch.float64).reshape(self.R).contiguous().to(device))
@@ -299,8 +298,7 @@ class ZState:
 
     def entries(self, lo, hi):
         """History entries [lo, hi) as [hi - lo][R][W]."""
-        h = self.hist[lo:hi].permute(0, 1, 3, 2).reshape(hi - lo, self.NC * _lib.Z_CHUNK, self.W)
-        return h[:, :self.R]
+        return self.hist[lo:hi].permute(0, 2, 1)
 
 
 class DeviceDEMetropolisZ:

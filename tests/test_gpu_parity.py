@@ -215,6 +215,28 @@ def test_published_models_c4_shape_vs_oracle(model):
     lp.close()
 
 
+@pytest.mark.parametrize("model", ["exponential", "exp_pist_flow", "exponential-piston"])
+def test_jacobian_plans_c4_shape_vs_oracle(model):
+    """Plans with the PyMC3 transform Jacobians (the transformed-space sampler's log-prob;
+    the joint single-component ones run the FULL + Jacobian kernel instances) at the c4
+    shape vs the per-walker oracle."""
+    import dataclasses
+    import oracle.models as om
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+    m1, _, m2 = model.partition("-")
+    pn = ["tau1"] + (["tau2", "f1"] if m2 else []) + (["eta1"] if m1 == "exp_pist_flow" else [])
+    spec = dataclasses.replace(wl.c4_spec(L=64, N=1200, mod_type1=m1, mod_type2=m2 or None, par_names=tuple(pn)),
+                               jacobian=True)
+    th = wl.sample_prior(spec, 2048, np.random.default_rng(34568))
+    lp = LogProb(spec, max_walkers=2048)
+    a = lp(th, soa=True)
+    walkers = [0, 1, 511, 512, 2047]
+    ref = om.log_prob(spec, th, walkers=walkers)
+    assert close(a[walkers], ref, 1e-12, 1e-9).all(), (a[walkers], ref)
+    lp.close()
+
+
 def test_c4_full_size_vs_oracle_and_properties():
     """c4 at full size (2048 x 64 x (5 gases + 5 tracers)): sampled walkers vs the oracle,
     bitwise determinism, device == host path, walker-permutation equivariance."""
