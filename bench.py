@@ -234,15 +234,18 @@ def main():
         dist.destroy_process_group()
 
 
-def pmc_summary(kfull):
-    """Committed PMC summary of the same command (tools/gpu_profile.sh -> tools/profile_summary.py)."""
+def pmc_summary(kfull, instance=None):
+    """Committed PMC summary of the same command (tools/gpu_profile.sh -> tools/profile_summary.py):
+    the entry of this exact kernel instance when present, else any launch of the kernel."""
     for name in PMC_SUMMARIES:
         path = os.environ.get("NGRTD_PMC_SUMMARY") or os.path.join(REPO, "profiles", name)
         if os.path.exists(path):
             with open(path) as f:
-                for k, e in json.load(f).items():
-                    if kfull in k:
-                        return e, os.path.relpath(path, REPO)
+                summ = json.load(f)
+            for key in ([instance] if instance else []) + [kfull]:
+                for k, e in summ.items():
+                    if key in k:
+                        return e, os.path.relpath(path, REPO) + (" [%s]" % key)
     return {}, None
 
 
@@ -256,7 +259,13 @@ def report(args, spec, lp, ks, dt, world, W_total, Wb, plan_build_ms, theta, the
     kname = "fused" if ks["fused"][1] else "rtd"
     kms = ks[kname][0] / max(ks[kname][1], 1)
     kfull = {"fused": "logp_fused_kernel", "rtd": "rtd_exp_mfma_kernel" if info["mfma_rows"] else "rtd_conc_kernel"}[kname]
-    pmc, pmc_path = pmc_summary(kfull)
+    instance = None
+    if kname == "fused":
+        r = spec.rtd
+        mix = (1 if r.mod_type2 == "piston" else 0) | (2 if r.mod_type1 == "exp_pist_flow" else 0)
+        full = spec.ce is not None and spec.include_like and spec.include_prior
+        instance = "logp_fused_kernel<%d, %s, 2, %d>" % (C, "true" if full else "false", mix)
+    pmc, pmc_path = pmc_summary(kfull, instance)
     traffic = pmc.get("hbm_bytes_per_launch")        # FETCH_SIZE x 2 (calibrated) + WRITE_SIZE
     exp_single = spec.rtd.mod_type1 == "exponential" and not spec.rtd.mod_type2
     if info.get("surrogate") and pmc.get("fp64_flop_per_unit"):

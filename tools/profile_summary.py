@@ -54,6 +54,13 @@ def main(src, prefix):
             e["units"] = units          # (walker, well) units per launch of the profiled command
             e["fp64_flop_per_unit"] = e["fp64_flop_per_launch"] / units
         out[k] = e
+    # several profiled commands (one per RTD model) merge into one summary, keyed by the
+    # kernel instance name (logp_fused_kernel<C, FULL, ROLES, MIX>)
+    if os.path.exists(prefix + "_pmc.json"):
+        with open(prefix + "_pmc.json") as f:
+            prev = json.load(f)
+        prev.update(out)
+        out = prev
     with open(prefix + "_pmc.json", "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
     print(json.dumps({k[:60]: {c: round(v, 1) for c, v in e.items() if not c.startswith("dur")}
