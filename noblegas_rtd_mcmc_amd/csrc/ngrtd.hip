@@ -538,9 +538,10 @@ static void launch_mfma(const RtdArgs& a, const UnitArgs& u, int32_t fuse, hipSt
 // read from global memory: they are needed only by waves with an uncovered tau) and the
 // packed per-well data (ce obs, 1/sd^2, sums of 0.5 log 1/sd^2, E_min; rtd obs, 1/sd^2,
 // sums; the Student-t normaliser table).
-static size_t fused_lds(const RtdArgs& a, const UnitArgs& u) {
+static size_t fused_lds(const RtdArgs& a, const UnitArgs& u, int dz_p = 0) {
     const size_t epm_tab = a.mod[0] == MOD_EPM ? (size_t)a.N * a.CP : 0;   // EPM: the channel table
-    return (size_t)(2 * kFusedUnits + kFusedUnits / 2 + a.cheb_np * cheb_lds_stride(a.C) + epm_tab + u.wd_n) *
+    const size_t dz = (size_t)dz_p * kFusedUnits;                          // DZ step: the proposals
+    return (size_t)(2 * kFusedUnits + kFusedUnits / 2 + a.cheb_np * cheb_lds_stride(a.C) + epm_tab + u.wd_n + dz) *
            sizeof(double);
 }
 // Surrogate pieces the fused kernel stages: when the unit's log-prob carries the tau1
@@ -557,7 +558,7 @@ static void cheb_window(RtdArgs& a, const UnitArgs& u) {
     a.cheb_p0 = pa;
     a.cheb_np = pb - pa + 1;
 }
-constexpr size_t kFusedMaxLds = 150 * 1024;
+constexpr size_t kFusedMaxLds = 157 * 1024;   // gfx950: 160 KiB per workgroup, less the static fexp/flog tables
 static bool fused_path(const RtdArgs& a0, const UnitArgs& u) {
     static const bool disabled = std::getenv("NGRTD_NO_FUSED") != nullptr;
     RtdArgs a = a0;
@@ -591,8 +592,9 @@ static void launch_fused_cfr(const RtdArgs& a, const UnitArgs& u, int WB, int64_
         return true;
     }();
     (void)attr;
+    const int dz_p = (MIX & 8) ? 2 : 0;          // DZ step: the lamb / scaling rows
     hipLaunchKernelGGL((logp_fused_kernel<C, FULL, ROLES, MIX>), dim3((unsigned)cdiv(W, WB)),
-                       dim3(64 * kFusedWaves * ROLES), fused_lds(a, u), st, a, u, WB, logp, da);
+                       dim3(64 * kFusedWaves * ROLES), fused_lds(a, u, dz_p), st, a, u, WB, logp, da);
 }
 template <int C, bool FULL>
 static void launch_fused_cf(const RtdArgs& a, const UnitArgs& u, int WB, int64_t W, double* logp,
@@ -618,6 +620,42 @@ static void launch_fused_c(const RtdArgs& a, const UnitArgs& u, int WB, int64_t 
     else if (joint && a.mod[1] == MOD_NONE && a.mod[0] == MOD_EXP) launch_fused_cfr<C, true, 2, 4>(a, u, WB, W, logp, da, st);
     else if (joint && a.mod[1] == MOD_NONE && a.mod[0] == MOD_EPM) launch_fused_cfr<C, true, 2, 6>(a, u, WB, W, logp, da, st);
     else launch_fused_cf<C, false>(a, u, WB, W, logp, da, st);
+}
+// Single-launch DEMetropolisZ step (logp_fused_kernel MIX bit 3): the joint plan on a
+// FULL instance with C = 5 channels (the c3 / c4 / published-model workloads), the role-split
+// layout, at most kDzMaxP parameter rows, and the proposals fitting in LDS.  -1: not
+// available (ngrtd_demcz_run then runs the proposal kernel + log-prob kernel pair).
+static int dz_mix(const RtdArgs& a0, const UnitArgs& u, int P, bool transformed) {
+    static const bool disabled = std::getenv("NGRTD_NO_DZ_FUSED") != nullptr;
+    RtdArgs a = a0;
+    cheb_window(a, u);
+    const bool joint = u.ce_on && u.rtd_on && (u.flags & NGRTD_WANT_LIKE) && (u.flags & NGRTD_WANT_PRIOR);
+    const bool jac = (u.flags & NGRTD_WANT_JACOBIAN) != 0;
+    // transformed chains <=> the Jacobian instance (its proposals go through backward())
+    if (disabled || !joint || jac != transformed || a.C != 5 || fused_roles() != 2 || P < 1 || P > kDzMaxP || !fused_path(a, u) ||
+        fused_lds(a, u, 2) > kFusedMaxLds)
+        return -1;
+    const int mix = (a.mod[1] == MOD_PISTON ? 1 : 0) | (a.mod[0] == MOD_EPM ? 2 : 0);
+    if (!jac) return 8 | mix;
+    if (a.mod[1] == MOD_NONE) return 8 | 4 | mix;   // 12 (exponential), 14 (exp_pist_flow)
+    return -1;
+}
+static int launch_fused_dz(ngrtd_ctx* ctx, const RtdArgs& a0, const UnitArgs& u, int64_t W, int L, double* logp,
+                           hipStream_t st, const DemcAccept& da, int mix) {
+    const int WB = kFusedUnits / L;
+    RtdArgs a = a0;
+    cheb_window(a, u);
+    switch (mix) {
+    case 8: launch_fused_cfr<5, true, 2, 8>(a, u, WB, W, logp, da, st); break;
+    case 9: launch_fused_cfr<5, true, 2, 9>(a, u, WB, W, logp, da, st); break;
+    case 10: launch_fused_cfr<5, true, 2, 10>(a, u, WB, W, logp, da, st); break;
+    case 11: launch_fused_cfr<5, true, 2, 11>(a, u, WB, W, logp, da, st); break;
+    case 12: launch_fused_cfr<5, true, 2, 12>(a, u, WB, W, logp, da, st); break;
+    case 14: launch_fused_cfr<5, true, 2, 14>(a, u, WB, W, logp, da, st); break;
+    default: return set_err(ctx, NGRTD_EINVAL, "no single-launch DEMetropolisZ instance %d", mix);
+    }
+    HIP_TRY(ctx, hipGetLastError());
+    return NGRTD_OK;
 }
 static int launch_fused(ngrtd_ctx* ctx, const RtdArgs& a0, const UnitArgs& u, int64_t W, int L, double* logp,
                         hipStream_t st, const DemcAccept* dap = nullptr) {
@@ -1580,7 +1618,47 @@ int ngrtd_demcz_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64
         base.tr_kind[i] = z->tr_kind[i]; base.tr_a[i] = z->tr_a[i]; base.tr_b[i] = z->tr_b[i];
     }
     const dim3 grid((unsigned)cdiv(W, kZTileW), (unsigned)cdiv(R, kZTileR));
-    for (int64_t j = 0; j < n_steps; ++j) {
+    // one launch per step where the plan has a single-launch DEMetropolisZ instance
+    int dzm = -1;
+    const char* dz_env = std::getenv("NGRTD_DZ_DIAG");
+    const int32_t dz_diag = dz_env ? std::atoi(dz_env) : 0;
+    UnitArgs du = p->unit;
+    RtdArgs dr = p->rtd;
+    if (p->desc.rtd_enabled) {
+        du.theta = prop_x; du.U = (int64_t)p->desc.n_wells * W; du.W = W;   // the launch's theta: the
+        dr.theta = prop_x; dr.U = du.U; dr.conc = nullptr;                   // proposals it forms
+        dzm = dz_mix(dr, du, p->desc.n_params, tr);
+    }
+    for (int64_t j = 0; dzm >= 0 && j < n_steps; ++j) {
+        const int64_t s = z->steps_done;
+        const uint64_t key = demc_key(z->seed, (uint64_t)s);
+        // the step appends its state (the previous step's q_new) at entry hist_len, then
+        // draws its partners from [hist_lo, hist_len] -- as the two-launch step below
+        const int64_t append_at = j > 0 ? z->hist_len : -1;
+        if (j > 0) z->hist_len += 1;
+        if (s == z->n_tune && z->n_tune > 0)
+            z->hist_lo += (int64_t)(z->drop_fraction * (double)(z->hist_len - z->hist_lo));
+        const int64_t next = s + 1;
+        const int32_t tune_now = (z->tune_target != NGRTD_TUNE_NONE && next < z->n_tune &&
+                                  next % z->tune_interval == 0) ? 1 : 0;
+        DemcAccept da{logp, acc, cnt, theta, nullptr, p->desc.n_params, key, z->n_acc_tune, z->lamb, z->scaling,
+                      tune_now, z->tune_target, z->tune_interval,
+                      accepted_log ? accepted_log + j * W : nullptr, logp_log ? logp_log + j * W : nullptr,
+                      z->chain0, tr ? z->theta_u : nullptr, nullptr};
+        da.zx = state; da.dz_prop = prop_x; da.hist = z->hist;
+        da.h_lo = z->hist_lo; da.h_it = z->hist_len - z->hist_lo; da.h_at = append_at;
+        da.Wg = Wg; da.S = z->S; da.L = p->desc.n_wells;
+        da.dz_diag = dz_diag;
+        for (int i = 0; i < kRoleCount; ++i) {
+            da.tr_kind[i] = z->tr_kind[i]; da.tr_a[i] = z->tr_a[i]; da.tr_b[i] = z->tr_b[i];
+        }
+        hipEvent_t ev = nullptr;
+        NG_CHECK(timed_begin(p, ctx->profiling, st, &ev));
+        NG_CHECK(launch_fused_dz(ctx, dr, du, W, p->desc.n_wells, p->demc_lp.d(), st, da, dzm));
+        NG_CHECK(timed_end(p, ctx->profiling, st, 3, ev));
+        z->steps_done = next;
+    }
+    for (int64_t j = 0; dzm < 0 && j < n_steps; ++j) {
         const int64_t s = z->steps_done;
         const uint64_t key = demc_key(z->seed, (uint64_t)s);
         // the previous step's state becomes history entry s - 1 (the previous call appended

@@ -172,6 +172,21 @@ struct DemcAccept {
     int64_t chain0;         // global index of chain 0 in the random stream
     double* xu;             // [P][L][W] transformed state (null: natural-space chains)
     const double* prop_u;   // [P][L][W] the transformed proposal, copied to xu on accept
+    // Single-launch DEMetropolisZ step (logp_fused_kernel MIX bit 3): the kernel forms the
+    // proposal itself from the state and two history entries (demcz_propose_kernel's
+    // arithmetic) into dz_prop, appends the state to the history and evaluates the
+    // proposal; prop and prop_u are unused.  Other fields as DemczArgs.
+    const double* zx;       // [P][L][W] state in the chains' space (x, or xu when transformed)
+    double* dz_prop;        // [P][L][W] out: the proposal, natural space (the launch's theta)
+    double* hist;           // [cap][W][R] chain-major histories
+    int64_t h_lo, h_it, h_at;   // partners from entries h_lo + [0, h_it); append x at h_at (-1: none)
+    int64_t Wg;             // chains of the whole ensemble (the noise stream's row stride)
+    const double* S;        // [R] proposal scale per row (null: ones)
+    int32_t L;
+    int32_t dz_diag;        // timing diagnostics only (NGRTD_DZ_DIAG, tools/dz_probe.py): bit 0: proposal =
+                            // state, 1: no history store, 2: no commit, 3: no staging (wrong results)
+    int32_t tr_kind[NGRTD_ROLE_COUNT];
+    double tr_a[NGRTD_ROLE_COUNT], tr_b[NGRTD_ROLE_COUNT];
 };
 
 // DEMetropolisZ proposal / history append over theta rows [R][W] (demcz_propose_kernel)

@@ -1038,6 +1038,14 @@ __host__ __device__ __forceinline__ double pymc3_backward(int kind, double a, do
     if (kind == NGRTD_TR_LOG) return exp(u);
     return u;
 }
+// The same values with ONE exp call and selects (straight-line: what an unrolled loop
+// over the parameter rows wants); bitwise equal to pymc3_backward.
+__device__ __forceinline__ double pymc3_backward_sel(int kind, double a, double b, double u) {
+    const double ex = exp(kind == NGRTD_TR_LOG ? u : -u);
+    const double s = 1.0 / (1.0 + ex);
+    const double iv = s * b + (1.0 - s) * a;
+    return kind == NGRTD_TR_LOGODDS ? s : kind == NGRTD_TR_INTERVAL ? iv : kind == NGRTD_TR_LOG ? ex : u;
+}
 
 // Partners of chain w for the step keyed `key` (DEMetropolisZ.astep: iz1 = randint(it),
 // iz2 = randint(it) redrawn until != iz1 -- i.e. uniform over the it - 1 others):
@@ -1155,6 +1163,131 @@ __global__ void __launch_bounds__(kZThreads) demcz_propose_kernel(const DemczArg
         if (i < nr && jr < nw) {
             d.prop[(r0 + i) * W + w0 + jr] = ps[jr][i];
             if (d.prop_x) d.prop_x[(r0 + i) * W + w0 + jr] = px[jr][i];
+        }
+    }
+}
+
+constexpr int kDzMaxP = 12;          // parameter rows of a single-launch DEMetropolisZ step
+constexpr int kFusedUnitsDz = 512;   // = kFusedUnits (units per logp_fused_kernel block)
+
+// One element of a DEMetropolisZ proposal, the arithmetic of demcz_propose_kernel (bitwise):
+// x + lamb (z1 - z2) + eps, eps = U(-1, 1) S_r scaling from the (row, global chain) stream.
+__device__ __forceinline__ double dz_value(const DemcAccept& d, bool de, double x, double z1, double z2, double lamb,
+                                          double sc, uint64_t ke, int64_t r, int64_t chain) {
+    const double y = de ? x + lamb * (z1 - z2) : x;
+    const uint64_t e = (uint64_t)r * (uint64_t)d.Wg + (uint64_t)chain;
+    const double u2 = 2.0 * rng_unit(rng_mix(ke + e)) - 1.0;
+    const double eps = (d.S ? u2 * d.S[r] : u2) * sc;
+    return y + eps;
+}
+
+// Single-launch DEMetropolisZ step (logp_fused_kernel MIX bit 3), unit (walker w, well l)
+// of block column i.  Partner entries of chain w (demcz_partners); e = -1 without DE.
+__device__ __forceinline__ void dz_partners(const DemcAccept& d, int64_t w, int64_t& e1, int64_t& e2) {
+    e1 = e2 = -1;
+    if (d.h_it > 1) {
+        uint64_t iz1, iz2;
+        demcz_partners(d.key, (uint64_t)(d.chain0 + w), (uint64_t)d.h_it, iz1, iz2);
+        e1 = d.h_lo + (int64_t)iz1;
+        e2 = d.h_lo + (int64_t)iz2;
+    }
+}
+// Load the unit's state rows and its two partners' rows (chain-major history: entry e of
+// chain w at (e W + w) R, row p L + l), append the state at entry h_at, form the proposal
+// and write it -- natural space -- to d.dz_prop [P][L][W], the theta rows the rest of the
+// launch reads (the block's own lines, behind the barrier); LDS rows 0 and 1 (th) keep
+// the chain's lamb and scaling as used (the decision may retune them) for dz_commit.
+// (Reading the proposals back from an LDS copy instead was slower: the extra uniform row
+// indices spilled SGPRs into the unit body.)
+template <int PMAX, bool TR>
+__device__ __forceinline__ void dz_stage(const DemcAccept& d, int64_t U, int64_t u, int i, int64_t w, int l, int L,
+                                         int64_t W, bool valid, double* th, int p0) {
+    const int64_t R = (int64_t)d.P * L;
+    if (!valid || (d.dz_diag & 8)) return;
+    if (d.dz_diag & 1) {   // timing diagnostics: the proposal is the state (no partners, no noise)
+        for (int p = p0; p < d.P; p += 2)
+            d.dz_prop[(int64_t)p * U + u] = d.zx[(int64_t)p * U + u];
+        return;
+    }
+    int64_t e1, e2;
+    dz_partners(d, w, e1, e2);
+    const bool de = e1 >= 0;
+    const double* z1 = d.hist + ((size_t)(de ? e1 : 0) * W + w) * R + l;
+    const double* z2 = d.hist + ((size_t)(de ? e2 : 0) * W + w) * R + l;
+    const double lamb = d.lamb[w], sc = d.scaling[w];
+    constexpr int KMAX = (PMAX + 1) / 2;
+    double x[KMAX], a1[KMAX], a2[KMAX];
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+        const int p = p0 + 2 * k;
+        if (p < d.P) {
+            x[k] = d.zx[(int64_t)p * U + u];
+            a1[k] = de ? z1[(int64_t)p * L] : 0.0;
+            a2[k] = de ? z2[(int64_t)p * L] : 0.0;
+        }
+    }
+    // an entry appended in this launch is the state itself (as demcz_propose_kernel)
+    const bool c1 = e1 == d.h_at, c2 = e2 == d.h_at;
+    double* hrow = d.hist + ((size_t)(d.h_at < 0 ? 0 : d.h_at) * W + w) * R + l;
+    const uint64_t ke = rng_mix(d.key + 2);
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+        const int p = p0 + 2 * k;
+        if (p < d.P) {
+            if (d.h_at >= 0 && !(d.dz_diag & 2)) hrow[(int64_t)p * L] = x[k];
+            double v = dz_value(d, de, x[k], c1 ? x[k] : a1[k], c2 ? x[k] : a2[k], lamb, sc, ke,
+                                (int64_t)p * L + l, d.chain0 + w);
+            // transformed chains: the natural-space value the log-prob reads
+            if (TR) v = pymc3_backward_sel(d.tr_kind[p], d.tr_a[p], d.tr_b[p], v);
+            d.dz_prop[(int64_t)p * U + u] = v;
+        }
+    }
+    if (p0 == 0) {
+        th[i] = lamb;
+        th[kFusedUnitsDz + i] = sc;
+    }
+}
+// An accepted unit takes the proposal: natural rows from d.dz_prop (this lane's own
+// stores); transformed chains also the chains'-space value, recomputed from the same loads
+// and the staged lamb / scaling.
+template <int PMAX, bool TR>
+__device__ __forceinline__ void dz_commit(const DemcAccept& d, int64_t U, int64_t u, int i, int64_t w, int l, int L,
+                                          int64_t W, const double* th, int p0) {
+    // every load first, then every store: the stores may alias the loads' arrays for the
+    // compiler, so a rolled load-compute-store loop would pay one memory round trip per row
+    const int64_t R = (int64_t)d.P * L;
+    int64_t e1 = -1, e2 = -1;
+    if (TR) dz_partners(d, w, e1, e2);
+    const bool de = e1 >= 0;
+    const double* z1 = d.hist + ((size_t)(de ? e1 : 0) * W + w) * R + l;
+    const double* z2 = d.hist + ((size_t)(de ? e2 : 0) * W + w) * R + l;
+    constexpr int KMAX = (PMAX + 1) / 2;
+    double pv[KMAX], x[KMAX], a1[KMAX], a2[KMAX];
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+        const int p = p0 + 2 * k;
+        if (p < d.P) {
+            const int64_t gi = (int64_t)p * U + u;
+            pv[k] = d.dz_prop[gi];
+            if (TR) {
+                x[k] = d.zx[gi];
+                a1[k] = de ? z1[(int64_t)p * L] : 0.0;
+                a2[k] = de ? z2[(int64_t)p * L] : 0.0;
+            }
+        }
+    }
+    const bool c1 = e1 == d.h_at, c2 = e2 == d.h_at;
+    const double lamb = th[i], sc = th[kFusedUnitsDz + i];
+    const uint64_t ke = rng_mix(d.key + 2);
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+        const int p = p0 + 2 * k;
+        if (p < d.P) {
+            const int64_t gi = (int64_t)p * U + u;
+            d.x[gi] = pv[k];
+            if (TR)
+                d.xu[gi] = dz_value(d, de, x[k], c1 ? x[k] : a1[k], c2 ? x[k] : a2[k], lamb, sc, ke,
+                                    (int64_t)p * L + l, d.chain0 + w);
         }
     }
 }
@@ -1335,10 +1468,24 @@ __host__ __device__ constexpr int cheb_lds_stride(int C) { return kChebN * cheb_
 // channel table is staged in LDS, every unit sums a head of <= kEpmBlock ages by Horner and
 // reads the block-tail surrogate a.epm at tau' = 1 / beta (epm_sums); lanes whose tau' the
 // surrogate does not cover sum their tail exactly (Horner over the LDS table).
+// MIX bit 3 (FULL, ROLES = 2): one whole DEMetropolisZ step per launch (ngrtd_demcz_run).
+// The theta waves load their unit's state rows x and the rows of the chain's two history
+// partners (chain-major: a wave's 8 lanes of one walker read 64 contiguous bytes, as they
+// do from theta), append x to the history, form the proposal (dz_value) and write it --
+// natural space, after the PyMC3 backward transform -- to the theta rows the launch reads
+// (a.theta = dacc.dz_prop; each block reads back only its own units' lines, behind the
+// barrier).  After the Metropolis decision the accepted units' lanes write the proposal
+// into the state (and, transformed, recompute and write the chains'-space value).  Per
+// step: 3 reads + 2 writes of the state's size in HBM, against 6 reads + 3 writes (+ the
+// accepted copies) for the proposal kernel + log-prob kernel pair.
 template <int C, bool FULL, int ROLES, int MIX>
-__global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(const RtdArgs a, const UnitArgs ua,
+__global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(const RtdArgs ak, const UnitArgs ua,
                                                                               int32_t WB, double* __restrict__ logp,
                                                                               const DemcAccept dacc) {
+    constexpr bool DZ = (MIX & 8) != 0;
+    static_assert(!DZ || (FULL && ROLES == 2), "the DEMetropolisZ step runs in the FULL role-split kernel");
+    static_assert(kFusedUnitsDz == kFusedUnits, "DZ staging stride");
+    const RtdArgs& a = ak;
     constexpr int NT = mfma_tiles(C);
     constexpr int CP = cheb_cp(C);
     constexpr int NTH = 64 * kFusedWaves * ROLES;           // threads per block
@@ -1400,11 +1547,13 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     // (A/B against loading them after the barrier: 11.87 vs 11.95 us, tools/gpu_ab_libs.sh)
     ThetaPre tp{};
     double tau = 1.0, eta = 1.0;
-    if (do_theta) theta_preload(ua, mu, tp);
-    if (do_rtd) {
-        tau = mvalid ? a.theta[(int64_t)a.row_tau[0] * a.U + mu] : 1.0;
-        if (EPM) eta = mvalid ? a.theta[(int64_t)a.row_eta[0] * a.U + mu] : 1.0;
-        tp.nub = (FULL || ua.rtd_on) ? a.theta[(int64_t)ua.row_nu * a.U + mu] : 0.0;
+    if (!DZ) {
+        if (do_theta) theta_preload(ua, mu, tp);
+        if (do_rtd) {
+            tau = mvalid ? a.theta[(int64_t)a.row_tau[0] * a.U + mu] : 1.0;
+            if (EPM) eta = mvalid ? a.theta[(int64_t)a.row_eta[0] * a.U + mu] : 1.0;
+            tp.nub = (FULL || ua.rtd_on) ? a.theta[(int64_t)ua.row_nu * a.U + mu] : 0.0;
+        }
     }
     if (EPM) {   // channel table -> LDS (rows of CP doubles, CP even: 16-B copies)
         const double2* src = reinterpret_cast<const double2*>(a.tab);
@@ -1442,8 +1591,21 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         }
         if (ua.c0_tab) ul.c0_tab = wd + (ua.c0_tab - ua.wd_src);
     }
+    // DZ: the theta waves form the proposals (a.theta = dacc.dz_prop), after the table stores
+    // so that the table registers are free for the 3 P loads
+    double* thl = wd + ua.wd_n;                           // DZ: [2][512] lamb, scaling
+    // both roles stage: theta waves the even parameter rows, RTD waves the odd ones
+    if (DZ) dz_stage<kDzMaxP, (MIX & 4) != 0>(dacc, ua.U, mu, mi, w0 + mwl, ml, L, W, mvalid, thl, do_theta ? 0 : 1);
     __syncthreads();
     NGRTD_PROBE(1);
+    if (DZ) {                                             // the proposal's rows
+        if (do_theta) theta_preload(ua, mu, tp);
+        if (do_rtd) {
+            tau = mvalid ? a.theta[(int64_t)a.row_tau[0] * a.U + mu] : 1.0;
+            if (EPM) eta = mvalid ? a.theta[(int64_t)a.row_eta[0] * a.U + mu] : 1.0;
+            tp.nub = a.theta[(int64_t)ua.row_nu * a.U + mu];
+        }
+    }
     double th = 0.0, like = 0.0;
     if (do_theta) th = mvalid ? unit_logp_theta(ul, mu, ml, &tp, FULL, (MIX & 4) != 0) : 0.0;
     if (EPM && do_rtd) {
@@ -1536,7 +1698,11 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         for (int l = 1; l < L; ++l) tot += part[l * WB + tid];
         walker_out(logp, dacc, w0 + tid, tot, dec + tid);
     }
-    if (dacc.lp) {   // DE-MC: accepted walkers take the proposal's theta rows of this unit
+    if (DZ) {
+        __syncthreads();
+        if (mvalid && dec[mwl] && !(dacc.dz_diag & 4))
+            dz_commit<kDzMaxP, (MIX & 4) != 0>(dacc, ua.U, mu, mi, w0 + mwl, ml, L, W, thl, do_theta ? 0 : 1);
+    } else if (dacc.lp) {   // DE-MC: accepted walkers take the proposal's theta rows of this unit
         __syncthreads();
         if (do_theta && mvalid && dec[mwl]) {
             for (int p = 0; p < dacc.P; ++p) dacc.x[(int64_t)p * a.U + mu] = dacc.prop[(int64_t)p * a.U + mu];

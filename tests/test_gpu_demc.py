@@ -15,12 +15,17 @@ def _same(a, b):
     return torch.equal(a, b) or bool(((a == b) | (torch.isnan(a) & torch.isnan(b))).all())
 
 
-@pytest.mark.parametrize("kind", ["joint", "ce_only", "joint_transformed", "bmm_transformed"])
+@pytest.mark.parametrize("kind", ["joint", "ce_only", "joint_transformed", "bmm_transformed", "bmm", "epm",
+                                  "epm_piston", "epm_transformed", "joint_c4_transformed"])
 def test_device_demcz_matches_torch_bitwise(kind):
     """Tuning (every 4 steps), stop_tuning's history drop and the draws: device chains ==
-    torch chains, bit for bit (joint: the single-launch kernel decides; ce_only: the
-    generic kernels + demc_accept_kernel; *_transformed: PyMC3's logodds / interval / log
-    space, the proposal kernel maps rows back, the plan adds the Jacobian)."""
+    torch chains, bit for bit.  joint / bmm / epm / epm_piston / joint_transformed /
+    epm_transformed / joint_c4_transformed run one launch per step (logp_fused_kernel forms the
+    proposal, appends the history, decides and commits); ce_only: the generic kernels +
+    demc_accept_kernel; bmm_transformed: the proposal kernel + the log-prob kernel pair.
+    *_transformed: PyMC3's logodds / interval / log space, the plan adds the Jacobian.
+    joint_c4_transformed: the c4 shape (64 wells, 8 walkers per block), 520 chains: the last
+    block is partial."""
     import dataclasses
     import torch
     from noblegas_rtd_mcmc_amd import workloads as wl
@@ -33,9 +38,18 @@ def test_device_demcz_matches_torch_bitwise(kind):
     if kind == "bmm_transformed":
         spec = wl.c4_spec(L=2, N=1200, mod_type1="exp_pist_flow", mod_type2="piston",
                           par_names=("tau1", "tau2", "f1", "eta1", "lamsf6"))
+    if kind == "bmm":
+        spec = wl.c4_spec(L=4, N=1200, mod_type1="exponential", mod_type2="piston", par_names=("tau1", "tau2", "f1"))
+    if kind in ("epm", "epm_transformed"):
+        spec = wl.c4_spec(L=4, N=1200, mod_type1="exp_pist_flow", par_names=("tau1", "eta1"))
+    if kind == "epm_piston":
+        spec = wl.c4_spec(L=4, N=1200, mod_type1="exp_pist_flow", mod_type2="piston",
+                          par_names=("tau1", "tau2", "f1", "eta1"))
+    if kind == "joint_c4_transformed":
+        spec = wl.c4_spec(L=64, N=1200)
     if kind.endswith("transformed"):
         spec = dataclasses.replace(spec, jacobian=True)
-    W = 40
+    W = 520 if kind == "joint_c4_transformed" else 40
     th0 = wl.sample_prior(spec, W, np.random.default_rng(5))
     lp = LogProb(spec, max_walkers=W)
     x0 = torch.from_numpy(th0).cuda()

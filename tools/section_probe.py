@@ -39,7 +39,7 @@ def main():
     ap.add_argument("--wells", type=int, default=64)
     ap.add_argument("--walkers", type=int, default=2048)
     ap.add_argument("--build-only", action="store_true")
-    ap.add_argument("--variant", default="joint", choices=["joint", "rtd_only", "rtd_bare"])
+    ap.add_argument("--variant", default="joint", choices=["joint", "rtd_only", "rtd_bare", "dz"])
     args = ap.parse_args()
     build()
     if args.build_only:
@@ -63,9 +63,17 @@ def main():
     for _ in range(20):
         lp(dev, out=out)
     torch.cuda.synchronize()
+    if args.variant == "dz":     # one single-launch DEMetropolisZ step after 10 steps
+        from noblegas_rtd_mcmc_amd.sampler import DeviceDEMetropolisZ
+        x, l, z = DeviceDEMetropolisZ(lp, tune=None, seed=7).start(dev, 0, 12)
+        lp.demcz(x, l, 10, z)
+        torch.cuda.synchronize()
     lp.ctx.set_profiling(True)
     lp.kernel_stats(reset=True)
-    lp(dev, out=out)
+    if args.variant == "dz":
+        lp.demcz(x, l, 1, z)
+    else:
+        lp(dev, out=out)
     torch.cuda.synchronize()
     ks = lp.kernel_stats(reset=True)
     lib = _lib.load()
@@ -80,6 +88,8 @@ def main():
         tt = t[sel]
         r = {"prologue": tt[:, 1] - tt[:, 0], "work": tt[:, 3] - tt[:, 1], "exchange": tt[:, 6] - tt[:, 3],
              "reduce": tt[:, 7] - tt[:, 6], "total": tt[:, 7] - tt[:, 0]}
+        if grp == "theta_role" and args.variant == "dz":
+            r["dz_stage"] = tt[:, 4] - tt[:, 0]
         if grp == "rtd_role":
             r["surrogate_like"] = tt[:, 2] - tt[:, 1]
             r["theta_load_piece"] = tt[:, 4] - tt[:, 1]
