@@ -5,7 +5,8 @@ Workload (BASELINE.json configs[3]): 2048 walkers x 64 wells 
 5 gases + RTD convolution of 5 tracers over a 1200-year input series, exponential RTD)
 in float64.  One step = one full batched log-prob of the rank's walker block (theta
 resident in HBM) + ONE all-gather of the per-block log-prob vector (N > 1), the loop of
-distributed.LogpStepLoop.
+distributed.LogpStepLoop (N = 1: LogpStepLoop.run enqueues the K launches with one native
+call, ngrtd_logp_n, instead of K Python round trips).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling weak|strong]
                     [--mod-type1 exponential|exp_pist_flow|piston|dispersion] [--mod-type2 piston|...]
@@ -177,7 +178,9 @@ def main():
     plan_build_ms = (time.perf_counter() - t0) * 1e3
     loop = LogpStepLoop(None, W_total, dev)
     fast = lp.bind(theta, loop.out)
+    fast_n = lp.bind_n(theta, loop.out)
     loop.evaluate = lambda out: fast()
+    loop.evaluate_n = lambda out, k: fast_n(k)     # N = 1: the K steps in one native call
 
     for _ in range(args.warmup):
         loop.step()
@@ -205,13 +208,16 @@ def main():
     per_step_events = world > 1 or not single_kernel
     t0 = time.perf_counter()
     ev0.record()
-    for i in range(args.steps):
-        sample = per_step_events and i % args.event_every == 0
-        if sample:
-            lp.ctx.set_profiling(True)
-        loop.step()
-        if sample:
-            lp.ctx.set_profiling(False)
+    if per_step_events:
+        for i in range(args.steps):
+            sample = i % args.event_every == 0
+            if sample:
+                lp.ctx.set_profiling(True)
+            loop.step()
+            if sample:
+                lp.ctx.set_profiling(False)
+    else:
+        loop.run(args.steps)
     ev1.record()
     torch.cuda.synchronize()
     if world > 1:

@@ -261,6 +261,13 @@ int ngrtd_plan_destroy(ngrtd_plan* plan);
  * laid out structure-of-arrays [P][L][W] (float64).  W <= max_walkers.               */
 int ngrtd_logp(ngrtd_plan* plan, const double* theta, int64_t W, double* logp, int32_t mem);
 
+/* n back-to-back log-probs of the same device buffers, enqueued by one call (device
+ * memory only): the shape of the reference's sampling loop -- one model log-prob per
+ * step, pm.sample in run_age_mcmc_utils.py:416 / noble_gas_mcmc.py:410-415 -- without
+ * the host round trip per step.  Every step is one full launch over all W walkers; logp
+ * holds the last one.  Used by bench.py (N = 1) via distributed.LogpStepLoop.run. */
+int ngrtd_logp_n(ngrtd_plan* plan, const double* theta, int64_t W, double* logp, int64_t n);
+
 /* Forward model outputs of the plan (posterior predictive, run_age_mcmc.py:251-319,
  * noble_gas_mcmc.py:645-653): ce_out [G][L][W] (may be NULL), rtd_out [K][L][W]
  * (may be NULL).                                                                     */

@@ -1539,6 +1539,16 @@ int ngrtd_logp(ngrtd_plan* p, const double* theta, int64_t W, double* logp, int3
     return NGRTD_OK;
 }
 
+int ngrtd_logp_n(ngrtd_plan* p, const double* theta, int64_t W, double* logp, int64_t n) {
+    if (!p) return NGRTD_ESTATE;
+    ngrtd_ctx* ctx = p->ctx;
+    if (!theta || !logp || W < 0 || W > p->max_w || n < 0)
+        return set_err(ctx, NGRTD_EINVAL, "bad theta/logp/W (max %lld)/n", (long long)p->max_w);
+    if (W == 0) return NGRTD_OK;
+    for (int64_t i = 0; i < n; ++i) NG_CHECK(plan_run(p, theta, W, logp, nullptr, nullptr));
+    return NGRTD_OK;
+}
+
 int ngrtd_forward(ngrtd_plan* p, const double* theta, int64_t W, double* ce_out, double* rtd_out, int32_t mem) {
     if (!p) return NGRTD_ESTATE;
     ngrtd_ctx* ctx = p->ctx;

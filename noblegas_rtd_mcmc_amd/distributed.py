@@ -32,8 +32,9 @@ class LogpStepLoop:
     (tests/test_distributed_cpu.py), so the bench's multi-GPU step has no untested branch.
     """
 
-    def __init__(self, evaluate, W_total, device, dtype=torch.float64, group=None):
+    def __init__(self, evaluate, W_total, device, dtype=torch.float64, group=None, evaluate_n=None):
         self.evaluate = evaluate
+        self.evaluate_n = evaluate_n      # optional: evaluate_n(out, k) = k evaluations in one call
         self.group = group
         self.W_total = int(W_total)
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
@@ -49,6 +50,16 @@ class LogpStepLoop:
         self.evaluate(self.out)
         if self.world > 1:
             dist.all_gather_into_tensor(self.gathered, self.buf, group=self.group)
+        return self.gathered
+
+    def run(self, k):
+        """k steps.  World 1 with ``evaluate_n``: one call enqueues the k evaluations (no
+        collective to interleave, so no host round trip per step); else k ``step()``s."""
+        if self.world == 1 and self.evaluate_n is not None:
+            self.evaluate_n(self.out, int(k))
+        else:
+            for _ in range(int(k)):
+                self.step()
         return self.gathered
 
     def ensemble(self):

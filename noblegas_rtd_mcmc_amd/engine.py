@@ -169,6 +169,23 @@ class LogProb:
             return keep[1]
         return run
 
+    def bind_n(self, theta, out):
+        """As ``bind``, for k back-to-back log-probs per call: returns ``run(k)`` (one
+        ngrtd_logp_n call enqueues k full launches; out holds the last)."""
+        W = self._check_dev(theta)
+        if out.dtype != theta.dtype or not out.is_cuda or not out.is_contiguous() or out.numel() != W:
+            raise ValueError("out must be a contiguous CUDA float64 tensor [W]")
+        f = self.lib.ngrtd_logp_n
+        base = (self.plan, C.c_void_p(theta.data_ptr()), C.c_int64(W), C.c_void_p(out.data_ptr()))
+        keep = (theta, out)
+
+        def run(k):
+            st = f(*base, C.c_int64(int(k)))
+            if st:
+                self.ctx.check(st, "ngrtd_logp_n")
+            return keep[1]
+        return run
+
     def forward(self, theta, soa=False):
         """Model outputs: (ce [G][L][W] or None, rtd [K][L][W] or None)."""
         spec = self.spec

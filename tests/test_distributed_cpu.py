@@ -106,6 +106,8 @@ def _step_loop_worker(rank, world, port, W_total, outdir):
         loop.evaluate = evaluate
         g1 = loop.step().clone()
         g2 = loop.step().clone()
+        loop.evaluate_n = lambda out, k: (_ for _ in ()).throw(AssertionError("world > 1 must gather per step"))
+        assert torch.equal(loop.run(2).nan_to_num(), g1.nan_to_num())   # (padding is NaN)
         np.savez(os.path.join(outdir, "s%d.npz" % rank), ens=loop.ensemble().numpy(), g1=g1.numpy(),
                  g2=g2.numpy(), lo=loop.lo, hi=loop.hi, per=loop.per)
     finally:
@@ -129,3 +131,17 @@ def test_bench_step_loop_gloo(tmp_path, W_total):
     assert int(r0["hi"]) == int(r1["lo"]) and int(r1["hi"]) == W_total
     if W_total % 2:                      # the short last block is NaN-padded in the gather
         assert np.isnan(r0["g1"][-1])
+
+
+def test_step_loop_run_world1_single_call():
+    """World 1 with evaluate_n: run(k) makes ONE evaluate_n(out, k) call (bench.py N = 1:
+    one ngrtd_logp_n call enqueues the K launches); without it, k step()s."""
+    from noblegas_rtd_mcmc_amd.distributed import LogpStepLoop
+    calls = []
+    loop = LogpStepLoop(lambda out: calls.append(("step", 1)) or out.fill_(1.0), 5, "cpu",
+                        evaluate_n=lambda out, k: calls.append(("n", k)) or out.fill_(2.0))
+    assert torch.equal(loop.run(7), torch.full((5,), 2.0, dtype=torch.float64)) and calls == [("n", 7)]
+    loop.evaluate_n = None
+    calls.clear()
+    loop.run(3)
+    assert calls == [("step", 1)] * 3

@@ -250,6 +250,8 @@ def test_c4_full_size_vs_oracle_and_properties():
     a = lp(dev).cpu().numpy()
     b = lp(dev).cpu().numpy()
     assert np.array_equal(a, b)
+    o = torch.full((th.shape[2],), float("nan"), dtype=torch.float64, device="cuda")
+    assert np.array_equal(lp.bind_n(dev, o)(3).cpu().numpy(), a)     # ngrtd_logp_n (bench.py N = 1)
     h = lp(th, soa=True)
     assert np.array_equal(a, h)
     walkers = [0, 1, 63, 64, 1000, 2047]

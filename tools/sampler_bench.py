@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
 """MCMC sampler throughput on the c4 workload (2048 chains x 64 wells): chain-steps/s of
-the device-resident DEMetropolisZ (ngrtd_demcz_run: proposal + history append, then the
-log-prob kernel with the Metropolis decision and tuning; 2 launches per step) in PyMC3's
-transformed space and in the natural space, and of the torch-op DEMetropolisZ loop
-around the same log-prob kernel.  With --profile the proposal kernel's own time is read
-from the plan's HIP-event profiling.  One JSON line.
+the device-resident DEMetropolisZ (ngrtd_demcz_run: ONE launch per step -- proposal from
+the state and two history partners, history append, log-prob, Metropolis decision,
+tuning, commit; NGRTD_NO_DZ_FUSED=1 selects the proposal kernel + log-prob kernel pair)
+in PyMC3's transformed space and in the natural space, and of the torch-op
+DEMetropolisZ loop around the same log-prob kernel.  One JSON line.
 
     python tools/sampler_bench.py [--steps 200]
 """
@@ -64,11 +64,16 @@ def main():
             run()
         torch.cuda.synchronize()
         out["logp_alone_us_" + key] = (time.perf_counter() - t0) / args.steps * 1e6
-    # proposal kernel traffic per step (algorithmic): x read, history append, two partner
-    # chunks, proposal write = 5 R W doubles (+ the natural-space copy when transformed)
-    out["device_demcz_natural"] = {"us_per_step": dn * 1e6, "chain_steps_per_s": W / dn}
-    out["device_demcz_transformed"] = {"us_per_step": dj * 1e6, "chain_steps_per_s": W / dj}
-    out["proposal_bytes_per_step"] = {"natural": 5 * R * W * 8, "transformed": 6 * R * W * 8}
+    # algorithmic HBM bytes of one single-launch step: state + two partner rows read,
+    # history append + proposal written = 5 R W doubles (+ the accepted chains' state
+    # copies, 1 or 2 R W doubles at acceptance 1)
+    nb = 5 * R * W * 8
+    out["device_demcz_natural"] = {"us_per_step": dn * 1e6, "chain_steps_per_s": W / dn,
+                                   "algorithmic_GBps": nb / dn * 1e-9}
+    out["device_demcz_transformed"] = {"us_per_step": dj * 1e6, "chain_steps_per_s": W / dj,
+                                       "algorithmic_GBps": nb / dj * 1e-9}
+    out["step_bytes_algorithmic"] = nb
+    out["single_launch_step"] = not os.environ.get("NGRTD_NO_DZ_FUSED")
     ts = max(10, args.steps // 10)
     f = lambda t: lpj(t)  # noqa: E731
     DEMetropolisZ(f, seed=3, transform=Transform.from_spec(spec)).run(x0, 3, 0)
