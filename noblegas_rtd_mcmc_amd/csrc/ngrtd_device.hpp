@@ -55,7 +55,7 @@ struct RtdArgs {
 // tp_m >= tau (1 - 1/eta); the channel sums Y = sum_{k >= m} A_k q^(k - m), q = exp(-beta),
 // split at the block boundary B = (m / S + 1) S into a head of < S + 1 ages (Horner over the
 // LDS-staged channel table) and q^(B - m) T_{B/S}(1 / beta) from the block-tail surrogates.
-constexpr int kEpmBlock = 32;
+constexpr int kEpmBlock = 16;
 
 // Chebyshev surrogate of Z_c(tau) = s01(tau) sum_{j>=0} A_{c,1+j} exp(-j / tau) (the
 // exponential RTD channel sums times s01 = exp(-(tp_1 - tp_0) / tau)) for every channel c,

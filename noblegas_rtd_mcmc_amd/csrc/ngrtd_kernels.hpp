@@ -1399,28 +1399,45 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
     }
     if (__any(bad) && !(a.epm_diag & 4)) {              // exact tails of the uncovered lanes
         // tau' < 1/2 (q < e^-2): the tail's terms fall below 2e-56 of its first after 64
-        // ages, so it is summed over [B, B + 64) only; other uncovered tau' (NaN, <= 0, beyond
-        // the table) over the whole series.  The loop runs the wave's union of those ranges.
+        // ages, so it is summed over [B, B + 64) only -- 64 iterations over each lane's own
+        // LDS rows, whatever the spread of B across the wave; other uncovered tau' (NaN,
+        // <= 0, beyond the table) over the whole series, the wave's union of those ranges.
+        // Both are the same top-down Horner as before per lane (same bits).
         const bool shortq = taup > 0.0 && taup < kChebTauLo;
-        const int kend = shortq ? ((B + 63) < (N - 1) ? (B + 63) : (N - 1)) : (N - 1);
-        int bmin = bad ? B : N, kmax = bad ? kend : -1;
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-            const int o = __shfl_xor(bmin, off, 64), o2 = __shfl_xor(kmax, off, 64);
-            bmin = o < bmin ? o : bmin;
-            kmax = o2 > kmax ? o2 : kmax;
-        }
+        const bool sb = bad && shortq, lb = bad && !shortq;
         double te[C];
 #pragma unroll
         for (int c = 0; c < C; ++c) te[c] = 0.0;
+        if (__any(sb)) {
 #pragma unroll 8
-        for (int k = kmax; k >= bmin; --k) {
-            const bool on = bad && k >= B && k <= kend;
-            const double* row = tabl + k * CP;
+            for (int j = 63; j >= 0; --j) {
+                const int k = B + j;
+                const bool on = sb && k <= N - 1;
+                const double* row = tabl + (on ? k : 0) * CP;
 #pragma unroll
-            for (int c = 0; c < C; ++c) {
-                const double t = fma(te[c], q, row[c]);
-                te[c] = on ? t : te[c];
+                for (int c = 0; c < C; ++c) {
+                    const double t = fma(te[c], q, row[c]);
+                    te[c] = on ? t : te[c];
+                }
+            }
+        }
+        if (__any(lb)) {
+            int bmin = lb ? B : N, kmax = lb ? N - 1 : -1;
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) {
+                const int o = __shfl_xor(bmin, off, 64), o2 = __shfl_xor(kmax, off, 64);
+                bmin = o < bmin ? o : bmin;
+                kmax = o2 > kmax ? o2 : kmax;
+            }
+#pragma unroll 8
+            for (int k = kmax; k >= bmin; --k) {
+                const bool on = lb && k >= B;
+                const double* row = tabl + k * CP;
+#pragma unroll
+                for (int c = 0; c < C; ++c) {
+                    const double t = fma(te[c], q, row[c]);
+                    te[c] = on ? t : te[c];
+                }
             }
         }
 #pragma unroll
