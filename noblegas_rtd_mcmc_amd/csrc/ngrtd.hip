@@ -592,7 +592,8 @@ static void launch_fused_cfr(const RtdArgs& a, const UnitArgs& u, int WB, int64_
         return true;
     }();
     (void)attr;
-    const int dz_p = (MIX & 8) ? 2 : 0;          // DZ step: the lamb / scaling rows
+    // DZ step, transformed chains: the chains'-space proposal rows
+    const int dz_p = ((MIX & 8) && (MIX & 4)) ? da.P : 0;
     hipLaunchKernelGGL((logp_fused_kernel<C, FULL, ROLES, MIX>), dim3((unsigned)cdiv(W, WB)),
                        dim3(64 * kFusedWaves * ROLES), fused_lds(a, u, dz_p), st, a, u, WB, logp, da);
 }
@@ -633,7 +634,7 @@ static int dz_mix(const RtdArgs& a0, const UnitArgs& u, int P, bool transformed)
     const bool jac = (u.flags & NGRTD_WANT_JACOBIAN) != 0;
     // transformed chains <=> the Jacobian instance (its proposals go through backward())
     if (disabled || !joint || jac != transformed || a.C != 5 || fused_roles() != 2 || P < 1 || P > kDzMaxP || !fused_path(a, u) ||
-        fused_lds(a, u, 2) > kFusedMaxLds)
+        fused_lds(a, u, transformed ? P : 0) > kFusedMaxLds)
         return -1;
     const int mix = (a.mod[1] == MOD_PISTON ? 1 : 0) | (a.mod[0] == MOD_EPM ? 2 : 0);
     if (!jac) return 8 | mix;

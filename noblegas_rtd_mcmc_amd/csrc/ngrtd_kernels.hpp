@@ -1195,10 +1195,10 @@ __device__ __forceinline__ void dz_partners(const DemcAccept& d, int64_t w, int6
 // Load the unit's state rows and its two partners' rows (chain-major history: entry e of
 // chain w at (e W + w) R, row p L + l), append the state at entry h_at, form the proposal
 // and write it -- natural space -- to d.dz_prop [P][L][W], the theta rows the rest of the
-// launch reads (the block's own lines, behind the barrier); LDS rows 0 and 1 (th) keep
-// the chain's lamb and scaling as used (the decision may retune them) for dz_commit.
-// (Reading the proposals back from an LDS copy instead was slower: the extra uniform row
-// indices spilled SGPRs into the unit body.)
+// launch reads (the block's own lines, behind the barrier); transformed chains keep the
+// chains'-space value in LDS row p of th for dz_commit.  (Reading the natural proposals
+// back from an LDS copy instead of d.dz_prop was slower: the extra uniform row indices
+// spilled SGPRs into the unit body.)
 template <int PMAX, bool TR>
 __device__ __forceinline__ void dz_stage(const DemcAccept& d, int64_t U, int64_t u, int i, int64_t w, int l, int L,
                                          int64_t W, bool valid, double* th, int p0) {
@@ -1237,57 +1237,36 @@ __device__ __forceinline__ void dz_stage(const DemcAccept& d, int64_t U, int64_t
             if (d.h_at >= 0 && !(d.dz_diag & 2)) hrow[(int64_t)p * L] = x[k];
             double v = dz_value(d, de, x[k], c1 ? x[k] : a1[k], c2 ? x[k] : a2[k], lamb, sc, ke,
                                 (int64_t)p * L + l, d.chain0 + w);
-            // transformed chains: the natural-space value the log-prob reads
-            if (TR) v = pymc3_backward_sel(d.tr_kind[p], d.tr_a[p], d.tr_b[p], v);
+            // transformed chains: the natural-space value the log-prob reads (and v itself,
+            // the chains'-space value, for dz_commit)
+            if (TR) {
+                th[p * kFusedUnitsDz + i] = v;
+                v = pymc3_backward_sel(d.tr_kind[p], d.tr_a[p], d.tr_b[p], v);
+            }
             d.dz_prop[(int64_t)p * U + u] = v;
         }
     }
-    if (p0 == 0) {
-        th[i] = lamb;
-        th[kFusedUnitsDz + i] = sc;
-    }
 }
-// An accepted unit takes the proposal: natural rows from d.dz_prop (this lane's own
-// stores); transformed chains also the chains'-space value, recomputed from the same loads
-// and the staged lamb / scaling.
+// An accepted unit takes the proposal: natural rows from d.dz_prop (written by this lane
+// role before the barriers), transformed chains also the chains'-space value that
+// dz_stage kept in LDS (row p of th).
 template <int PMAX, bool TR>
-__device__ __forceinline__ void dz_commit(const DemcAccept& d, int64_t U, int64_t u, int i, int64_t w, int l, int L,
-                                          int64_t W, const double* th, int p0) {
-    // every load first, then every store: the stores may alias the loads' arrays for the
-    // compiler, so a rolled load-compute-store loop would pay one memory round trip per row
-    const int64_t R = (int64_t)d.P * L;
-    int64_t e1 = -1, e2 = -1;
-    if (TR) dz_partners(d, w, e1, e2);
-    const bool de = e1 >= 0;
-    const double* z1 = d.hist + ((size_t)(de ? e1 : 0) * W + w) * R + l;
-    const double* z2 = d.hist + ((size_t)(de ? e2 : 0) * W + w) * R + l;
+__device__ __forceinline__ void dz_commit(const DemcAccept& d, int64_t U, int64_t u, int i, const double* th,
+                                          int p0) {
     constexpr int KMAX = (PMAX + 1) / 2;
-    double pv[KMAX], x[KMAX], a1[KMAX], a2[KMAX];
+    double pv[KMAX];
 #pragma unroll
-    for (int k = 0; k < KMAX; ++k) {
+    for (int k = 0; k < KMAX; ++k) {   // every load first, then every store
         const int p = p0 + 2 * k;
-        if (p < d.P) {
-            const int64_t gi = (int64_t)p * U + u;
-            pv[k] = d.dz_prop[gi];
-            if (TR) {
-                x[k] = d.zx[gi];
-                a1[k] = de ? z1[(int64_t)p * L] : 0.0;
-                a2[k] = de ? z2[(int64_t)p * L] : 0.0;
-            }
-        }
+        if (p < d.P) pv[k] = d.dz_prop[(int64_t)p * U + u];
     }
-    const bool c1 = e1 == d.h_at, c2 = e2 == d.h_at;
-    const double lamb = th[i], sc = th[kFusedUnitsDz + i];
-    const uint64_t ke = rng_mix(d.key + 2);
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
         const int p = p0 + 2 * k;
         if (p < d.P) {
             const int64_t gi = (int64_t)p * U + u;
             d.x[gi] = pv[k];
-            if (TR)
-                d.xu[gi] = dz_value(d, de, x[k], c1 ? x[k] : a1[k], c2 ? x[k] : a2[k], lamb, sc, ke,
-                                    (int64_t)p * L + l, d.chain0 + w);
+            if (TR) d.xu[gi] = th[p * kFusedUnitsDz + i];
         }
     }
 }
@@ -1610,7 +1589,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     }
     // DZ: the theta waves form the proposals (a.theta = dacc.dz_prop), after the table stores
     // so that the table registers are free for the 3 P loads
-    double* thl = wd + ua.wd_n;                           // DZ: [2][512] lamb, scaling
+    double* thl = wd + ua.wd_n;                           // DZ, transformed: [P][512] u
     // both roles stage: theta waves the even parameter rows, RTD waves the odd ones
     if (DZ) dz_stage<kDzMaxP, (MIX & 4) != 0>(dacc, ua.U, mu, mi, w0 + mwl, ml, L, W, mvalid, thl, do_theta ? 0 : 1);
     __syncthreads();
@@ -1718,7 +1697,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     if (DZ) {
         __syncthreads();
         if (mvalid && dec[mwl] && !(dacc.dz_diag & 4))
-            dz_commit<kDzMaxP, (MIX & 4) != 0>(dacc, ua.U, mu, mi, w0 + mwl, ml, L, W, thl, do_theta ? 0 : 1);
+            dz_commit<kDzMaxP, (MIX & 4) != 0>(dacc, ua.U, mu, mi, thl, do_theta ? 0 : 1);
     } else if (dacc.lp) {   // DE-MC: accepted walkers take the proposal's theta rows of this unit
         __syncthreads();
         if (do_theta && mvalid && dec[mwl]) {
