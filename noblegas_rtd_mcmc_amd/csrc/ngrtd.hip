@@ -107,6 +107,7 @@ struct ngrtd_plan {
     // workspaces
     DevBuf conc, ulogp, theta_stage, out_stage, ce_stage;
     DevBuf demc_prop[2], demc_lp, demc_acc, demc_cnt;   // ngrtd_demcz_run scratch
+
     RtdArgs rtd{};
     UnitArgs unit{};
     LaunchStats stats;
@@ -627,13 +628,12 @@ static void launch_fused_c(const RtdArgs& a, const UnitArgs& u, int WB, int64_t 
 // layout, at most kDzMaxP parameter rows, and the proposals fitting in LDS.  -1: not
 // available (ngrtd_demcz_run then runs the proposal kernel + log-prob kernel pair).
 static int dz_mix(const RtdArgs& a0, const UnitArgs& u, int P, bool transformed) {
-    static const bool disabled = std::getenv("NGRTD_NO_DZ_FUSED") != nullptr;
     RtdArgs a = a0;
     cheb_window(a, u);
     const bool joint = u.ce_on && u.rtd_on && (u.flags & NGRTD_WANT_LIKE) && (u.flags & NGRTD_WANT_PRIOR);
     const bool jac = (u.flags & NGRTD_WANT_JACOBIAN) != 0;
     // transformed chains <=> the Jacobian instance (its proposals go through backward())
-    if (disabled || !joint || jac != transformed || a.C != 5 || fused_roles() != 2 || P < 1 || P > kDzMaxP || !fused_path(a, u) ||
+    if (!joint || jac != transformed || a.C != 5 || fused_roles() != 2 || P < 1 || P > kDzMaxP || !fused_path(a, u) ||
         fused_lds(a, u, transformed ? P : 0) > kFusedMaxLds)
         return -1;
     const int mix = (a.mod[1] == MOD_PISTON ? 1 : 0) | (a.mod[0] == MOD_EPM ? 2 : 0);
@@ -1638,7 +1638,10 @@ int ngrtd_demcz_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64
     if (p->desc.rtd_enabled) {
         du.theta = prop_x; du.U = (int64_t)p->desc.n_wells * W; du.W = W;   // the launch's theta: the
         dr.theta = prop_x; dr.U = du.U; dr.conc = nullptr;                   // proposals it forms
-        dzm = dz_mix(dr, du, p->desc.n_params, tr);
+        // NGRTD_DZ_MODE=pair: the proposal kernel + log-prob kernel pair even where a
+        // single-launch instance exists (A/B runs, tests/test_gpu_demc.py)
+        const char* m_env = std::getenv("NGRTD_DZ_MODE");
+        if (!(m_env && std::strcmp(m_env, "pair") == 0)) dzm = dz_mix(dr, du, p->desc.n_params, tr);
     }
     for (int64_t j = 0; dzm >= 0 && j < n_steps; ++j) {
         const int64_t s = z->steps_done;

@@ -63,6 +63,38 @@ def test_device_demcz_matches_torch_bitwise(kind):
     lp.close()
 
 
+@pytest.mark.parametrize("jac", [False, True])
+def test_device_demcz_step_modes_bitwise(jac):
+    """Both device step schedules give the same chains bit for bit at the c4 shape (520
+    chains: 65 walker blocks, the last partial): one launch per step (default) and the
+    proposal kernel + log-prob kernel pair (NGRTD_DZ_MODE=pair)."""
+    import dataclasses
+    import os
+    import torch
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+    from noblegas_rtd_mcmc_amd.sampler import DeviceDEMetropolisZ
+    spec = wl.c4_spec(L=64, N=1200)
+    if jac:
+        spec = dataclasses.replace(spec, jacobian=True)
+    W = 520
+    x0 = torch.from_numpy(wl.sample_prior(spec, W, np.random.default_rng(15))).cuda()
+    lp = LogProb(spec, max_walkers=W)
+    res = {}
+    try:
+        for mode in ("fused", "pair"):
+            os.environ["NGRTD_DZ_MODE"] = mode
+            res[mode] = DeviceDEMetropolisZ(lp, tune_interval=4, seed=99).run(x0, tune=8, draws=6)
+    finally:
+        os.environ.pop("NGRTD_DZ_MODE", None)
+    for mode in ("pair",):
+        for k in ("x", "lp", "samples", "logp", "accepted", "lamb", "scaling"):
+            assert _same(res[mode][k], res["fused"][k]), (mode, k)
+    if jac:
+        assert 0 < int(res["fused"]["accepted"].sum()) < res["fused"]["accepted"].numel()
+    lp.close()
+
+
 def test_device_demcz_split_calls_and_shard_offsets():
     """A run split over two calls equals one call; a walker block with chain0 / the
     ensemble size equals the same chains of the whole-ensemble run."""

@@ -2,7 +2,7 @@
 """MCMC sampler throughput on the c4 workload (2048 chains x 64 wells): chain-steps/s of
 the device-resident DEMetropolisZ (ngrtd_demcz_run: ONE launch per step -- proposal from
 the state and two history partners, history append, log-prob, Metropolis decision,
-tuning, commit; NGRTD_NO_DZ_FUSED=1 selects the proposal kernel + log-prob kernel pair)
+tuning, commit; NGRTD_DZ_MODE=pair selects the proposal kernel + log-prob kernel pair)
 in PyMC3's transformed space and in the natural space, and of the torch-op
 DEMetropolisZ loop around the same log-prob kernel.  One JSON line.
 
@@ -73,7 +73,7 @@ def main():
     out["device_demcz_transformed"] = {"us_per_step": dj * 1e6, "chain_steps_per_s": W / dj,
                                        "algorithmic_GBps": nb / dj * 1e-9}
     out["step_bytes_algorithmic"] = nb
-    out["single_launch_step"] = not os.environ.get("NGRTD_NO_DZ_FUSED")
+    out["single_launch_step"] = os.environ.get("NGRTD_DZ_MODE") != "pair"
     ts = max(10, args.steps // 10)
     f = lambda t: lpj(t)  # noqa: E731
     DEMetropolisZ(f, seed=3, transform=Transform.from_spec(spec)).run(x0, 3, 0)
