@@ -26,6 +26,12 @@
 
 using namespace ngrtd;
 
+namespace ngrtd {
+// ngrtd_dz.hip: the single-launch DEMetropolisZ instances (compiled without machine LICM)
+hipError_t launch_fused_dz_instance(int mix, const RtdArgs& a, const UnitArgs& u, int WB, int64_t W, double* logp,
+                                    const DemcAccept& da, size_t lds, size_t max_lds, hipStream_t st);
+}
+
 namespace {
 
 struct DevBuf {
@@ -646,16 +652,10 @@ static int launch_fused_dz(ngrtd_ctx* ctx, const RtdArgs& a0, const UnitArgs& u,
     const int WB = kFusedUnits / L;
     RtdArgs a = a0;
     cheb_window(a, u);
-    switch (mix) {
-    case 8: launch_fused_cfr<5, true, 2, 8>(a, u, WB, W, logp, da, st); break;
-    case 9: launch_fused_cfr<5, true, 2, 9>(a, u, WB, W, logp, da, st); break;
-    case 10: launch_fused_cfr<5, true, 2, 10>(a, u, WB, W, logp, da, st); break;
-    case 11: launch_fused_cfr<5, true, 2, 11>(a, u, WB, W, logp, da, st); break;
-    case 12: launch_fused_cfr<5, true, 2, 12>(a, u, WB, W, logp, da, st); break;
-    case 14: launch_fused_cfr<5, true, 2, 14>(a, u, WB, W, logp, da, st); break;
-    default: return set_err(ctx, NGRTD_EINVAL, "no single-launch DEMetropolisZ instance %d", mix);
-    }
-    HIP_TRY(ctx, hipGetLastError());
+    const int dz_p = (mix & 4) ? da.P : 0;    // transformed chains: the chains'-space proposal rows
+    const hipError_t e = launch_fused_dz_instance(mix, a, u, WB, W, logp, da, fused_lds(a, u, dz_p), kFusedMaxLds, st);
+    if (e == hipErrorInvalidValue) return set_err(ctx, NGRTD_EINVAL, "no single-launch DEMetropolisZ instance %d", mix);
+    HIP_TRY(ctx, e);
     return NGRTD_OK;
 }
 static int launch_fused(ngrtd_ctx* ctx, const RtdArgs& a0, const UnitArgs& u, int64_t W, int L, double* logp,
@@ -1643,34 +1643,36 @@ int ngrtd_demcz_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64
         const char* m_env = std::getenv("NGRTD_DZ_MODE");
         if (!(m_env && std::strcmp(m_env, "pair") == 0)) dzm = dz_mix(dr, du, p->desc.n_params, tr);
     }
-    for (int64_t j = 0; dzm >= 0 && j < n_steps; ++j) {
-        const int64_t s = z->steps_done;
-        const uint64_t key = demc_key(z->seed, (uint64_t)s);
-        // the step appends its state (the previous step's q_new) at entry hist_len, then
-        // draws its partners from [hist_lo, hist_len] -- as the two-launch step below
-        const int64_t append_at = j > 0 ? z->hist_len : -1;
-        if (j > 0) z->hist_len += 1;
-        if (s == z->n_tune && z->n_tune > 0)
-            z->hist_lo += (int64_t)(z->drop_fraction * (double)(z->hist_len - z->hist_lo));
-        const int64_t next = s + 1;
-        const int32_t tune_now = (z->tune_target != NGRTD_TUNE_NONE && next < z->n_tune &&
-                                  next % z->tune_interval == 0) ? 1 : 0;
-        DemcAccept da{logp, acc, cnt, theta, nullptr, p->desc.n_params, key, z->n_acc_tune, z->lamb, z->scaling,
-                      tune_now, z->tune_target, z->tune_interval,
-                      accepted_log ? accepted_log + j * W : nullptr, logp_log ? logp_log + j * W : nullptr,
-                      z->chain0, tr ? z->theta_u : nullptr, nullptr};
+    // single-launch instance: chunks of up to NGRTD_DZ_CHUNK (default 256) steps per launch,
+    // each block running its own chains through the chunk (DemcAccept::Sched / dz_step)
+    const char* chunk_env = std::getenv("NGRTD_DZ_CHUNK");
+    const int64_t chunk = std::max<int64_t>(1, chunk_env ? std::atoll(chunk_env) : 256);
+    for (int64_t j = 0; dzm >= 0 && j < n_steps;) {
+        const int64_t k = std::min(chunk, n_steps - j);
+        DemcAccept da{logp, acc, cnt, theta, nullptr, p->desc.n_params, 0, z->n_acc_tune, z->lamb, z->scaling,
+                      0, z->tune_target, z->tune_interval, accepted_log ? accepted_log + j * W : nullptr,
+                      logp_log ? logp_log + j * W : nullptr, z->chain0, tr ? z->theta_u : nullptr, nullptr};
         da.zx = state; da.dz_prop = prop_x; da.hist = z->hist;
-        da.h_lo = z->hist_lo; da.h_it = z->hist_len - z->hist_lo; da.h_at = append_at;
         da.Wg = Wg; da.S = z->S; da.L = p->desc.n_wells;
         da.dz_diag = dz_diag;
         for (int i = 0; i < kRoleCount; ++i) {
             da.tr_kind[i] = z->tr_kind[i]; da.tr_a[i] = z->tr_a[i]; da.tr_b[i] = z->tr_b[i];
         }
+        da.n_steps = (int32_t)k;
+        da.sch.seed = z->seed; da.sch.s0 = z->steps_done;
+        da.sch.h_len0 = z->hist_len; da.sch.h_lo0 = z->hist_lo; da.sch.append0 = j > 0 ? 1 : 0;
+        da.sch.n_tune = z->n_tune; da.sch.drop = z->drop_fraction;
+        da.sch.tune_target = z->tune_target; da.sch.tune_interval = z->tune_interval;
         hipEvent_t ev = nullptr;
         NG_CHECK(timed_begin(p, ctx->profiling, st, &ev));
         NG_CHECK(launch_fused_dz(ctx, dr, du, W, p->desc.n_wells, p->demc_lp.d(), st, da, dzm));
         NG_CHECK(timed_end(p, ctx->profiling, st, 3, ev));
-        z->steps_done = next;
+        // the host state after the chunk's last step (the kernel's own schedule)
+        const DzStep last = dz_step(da.sch, k - 1);
+        z->hist_len = last.len;
+        z->hist_lo = last.lo;
+        z->steps_done += k;
+        j += k;
     }
     for (int64_t j = 0; dzm < 0 && j < n_steps; ++j) {
         const int64_t s = z->steps_done;

@@ -187,6 +187,29 @@ struct DemcAccept {
                             // state, 1: no history store, 2: no commit, 3: no staging (wrong results)
     int32_t tr_kind[NGRTD_ROLE_COUNT];
     double tr_a[NGRTD_ROLE_COUNT], tr_b[NGRTD_ROLE_COUNT];
+    // Multi-step launch (MIX bit 3): the block runs n_steps consecutive steps of its own
+    // chains (chains exchange nothing, so no grid-wide sync); step j's key / partner range /
+    // append entry / tune flag come from dz_step(sch, j), the host loop's own schedule, and
+    // its logs from acc_log / lp_log + j W.  n_steps = 1 with the fields above otherwise.
+    int32_t n_steps;
+    struct Sched {
+        uint64_t seed;
+        int64_t s0;         // steps_done at the launch's first step
+        int64_t h_len0, h_lo0;   // history length / first usable entry before it
+        int32_t append0;    // the first step appends its state (not the call's first step)
+        int64_t n_tune;
+        double drop;        // stop_tuning's drop fraction, applied at step n_tune
+        int32_t tune_target, tune_interval;
+    } sch;
+};
+
+// One DEMetropolisZ step's schedule (ngrtd_demcz_run's host loop, restated so that a
+// multi-step launch derives it on the device): random key, partner range [lo, lo + it),
+// append entry at (-1: none), tune flag, and the history length after the append.
+struct DzStep {
+    uint64_t key;
+    int64_t lo, it, at, len;
+    int32_t tune_now;
 };
 
 // DEMetropolisZ proposal / history append over theta rows [R][W] (demcz_propose_kernel)

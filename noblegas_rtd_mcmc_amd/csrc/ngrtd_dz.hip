@@ -1,0 +1,43 @@
+// ngrtd_dz.hip -- the single-launch DEMetropolisZ instances of logp_fused_kernel (MIX bit 3),
+// in a translation unit of their own so that they compile with machine LICM off
+// (__graft_entry__.py): a launch runs many steps of its chains (the DemcAccept::Sched loop),
+// and hoisting the log-prob body's loop-invariant constants and addresses out of that loop
+// held them in registers for the whole launch and spilled to scratch (257 VGPRs of scratch
+// spills with it; 0 without).  The plain log-prob instances stay in ngrtd.hip with the
+// default pipeline, so their code does not change.
+#include <hip/hip_runtime.h>
+
+#include "../../include/ngrtd.h"
+#define NGRTD_FUSED_ONLY
+#include "ngrtd_kernels.hpp"
+
+namespace ngrtd {
+
+template <int MIX>
+static hipError_t launch_dz_mix(const RtdArgs& a, const UnitArgs& u, int WB, int64_t W, double* logp,
+                                const DemcAccept& da, size_t lds, size_t max_lds, hipStream_t st) {
+    static const hipError_t attr = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&logp_fused_kernel<5, true, 2, MIX>), hipFuncAttributeMaxDynamicSharedMemorySize,
+        (int)max_lds);
+    (void)attr;
+    const unsigned nb = (unsigned)((W + WB - 1) / WB);
+    hipLaunchKernelGGL((logp_fused_kernel<5, true, 2, MIX>), dim3(nb), dim3(64 * kFusedWaves * 2), lds, st, a, u, WB,
+                       logp, da);
+    return hipGetLastError();
+}
+
+// The DZ instance `mix` (8 | piston 1 | EPM 2 | Jacobian 4) over W chains in blocks of WB.
+hipError_t launch_fused_dz_instance(int mix, const RtdArgs& a, const UnitArgs& u, int WB, int64_t W, double* logp,
+                                    const DemcAccept& da, size_t lds, size_t max_lds, hipStream_t st) {
+    switch (mix) {
+    case 8: return launch_dz_mix<8>(a, u, WB, W, logp, da, lds, max_lds, st);
+    case 9: return launch_dz_mix<9>(a, u, WB, W, logp, da, lds, max_lds, st);
+    case 10: return launch_dz_mix<10>(a, u, WB, W, logp, da, lds, max_lds, st);
+    case 11: return launch_dz_mix<11>(a, u, WB, W, logp, da, lds, max_lds, st);
+    case 12: return launch_dz_mix<12>(a, u, WB, W, logp, da, lds, max_lds, st);
+    case 14: return launch_dz_mix<14>(a, u, WB, W, logp, da, lds, max_lds, st);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace ngrtd

@@ -27,6 +27,15 @@
 #include "ngrtd_math.hpp"
 #include "../../include/ngrtd.h"
 
+// A translation unit that uses only the logp_fused_kernel template (ngrtd_dz.hip) defines
+// NGRTD_FUSED_ONLY: the header's plain kernels then have internal linkage there and do not
+// collide with ngrtd.hip's definitions at link time.
+#ifdef NGRTD_FUSED_ONLY
+#define NGRTD_KLINK static
+#else
+#define NGRTD_KLINK
+#endif
+
 namespace ngrtd {
 
 // Section-timing probe (tools/section_probe.py builds a separate library with
@@ -54,7 +63,7 @@ struct CeArgs {
     double* out;
 };
 
-__global__ void __launch_bounds__(256) ce_forward_kernel(const CeArgs a) {
+NGRTD_KLINK __global__ void __launch_bounds__(256) ce_forward_kernel(const CeArgs a) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.n) return;
     const double E = a.E ? a.E[i] : 0.0;
@@ -600,7 +609,7 @@ __device__ __forceinline__ double unit_logp(const UnitArgs& a, int64_t u, const 
     return unit_logp_theta(a, u, l) + unit_like_rtd(a, u, l, conc);
 }
 
-__global__ void __launch_bounds__(256) unit_logp_kernel(const UnitArgs a) {
+NGRTD_KLINK __global__ void __launch_bounds__(256) unit_logp_kernel(const UnitArgs a) {
     fm_lds_init();
     __syncthreads();
     const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -614,7 +623,7 @@ __global__ void __launch_bounds__(256) unit_logp_kernel(const UnitArgs a) {
 // Per-unit log-prob AND the per-walker sum over wells in one launch (L <= 512): a block
 // owns WB walkers x LS >= L well slots, one unit per thread; the wells of each walker are
 // then added in well order through LDS (deterministic, no atomics, no second launch).
-__global__ void __launch_bounds__(512) unit_walker_kernel(const UnitArgs a, int32_t WB, int32_t LS,
+NGRTD_KLINK __global__ void __launch_bounds__(512) unit_walker_kernel(const UnitArgs a, int32_t WB, int32_t LS,
                                                           double* __restrict__ logp) {
     extern __shared__ __attribute__((aligned(16))) double part[];   // [LS][WB]
     fm_lds_init();
@@ -967,6 +976,28 @@ __host__ __device__ __forceinline__ uint64_t rng_mix(uint64_t z) {
 __host__ __device__ __forceinline__ uint64_t demc_key(uint64_t seed, uint64_t step) {
     return rng_mix(rng_mix(seed) + step);
 }
+// Step j of a multi-step DEMetropolisZ launch (DemcAccept::Sched): ngrtd_demcz_run's
+// per-step bookkeeping -- every step but the call's first appends its state (the previous
+// step's q_new) at the current history length; stop_tuning drops the oldest drop * (len - lo)
+// entries at step n_tune (after that step's append); tune() after the decision of a step
+// whose successor is a multiple of tune_interval below n_tune.
+__host__ __device__ __forceinline__ DzStep dz_step(const DemcAccept::Sched& c, int64_t j) {
+    DzStep r;
+    const int64_t s = c.s0 + j;
+    r.key = demc_key(c.seed, (uint64_t)s);
+    r.len = c.h_len0 + (c.append0 ? j + 1 : j);
+    r.at = (c.append0 || j > 0) ? r.len - 1 : -1;
+    r.lo = c.h_lo0;
+    if (c.n_tune > 0 && c.s0 <= c.n_tune && c.n_tune <= s) {
+        const int64_t jd = c.n_tune - c.s0;
+        const int64_t lend = c.h_len0 + (c.append0 ? jd + 1 : jd);
+        r.lo += (int64_t)(c.drop * (double)(lend - c.h_lo0));
+    }
+    r.it = r.len - r.lo;
+    const int64_t next = s + 1;
+    r.tune_now = (c.tune_target != NGRTD_TUNE_NONE && next < c.n_tune && next % c.tune_interval == 0) ? 1 : 0;
+    return r;
+}
 __host__ __device__ __forceinline__ double rng_unit(uint64_t h) {
     return ((double)(h >> 11) + 0.5) * (1.0 / 9007199254740992.0);
 }
@@ -988,9 +1019,10 @@ __host__ __device__ __forceinline__ double pymc3_tune(double scale, double acc_r
 // chain.  Then the chain's tuning counter and, at the end of a tune interval, its lamb or
 // scaling (DEMetropolisZ.astep: tuned at the start of the next step from the interval's
 // acceptance rate, counter reset).  Returns the decision.
-__device__ __forceinline__ bool demc_decide(const DemcAccept& d, int64_t w, double lp_prop) {
+__device__ __forceinline__ bool demc_decide(const DemcAccept& d, int64_t w, double lp_prop, uint64_t key,
+                                            int32_t tune_now, int64_t log_off) {
     const double cur = d.lp[w];
-    const double logu = log(rng_unit(rng_mix(rng_mix(d.key + 3) + (uint64_t)(d.chain0 + w))));
+    const double logu = log(rng_unit(rng_mix(rng_mix(key + 3) + (uint64_t)(d.chain0 + w))));
     const double mr = lp_prop - cur;
     const bool acc = __builtin_isfinite(mr) && logu < mr;
     d.acc[w] = acc;
@@ -1000,7 +1032,7 @@ __device__ __forceinline__ bool demc_decide(const DemcAccept& d, int64_t w, doub
     }
     if (d.n_acc_tune) {
         int32_t na = d.n_acc_tune[w] + (acc ? 1 : 0);
-        if (d.tune_now) {
+        if (tune_now) {
             const double rate = (double)na / (double)d.tune_interval;
             if (d.tune_target == 2) d.lamb[w] = pymc3_tune(d.lamb[w], rate);
             else if (d.tune_target == 1) d.scaling[w] = pymc3_tune(d.scaling[w], rate);
@@ -1008,14 +1040,17 @@ __device__ __forceinline__ bool demc_decide(const DemcAccept& d, int64_t w, doub
         }
         d.n_acc_tune[w] = na;
     }
-    if (d.acc_log) d.acc_log[w] = (uint8_t)acc;
-    if (d.lp_log) d.lp_log[w] = acc ? lp_prop : cur;
+    if (d.acc_log) d.acc_log[log_off + w] = (uint8_t)acc;
+    if (d.lp_log) d.lp_log[log_off + w] = acc ? lp_prop : cur;
     return acc;
+}
+__device__ __forceinline__ bool demc_decide(const DemcAccept& d, int64_t w, double lp_prop) {
+    return demc_decide(d, w, lp_prop, d.key, d.tune_now, 0);
 }
 
 // accept after the generic kernels: one thread per walker decides and copies the
 // walker's P*L proposal rows into the state (coalesced across the walkers of a wave)
-__global__ void __launch_bounds__(256) demc_accept_kernel(const DemcAccept d, const double* __restrict__ lp_prop,
+NGRTD_KLINK __global__ void __launch_bounds__(256) demc_accept_kernel(const DemcAccept d, const double* __restrict__ lp_prop,
                                                           int64_t W, int64_t R) {
     const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= W) return;
@@ -1071,7 +1106,7 @@ __host__ __device__ __forceinline__ void demcz_partners(uint64_t key, uint64_t w
 // (and proposals written) 128 B per row, history rows 1 KiB per chain.
 constexpr int kZTileW = 16, kZTileR = 128, kZThreads = 256;
 constexpr int kZPer = kZTileW * kZTileR / kZThreads;   // tile elements per thread (8)
-__global__ void __launch_bounds__(kZThreads) demcz_propose_kernel(const DemczArgs d) {
+NGRTD_KLINK __global__ void __launch_bounds__(kZThreads) demcz_propose_kernel(const DemczArgs d) {
     __shared__ double xs[kZTileW][kZTileR + 1];       // chain-major tiles (+1: no bank conflicts)
     __shared__ double ps[kZTileW][kZTileR + 1];
     __shared__ double px[kZTileW][kZTileR + 1];
@@ -1183,13 +1218,14 @@ __device__ __forceinline__ double dz_value(const DemcAccept& d, bool de, double 
 
 // Single-launch DEMetropolisZ step (logp_fused_kernel MIX bit 3), unit (walker w, well l)
 // of block column i.  Partner entries of chain w (demcz_partners); e = -1 without DE.
-__device__ __forceinline__ void dz_partners(const DemcAccept& d, int64_t w, int64_t& e1, int64_t& e2) {
+__device__ __forceinline__ void dz_partners(const DemcAccept& d, const DzStep& sj, int64_t w, int64_t& e1,
+                                            int64_t& e2) {
     e1 = e2 = -1;
-    if (d.h_it > 1) {
+    if (sj.it > 1) {
         uint64_t iz1, iz2;
-        demcz_partners(d.key, (uint64_t)(d.chain0 + w), (uint64_t)d.h_it, iz1, iz2);
-        e1 = d.h_lo + (int64_t)iz1;
-        e2 = d.h_lo + (int64_t)iz2;
+        demcz_partners(sj.key, (uint64_t)(d.chain0 + w), (uint64_t)sj.it, iz1, iz2);
+        e1 = sj.lo + (int64_t)iz1;
+        e2 = sj.lo + (int64_t)iz2;
     }
 }
 // Load the unit's state rows and its two partners' rows (chain-major history: entry e of
@@ -1200,8 +1236,8 @@ __device__ __forceinline__ void dz_partners(const DemcAccept& d, int64_t w, int6
 // back from an LDS copy instead of d.dz_prop was slower: the extra uniform row indices
 // spilled SGPRs into the unit body.)
 template <int PMAX, bool TR>
-__device__ __forceinline__ void dz_stage(const DemcAccept& d, int64_t U, int64_t u, int i, int64_t w, int l, int L,
-                                         int64_t W, bool valid, double* th, int p0) {
+__device__ __forceinline__ void dz_stage(const DemcAccept& d, const DzStep& sj, int64_t U, int64_t u, int i, int64_t w,
+                                         int l, int L, int64_t W, bool valid, double* th, int p0) {
     const int64_t R = (int64_t)d.P * L;
     if (!valid || (d.dz_diag & 8)) return;
     if (d.dz_diag & 1) {   // timing diagnostics: the proposal is the state (no partners, no noise)
@@ -1210,7 +1246,7 @@ __device__ __forceinline__ void dz_stage(const DemcAccept& d, int64_t U, int64_t
         return;
     }
     int64_t e1, e2;
-    dz_partners(d, w, e1, e2);
+    dz_partners(d, sj, w, e1, e2);
     const bool de = e1 >= 0;
     const double* z1 = d.hist + ((size_t)(de ? e1 : 0) * W + w) * R + l;
     const double* z2 = d.hist + ((size_t)(de ? e2 : 0) * W + w) * R + l;
@@ -1227,14 +1263,14 @@ __device__ __forceinline__ void dz_stage(const DemcAccept& d, int64_t U, int64_t
         }
     }
     // an entry appended in this launch is the state itself (as demcz_propose_kernel)
-    const bool c1 = e1 == d.h_at, c2 = e2 == d.h_at;
-    double* hrow = d.hist + ((size_t)(d.h_at < 0 ? 0 : d.h_at) * W + w) * R + l;
-    const uint64_t ke = rng_mix(d.key + 2);
+    const bool c1 = e1 == sj.at, c2 = e2 == sj.at;
+    double* hrow = d.hist + ((size_t)(sj.at < 0 ? 0 : sj.at) * W + w) * R + l;
+    const uint64_t ke = rng_mix(sj.key + 2);
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
         const int p = p0 + 2 * k;
         if (p < d.P) {
-            if (d.h_at >= 0 && !(d.dz_diag & 2)) hrow[(int64_t)p * L] = x[k];
+            if (sj.at >= 0 && !(d.dz_diag & 2)) hrow[(int64_t)p * L] = x[k];
             double v = dz_value(d, de, x[k], c1 ? x[k] : a1[k], c2 ? x[k] : a2[k], lamb, sc, ke,
                                 (int64_t)p * L + l, d.chain0 + w);
             // transformed chains: the natural-space value the log-prob reads (and v itself,
@@ -1271,9 +1307,13 @@ __device__ __forceinline__ void dz_commit(const DemcAccept& d, int64_t U, int64_
     }
 }
 
-__device__ __forceinline__ void walker_out(double* logp, const DemcAccept& d, int64_t w, double tot, int* dec) {
+// STEP: a multi-step DEMetropolisZ launch (the step's schedule sj and log offset), else the
+// launch's own DemcAccept fields
+template <bool STEP>
+__device__ __forceinline__ void walker_out(double* logp, const DemcAccept& d, const DzStep& sj, int64_t log_off,
+                                           int64_t w, double tot, int* dec) {
     if (logp) logp[w] = tot;
-    if (d.lp) *dec = demc_decide(d, w, tot);
+    if (d.lp) *dec = STEP ? demc_decide(d, w, tot, sj.key, sj.tune_now, log_off) : demc_decide(d, w, tot);
 }
 
 // Exact (matrix-core) channel sums for a wave of logp_fused_kernel with an uncovered tau:
@@ -1441,6 +1481,37 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
     }
 }
 
+// A kernel argument read through a pointer the compiler cannot see through (an empty asm
+// redefines the kernarg segment pointer): loads of its fields stay where they are used --
+// a multi-step loop would otherwise hoist every field into registers for the whole loop.
+// The pointer is the kernarg segment itself, so the loads stay scalar loads.  (Taking the
+// address of the by-value parameter instead makes the compiler copy it to scratch.)
+// Explicit kernel arguments sit in order at their natural alignment (the code object's
+// .args metadata: RtdArgs at 0, UnitArgs, WB, logp, DemcAccept at kFusedArgD).
+__host__ __device__ constexpr size_t ka_align(size_t o, size_t a) { return (o + a - 1) / a * a; }
+constexpr size_t kFusedArgU = ka_align(sizeof(RtdArgs), alignof(UnitArgs));
+constexpr size_t kFusedArgD =
+    ka_align(ka_align(ka_align(kFusedArgU + sizeof(UnitArgs), alignof(int32_t)) + sizeof(int32_t), alignof(double*)) +
+                 sizeof(double*),
+             alignof(DemcAccept));
+template <class T>
+__device__ __forceinline__ const T& kernarg_opaque(size_t off) {
+    typedef const __attribute__((address_space(4))) char* CP;
+    CP p = (CP)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *(const T*)(p + off);
+}
+template <class T>
+__device__ __forceinline__ T opaque_v(T x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+template <class T>
+__device__ __forceinline__ T opaque_s(T x) {
+    asm volatile("" : "+s"(x));
+    return x;
+}
+
 constexpr int kFusedWaves = 8;                 // waves of units per block (512 units)
 constexpr int kFusedUnits = 64 * kFusedWaves;
 constexpr int kFusedPrefetch = 6;   // double2 per thread (512 threads): covers kChebPieces*kChebN*6 doubles
@@ -1541,14 +1612,14 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     // theta rows of this lane's unit, issued behind the table loads (the LDS stores below
     // wait only for those) so that their HBM latency overlaps the prologue's barrier
     // (A/B against loading them after the barrier: 11.87 vs 11.95 us, tools/gpu_ab_libs.sh)
-    ThetaPre tp{};
-    double tau = 1.0, eta = 1.0;
+    ThetaPre tp0{};
+    double tau0 = 1.0, eta0 = 1.0;
     if (!DZ) {
-        if (do_theta) theta_preload(ua, mu, tp);
+        if (do_theta) theta_preload(ua, mu, tp0);
         if (do_rtd) {
-            tau = mvalid ? a.theta[(int64_t)a.row_tau[0] * a.U + mu] : 1.0;
-            if (EPM) eta = mvalid ? a.theta[(int64_t)a.row_eta[0] * a.U + mu] : 1.0;
-            tp.nub = (FULL || ua.rtd_on) ? a.theta[(int64_t)ua.row_nu * a.U + mu] : 0.0;
+            tau0 = mvalid ? a.theta[(int64_t)a.row_tau[0] * a.U + mu] : 1.0;
+            if (EPM) eta0 = mvalid ? a.theta[(int64_t)a.row_eta[0] * a.U + mu] : 1.0;
+            tp0.nub = (FULL || ua.rtd_on) ? a.theta[(int64_t)ua.row_nu * a.U + mu] : 0.0;
         }
     }
     if (EPM) {   // channel table -> LDS (rows of CP doubles, CP even: 16-B copies)
@@ -1570,148 +1641,187 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             if (i < TAB2) dst[(i / (kChebN * CP / 2)) * (PST / 2) + i % (kChebN * CP / 2)] = pre[r];
         }
     }
-    UnitArgs ul = ua;
-    {
-        const int nce = ua.ce_on ? L * ua.G : 0, nrt = ua.rtd_on ? L * ua.K : 0;
-        double* q = wd;
-        if (ua.ce_on) {
-            ul.ce_obs = q; q += nce;
-            ul.ce_lam = q; q += nce;
-            ul.ce_hll_sum = q; q += L;
-            ul.ce_Emin = q; q += L;
-        }
-        if (ua.rtd_on) {
-            ul.rtd_obs = q; q += nrt;
-            ul.rtd_lam = q; q += nrt;
-            ul.rtd_hll_sum = q;
-        }
-        if (ua.c0_tab) ul.c0_tab = wd + (ua.c0_tab - ua.wd_src);
-    }
     // DZ: the theta waves form the proposals (a.theta = dacc.dz_prop), after the table stores
     // so that the table registers are free for the 3 P loads
     double* thl = wd + ua.wd_n;                           // DZ, transformed: [P][512] u
-    // both roles stage: theta waves the even parameter rows, RTD waves the odd ones
-    if (DZ) dz_stage<kDzMaxP, (MIX & 4) != 0>(dacc, ua.U, mu, mi, w0 + mwl, ml, L, W, mvalid, thl, do_theta ? 0 : 1);
-    __syncthreads();
-    NGRTD_PROBE(1);
-    if (DZ) {                                             // the proposal's rows
-        if (do_theta) theta_preload(ua, mu, tp);
-        if (do_rtd) {
-            tau = mvalid ? a.theta[(int64_t)a.row_tau[0] * a.U + mu] : 1.0;
-            if (EPM) eta = mvalid ? a.theta[(int64_t)a.row_eta[0] * a.U + mu] : 1.0;
-            tp.nub = a.theta[(int64_t)ua.row_nu * a.U + mu];
-        }
-    }
-    double th = 0.0, like = 0.0;
-    if (do_theta) th = mvalid ? unit_logp_theta(ul, mu, ml, &tp, FULL, (MIX & 4) != 0) : 0.0;
-    if (EPM && do_rtd) {
-        double conc[kMaxTracer];
+    // DZ: dacc.n_steps steps of the block's own chains, the tables staged once above
+    // (a do-while: without DZ there is no back edge at all -- a one-trip for loop changed the
+    // register allocation of the plain log-prob instances)
+    const int nst = DZ ? dacc.n_steps : 1;
+    int js = 0;
+    do {
+        ThetaPre tp = tp0;                                // DZ: loaded per step below
+        double tau = tau0, eta = eta0;
+        // DZ: the argument structs through an opaque kernarg pointer per step, so that the
+        // compiler re-reads their fields where they are used instead of hoisting every field
+        // out of the step loop into registers (which spilled to scratch)
+        const RtdArgs& a = DZ ? kernarg_opaque<RtdArgs>(0) : ak;
+        const UnitArgs& uk = DZ ? kernarg_opaque<UnitArgs>(kFusedArgU) : ua;
+        const DemcAccept& dk = DZ ? kernarg_opaque<DemcAccept>(kFusedArgD) : dacc;
+        // ... and likewise the lane's unit and the LDS carve-up, re-derived per step from
+        // opaque copies (loop-invariant lane addresses hoisted out of the loop spilled too)
+        const int tid_s = DZ ? opaque_v(tid) : tid;
+        const int64_t w0_s = DZ ? opaque_s(w0) : w0;
+        const int tid = tid_s;
+        const int64_t w0 = w0_s;
+        const int wave = tid >> 6, lane = tid & 63;
+        const int uw = wave % kFusedWaves;
+        const bool do_theta = ROLES == 1 || wave < kFusedWaves;
+        const bool do_rtd = ROLES == 1 || wave >= kFusedWaves;
+        const int L = uk.L;
+        const int64_t W = uk.W;
+        const int mi = 64 * uw + lane;
+        const int mwl = mi % WB, ml = mi / WB;
+        const bool mvalid = ml < L && w0 + mwl < W;
+        const int64_t mu = mvalid ? (int64_t)ml * W + w0 + mwl : 0;
+        double* tabl = cheb + a.cheb_np * PST;
+        double* wd = tabl + (EPM ? a.N * CP : 0);
+        double* thl = wd + uk.wd_n;
+        UnitArgs ul = uk;
         {
-            double num[C], den;
-            epm_sums<C>(a, tabl, mvalid, tau, eta, num, den);
-            const double dr[2] = {den, tp.nub * (ua.rnu_max - ua.rnu_min) + ua.rnu_min};
-            double rr[2];
-            batch_recip<2>(dr, rr);
-            double num2[C];
-            if (MIX & 1) piston_num<C>(a, mu, num2);
-            unit_conc<C>(a, mu, num, rr[0], conc, (MIX & 1) ? num2 : nullptr);
-            like = mvalid ? unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL, &rr[1]) : 0.0;
+            const int nce = uk.ce_on ? L * uk.G : 0, nrt = uk.rtd_on ? L * uk.K : 0;
+            double* q = wd;
+            if (uk.ce_on) {
+                ul.ce_obs = q; q += nce;
+                ul.ce_lam = q; q += nce;
+                ul.ce_hll_sum = q; q += L;
+                ul.ce_Emin = q; q += L;
+            }
+            if (uk.rtd_on) {
+                ul.rtd_obs = q; q += nrt;
+                ul.rtd_lam = q; q += nrt;
+                ul.rtd_hll_sum = q;
+            }
+            if (uk.c0_tab) ul.c0_tab = wd + (uk.c0_tab - uk.wd_src);
         }
-        if (!FULL && a.conc && mvalid)                        // forward(): model concentrations
-            for (int t = 0; t < a.K; ++t) a.conc[(int64_t)t * a.U + mu] = conc[t];
-    } else if (do_rtd) {
-        // The surrogate channel sums, the concentrations and the RTD likelihood.  Lanes
-        // whose tau the surrogate does not cover evaluate piece 0 here and are redone
-        // exactly below.
-        double cx = 0.0;
-        int cpc = a.cheb ? cheb_piece(tau, cx) - a.cheb_p0 : -1;
-        cpc = (unsigned)cpc < (unsigned)a.cheb_np ? cpc : -1;   // outside the staged window
-        // An uncovered tau (< 1/2, NaN) outside the support of the tau1 Uniform prior makes the
-        // unit's log-prob -inf whatever the concentrations are -- unless they are NaN, which
-        // the reference's weights produce exactly when (1/tau) exp(-tp/tau) overflows or
-        // divides by 0 (convolution_integral_utils.py:184, then g / g.sum(), :270): such a
-        // lane needs no channel sums, only that NaN predicate.  DE-MC proposals below the
-        // prior bound are common; they would otherwise send whole waves to the exact path.
-        bool skip = false, cnan = false;
-        if (cpc < 0 && a.cheb && (FULL || (ua.rtd_on && (ua.flags & NGRTD_WANT_PRIOR))) &&
-            a.row_tau[0] == ua.row_tau1 && !(tau >= ua.tau1_lo && tau <= ua.tau1_hi) &&
-            !(ua.tau1_lo < kChebTauLo && tau >= ua.tau1_lo)) {
-            skip = true;
-            cnan = exp_rtd_nan(a, tau);
+        DzStep sj{};
+        if (DZ) sj = dz_step(dk.sch, js);
+        const int64_t log_off = (int64_t)js * W;
+        // both roles stage: theta waves the even parameter rows, RTD waves the odd ones
+        if (DZ)
+            dz_stage<kDzMaxP, (MIX & 4) != 0>(dk, sj, uk.U, mu, mi, w0 + mwl, ml, L, W, mvalid, thl,
+                                              do_theta ? 0 : 1);
+        __syncthreads();
+        NGRTD_PROBE(1);
+        if (DZ) {                                             // the proposal's rows
+            if (do_theta) theta_preload(uk, mu, tp);
+            if (do_rtd) {
+                tau = mvalid ? a.theta[(int64_t)a.row_tau[0] * a.U + mu] : 1.0;
+                if (EPM) eta = mvalid ? a.theta[(int64_t)a.row_eta[0] * a.U + mu] : 1.0;
+                tp.nub = a.theta[(int64_t)uk.row_nu * a.U + mu];
+            }
         }
-        const bool bad = cpc < 0 && !skip;
-        cpc = cpc < 0 ? 0 : cpc;
-        double zz[C + 1];
-        NGRTD_PROBE(4);
-        cheb_sums<C + 1, ROLES == 2>(cheb + cpc * PST, CP, cx, zz);   // s01 Y_c (c < C), s01 G
-        NGRTD_PROBE(5);
-        double conc[kMaxTracer];
-        {
-            double num[C];
+        double th = 0.0, like = 0.0;
+        if (do_theta) th = mvalid ? unit_logp_theta(ul, mu, ml, &tp, FULL, (MIX & 4) != 0) : 0.0;
+        if (EPM && do_rtd) {
+            double conc[kMaxTracer];
+            {
+                double num[C], den;
+                epm_sums<C>(a, tabl, mvalid, tau, eta, num, den);
+                const double dr[2] = {den, tp.nub * (uk.rnu_max - uk.rnu_min) + uk.rnu_min};
+                double rr[2];
+                batch_recip<2>(dr, rr);
+                double num2[C];
+                if (MIX & 1) piston_num<C>(a, mu, num2);
+                unit_conc<C>(a, mu, num, rr[0], conc, (MIX & 1) ? num2 : nullptr);
+                like = mvalid ? unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL, &rr[1]) : 0.0;
+            }
+            if (!FULL && a.conc && mvalid)                        // forward(): model concentrations
+                for (int t = 0; t < a.K; ++t) a.conc[(int64_t)t * a.U + mu] = conc[t];
+        } else if (do_rtd) {
+            // The surrogate channel sums, the concentrations and the RTD likelihood.  Lanes
+            // whose tau the surrogate does not cover evaluate piece 0 here and are redone
+            // exactly below.
+            double cx = 0.0;
+            int cpc = a.cheb ? cheb_piece(tau, cx) - a.cheb_p0 : -1;
+            cpc = (unsigned)cpc < (unsigned)a.cheb_np ? cpc : -1;   // outside the staged window
+            // An uncovered tau (< 1/2, NaN) outside the support of the tau1 Uniform prior makes the
+            // unit's log-prob -inf whatever the concentrations are -- unless they are NaN, which
+            // the reference's weights produce exactly when (1/tau) exp(-tp/tau) overflows or
+            // divides by 0 (convolution_integral_utils.py:184, then g / g.sum(), :270): such a
+            // lane needs no channel sums, only that NaN predicate.  DE-MC proposals below the
+            // prior bound are common; they would otherwise send whole waves to the exact path.
+            bool skip = false, cnan = false;
+            if (cpc < 0 && a.cheb && (FULL || (uk.rtd_on && (uk.flags & NGRTD_WANT_PRIOR))) &&
+                a.row_tau[0] == uk.row_tau1 && !(tau >= uk.tau1_lo && tau <= uk.tau1_hi) &&
+                !(uk.tau1_lo < kChebTauLo && tau >= uk.tau1_lo)) {
+                skip = true;
+                cnan = exp_rtd_nan(a, tau);
+            }
+            const bool bad = cpc < 0 && !skip;
+            cpc = cpc < 0 ? 0 : cpc;
+            double zz[C + 1];
+            NGRTD_PROBE(4);
+            cheb_sums<C + 1, ROLES == 2>(cheb + cpc * PST, CP, cx, zz);   // s01 Y_c (c < C), s01 G
+            NGRTD_PROBE(5);
+            double conc[kMaxTracer];
+            {
+                double num[C];
 #pragma unroll
-            for (int c = 0; c < C; ++c) num[c] = a.tab0[c] + zz[c];
-            // the normaliser's reciprocal and the Student-t 1/nu: one division
-            const double dr[2] = {1.0 + zz[C], tp.nub * (ua.rnu_max - ua.rnu_min) + ua.rnu_min};
-            double rr[2];
-            batch_recip<2>(dr, rr);
-            double num2[C];
-            if (MIX & 1) piston_num<C>(a, mu, num2);
-            unit_conc<C>(a, mu, num, rr[0], conc, (MIX & 1) ? num2 : nullptr);
-            if (cnan)
-                for (int t = 0; t < a.K; ++t) conc[t] = __builtin_nan("");
-            like = mvalid ? unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL, &rr[1]) : 0.0;
+                for (int c = 0; c < C; ++c) num[c] = a.tab0[c] + zz[c];
+                // the normaliser's reciprocal and the Student-t 1/nu: one division
+                const double dr[2] = {1.0 + zz[C], tp.nub * (uk.rnu_max - uk.rnu_min) + uk.rnu_min};
+                double rr[2];
+                batch_recip<2>(dr, rr);
+                double num2[C];
+                if (MIX & 1) piston_num<C>(a, mu, num2);
+                unit_conc<C>(a, mu, num, rr[0], conc, (MIX & 1) ? num2 : nullptr);
+                if (cnan)
+                    for (int t = 0; t < a.K; ++t) conc[t] = __builtin_nan("");
+                like = mvalid ? unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL, &rr[1]) : 0.0;
+            }
+            NGRTD_PROBE(2);
+            if (__any(bad)) {                                     // wave-uniform: exact channel sums
+                // ROLES = 2: one tile per pass keeps the exact path inside the 128-VGPR budget
+                fused_exact<C, FULL, ROLES == 2, MIX>(a, ul, WB, w0, uw, mvalid, mu, ml, tp.nub, conc, like);
+            }
+            if (!FULL && a.conc && mvalid)                        // forward(): model concentrations
+                for (int t = 0; t < a.K; ++t) a.conc[(int64_t)t * a.U + mu] = conc[t];
         }
-        NGRTD_PROBE(2);
-        if (__any(bad)) {                                     // wave-uniform: exact channel sums
-            // ROLES = 2: one tile per pass keeps the exact path inside the 128-VGPR budget
-            fused_exact<C, FULL, ROLES == 2, MIX>(a, ul, WB, w0, uw, mvalid, mu, ml, tp.nub, conc, like);
+        NGRTD_PROBE(3);
+        if (!logp && !dk.lp) return;                        // forward() launch: no log-prob
+        if (ROLES == 1) {
+            part[mi] = th + like;
+        } else {
+            if (do_rtd) part2[mi] = like;
+            __syncthreads();
+            if (do_theta) part[mi] = th + part2[mi];          // th + like, as ROLES = 1
         }
-        if (!FULL && a.conc && mvalid)                        // forward(): model concentrations
-            for (int t = 0; t < a.K; ++t) a.conc[(int64_t)t * a.U + mu] = conc[t];
-    }
-    NGRTD_PROBE(3);
-    if (!logp && !dacc.lp) return;                        // forward() launch: no log-prob
-    if (ROLES == 1) {
-        part[mi] = th + like;
-    } else {
-        if (do_rtd) part2[mi] = like;
+        NGRTD_PROBE(6);
         __syncthreads();
-        if (do_theta) part[mi] = th + part2[mi];          // th + like, as ROLES = 1
-    }
-    NGRTD_PROBE(6);
-    __syncthreads();
-    if (WB <= 64 && (WB & (WB - 1)) == 0) {
-        if (wave == 0) {
-            const int G = 64 / WB;                        // well groups (power of two)
-            const int wl = lane % WB, g = lane / WB;
-            double tot = 0.0;
-            for (int l = g; l < L; l += G) tot += part[l * WB + wl];
-            for (int off = WB; off < 64; off <<= 1) tot += __shfl_xor(tot, off);
-            if (g == 0 && w0 + wl < W) walker_out(logp, dacc, w0 + wl, tot, dec + wl);
+        if (WB <= 64 && (WB & (WB - 1)) == 0) {
+            if (wave == 0) {
+                const int G = 64 / WB;                        // well groups (power of two)
+                const int wl = lane % WB, g = lane / WB;
+                double tot = 0.0;
+                for (int l = g; l < L; l += G) tot += part[l * WB + wl];
+                for (int off = WB; off < 64; off <<= 1) tot += __shfl_xor(tot, off);
+                if (g == 0 && w0 + wl < W) walker_out<DZ>(logp, dk, sj, log_off, w0 + wl, tot, dec + wl);
+            }
+        } else if (tid < WB && w0 + tid < W) {
+            double tot = part[tid];
+            for (int l = 1; l < L; ++l) tot += part[l * WB + tid];
+            walker_out<DZ>(logp, dk, sj, log_off, w0 + tid, tot, dec + tid);
         }
-    } else if (tid < WB && w0 + tid < W) {
-        double tot = part[tid];
-        for (int l = 1; l < L; ++l) tot += part[l * WB + tid];
-        walker_out(logp, dacc, w0 + tid, tot, dec + tid);
-    }
-    if (DZ) {
-        __syncthreads();
-        if (mvalid && dec[mwl] && !(dacc.dz_diag & 4))
-            dz_commit<kDzMaxP, (MIX & 4) != 0>(dacc, ua.U, mu, mi, thl, do_theta ? 0 : 1);
-    } else if (dacc.lp) {   // DE-MC: accepted walkers take the proposal's theta rows of this unit
-        __syncthreads();
-        if (do_theta && mvalid && dec[mwl]) {
-            for (int p = 0; p < dacc.P; ++p) dacc.x[(int64_t)p * a.U + mu] = dacc.prop[(int64_t)p * a.U + mu];
-            if (dacc.xu)
-                for (int p = 0; p < dacc.P; ++p) dacc.xu[(int64_t)p * a.U + mu] = dacc.prop_u[(int64_t)p * a.U + mu];
+        if (DZ) {
+            __syncthreads();
+            if (mvalid && dec[mwl] && !(dk.dz_diag & 4))
+                dz_commit<kDzMaxP, (MIX & 4) != 0>(dk, uk.U, mu, mi, thl, do_theta ? 0 : 1);
+        } else if (dk.lp) {   // DE-MC: accepted walkers take the proposal's theta rows of this unit
+            __syncthreads();
+            if (do_theta && mvalid && dec[mwl]) {
+                for (int p = 0; p < dk.P; ++p) dk.x[(int64_t)p * a.U + mu] = dk.prop[(int64_t)p * a.U + mu];
+                if (dk.xu)
+                    for (int p = 0; p < dk.P; ++p) dk.xu[(int64_t)p * a.U + mu] = dk.prop_u[(int64_t)p * a.U + mu];
+            }
         }
-    }
+    } while (DZ && ++js < nst);   // steps
     NGRTD_PROBE(7);
 }
 
 // logp[w] = sum over wells of ulogp[l*W + w]: 16 fixed well groups per walker summed
 // in registers, then combined in a fixed order through LDS (deterministic, no atomics).
-__global__ void __launch_bounds__(1024) walker_reduce_kernel(const double* __restrict__ ulogp, int64_t W,
+NGRTD_KLINK __global__ void __launch_bounds__(1024) walker_reduce_kernel(const double* __restrict__ ulogp, int64_t W,
                                                              int32_t L, double* __restrict__ logp) {
     __shared__ double sh[16][64];
     const int wl = threadIdx.x & 63, g = threadIdx.x >> 6;
@@ -1730,7 +1840,7 @@ __global__ void __launch_bounds__(1024) walker_reduce_kernel(const double* __res
 
 // ------------------------------------------ gen_g_tp() materialised weights
 // One block computes the unnormalised weights, a fixed-order block sum, then g /= sum.
-__global__ void __launch_bounds__(1024) rtd_weights_kernel(int32_t mod, double tau, double eta, double D,
+NGRTD_KLINK __global__ void __launch_bounds__(1024) rtd_weights_kernel(int32_t mod, double tau, double eta, double D,
                                                            double tp0, double dtp, int32_t N, double* g) {
     __shared__ double red[1024];
     double s = 0.0;
@@ -1766,7 +1876,7 @@ __global__ void __launch_bounds__(1024) rtd_weights_kernel(int32_t mod, double t
 }
 
 // convolve(g_tau=g), :298-340: dot(flip(C'), g * decay) with a fixed-order block sum
-__global__ void __launch_bounds__(1024) conv_dot_kernel(const double* c, const double* idx, const double* g,
+NGRTD_KLINK __global__ void __launch_bounds__(1024) conv_dot_kernel(const double* c, const double* idx, const double* g,
                                                         double lam, int32_t accum, double J, double tp0,
                                                         double dtp, int32_t N, double* out) {
     __shared__ double red[1024];

@@ -65,9 +65,12 @@ def test_device_demcz_matches_torch_bitwise(kind):
 
 @pytest.mark.parametrize("jac", [False, True])
 def test_device_demcz_step_modes_bitwise(jac):
-    """Both device step schedules give the same chains bit for bit at the c4 shape (520
-    chains: 65 walker blocks, the last partial): one launch per step (default) and the
-    proposal kernel + log-prob kernel pair (NGRTD_DZ_MODE=pair)."""
+    """Every device step schedule gives the same chains bit for bit at the c4 shape (520
+    chains: 65 walker blocks, the last partial): the multi-step launch (default: up to 256
+    steps per launch, each block running its chains through them), one step per launch
+    (NGRTD_DZ_CHUNK=1), chunks of 3 (launch boundaries between the tune steps and across
+    stop_tuning's history drop at step 8) and the proposal kernel + log-prob kernel pair
+    (NGRTD_DZ_MODE=pair)."""
     import dataclasses
     import os
     import torch
@@ -81,13 +84,16 @@ def test_device_demcz_step_modes_bitwise(jac):
     x0 = torch.from_numpy(wl.sample_prior(spec, W, np.random.default_rng(15))).cuda()
     lp = LogProb(spec, max_walkers=W)
     res = {}
+    modes = {"fused": ("fused", "256"), "pair": ("pair", "256"), "chunk1": ("fused", "1"), "chunk3": ("fused", "3")}
     try:
-        for mode in ("fused", "pair"):
-            os.environ["NGRTD_DZ_MODE"] = mode
+        for mode, (m, ch) in modes.items():
+            os.environ["NGRTD_DZ_MODE"] = m
+            os.environ["NGRTD_DZ_CHUNK"] = ch
             res[mode] = DeviceDEMetropolisZ(lp, tune_interval=4, seed=99).run(x0, tune=8, draws=6)
     finally:
         os.environ.pop("NGRTD_DZ_MODE", None)
-    for mode in ("pair",):
+        os.environ.pop("NGRTD_DZ_CHUNK", None)
+    for mode in ("pair", "chunk1", "chunk3"):
         for k in ("x", "lp", "samples", "logp", "accepted", "lamb", "scaling"):
             assert _same(res[mode][k], res["fused"][k]), (mode, k)
     if jac:
