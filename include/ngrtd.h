@@ -321,8 +321,12 @@ int ngrtd_plan_info(ngrtd_plan* plan, int64_t W, int64_t* info, int32_t n);
  * step e (hist_len == steps_done after every call).
  * accepted_log [n_steps][W] (uint8) and logp_log [n_steps][W] (each chain's log-prob after
  * the step) may be NULL.  n_accepted (device uint64, may be NULL) counts acceptances.
- * 2 launches per step: the proposal kernel (which also appends the previous state) and the
- * log-prob kernel with the accept in its per-walker reduction; one append at the end. */
+ * Joint plans with a single-launch instance (C = 5 channels: c3, c4, the published models):
+ * one launch per chunk of up to NGRTD_DZ_CHUNK (default 256) steps, each block stepping its
+ * own chains (proposal, history append, log-prob, decision, tuning, commit per step).
+ * Other plans (or NGRTD_DZ_MODE=pair): 2 launches per step, the proposal kernel (which also
+ * appends the previous state) and the log-prob kernel with the accept in its per-walker
+ * reduction.  One append at the end. */
 enum ngrtd_tune_target { NGRTD_TUNE_NONE = 0, NGRTD_TUNE_SCALING = 1, NGRTD_TUNE_LAMBDA = 2 };
 enum ngrtd_transform { NGRTD_TR_NONE = 0, NGRTD_TR_LOGODDS = 1, NGRTD_TR_INTERVAL = 2, NGRTD_TR_LOG = 3 };
 typedef struct {

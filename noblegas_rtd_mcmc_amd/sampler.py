@@ -27,8 +27,9 @@ distribution: analytic prior moments, and the reference's posterior summaries).
 
 Random numbers are counter-based (splitmix64 of (seed, step, chain[, element])), the same
 stream in ``DEMetropolisZ`` (torch ops, any device, any batched log_prob) and
-``DeviceDEMetropolisZ`` (libngrtd ``ngrtd_demcz_run``: proposal + history append in one
-kernel, log-prob + Metropolis decision + tuning in the next; no host round trip per step),
+``DeviceDEMetropolisZ`` (libngrtd ``ngrtd_demcz_run``: joint plans run up to 256 whole
+steps per launch, each block stepping its own chains; other plans a proposal + history
+append kernel and a log-prob + decision + tuning kernel per step; no host round trip),
 so on the same log-prob the two produce bitwise the same chains.
 """
 import math
@@ -303,7 +304,8 @@ class ZState:
 
 class DeviceDEMetropolisZ:
     """The same DEMetropolisZ run device-resident by libngrtd (ngrtd_demcz_run): one C call
-    for the whole run, two launches per step, no host synchronisation until the end.
+    for the whole run (up to 256 steps per launch for the joint plans, else two launches per
+    step), no host synchronisation until the end.
     Same random stream as DEMetropolisZ, so on the same log-prob the chains agree bitwise.
 
     transformed: chains in PyMC3's transformed space (Transform.from_spec) -- the default

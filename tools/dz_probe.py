@@ -52,9 +52,11 @@ def main():
         xn = (x0 + noise).contiguous()
     out["logp_noisy_us"] = ev_time(lp, lambda: lp(xn, out=o))
     s = DeviceDEMetropolisZ(lp, seed=7, tune=None)
-    x, l, z = s.start(x0, 0, 120)
+    x, l, z = s.start(x0, 0, 400)
     lp.demcz(x, l, 10, z)
-    out["dz_step_us"] = ev_time(lp, lambda: lp.demcz(x, l, 2, z), n=40)
+    # one launch runs K steps (NGRTD_DZ_CHUNK caps it): per-step time = launch time / K
+    K = 32
+    out["dz_step_us"] = ev_time(lp, lambda: lp.demcz(x, l, K, z), n=8) / K
     print(json.dumps(out))
 
 
