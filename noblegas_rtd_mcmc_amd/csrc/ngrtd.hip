@@ -113,6 +113,7 @@ struct ngrtd_plan {
     // workspaces
     DevBuf conc, ulogp, theta_stage, out_stage, ce_stage;
     DevBuf demc_prop[2], demc_lp, demc_acc, demc_cnt;   // ngrtd_demcz_run scratch
+    DevBuf demc_xw[2];      // the multi-step launch's walker-major state [P][W][L] (natural, transformed)
 
     RtdArgs rtd{};
     UnitArgs unit{};
@@ -1647,12 +1648,26 @@ int ngrtd_demcz_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64
     // each block running its own chains through the chunk (DemcAccept::Sched / dz_step)
     const char* chunk_env = std::getenv("NGRTD_DZ_CHUNK");
     const int64_t chunk = std::max<int64_t>(1, chunk_env ? std::atoll(chunk_env) : 256);
+    // the multi-step launch keeps the state walker-major ([P][W][L], a chain's rows contiguous
+    // like its history entries) for the whole call: transposed in here, back after the loop
+    const int Lw = p->desc.n_wells;
+    double* xw[2] = {nullptr, nullptr};
+    if (dzm >= 0) {
+        for (int i = 0; i < (tr ? 2 : 1); ++i) {
+            HIP_TRY(ctx, p->demc_xw[i].ensure((size_t)E * sizeof(double)));
+            xw[i] = p->demc_xw[i].d();
+        }
+        const dim3 g((unsigned)cdiv(W, 32), (unsigned)cdiv(Lw, 32), (unsigned)p->desc.n_params);
+        hipLaunchKernelGGL(dz_layout_kernel, g, dim3(256), 0, st, theta, xw[0], (int64_t)Lw, W);
+        if (tr) hipLaunchKernelGGL(dz_layout_kernel, g, dim3(256), 0, st, z->theta_u, xw[1], (int64_t)Lw, W);
+        HIP_TRY(ctx, hipGetLastError());
+    }
     for (int64_t j = 0; dzm >= 0 && j < n_steps;) {
         const int64_t k = std::min(chunk, n_steps - j);
-        DemcAccept da{logp, acc, cnt, theta, nullptr, p->desc.n_params, 0, z->n_acc_tune, z->lamb, z->scaling,
+        DemcAccept da{logp, acc, cnt, xw[0], nullptr, p->desc.n_params, 0, z->n_acc_tune, z->lamb, z->scaling,
                       0, z->tune_target, z->tune_interval, accepted_log ? accepted_log + j * W : nullptr,
-                      logp_log ? logp_log + j * W : nullptr, z->chain0, tr ? z->theta_u : nullptr, nullptr};
-        da.zx = state; da.dz_prop = prop_x; da.hist = z->hist;
+                      logp_log ? logp_log + j * W : nullptr, z->chain0, tr ? xw[1] : nullptr, nullptr};
+        da.zx = tr ? xw[1] : xw[0]; da.dz_prop = prop_x; da.hist = z->hist;
         da.Wg = Wg; da.S = z->S; da.L = p->desc.n_wells;
         da.dz_diag = dz_diag;
         for (int i = 0; i < kRoleCount; ++i) {
@@ -1673,6 +1688,12 @@ int ngrtd_demcz_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64
         z->hist_lo = last.lo;
         z->steps_done += k;
         j += k;
+    }
+    if (dzm >= 0) {
+        const dim3 g((unsigned)cdiv(Lw, 32), (unsigned)cdiv(W, 32), (unsigned)p->desc.n_params);
+        hipLaunchKernelGGL(dz_layout_kernel, g, dim3(256), 0, st, xw[0], theta, W, (int64_t)Lw);
+        if (tr) hipLaunchKernelGGL(dz_layout_kernel, g, dim3(256), 0, st, xw[1], z->theta_u, W, (int64_t)Lw);
+        HIP_TRY(ctx, hipGetLastError());
     }
     for (int64_t j = 0; dzm < 0 && j < n_steps; ++j) {
         const int64_t s = z->steps_done;

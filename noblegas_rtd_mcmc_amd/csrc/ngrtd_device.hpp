@@ -184,7 +184,8 @@ struct DemcAccept {
     const double* S;        // [R] proposal scale per row (null: ones)
     int32_t L;
     int32_t dz_diag;        // timing diagnostics only (NGRTD_DZ_DIAG, tools/dz_probe.py): bit 0: proposal =
-                            // state, 1: no history store, 2: no commit, 3: no staging (wrong results)
+                            // state, 1: no history store, 2: no commit, 3: no staging, 4: no partner
+                            // loads (noise-only proposals) (wrong results)
     int32_t tr_kind[NGRTD_ROLE_COUNT];
     double tr_a[NGRTD_ROLE_COUNT], tr_b[NGRTD_ROLE_COUNT];
     // Multi-step launch (MIX bit 3): the block runs n_steps consecutive steps of its own

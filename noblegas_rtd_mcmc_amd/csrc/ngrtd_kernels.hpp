@@ -1202,6 +1202,29 @@ NGRTD_KLINK __global__ void __launch_bounds__(kZThreads) demcz_propose_kernel(co
     }
 }
 
+// out[p][b][a] = in[p][a][b] for p < P (a < A, b < B): the caller's [P][L][W] state into the
+// multi-step DEMetropolisZ launch's walker-major [P][W][L] and back.  32 x 32 LDS tiles.
+NGRTD_KLINK __global__ void __launch_bounds__(256) dz_layout_kernel(const double* __restrict__ in,
+                                                                    double* __restrict__ out, int64_t A, int64_t B) {
+    __shared__ double t[32][33];
+    const int64_t p = blockIdx.z;
+    const int64_t a0 = (int64_t)blockIdx.y * 32, b0 = (int64_t)blockIdx.x * 32;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+    const double* src = in + p * A * B;
+    double* dst = out + p * A * B;
+#pragma unroll
+    for (int k = 0; k < 32; k += 8) {
+        const int64_t a = a0 + ty + k, b = b0 + tx;
+        if (a < A && b < B) t[ty + k][tx] = src[a * B + b];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 32; k += 8) {
+        const int64_t b = b0 + ty + k, a = a0 + tx;
+        if (a < A && b < B) dst[b * A + a] = t[tx][ty + k];
+    }
+}
+
 constexpr int kDzMaxP = 12;          // parameter rows of a single-launch DEMetropolisZ step
 constexpr int kFusedUnitsDz = 512;   // = kFusedUnits (units per logp_fused_kernel block)
 
@@ -1247,6 +1270,7 @@ __device__ __forceinline__ void dz_stage(const DemcAccept& d, const DzStep& sj, 
     }
     int64_t e1, e2;
     dz_partners(d, sj, w, e1, e2);
+    if (d.dz_diag & 16) e1 = e2 = -1;   // timing diagnostics: no partner loads (noise only)
     const bool de = e1 >= 0;
     const double* z1 = d.hist + ((size_t)(de ? e1 : 0) * W + w) * R + l;
     const double* z2 = d.hist + ((size_t)(de ? e2 : 0) * W + w) * R + l;
@@ -1330,8 +1354,13 @@ __device__ __forceinline__ void fused_exact(const RtdArgs& a, const UnitArgs& ul
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
         const int i = (uw * NT + t) * 16 + col;
-        const int wl = i % WB, l = i / WB;
-        uoff[t] = (l < L && w0 + wl < W) ? (int64_t)l * W + w0 + wl : 0;
+        if (MIX & 8) {   // DZ: walker-major units and theta (logp_fused_kernel)
+            const int wl = i / L, l = i % L;
+            uoff[t] = (wl < WB && w0 + wl < W) ? (w0 + wl) * (int64_t)L + l : 0;
+        } else {
+            const int wl = i % WB, l = i / WB;
+            uoff[t] = (l < L && w0 + wl < W) ? (int64_t)l * W + w0 + wl : 0;
+        }
     }
     double yy[C], bu;
     if (SEQ) {   // one 16-unit tile per pass: 1/NT of the accumulators live
@@ -1671,9 +1700,14 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         const int L = uk.L;
         const int64_t W = uk.W;
         const int mi = 64 * uw + lane;
-        const int mwl = mi % WB, ml = mi / WB;
-        const bool mvalid = ml < L && w0 + mwl < W;
-        const int64_t mu = mvalid ? (int64_t)ml * W + w0 + mwl : 0;
+        // DZ: walker-major units (a wave holds one walker's 64 wells at c4) over the
+        // walker-major state / proposal buffers [P][W][L] (ngrtd_demcz_run transposes the
+        // caller's [P][L][W] state in and out): every row a lane stages -- state, history
+        // append, both partners, proposal -- is then one contiguous 512-B run per wave
+        const int mwl = DZ ? mi / L : mi % WB, ml = DZ ? mi % L : mi / WB;
+        const bool mvalid = (DZ ? mwl < WB : ml < L) && w0 + mwl < W;
+        const int64_t mu = !mvalid ? 0 : DZ ? (w0 + mwl) * (int64_t)L + ml : (int64_t)ml * W + w0 + mwl;
+        const int pi = ml * WB + mwl;                     // the unit's slot in part / part2
         double* tabl = cheb + a.cheb_np * PST;
         double* wd = tabl + (EPM ? a.N * CP : 0);
         double* thl = wd + uk.wd_n;
@@ -1781,11 +1815,11 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         NGRTD_PROBE(3);
         if (!logp && !dk.lp) return;                        // forward() launch: no log-prob
         if (ROLES == 1) {
-            part[mi] = th + like;
+            part[pi] = th + like;
         } else {
-            if (do_rtd) part2[mi] = like;
+            if (do_rtd) part2[pi] = like;
             __syncthreads();
-            if (do_theta) part[mi] = th + part2[mi];          // th + like, as ROLES = 1
+            if (do_theta) part[pi] = th + part2[pi];          // th + like, as ROLES = 1
         }
         NGRTD_PROBE(6);
         __syncthreads();

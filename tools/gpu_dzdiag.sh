@@ -5,9 +5,9 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/${1:-dzdiag}
 mkdir -p $OUT
-for j in "" 1; do for d in 0 1 2 4 8; do
+for j in "" 1; do for d in 0 1 8 16; do
   DZ_JAC=$j NGRTD_DZ_DIAG=$d timeout -k 10 120 python tools/dz_probe.py >> $OUT/probe.jsonl 2>> $OUT/probe.err || exit 1
 done; done
 cat $OUT/probe.jsonl
-NGRTD_DZ_CHUNK=1 timeout -k 10 120 python tools/dz_probe.py > $OUT/probe_chunk1.json 2>> $OUT/probe.err || exit 1
-cat $OUT/probe_chunk1.json
+
+
