@@ -16,3 +16,4 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$OUT/sprof -o sampler -- python3 $GRAFT_REPO_ROOT/tools/sampler_bench.py --steps 200 > $GRAFT_REPO_ROOT/$OUT/sprof.json 2> $GRAFT_REPO_ROOT/$OUT/sprof.err || exit 1
 cd $GRAFT_REPO_ROOT
 cat $OUT/smoke.log; cat $OUT/bench.json; cat $OUT/bench20.json; cat $OUT/sampler.json
+bash tools/gpu_dzpmc.sh ${1:-r02final2}_pmc > /dev/null || exit 1
