@@ -654,7 +654,14 @@ static int launch_fused_dz(ngrtd_ctx* ctx, const RtdArgs& a0, const UnitArgs& u,
     RtdArgs a = a0;
     cheb_window(a, u);
     const int dz_p = (mix & 4) ? da.P : 0;    // transformed chains: the chains'-space proposal rows
-    const hipError_t e = launch_fused_dz_instance(mix, a, u, WB, W, logp, da, fused_lds(a, u, dz_p), kFusedMaxLds, st);
+    size_t lds = fused_lds(a, u, dz_p);
+    // the natural proposal rows in LDS too where they fit (not next to the EPM channel
+    // table); NGRTD_DZ_PROP_GLOBAL=1 reads them back from dz_prop instead (A/B runs)
+    DemcAccept d = da;
+    const size_t pb = (size_t)da.P * kFusedUnits * sizeof(double);
+    d.prop_lds = (lds + pb <= kFusedMaxLds && !std::getenv("NGRTD_DZ_PROP_GLOBAL")) ? 1 : 0;
+    if (d.prop_lds) lds += pb;
+    const hipError_t e = launch_fused_dz_instance(mix, a, u, WB, W, logp, d, lds, kFusedMaxLds, st);
     if (e == hipErrorInvalidValue) return set_err(ctx, NGRTD_EINVAL, "no single-launch DEMetropolisZ instance %d", mix);
     HIP_TRY(ctx, e);
     return NGRTD_OK;

@@ -193,6 +193,10 @@ struct DemcAccept {
     // append entry / tune flag come from dz_step(sch, j), the host loop's own schedule, and
     // its logs from acc_log / lp_log + j W.  n_steps = 1 with the fields above otherwise.
     int32_t n_steps;
+    // 1: the block's LDS also holds the natural-space proposal rows [P][512] (after the
+    // transformed rows): dz_stage writes them there as well as to dz_prop, and the step's
+    // own theta loads and commit read them from LDS instead of back from L2
+    int32_t prop_lds;
     struct Sched {
         uint64_t seed;
         int64_t s0;         // steps_done at the launch's first step

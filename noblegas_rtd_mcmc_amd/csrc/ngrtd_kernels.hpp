@@ -1260,7 +1260,7 @@ __device__ __forceinline__ void dz_partners(const DemcAccept& d, const DzStep& s
 // spilled SGPRs into the unit body.)
 template <int PMAX, bool TR>
 __device__ __forceinline__ void dz_stage(const DemcAccept& d, const DzStep& sj, int64_t U, int64_t u, int i, int64_t w,
-                                         int l, int L, int64_t W, bool valid, double* th, int p0) {
+                                         int l, int L, int64_t W, bool valid, double* th, int p0, double* pl) {
     const int64_t R = (int64_t)d.P * L;
     if (!valid || (d.dz_diag & 8)) return;
     if (d.dz_diag & 1) {   // timing diagnostics: the proposal is the state (no partners, no noise)
@@ -1304,6 +1304,7 @@ __device__ __forceinline__ void dz_stage(const DemcAccept& d, const DzStep& sj, 
                 v = pymc3_backward_sel(d.tr_kind[p], d.tr_a[p], d.tr_b[p], v);
             }
             d.dz_prop[(int64_t)p * U + u] = v;
+            if (pl) pl[p * kFusedUnitsDz + i] = v;
         }
     }
 }
@@ -1312,13 +1313,13 @@ __device__ __forceinline__ void dz_stage(const DemcAccept& d, const DzStep& sj, 
 // dz_stage kept in LDS (row p of th).
 template <int PMAX, bool TR>
 __device__ __forceinline__ void dz_commit(const DemcAccept& d, int64_t U, int64_t u, int i, const double* th,
-                                          int p0) {
+                                          int p0, const double* pl) {
     constexpr int KMAX = (PMAX + 1) / 2;
     double pv[KMAX];
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {   // every load first, then every store
         const int p = p0 + 2 * k;
-        if (p < d.P) pv[k] = d.dz_prop[(int64_t)p * U + u];
+        if (p < d.P) pv[k] = pl ? pl[p * kFusedUnitsDz + i] : d.dz_prop[(int64_t)p * U + u];
     }
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
@@ -1711,6 +1712,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         double* tabl = cheb + a.cheb_np * PST;
         double* wd = tabl + (EPM ? a.N * CP : 0);
         double* thl = wd + uk.wd_n;
+        double* propl = thl + (((MIX & 4) && DZ) ? dk.P * kFusedUnits : 0);   // DZ: [P][512] proposals
         UnitArgs ul = uk;
         {
             const int nce = uk.ce_on ? L * uk.G : 0, nrt = uk.rtd_on ? L * uk.K : 0;
@@ -1734,10 +1736,22 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         // both roles stage: theta waves the even parameter rows, RTD waves the odd ones
         if (DZ)
             dz_stage<kDzMaxP, (MIX & 4) != 0>(dk, sj, uk.U, mu, mi, w0 + mwl, ml, L, W, mvalid, thl,
-                                              do_theta ? 0 : 1);
+                                              do_theta ? 0 : 1, dk.prop_lds ? propl : nullptr);
         __syncthreads();
         NGRTD_PROBE(1);
-        if (DZ) {                                             // the proposal's rows
+        if (DZ && dk.prop_lds) {                              // the proposal's rows, from LDS
+            if (do_theta) {
+#pragma unroll
+                for (int i = 0; i < 6; ++i) tp.ce[i] = propl[uk.row_ce[i] * kFusedUnits + mi];
+                tp.tau1 = propl[uk.row_tau1 * kFusedUnits + mi];
+                tp.nub = propl[uk.row_nu * kFusedUnits + mi];
+            }
+            if (do_rtd) {
+                tau = mvalid ? propl[a.row_tau[0] * kFusedUnits + mi] : 1.0;
+                if (EPM) eta = mvalid ? propl[a.row_eta[0] * kFusedUnits + mi] : 1.0;
+                tp.nub = propl[uk.row_nu * kFusedUnits + mi];
+            }
+        } else if (DZ) {                                      // the proposal's rows
             if (do_theta) theta_preload(uk, mu, tp);
             if (do_rtd) {
                 tau = mvalid ? a.theta[(int64_t)a.row_tau[0] * a.U + mu] : 1.0;
@@ -1840,7 +1854,8 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         if (DZ) {
             __syncthreads();
             if (mvalid && dec[mwl] && !(dk.dz_diag & 4))
-                dz_commit<kDzMaxP, (MIX & 4) != 0>(dk, uk.U, mu, mi, thl, do_theta ? 0 : 1);
+                dz_commit<kDzMaxP, (MIX & 4) != 0>(dk, uk.U, mu, mi, thl, do_theta ? 0 : 1,
+                                                   dk.prop_lds ? propl : nullptr);
         } else if (dk.lp) {   // DE-MC: accepted walkers take the proposal's theta rows of this unit
             __syncthreads();
             if (do_theta && mvalid && dec[mwl]) {
