@@ -1708,7 +1708,10 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         const int mwl = DZ ? mi / L : mi % WB, ml = DZ ? mi % L : mi / WB;
         const bool mvalid = (DZ ? mwl < WB : ml < L) && w0 + mwl < W;
         const int64_t mu = !mvalid ? 0 : DZ ? (w0 + mwl) * (int64_t)L + ml : (int64_t)ml * W + w0 + mwl;
-        const int pi = ml * WB + mwl;                     // the unit's slot in part / part2
+        // the unit's slot in part / part2 ((well, walker) order, as the reduction reads it);
+        // DZ lanes past the block's WB L units keep their own slot mi >= WB L, so that their
+        // zero partial sums land on no walker's slots
+        const int pi = (DZ && mwl >= WB) ? mi : ml * WB + mwl;
         double* tabl = cheb + a.cheb_np * PST;
         double* wd = tabl + (EPM ? a.N * CP : 0);
         double* thl = wd + uk.wd_n;

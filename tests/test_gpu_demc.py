@@ -16,7 +16,7 @@ def _same(a, b):
 
 
 @pytest.mark.parametrize("kind", ["joint", "ce_only", "joint_transformed", "bmm_transformed", "bmm", "epm",
-                                  "epm_piston", "epm_transformed", "joint_c4_transformed"])
+                                  "epm_piston", "epm_transformed", "joint_c4_transformed", "joint_l3"])
 def test_device_demcz_matches_torch_bitwise(kind):
     """Tuning (every 4 steps), stop_tuning's history drop and the draws: device chains ==
     torch chains, bit for bit.  joint / bmm / epm / epm_piston / joint_transformed /
@@ -25,7 +25,8 @@ def test_device_demcz_matches_torch_bitwise(kind):
     demc_accept_kernel; bmm_transformed: the proposal kernel + the log-prob kernel pair.
     *_transformed: PyMC3's logodds / interval / log space, the plan adds the Jacobian.
     joint_c4_transformed: the c4 shape (64 wells, 8 walkers per block), 520 chains: the last
-    block is partial."""
+    block is partial.  joint_l3: 3 wells, so a block holds 170 walkers (510 of its 512 unit
+    slots) and the walker-major unit mapping of the multi-step launch leaves a ragged tail."""
     import dataclasses
     import torch
     from noblegas_rtd_mcmc_amd import workloads as wl
@@ -47,9 +48,11 @@ def test_device_demcz_matches_torch_bitwise(kind):
                           par_names=("tau1", "tau2", "f1", "eta1"))
     if kind == "joint_c4_transformed":
         spec = wl.c4_spec(L=64, N=1200)
+    if kind == "joint_l3":      # 3 wells: 170 walkers per block (510 units), not a power of two
+        spec = wl.c4_spec(L=3, N=300)
     if kind.endswith("transformed"):
         spec = dataclasses.replace(spec, jacobian=True)
-    W = 520 if kind == "joint_c4_transformed" else 40
+    W = 520 if kind == "joint_c4_transformed" else 200 if kind == "joint_l3" else 40
     th0 = wl.sample_prior(spec, W, np.random.default_rng(5))
     lp = LogProb(spec, max_walkers=W)
     x0 = torch.from_numpy(th0).cuda()
@@ -98,6 +101,36 @@ def test_device_demcz_step_modes_bitwise(jac):
             assert _same(res[mode][k], res["fused"][k]), (mode, k)
     if jac:
         assert 0 < int(res["fused"]["accepted"].sum()) < res["fused"]["accepted"].numel()
+    lp.close()
+
+
+def test_device_demcz_many_blocks_chunks_bitwise():
+    """More walker blocks than CUs (8200 chains at the c4 shape: 1025 blocks, the last
+    partial; W not a multiple of the 32-wide layout tiles): the multi-step launch (one chunk)
+    equals one step per launch bit for bit, and the caller's [P][L][W] state comes back in
+    its own layout (the walker-major scratch copy is transposed in and out)."""
+    import os
+    import torch
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+    from noblegas_rtd_mcmc_amd.sampler import DeviceDEMetropolisZ
+    spec = wl.c4_spec(L=64, N=1200)
+    W = 8200
+    x0 = torch.from_numpy(wl.sample_prior(spec, W, np.random.default_rng(21))).cuda()
+    lp = LogProb(spec, max_walkers=W)
+    res = {}
+    try:
+        for ch in ("256", "1"):
+            os.environ["NGRTD_DZ_CHUNK"] = ch
+            res[ch] = DeviceDEMetropolisZ(lp, tune_interval=3, seed=5).run(x0, tune=4, draws=3)
+    finally:
+        os.environ.pop("NGRTD_DZ_CHUNK", None)
+    for k in ("x", "lp", "samples", "logp", "accepted", "lamb", "scaling"):
+        assert _same(res["256"][k], res["1"][k]), k
+    # the final state is the last draw, in the caller's layout
+    assert _same(res["256"]["x"], res["256"]["samples"][-1])
+    # the log-prob of the returned state is the chains' current log-prob
+    assert _same(lp(res["256"]["x"].contiguous()), res["256"]["lp"])
     lp.close()
 
 
