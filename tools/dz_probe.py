@@ -34,13 +34,20 @@ def main():
     from noblegas_rtd_mcmc_amd.engine import LogProb
     from noblegas_rtd_mcmc_amd.sampler import DeviceDEMetropolisZ, Transform
     W = 2048
-    spec = workloads.c4_spec(L=64)
+    # DZ_MODEL: the published RTD models on the same shape (exponential-piston BMM,
+    # exp_pist_flow, exp_pist_flow-piston BMM); default the exponential c4 workload
+    models = {"bmm": dict(mod_type1="exponential", mod_type2="piston", par_names=("tau1", "tau2", "f1")),
+              "epm": dict(mod_type1="exp_pist_flow", par_names=("tau1", "eta1")),
+              "epm_piston": dict(mod_type1="exp_pist_flow", mod_type2="piston",
+                                 par_names=("tau1", "tau2", "f1", "eta1"))}
+    model = os.environ.get("DZ_MODEL", "")
+    spec = workloads.c4_spec(L=64, **models.get(model, {}))
     jac = bool(os.environ.get("DZ_JAC"))
     if jac:
         spec = dataclasses.replace(spec, jacobian=True)
     x0 = torch.from_numpy(workloads.sample_prior(spec, W, np.random.default_rng(34568))).cuda()
     lp = LogProb(spec, max_walkers=W)
-    out = {"diag": os.environ.get("NGRTD_DZ_DIAG", "0"), "jacobian": jac}
+    out = {"diag": os.environ.get("NGRTD_DZ_DIAG", "0"), "jacobian": jac, "model": model or "exponential"}
     o = torch.empty(W, dtype=torch.float64, device="cuda")
     out["logp_state_us"] = ev_time(lp, lambda: lp(x0, out=o))
     g = torch.Generator(device="cuda").manual_seed(1)
