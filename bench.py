@@ -56,6 +56,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=16.0, help="bounded CPU-baseline budget (both variants)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-exact", action="store_true", help="skip the exact-path (no surrogate) line")
+    ap.add_argument("--no-sampler", action="store_true", help="skip the device DEMetropolisZ line")
     ap.add_argument("--event-every", type=int, default=8,
                     help="bracket the kernels of every k-th timed step with HIP events (multi-kernel / N > 1)")
     return ap.parse_args()
@@ -332,6 +333,11 @@ def report(args, spec, lp, ks, dt, world, W_total, Wb, plan_build_ms, theta, the
     }
     if world == 1 and exp_single and info.get("surrogate") and not args.no_exact:
         line.update(exact_line(args, spec, theta, Wb, C, N))
+    if world == 1 and not args.no_sampler:
+        try:                          # a side measurement: never lose the headline line to it
+            line["sampler"] = sampler_line(args, lp, theta)
+        except Exception as e:        # noqa: BLE001
+            line["sampler"] = {"error": repr(e)}
     # PCIe-inclusive rate: theta handed over as host memory (staged H2D per call, results
     # copied back) -- reported beside `value`, never as it
     hs = max(5, args.steps // 20)
@@ -346,6 +352,25 @@ def report(args, spec, lp, ks, dt, world, W_total, Wb, plan_build_ms, theta, the
     else:
         line["cpu_baseline"] = None
     return line
+
+
+def sampler_line(args, lp, theta):
+    """The device DEMetropolisZ (ngrtd_demcz_run, natural space) on the same plan and
+    walkers, outside the timed region: per-step time of ONE call of args.steps steps (the
+    multi-step launch) after a 10-step warm-up.  Reported beside the headline, never as it."""
+    import torch
+    from noblegas_rtd_mcmc_amd.sampler import DeviceDEMetropolisZ
+    s = DeviceDEMetropolisZ(lp, tune_interval=100, seed=7)
+    x, l, z = s.start(theta, 50, 10 + args.steps)
+    lp.demcz(x, l, 10, z)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    lp.demcz(x, l, args.steps, z)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.steps
+    W = theta.shape[-1]
+    return {"method": "PyMC3 DEMetropolisZ, device-resident (one launch per <= 256 steps), natural space",
+            "steps": args.steps, "us_per_step": dt * 1e6, "chain_steps_per_s": W / dt}
 
 
 def exact_line(args, spec, theta, Wb, C, N):
