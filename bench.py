@@ -57,8 +57,17 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-exact", action="store_true", help="skip the exact-path (no surrogate) line")
     ap.add_argument("--no-sampler", action="store_true", help="skip the device DEMetropolisZ line")
+    ap.add_argument("--no-models", action="store_true",
+                    help="skip the published-model / c2 / c3 side lines (N = 1)")
+    ap.add_argument("--sampler-steps", type=int, default=256,
+                    help="steps of the timed device DEMetropolisZ call (one multi-step launch chunk)")
     ap.add_argument("--event-every", type=int, default=8,
                     help="bracket the kernels of every k-th timed step with HIP events (multi-kernel / N > 1)")
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
+                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo stages the "
+                         "all-gather through host memory: the multi-rank rehearsal on a one-GPU box)")
+    ap.add_argument("--one-device", action="store_true",
+                    help="every rank uses cuda:0 (rehearsal of the N > 1 path on a one-GPU box; needs --backend gloo)")
     return ap.parse_args()
 
 
@@ -158,10 +167,16 @@ def main():
     from noblegas_rtd_mcmc_amd.distributed import LogpStepLoop
     from noblegas_rtd_mcmc_amd.engine import LogProb
 
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    if args.one_device and args.backend != "gloo" and world > 1:
+        raise SystemExit("--one-device needs --backend gloo (RCCL refuses two ranks on one device)")
+    gpu = 0 if args.one_device else local
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     W_total = args.walkers * world if args.scaling == "weak" else args.walkers
     spec = model_spec(args)
@@ -174,7 +189,7 @@ def main():
     theta = torch.from_numpy(theta_h).to(dev)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    lp = LogProb(spec, max_walkers=Wb, device=local)     # plan: tables, surrogate fit + validation, c0 table
+    lp = LogProb(spec, max_walkers=Wb, device=gpu)       # plan: tables, surrogate fit + validation, c0 table
     torch.cuda.synchronize()
     plan_build_ms = (time.perf_counter() - t0) * 1e3
     loop = LogpStepLoop(None, W_total, dev)
@@ -193,6 +208,9 @@ def main():
     single_kernel = kinds == {"fused"}
     for _ in range(args.warmup):
         loop.step()
+    torch.cuda.synchronize()
+    # the ensemble vector of an untimed step: the timed steps must reproduce it bit for bit
+    ref_ens = loop.step().clone() if world > 1 else loop.out.clone()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -231,15 +249,50 @@ def main():
         ks["fused"] = (ev0.elapsed_time(ev1), args.steps)
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX) if args.backend == "nccl" else _host_max(t)
         dt = float(t.item())
-    assert torch.isfinite(loop.ensemble()).any()
+    last = loop.gathered if world > 1 else loop.out
+    if not torch.equal(last.nan_to_num(), ref_ens.nan_to_num()) or \
+            not torch.equal(torch.isnan(last), torch.isnan(ref_ens)):
+        raise SystemExit("bench: the timed steps' log-probs differ from an untimed evaluation")
+    finite_frac = float(torch.isfinite(loop.ensemble()).double().mean())
+    if not finite_frac > 0.5:
+        raise SystemExit("bench: only %.3f of the ensemble log-probs are finite" % finite_frac)
 
+    # device DEMetropolisZ on every rank (its own chains: no collective), max over ranks
+    samp = None
+    if not args.no_sampler:
+        samp, us = {}, {}
+        try:                          # a side measurement: never lose the headline line to it
+            samp, us = sampler_line(args, spec, lp, theta, gpu)
+        except Exception as e:        # noqa: BLE001
+            samp = {"error": repr(e)}
+        for space in ("transformed", "natural"):   # max over ranks (every rank reaches this)
+            t = torch.tensor([us.get(space, float("nan"))], dtype=torch.float64, device=dev)
+            if world > 1:
+                dist.all_reduce(t, op=dist.ReduceOp.MAX) if args.backend == "nccl" else _host_max(t)
+            if space in samp and "us_per_step" in samp[space]:
+                samp[space]["us_per_step"] = float(t.item())
+                samp[space]["chain_steps_per_s"] = W_total / (float(t.item()) * 1e-6)
     if rank == 0:
         line = report(args, spec, lp, ks, dt, world, W_total, Wb, plan_build_ms, theta, theta_h)
+        line["ensemble_finite_frac"] = finite_frac
+        if samp is not None:
+            line["sampler"] = samp
+        if world > 1:
+            line["config"]["backend"] = args.backend + (" (host-staged all-gather)" if args.backend == "gloo" else "")
+            line["config"]["one_device"] = bool(args.one_device)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _host_max(t):
+    """MAX all-reduce through host memory (gloo: the one-GPU rehearsal of N > 1)."""
+    import torch.distributed as dist
+    h = t.cpu()
+    dist.all_reduce(h, op=dist.ReduceOp.MAX)
+    t.copy_(h)
 
 
 def pmc_summary(kfull, instance=None):
@@ -333,11 +386,15 @@ def report(args, spec, lp, ks, dt, world, W_total, Wb, plan_build_ms, theta, the
     }
     if world == 1 and exp_single and info.get("surrogate") and not args.no_exact:
         line.update(exact_line(args, spec, theta, Wb, C, N))
-    if world == 1 and not args.no_sampler:
-        try:                          # a side measurement: never lose the headline line to it
-            line["sampler"] = sampler_line(args, lp, theta)
+    # the reference's run length (run_age_mcmc_utils.py:412-417: tune 10 000 + draws 10 000)
+    # with the plan build paid once: W S / (S t_step + plan_build)
+    S20k = 20000
+    line["value_amortized_20k"] = W_total * S20k / (S20k * dt / args.steps + plan_build_ms * 1e-3)
+    if world == 1 and not args.no_models:
+        try:
+            line["models"] = model_lines(args, theta.device.index)
         except Exception as e:        # noqa: BLE001
-            line["sampler"] = {"error": repr(e)}
+            line["models"] = {"error": repr(e)}
     # PCIe-inclusive rate: theta handed over as host memory (staged H2D per call, results
     # copied back) -- reported beside `value`, never as it
     hs = max(5, args.steps // 20)
@@ -354,23 +411,114 @@ def report(args, spec, lp, ks, dt, world, W_total, Wb, plan_build_ms, theta, the
     return line
 
 
-def sampler_line(args, lp, theta):
-    """The device DEMetropolisZ (ngrtd_demcz_run, natural space) on the same plan and
-    walkers, outside the timed region: per-step time of ONE call of args.steps steps (the
-    multi-step launch) after a 10-step warm-up.  Reported beside the headline, never as it."""
+def sampler_line(args, spec, lp, theta, gpu):
+    """The device DEMetropolisZ (ngrtd_demcz_run) on the same walkers, outside the timed
+    region: per-step time of ONE call of --sampler-steps steps (the multi-step launch; the
+    call's two layout transposes included) after a 10-step warm-up.  Primary: PyMC3's
+    transformed space (a plan with the Jacobians -- the space the reference samples in);
+    beside it the natural space on the headline plan.  Reported beside the headline, never
+    as it.  Returns (fields, {space: us per step}) -- the caller takes the max over ranks."""
+    import dataclasses
     import torch
+    from noblegas_rtd_mcmc_amd.engine import LogProb
     from noblegas_rtd_mcmc_amd.sampler import DeviceDEMetropolisZ
-    s = DeviceDEMetropolisZ(lp, tune_interval=100, seed=7)
-    x, l, z = s.start(theta, 50, 10 + args.steps)
-    lp.demcz(x, l, 10, z)
+    n = max(1, args.sampler_steps)
+    W = theta.shape[-1]
+    out, us = {}, {}
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    lp.demcz(x, l, args.steps, z)
+    lpj = LogProb(dataclasses.replace(spec, jacobian=True), max_walkers=W, device=gpu)
     torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / args.steps
-    W = theta.shape[-1]
-    return {"method": "PyMC3 DEMetropolisZ, device-resident (one launch per <= 256 steps), natural space",
-            "steps": args.steps, "us_per_step": dt * 1e6, "chain_steps_per_s": W / dt}
+    build_ms = (time.perf_counter() - t0) * 1e3
+    for space, plan in (("transformed", lpj), ("natural", lp)):
+        s = DeviceDEMetropolisZ(plan, tune_interval=100, seed=7, transformed=space == "transformed")
+        x, l, z = s.start(theta, 50, 10 + n)
+        cnt = torch.zeros(1, dtype=torch.int64, device=theta.device)
+        plan.demcz(x, l, 10, z)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        plan.demcz(x, l, n, z, n_accepted=cnt)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / n
+        us[space] = dt * 1e6
+        out[space] = {"us_per_step": dt * 1e6, "chain_steps_per_s": W / dt, "steps": n,
+                      "accept_rate": int(cnt.item()) / float(n * W)}
+    out["transformed"]["plan_build_ms"] = build_ms
+    lpj.close()
+    out["method"] = ("PyMC3 DEMetropolisZ, device-resident (ngrtd_demcz_run: one launch per <= 256 steps, "
+                     "each block stepping its own chains), one chain per walker over all its wells; "
+                     "primary = PyMC3's transformed space")
+    out["us_per_step"] = out["transformed"]["us_per_step"]
+    return out, us
+
+
+PUBLISHED_MODELS = (("exponential", "piston"), ("exp_pist_flow", None), ("exp_pist_flow", "piston"))
+
+
+def _time_plan(spec, W, gpu, steps, seed=34568):
+    """Plan build time and the per-launch time of the plan's log-prob (HIP events on the
+    launch stream around `steps` back-to-back launches) on a seeded prior ensemble."""
+    import torch
+    from noblegas_rtd_mcmc_amd import workloads
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+    th = torch.from_numpy(workloads.sample_prior(spec, W, np.random.default_rng(seed))).cuda(gpu)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    lp = LogProb(spec, max_walkers=W, device=gpu)
+    torch.cuda.synchronize()
+    build_ms = (time.perf_counter() - t0) * 1e3
+    out = torch.empty(W, dtype=torch.float64, device=th.device)
+    run = lp.bind_n(th, out)
+    run(5)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    run(steps)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    finite = float(torch.isfinite(out).double().mean())
+    info = lp.info(W)
+    lp.close()
+    return build_ms, ms, finite, info
+
+
+def model_lines(args, gpu):
+    """Side lines (N = 1, outside the headline's timed region): the RTD models the reference
+    published runs of (run_age_mcmc.py:61-70) on the c4 shape, and
+    the CE-only (c2) and RTD-only (c3) configurations of BASELINE.json.  Each: plan build,
+    kernel time per launch, evals/s, PMC FP64 fraction (committed summary of the same kernel
+    instance) and the rate amortised over a 20 000-step run."""
+    import argparse as ap
+    from noblegas_rtd_mcmc_amd import workloads
+    steps = max(50, args.steps)
+    W = args.walkers
+    res = {}
+    for m1, m2 in PUBLISHED_MODELS:
+        a = ap.Namespace(wells=args.wells, ages=args.ages, mod_type1=m1, mod_type2=m2)
+        spec = model_spec(a)
+        build_ms, ms, finite, info = _time_plan(spec, W, gpu, steps)
+        mix = (1 if m2 == "piston" else 0) | (2 if m1 == "exp_pist_flow" else 0)
+        inst = "logp_fused_kernel<5, true, 2, %d>" % mix
+        pmc, pmc_path = pmc_summary("logp_fused_kernel", inst)
+        U = W * args.wells
+        e = {"kernel_ms": ms, "evals_per_s": W / (ms * 1e-3), "plan_build_ms": build_ms,
+             "value_amortized_20k": W * 20000 / (20000 * ms * 1e-3 + build_ms * 1e-3),
+             "finite_frac": finite, "kernel": inst, "surrogate": info.get("surrogate")}
+        if pmc.get("fp64_flop_per_unit") and inst in (pmc_path or ""):
+            fl = pmc["fp64_flop_per_unit"] * U
+            e["roofline"] = {"bound": "fp64_valu", "achieved": fl / (ms * 1e-3) / 1e12, "peak": FP64_PEAK / 1e12,
+                             "unit": "TFLOP/s", "frac": fl / (ms * 1e-3) / FP64_PEAK, "traffic": pmc.get("hbm_bytes_per_launch"),
+                             "flop_source": "PMC fp64_flop_per_unit %.1f x %d units (%s)" % (pmc["fp64_flop_per_unit"], U, pmc_path)}
+        res[m1 + ("-" + m2 if m2 else "")] = e
+    for name, (spec, _) in (("c2", workloads.c2(W=8)), ("c3", workloads.c3(W=8))):
+        build_ms, ms, finite, info = _time_plan(spec, W, gpu, steps, seed=12345 if name == "c2" else 23456)
+        res[name] = {"workload": {"c2": "CE log-prob, %d walkers x 3 wells (PLM1, PLM6, PLM7) x 5 gases" % W,
+                                  "c3": "RTD log-prob, %d walkers x 4 tracers (CFC12, SF6, H3, He4_ter), exponential, "
+                                        "N=1200 shipped series, sampled log10 J" % W}[name],
+                     "kernel_ms": ms, "evals_per_s": W / (ms * 1e-3), "plan_build_ms": build_ms,
+                     "value_amortized_20k": W * 20000 / (20000 * ms * 1e-3 + build_ms * 1e-3), "finite_frac": finite}
+    return res
 
 
 def exact_line(args, spec, theta, Wb, C, N):

@@ -18,6 +18,27 @@ import torch.distributed as dist
 from .workloads import shard_walkers
 
 
+def host_staged(group=None, t=None):
+    """True when the collective of ``group`` cannot take device tensors directly: the gloo
+    backend (CPU rehearsals of the multi-rank path, e.g. several ranks sharing the one GPU of
+    a test box -- RCCL refuses two ranks on one device) with a CUDA tensor.  The tensor then
+    goes through a host copy around the collective."""
+    if not dist.is_initialized() or (t is not None and not t.is_cuda):
+        return False
+    return dist.get_backend(group) == "gloo"
+
+
+def all_gather_into(out, buf, group=None):
+    """``dist.all_gather_into_tensor(out, buf)``; through host copies when host_staged."""
+    if not host_staged(group, buf):
+        dist.all_gather_into_tensor(out, buf, group=group)
+        return out
+    ho = torch.empty(out.shape, dtype=out.dtype)
+    dist.all_gather_into_tensor(ho, buf.cpu(), group=group)
+    out.copy_(ho)
+    return out
+
+
 class LogpStepLoop:
     """The per-step work of ``bench.py`` on one rank (and of any caller that shards a
     walker ensemble): the batched log-prob of the rank's walker block, then -- world > 1
@@ -49,7 +70,7 @@ class LogpStepLoop:
     def step(self):
         self.evaluate(self.out)
         if self.world > 1:
-            dist.all_gather_into_tensor(self.gathered, self.buf, group=self.group)
+            all_gather_into(self.gathered, self.buf, group=self.group)
         return self.gathered
 
     def run(self, k):
@@ -96,7 +117,7 @@ class ShardedLogProb:
         buf = torch.full((self.per,), float("nan"), dtype=lp_block.dtype, device=lp_block.device)
         buf[: lp_block.shape[0]] = lp_block
         out = torch.empty(self.per * self.world, dtype=lp_block.dtype, device=lp_block.device)
-        dist.all_gather_into_tensor(out, buf, group=self.group)
+        all_gather_into(out, buf, group=self.group)
         return torch.cat([out[r * self.per: r * self.per + (shard_walkers(self.W_total, r, self.world)[1]
                                                             - shard_walkers(self.W_total, r, self.world)[0])]
                           for r in range(self.world)])
@@ -109,7 +130,7 @@ class ShardedLogProb:
         buf[..., : x_block.shape[-1]] = x_block
         flat = buf.contiguous().reshape(-1)
         out = torch.empty(self.world * flat.numel(), dtype=x_block.dtype, device=x_block.device)
-        dist.all_gather_into_tensor(out, flat, group=self.group)
+        all_gather_into(out, flat, group=self.group)
         out = out.reshape((self.world,) + lead + (self.per,))
         parts = []
         for r in range(self.world):
@@ -143,7 +164,7 @@ def sharded_demcz(log_prob, x_block, W_total, tune, draws, device_sampler=False,
         buf = torch.full((t.shape[0], per), fill, dtype=t.dtype, device=t.device)
         buf[:, : t.shape[1]] = t
         out = torch.empty((world * t.shape[0], per), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(out, buf.contiguous(), group=group)
+        all_gather_into(out, buf.contiguous(), group=group)
         out = out.view(world, t.shape[0], per)
         return torch.cat([out[r, :, : shard_walkers(int(W_total), r, world)[1] - shard_walkers(int(W_total), r, world)[0]]
                           for r in range(world)], dim=1)

@@ -1,0 +1,84 @@
+"""c5 on the GPU: the sharded path with the real HIP kernels and two ranks.
+
+The test box has one MI355X, so both ranks run on cuda:0 over gloo (RCCL refuses two ranks
+on one device; the all-gathers go through host memory).  The ranks are separate processes
+started by torch.distributed.run as children of this one (never an exec of a process that
+touched the GPU).  Checked bitwise against one process evaluating / sampling the whole
+ensemble: the gathered log-prob vector (bench.py's LogpStepLoop) and the union of the
+ranks' device DEMetropolisZ chains (sharded_demcz(device_sampler=True)).  Then bench.py's
+own N > 1 branch runs the same way (--backend gloo --one-device)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _torchrun(args, timeout=300):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    return subprocess.run(cmd, check=True, timeout=timeout, env=env, capture_output=True, text=True, cwd=REPO)
+
+
+@pytest.mark.parametrize("W,L,per_well", [(2048, 64, 0), (130, 3, 0)])
+def test_two_ranks_on_gpu_equal_one_process(tmp_path, W, L, per_well):
+    """Strong sharding of one seeded ensemble (c5's partition at N = 2; W = 130 at L = 3:
+    ragged walker-major blocks): the gathered ensemble log-prob == the single-process
+    log-prob, and the ranks' device DEMetropolisZ chains == the same chains of the
+    single-process device run, bit for bit."""
+    import torch
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+    from noblegas_rtd_mcmc_amd.sampler import DeviceDEMetropolisZ
+    _torchrun([os.path.join(REPO, "tests", "dist_gpu_worker.py"), str(tmp_path), str(W), str(L), str(per_well)])
+    r0, r1 = (np.load(tmp_path / ("rank%d.npz" % r)) for r in (0, 1))
+    spec = wl.c4_spec(L=L, N=1200)
+    full = torch.from_numpy(wl.sample_prior(spec, W, np.random.default_rng(34568))).cuda()
+    lp = LogProb(spec, max_walkers=W)
+    ref = lp(full).cpu().numpy()
+    assert int(r0["lo"]) == 0 and int(r0["hi"]) == int(r1["lo"]) and int(r1["hi"]) == W
+    for r in (r0, r1):
+        assert np.array_equal(r["ens"], ref, equal_nan=True)
+        assert np.array_equal(r["g1"], r["g2"], equal_nan=True)
+    kw = dict(tune_interval=4, seed=2024)
+    if per_well:
+        kw["per_well"] = True
+    one = DeviceDEMetropolisZ(lp, **kw).run(full, tune=8, draws=6)
+    cat = lambda k: np.concatenate([r0[k], r1[k]], axis=-1)   # noqa: E731
+    assert np.array_equal(cat("x"), one["x"].cpu().numpy())
+    assert np.array_equal(cat("lp"), one["lp"].cpu().numpy())
+    assert np.array_equal(cat("samples"), one["samples"].cpu().numpy())
+    for r in (r0, r1):
+        assert np.array_equal(r["lp_tr"], one["logp"].cpu().numpy())
+        assert np.array_equal(r["acc_tr"], one["accepted"].cpu().numpy())
+    assert 0 < int(one["accepted"].sum()) < one["accepted"].numel()
+    lp.close()
+
+
+def test_bench_two_ranks_one_gpu():
+    """bench.py's N > 1 branch (LogpStepLoop + all-gather, max-over-ranks timing, the
+    sampler leg on every rank) end to end on the one GPU: a valid JSON line."""
+    r = _torchrun(["bench.py", "--gpus", "2", "--steps", "10", "--warmup", "2", "--scaling", "strong",
+                   "--backend", "gloo", "--one-device", "--sampler-steps", "16", "--no-cpu-baseline"])
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:] + r.stderr[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["walkers_per_gpu"] == 1024
+    assert d["config"]["one_device"] is True and d["ensemble_finite_frac"] > 0.5
+    assert "error" not in d["sampler"] and d["sampler"]["transformed"]["us_per_step"] > 0
