@@ -9,6 +9,7 @@ runs, with the real HIP log-prob:
   2. distributed.sharded_demcz(device_sampler=True): the device DEMetropolisZ chains of its
      block, drawing the random numbers of their global chain indices.
 It saves what it saw to <outdir>/rank<r>.npz; the test compares with one process."""
+import dataclasses
 import os
 import sys
 
@@ -41,12 +42,15 @@ def main():
         kw = dict(tune_interval=4, seed=2024)
         if per_well:
             kw["per_well"] = True
-        res, lp_tr, acc_tr = sharded_demcz(lp, blk, W, tune=8, draws=6, device_sampler=True, **kw)
+        # the sampler in PyMC3's transformed space (a plan with the Jacobians)
+        lpj = LogProb(dataclasses.replace(spec, jacobian=True), max_walkers=loop.hi - loop.lo, device=0)
+        res, lp_tr, acc_tr = sharded_demcz(lpj, blk, W, tune=8, draws=6, device_sampler=True, **kw)
         np.savez(os.path.join(outdir, "rank%d.npz" % rank), ens=loop.ensemble().cpu().numpy(),
                  g1=g1.cpu().numpy(), g2=g2.cpu().numpy(), lo=loop.lo, hi=loop.hi,
                  x=res["x"].cpu().numpy(), lp=res["lp"].cpu().numpy(), samples=res["samples"].cpu().numpy(),
                  lp_tr=lp_tr.cpu().numpy(), acc_tr=acc_tr.cpu().numpy())
         lp.close()
+        lpj.close()
     finally:
         dist.destroy_process_group()
 

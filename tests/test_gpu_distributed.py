@@ -7,6 +7,7 @@ touched the GPU).  Checked bitwise against one process evaluating / sampling the
 ensemble: the gathered log-prob vector (bench.py's LogpStepLoop) and the union of the
 ranks' device DEMetropolisZ chains (sharded_demcz(device_sampler=True)).  Then bench.py's
 own N > 1 branch runs the same way (--backend gloo --one-device)."""
+import dataclasses
 import json
 import os
 import socket
@@ -59,7 +60,8 @@ def test_two_ranks_on_gpu_equal_one_process(tmp_path, W, L, per_well):
     kw = dict(tune_interval=4, seed=2024)
     if per_well:
         kw["per_well"] = True
-    one = DeviceDEMetropolisZ(lp, **kw).run(full, tune=8, draws=6)
+    lpj = LogProb(dataclasses.replace(spec, jacobian=True), max_walkers=W)
+    one = DeviceDEMetropolisZ(lpj, **kw).run(full, tune=8, draws=6)
     cat = lambda k: np.concatenate([r0[k], r1[k]], axis=-1)   # noqa: E731
     assert np.array_equal(cat("x"), one["x"].cpu().numpy())
     assert np.array_equal(cat("lp"), one["lp"].cpu().numpy())
@@ -69,6 +71,7 @@ def test_two_ranks_on_gpu_equal_one_process(tmp_path, W, L, per_well):
         assert np.array_equal(r["acc_tr"], one["accepted"].cpu().numpy())
     assert 0 < int(one["accepted"].sum()) < one["accepted"].numel()
     lp.close()
+    lpj.close()
 
 
 def test_bench_two_ranks_one_gpu():
