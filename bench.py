@@ -267,13 +267,17 @@ def main():
             samp, us = sampler_line(args, spec, lp, theta, gpu)
         except Exception as e:        # noqa: BLE001
             samp = {"error": repr(e)}
-        for space in ("transformed", "natural"):   # max over ranks (every rank reaches this)
+        for space in ("transformed", "natural", "transformed_joint"):   # max over ranks (all ranks reach this)
             t = torch.tensor([us.get(space, float("nan"))], dtype=torch.float64, device=dev)
             if world > 1:
                 dist.all_reduce(t, op=dist.ReduceOp.MAX) if args.backend == "nccl" else _host_max(t)
             if space in samp and "us_per_step" in samp[space]:
-                samp[space]["us_per_step"] = float(t.item())
-                samp[space]["chain_steps_per_s"] = W_total / (float(t.item()) * 1e-6)
+                e = samp[space]
+                e["us_per_step"] = float(t.item())
+                e["walker_steps_per_s"] = W_total / (float(t.item()) * 1e-6)
+                e["chain_steps_per_s"] = e["walker_steps_per_s"] * e["chains"] / Wb
+        if "transformed" in samp:
+            samp["us_per_step"] = samp["transformed"]["us_per_step"]
     if rank == 0:
         line = report(args, spec, lp, ks, dt, world, W_total, Wb, plan_build_ms, theta, theta_h)
         line["ensemble_finite_frac"] = finite_frac
@@ -430,8 +434,9 @@ def sampler_line(args, spec, lp, theta, gpu):
     lpj = LogProb(dataclasses.replace(spec, jacobian=True), max_walkers=W, device=gpu)
     torch.cuda.synchronize()
     build_ms = (time.perf_counter() - t0) * 1e3
-    for space, plan in (("transformed", lpj), ("natural", lp)):
-        s = DeviceDEMetropolisZ(plan, tune_interval=100, seed=7, transformed=space == "transformed")
+    L = spec.n_wells
+    for name, plan, pw in (("transformed", lpj, True), ("natural", lp, True), ("transformed_joint", lpj, False)):
+        s = DeviceDEMetropolisZ(plan, tune_interval=100, seed=7, transformed=plan is lpj, per_well=pw)
         x, l, z = s.start(theta, 50, 10 + n)
         cnt = torch.zeros(1, dtype=torch.int64, device=theta.device)
         plan.demcz(x, l, 10, z)
@@ -440,14 +445,17 @@ def sampler_line(args, spec, lp, theta, gpu):
         plan.demcz(x, l, n, z, n_accepted=cnt)
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / n
-        us[space] = dt * 1e6
-        out[space] = {"us_per_step": dt * 1e6, "chain_steps_per_s": W / dt, "steps": n,
-                      "accept_rate": int(cnt.item()) / float(n * W)}
+        us[name] = dt * 1e6
+        nch = W * (L if pw else 1)
+        out[name] = {"us_per_step": dt * 1e6, "chains": nch, "chain_steps_per_s": nch / dt,
+                     "walker_steps_per_s": W / dt, "steps": n, "accept_rate": int(cnt.item()) / float(n * nch),
+                     "chain": "one per (walker, well)" if pw else "one per walker over its %d wells" % L}
+        del x, l, z
     out["transformed"]["plan_build_ms"] = build_ms
     lpj.close()
     out["method"] = ("PyMC3 DEMetropolisZ, device-resident (ngrtd_demcz_run: one launch per <= 256 steps, "
-                     "each block stepping its own chains), one chain per walker over all its wells; "
-                     "primary = PyMC3's transformed space")
+                     "each block stepping its own chains); primary = per-well chains (one PyMC3 model per well, "
+                     "as the reference runs them) in PyMC3's transformed space")
     out["us_per_step"] = out["transformed"]["us_per_step"]
     return out, us
 

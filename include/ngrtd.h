@@ -320,7 +320,7 @@ int ngrtd_plan_info(ngrtd_plan* plan, int64_t W, int64_t* info, int32_t n);
  * (e*W + w)*P*L + r -- a chain's state is one contiguous run.  Entry e is the state after
  * step e (hist_len == steps_done after every call).
  * accepted_log [n_steps][W] (uint8) and logp_log [n_steps][W] (each chain's log-prob after
- * the step) may be NULL.  n_accepted (device uint64, may be NULL) counts acceptances.
+ * the step; per-well chains: [n_steps][L][W], and logp is [L][W]) may be NULL.  n_accepted (device uint64, may be NULL) counts acceptances.
  * Joint plans with a single-launch instance (C = 5 channels: c3, c4, the published models):
  * one launch per chunk of up to NGRTD_DZ_CHUNK (default 256) steps, each block stepping its
  * own chains (proposal, history append, log-prob, decision, tuning, commit per step).
@@ -350,10 +350,28 @@ typedef struct {
     double* theta_u;         /* [P][L][W] transformed state (device), NULL = natural space */
     int32_t tr_kind[NGRTD_ROLE_COUNT];  /* per parameter row p < P: enum ngrtd_transform */
     double tr_a[NGRTD_ROLE_COUNT], tr_b[NGRTD_ROLE_COUNT];   /* interval bounds */
+    /* Per-well chains (1) -- the reference's structure: one PyMC3 model, hence one chain,
+     * per well (age_ens_runs_mcmc/run_age_mcmc.py:122-231 loops `for ww in wells`;
+     * ng_interp/noble_gas_mcmc.py:95-104 runs one well) -- or one chain per walker over all
+     * its wells (0).  Per-well: every (walker w, well l) is a P-dimensional chain c = l W + w
+     * with its own Metropolis decision, partners, lamb / scaling / n_acc_tune (PyMC3 default
+     * lamb 2.38 / sqrt(2 P)); logp, lamb, scaling, n_acc_tune and the logs are [L][W] (the
+     * order of theta's rows); the history is unit-major [hist_cap][W][L][P]; random streams
+     * are keyed by cid = (well0 + l) n_chains_total + chain0 + w, so a run of all L wells
+     * equals L runs of one well each (well0 = l) chain for chain. */
+    int32_t per_well;
+    int32_t reserved0;
+    int64_t well0;           /* global index of well 0 (per-well streams) */
 } ngrtd_demcz_state;
 int ngrtd_demcz_run(ngrtd_plan* plan, double* theta, double* logp, int64_t W, int64_t n_steps,
                     ngrtd_demcz_state* state, uint8_t* accepted_log, double* logp_log,
                     uint64_t* n_accepted);
+
+/* Per-unit log-probabilities: out[l][w] = log-likelihood + log-prior [+ log|Jacobian|] of
+ * (walker w, well l) alone -- the log-prob of one well's PyMC3 model (the reference builds
+ * one model per well, run_age_mcmc.py:122-231 / noble_gas_mcmc.py:216-267); ngrtd_logp is
+ * its sum over wells.  The per-well sampler's initial log-probs. */
+int ngrtd_logp_units(ngrtd_plan* plan, const double* theta, int64_t W, double* out, int32_t mem);
 
 /* Host-only (no device needed): build the piecewise-Chebyshev surrogate the exponential
  * log-prob kernel uses for its channel sums and validate it against a long-double

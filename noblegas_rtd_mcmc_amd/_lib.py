@@ -45,7 +45,8 @@ class DemczState(C.Structure):
                 ("tune_target", C.c_int32), ("drop_fraction", C.c_double), ("seed", C.c_uint64),
                 ("chain0", C.c_int64), ("n_chains_total", C.c_int64), ("S", C.c_void_p),
                 ("theta_u", C.c_void_p), ("tr_kind", C.c_int32 * ROLE_COUNT), ("tr_a", C.c_double * ROLE_COUNT),
-                ("tr_b", C.c_double * ROLE_COUNT)]
+                ("tr_b", C.c_double * ROLE_COUNT), ("per_well", C.c_int32), ("reserved0", C.c_int32),
+                ("well0", C.c_int64)]
 
 
 class ModelDesc(C.Structure):
@@ -106,6 +107,7 @@ PROTOTYPES = {
     "ngrtd_plan_info": (C.c_int, [C.c_void_p, C.c_int64, _i64p, C.c_int32]),
     "ngrtd_demcz_run": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_void_p,
                                   C.c_void_p, C.c_void_p, C.c_void_p]),
+    "ngrtd_logp_units": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int32]),
     "ngrtd_surrogate_check": (C.c_int, [_dp, C.c_int32, C.c_int64, C.c_double, _dp, _dp]),
     "ngrtd_c0_check": (C.c_int, [C.c_double, C.c_double, _dp, _i32p, _i32p, _dp]),
 }

@@ -100,11 +100,11 @@ class tracer_conv_integral:
     def g_tp(self, value):
         self._g_tp, self._g_lazy = value, None
 
-    def _decayed(self, g, n, index_last, lamba, rad_accum):
+    def _decayed(self, g, n, index_last, lamba, rad_accum, t_samp):
         """:305-316: g x exp(-lamba tp), or g x (1 - exp(-lamba tp)) for 3He."""
         tp = np.arange(0, n).astype(float)
         tp[0] += 1e-5
-        tp += np.floor(self.t_samp - index_last)
+        tp += np.floor(t_samp - index_last)
         lam = np.asarray(lamba, dtype=np.float64)
         if lam.ndim:
             lam = lam.reshape(lam.shape + (1,))
@@ -114,9 +114,11 @@ class tracer_conv_integral:
 
     def _defer_g_tp(self, n, index_last, g_tau=None):
         """Record what convolve() used so that g_tp can be built on access."""
+        # everything gen_g_tp() and the decay read, as of this convolve() (t_samp / C_t too:
+        # the reference applies the decay with convolve()'s t_samp, :307-316)
         snap = dict(tau=self.tau, mod_type=self.mod_type, eta=self.eta, D=self.D, lamba=self.lamba,
                     rad_accum=self.rad_accum, bbar=self.bbar, Phi_im=self.Phi_im, f_tadv_ext=self.f_tadv_ext,
-                    t_half=getattr(self, "_thalf_src", None))
+                    t_samp=self.t_samp, C_t=self.C_t, t_half=getattr(self, "_thalf_src", None))
 
         def build():
             if g_tau is not None:
@@ -146,7 +148,7 @@ class tracer_conv_integral:
                     for k, v in saved.items():
                         setattr(self, k, v)
                     self._thalf_src = saved_src
-            return self._decayed(g, n, index_last, snap["lamba"], snap["rad_accum"])
+            return self._decayed(g, n, index_last, snap["lamba"], snap["rad_accum"], snap["t_samp"])
 
         self._g_tp, self._g_lazy = None, build
 

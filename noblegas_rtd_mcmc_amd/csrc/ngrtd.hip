@@ -30,6 +30,7 @@ namespace ngrtd {
 // ngrtd_dz.hip: the single-launch DEMetropolisZ instances (compiled without machine LICM)
 hipError_t launch_fused_dz_instance(int mix, const RtdArgs& a, const UnitArgs& u, int WB, int64_t W, double* logp,
                                     const DemcAccept& da, size_t lds, size_t max_lds, hipStream_t st);
+bool fused_dz_instance_exists(int mix);
 }
 
 namespace {
@@ -661,9 +662,8 @@ static int launch_fused_dz(ngrtd_ctx* ctx, const RtdArgs& a0, const UnitArgs& u,
     const size_t pb = (size_t)da.P * kFusedUnits * sizeof(double);
     d.prop_lds = (lds + pb <= kFusedMaxLds && !std::getenv("NGRTD_DZ_PROP_GLOBAL")) ? 1 : 0;
     if (d.prop_lds) lds += pb;
-    const hipError_t e = launch_fused_dz_instance(mix, a, u, WB, W, logp, d, lds, kFusedMaxLds, st);
-    if (e == hipErrorInvalidValue) return set_err(ctx, NGRTD_EINVAL, "no single-launch DEMetropolisZ instance %d", mix);
-    HIP_TRY(ctx, e);
+    if (!fused_dz_instance_exists(mix)) return set_err(ctx, NGRTD_EINVAL, "no single-launch DEMetropolisZ instance %d", mix);
+    HIP_TRY(ctx, launch_fused_dz_instance(mix, a, u, WB, W, logp, d, lds, kFusedMaxLds, st));
     return NGRTD_OK;
 }
 static int launch_fused(ngrtd_ctx* ctx, const RtdArgs& a0, const UnitArgs& u, int64_t W, int L, double* logp,
@@ -1558,6 +1558,47 @@ int ngrtd_logp_n(ngrtd_plan* p, const double* theta, int64_t W, double* logp, in
     return NGRTD_OK;
 }
 
+// Per-unit log-probs out[l][w] (device): the single-launch kernel writing each unit's
+// value before the per-walker sum, else the RTD kernel + unit_logp_kernel.
+static int plan_run_units(ngrtd_plan* p, const double* theta, int64_t W, double* out) {
+    ngrtd_ctx* ctx = p->ctx;
+    const int L = p->desc.n_wells;
+    const int64_t U = (int64_t)L * W;
+    hipStream_t st = S(ctx);
+    UnitArgs u = p->unit;
+    u.theta = theta; u.U = U; u.W = W; u.ce_out = nullptr;
+    if (p->desc.rtd_enabled) {
+        RtdArgs a = p->rtd;
+        a.theta = theta; a.U = U; a.conc = nullptr;
+        if (fused_path(a, u)) {
+            u.unit_out = out;
+            return launch_fused(ctx, a, u, W, L, out, st);
+        }
+        a.conc = p->conc.d();
+        NG_CHECK(launch_rtd(ctx, a, a.row_thalf >= 0, st));
+    }
+    u.ulogp = out;
+    hipLaunchKernelGGL(unit_logp_kernel, dim3((unsigned)cdiv(U, 256)), dim3(256), 0, st, u);
+    HIP_TRY(ctx, hipGetLastError());
+    return NGRTD_OK;
+}
+
+int ngrtd_logp_units(ngrtd_plan* p, const double* theta, int64_t W, double* out, int32_t mem) {
+    if (!p) return NGRTD_ESTATE;
+    ngrtd_ctx* ctx = p->ctx;
+    if (!theta || !out || W < 0 || W > p->max_w) return set_err(ctx, NGRTD_EINVAL, "bad theta/out/W (max %lld)", (long long)p->max_w);
+    if (W == 0) return NGRTD_OK;
+    const int64_t U = (int64_t)p->desc.n_wells * W, nth = (int64_t)p->desc.n_params * U;
+    if (mem == NGRTD_MEM_DEVICE) return plan_run_units(p, theta, W, out);
+    HIP_TRY(ctx, p->theta_stage.ensure((size_t)nth * sizeof(double)));
+    HIP_TRY(ctx, p->out_stage.ensure((size_t)U * sizeof(double)));
+    HIP_TRY(ctx, hipMemcpyAsync(p->theta_stage.p, theta, nth * sizeof(double), hipMemcpyHostToDevice, S(ctx)));
+    NG_CHECK(plan_run_units(p, p->theta_stage.d(), W, p->out_stage.d()));
+    HIP_TRY(ctx, hipMemcpyAsync(out, p->out_stage.p, U * sizeof(double), hipMemcpyDeviceToHost, S(ctx)));
+    HIP_TRY(ctx, hipStreamSynchronize(S(ctx)));
+    return NGRTD_OK;
+}
+
 int ngrtd_forward(ngrtd_plan* p, const double* theta, int64_t W, double* ce_out, double* rtd_out, int32_t mem) {
     if (!p) return NGRTD_ESTATE;
     ngrtd_ctx* ctx = p->ctx;
@@ -1604,8 +1645,10 @@ int ngrtd_demcz_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64
     if (!z->lamb || !z->scaling || !z->n_acc_tune || !z->hist || z->hist_cap < 1 || z->hist_len < 0 ||
         z->hist_lo < 0 || z->hist_lo > z->hist_len || z->steps_done < 0 || z->tune_interval < 1 ||
         z->tune_target < 0 || z->tune_target > 2 || !(z->drop_fraction >= 0.0 && z->drop_fraction <= 1.0) ||
-        z->chain0 < 0 || (z->n_chains_total != 0 && z->chain0 + W > z->n_chains_total))
+        z->chain0 < 0 || (z->n_chains_total != 0 && z->chain0 + W > z->n_chains_total) ||
+        (z->per_well != 0 && z->per_well != 1) || z->well0 < 0)
         return set_err(ctx, NGRTD_EINVAL, "bad DEMetropolisZ state");
+    const bool pw = z->per_well != 0;
     const int64_t Wg = z->n_chains_total ? z->n_chains_total : W;
     if (z->hist_len + n_steps > z->hist_cap)
         return set_err(ctx, NGRTD_EINVAL, "history full: %lld entries + %lld steps > capacity %lld",
@@ -1613,9 +1656,10 @@ int ngrtd_demcz_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64
     if (n_steps == 0) return NGRTD_OK;
     hipStream_t st = S(ctx);
     const int64_t R = (int64_t)p->desc.n_params * p->desc.n_wells, E = R * W;
+    const int64_t U = (int64_t)p->desc.n_wells * W, NC = pw ? U : W;   // chains
     HIP_TRY(ctx, p->demc_prop[0].ensure((size_t)E * sizeof(double)));
-    HIP_TRY(ctx, p->demc_lp.ensure((size_t)W * sizeof(double)));
-    HIP_TRY(ctx, p->demc_acc.ensure((size_t)W * sizeof(int32_t)));
+    HIP_TRY(ctx, p->demc_lp.ensure((size_t)NC * sizeof(double)));
+    HIP_TRY(ctx, p->demc_acc.ensure((size_t)NC * sizeof(int32_t)));
     unsigned long long* cnt = reinterpret_cast<unsigned long long*>(n_accepted);
     if (!cnt) {
         HIP_TRY(ctx, p->demc_cnt.ensure(sizeof(unsigned long long)));
@@ -1633,6 +1677,7 @@ int ngrtd_demcz_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64
     base.x = state; base.prop = prop; base.hist = z->hist; base.lamb = z->lamb; base.scaling = z->scaling;
     base.W = W; base.R = R; base.chain0 = z->chain0; base.Wg = Wg; base.S = z->S;
     base.prop_x = tr ? prop_x : nullptr; base.L = p->desc.n_wells;
+    base.per_well = pw ? 1 : 0; base.well0 = z->well0; base.P = p->desc.n_params;
     for (int i = 0; i < kRoleCount; ++i) {
         base.tr_kind[i] = z->tr_kind[i]; base.tr_a[i] = z->tr_a[i]; base.tr_b[i] = z->tr_b[i];
     }
@@ -1650,7 +1695,9 @@ int ngrtd_demcz_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64
         // single-launch instance exists (A/B runs, tests/test_gpu_demc.py)
         const char* m_env = std::getenv("NGRTD_DZ_MODE");
         if (!(m_env && std::strcmp(m_env, "pair") == 0)) dzm = dz_mix(dr, du, p->desc.n_params, tr);
+        if (dzm >= 0 && pw) dzm |= 16;   // per-well chains: one decision per unit
     }
+    const dim3 gpw((unsigned)cdiv(U, 256));   // per-well proposal / accept kernels
     // single-launch instance: chunks of up to NGRTD_DZ_CHUNK (default 256) steps per launch,
     // each block running its own chains through the chunk (DemcAccept::Sched / dz_step)
     const char* chunk_env = std::getenv("NGRTD_DZ_CHUNK");
@@ -1672,8 +1719,9 @@ int ngrtd_demcz_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64
     for (int64_t j = 0; dzm >= 0 && j < n_steps;) {
         const int64_t k = std::min(chunk, n_steps - j);
         DemcAccept da{logp, acc, cnt, xw[0], nullptr, p->desc.n_params, 0, z->n_acc_tune, z->lamb, z->scaling,
-                      0, z->tune_target, z->tune_interval, accepted_log ? accepted_log + j * W : nullptr,
-                      logp_log ? logp_log + j * W : nullptr, z->chain0, tr ? xw[1] : nullptr, nullptr};
+                      0, z->tune_target, z->tune_interval, accepted_log ? accepted_log + j * NC : nullptr,
+                      logp_log ? logp_log + j * NC : nullptr, z->chain0, tr ? xw[1] : nullptr, nullptr};
+        da.per_well = pw ? 1 : 0; da.well0 = z->well0;
         da.zx = tr ? xw[1] : xw[0]; da.dz_prop = prop_x; da.hist = z->hist;
         da.Wg = Wg; da.S = z->S; da.L = p->desc.n_wells;
         da.dz_diag = dz_diag;
@@ -1713,22 +1761,31 @@ int ngrtd_demcz_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64
             z->hist_lo += (int64_t)(z->drop_fraction * (double)(z->hist_len - z->hist_lo));   // oldest
         DemczArgs d = base;
         d.propose = 1; d.append_at = append_at; d.lo = z->hist_lo; d.it = z->hist_len - z->hist_lo; d.key = key;
-        hipLaunchKernelGGL(demcz_propose_kernel, grid, dim3(kZThreads), 0, st, d);
+        if (pw) hipLaunchKernelGGL(demcz_propose_pw_kernel, gpw, dim3(256), 0, st, d);
+        else hipLaunchKernelGGL(demcz_propose_kernel, grid, dim3(kZThreads), 0, st, d);
         HIP_TRY(ctx, hipGetLastError());
         const int64_t next = s + 1;
         const int32_t tune_now = (z->tune_target != NGRTD_TUNE_NONE && next < z->n_tune &&
                                   next % z->tune_interval == 0) ? 1 : 0;
-        const DemcAccept da{logp, acc, cnt, theta, prop_x, p->desc.n_params, key, z->n_acc_tune, z->lamb, z->scaling,
-                            tune_now, z->tune_target, z->tune_interval,
-                            accepted_log ? accepted_log + j * W : nullptr, logp_log ? logp_log + j * W : nullptr,
-                            z->chain0, tr ? z->theta_u : nullptr, tr ? prop : nullptr};
-        NG_CHECK(plan_run(p, prop_x, W, p->demc_lp.d(), nullptr, nullptr, &da));
+        DemcAccept da{logp, acc, cnt, theta, prop_x, p->desc.n_params, key, z->n_acc_tune, z->lamb, z->scaling,
+                      tune_now, z->tune_target, z->tune_interval,
+                      accepted_log ? accepted_log + j * NC : nullptr, logp_log ? logp_log + j * NC : nullptr,
+                      z->chain0, tr ? z->theta_u : nullptr, tr ? prop : nullptr};
+        if (pw) {   // per-unit log-probs of the proposal, then one decision per unit
+            da.L = p->desc.n_wells; da.Wg = Wg; da.per_well = 1; da.well0 = z->well0;
+            NG_CHECK(plan_run_units(p, prop_x, W, p->demc_lp.d()));
+            hipLaunchKernelGGL(demc_accept_pw_kernel, gpw, dim3(256), 0, st, da, (const double*)p->demc_lp.d(), W);
+            HIP_TRY(ctx, hipGetLastError());
+        } else {
+            NG_CHECK(plan_run(p, prop_x, W, p->demc_lp.d(), nullptr, nullptr, &da));
+        }
         z->steps_done = next;
     }
     // the last step's state: history entry steps_done - 1
     DemczArgs d = base;
     d.propose = 0; d.append_at = z->hist_len;
-    hipLaunchKernelGGL(demcz_propose_kernel, grid, dim3(kZThreads), 0, st, d);
+    if (pw) hipLaunchKernelGGL(demcz_propose_pw_kernel, gpw, dim3(256), 0, st, d);
+    else hipLaunchKernelGGL(demcz_propose_kernel, grid, dim3(kZThreads), 0, st, d);
     HIP_TRY(ctx, hipGetLastError());
     z->hist_len += 1;
     return NGRTD_OK;

@@ -145,6 +145,9 @@ struct UnitArgs {
     int32_t bt_row[kMaxBeta], bt_ia[kMaxBeta], bt_ib[kMaxBeta];
     double bt_fa[kMaxBeta], bt_fb[kMaxBeta];
     double bt_betaln;
+    // out [L][W]: logp_fused_kernel writes each unit's log-prob here and returns before the
+    // per-walker sum (ngrtd_logp_units; null: the per-walker log-prob)
+    double* unit_out;
 };
 
 // Metropolis accept of a device DEMetropolisZ step, done where the proposal's log-prob is
@@ -206,6 +209,13 @@ struct DemcAccept {
         double drop;        // stop_tuning's drop fraction, applied at step n_tune
         int32_t tune_target, tune_interval;
     } sch;
+    // Per-well chains (ngrtd_demcz_state.per_well): every (walker w, well l) unit is its own
+    // chain -- the reference runs one PyMC3 model per well (run_age_mcmc.py:122-231,
+    // noble_gas_mcmc.py:95-104).  Chain c = l W + w: lp / acc / n_acc_tune / lamb / scaling
+    // and the logs are [L][W]; random streams are keyed by cid = (well0 + l) Wg + chain0 + w;
+    // the history is unit-major [cap][W][L][P] (a chain's entry is P contiguous doubles).
+    int32_t per_well;
+    int64_t well0;
 };
 
 // One DEMetropolisZ step's schedule (ngrtd_demcz_run's host loop, restated so that a
@@ -237,6 +247,9 @@ struct DemczArgs {
     int32_t L;              // wells: row r belongs to parameter r / L
     int32_t tr_kind[kRoleCount];
     double tr_a[kRoleCount], tr_b[kRoleCount];
+    int32_t per_well;       // per-well chains (demcz_propose_pw_kernel; DemcAccept::per_well)
+    int64_t well0;
+    int32_t P;
 };
 
 }  // namespace ngrtd

@@ -26,7 +26,14 @@ static hipError_t launch_dz_mix(const RtdArgs& a, const UnitArgs& u, int WB, int
     return hipGetLastError();
 }
 
-// The DZ instance `mix` (8 | piston 1 | EPM 2 | Jacobian 4) over W chains in blocks of WB.
+// The DZ instances: 8 | piston 1 | EPM 2 | Jacobian 4 | per-well chains 16.
+bool fused_dz_instance_exists(int mix) {
+    switch (mix & ~16) {
+    case 8: case 9: case 10: case 11: case 12: case 14: return true;
+    default: return false;
+    }
+}
+// The DZ instance `mix` over W chains in blocks of WB (fused_dz_instance_exists(mix)).
 hipError_t launch_fused_dz_instance(int mix, const RtdArgs& a, const UnitArgs& u, int WB, int64_t W, double* logp,
                                     const DemcAccept& da, size_t lds, size_t max_lds, hipStream_t st) {
     switch (mix) {
@@ -36,6 +43,12 @@ hipError_t launch_fused_dz_instance(int mix, const RtdArgs& a, const UnitArgs& u
     case 11: return launch_dz_mix<11>(a, u, WB, W, logp, da, lds, max_lds, st);
     case 12: return launch_dz_mix<12>(a, u, WB, W, logp, da, lds, max_lds, st);
     case 14: return launch_dz_mix<14>(a, u, WB, W, logp, da, lds, max_lds, st);
+    case 24: return launch_dz_mix<24>(a, u, WB, W, logp, da, lds, max_lds, st);
+    case 25: return launch_dz_mix<25>(a, u, WB, W, logp, da, lds, max_lds, st);
+    case 26: return launch_dz_mix<26>(a, u, WB, W, logp, da, lds, max_lds, st);
+    case 27: return launch_dz_mix<27>(a, u, WB, W, logp, da, lds, max_lds, st);
+    case 28: return launch_dz_mix<28>(a, u, WB, W, logp, da, lds, max_lds, st);
+    case 30: return launch_dz_mix<30>(a, u, WB, W, logp, da, lds, max_lds, st);
     default: return hipErrorInvalidValue;
     }
 }

@@ -1019,10 +1019,12 @@ __host__ __device__ __forceinline__ double pymc3_tune(double scale, double acc_r
 // chain.  Then the chain's tuning counter and, at the end of a tune interval, its lamb or
 // scaling (DEMetropolisZ.astep: tuned at the start of the next step from the interval's
 // acceptance rate, counter reset).  Returns the decision.
-__device__ __forceinline__ bool demc_decide(const DemcAccept& d, int64_t w, double lp_prop, uint64_t key,
-                                            int32_t tune_now, int64_t log_off) {
+// Chain index w of the per-chain arrays, random-stream id rid (joint chains: chain0 + w;
+// per-well chains: the unit's cid, dz_cid).
+__device__ __forceinline__ bool demc_decide(const DemcAccept& d, int64_t w, uint64_t rid, double lp_prop,
+                                            uint64_t key, int32_t tune_now, int64_t log_off) {
     const double cur = d.lp[w];
-    const double logu = log(rng_unit(rng_mix(rng_mix(key + 3) + (uint64_t)(d.chain0 + w))));
+    const double logu = log(rng_unit(rng_mix(rng_mix(key + 3) + rid)));
     const double mr = lp_prop - cur;
     const bool acc = __builtin_isfinite(mr) && logu < mr;
     d.acc[w] = acc;
@@ -1044,8 +1046,22 @@ __device__ __forceinline__ bool demc_decide(const DemcAccept& d, int64_t w, doub
     if (d.lp_log) d.lp_log[log_off + w] = acc ? lp_prop : cur;
     return acc;
 }
+__device__ __forceinline__ bool demc_decide(const DemcAccept& d, int64_t w, double lp_prop, uint64_t key,
+                                            int32_t tune_now, int64_t log_off) {
+    return demc_decide(d, w, (uint64_t)(d.chain0 + w), lp_prop, key, tune_now, log_off);
+}
 __device__ __forceinline__ bool demc_decide(const DemcAccept& d, int64_t w, double lp_prop) {
     return demc_decide(d, w, lp_prop, d.key, d.tune_now, 0);
+}
+// Per-well chains: the random-stream id of unit (walker w, well l) -- the same in a run of
+// all L wells and in a run of well l alone (well0 = l), and in any walker-block shard.
+__host__ __device__ __forceinline__ uint64_t dz_cid(int64_t well0, int64_t l, int64_t Wg, int64_t chain0, int64_t w) {
+    return (uint64_t)(well0 + l) * (uint64_t)Wg + (uint64_t)(chain0 + w);
+}
+// ... and the noise element of its parameter row p (rows of one chain are contiguous)
+constexpr int kPwRowStride = 32;   // >= NGRTD_ROLE_COUNT
+__host__ __device__ __forceinline__ uint64_t dz_pw_elem(uint64_t cid, int p) {
+    return cid * (uint64_t)kPwRowStride + (uint64_t)p;
 }
 
 // accept after the generic kernels: one thread per walker decides and copies the
@@ -1230,13 +1246,73 @@ constexpr int kFusedUnitsDz = 512;   // = kFusedUnits (units per logp_fused_kern
 
 // One element of a DEMetropolisZ proposal, the arithmetic of demcz_propose_kernel (bitwise):
 // x + lamb (z1 - z2) + eps, eps = U(-1, 1) S_r scaling from the (row, global chain) stream.
-__device__ __forceinline__ double dz_value(const DemcAccept& d, bool de, double x, double z1, double z2, double lamb,
-                                          double sc, uint64_t ke, int64_t r, int64_t chain) {
+// e: the noise element (row-major (row, global chain) for joint chains, dz_pw_elem for
+// per-well chains); r: the theta row p L + l (the index of S).
+template <class A>
+__device__ __forceinline__ double dz_value_e(const A& d, bool de, double x, double z1, double z2, double lamb,
+                                            double sc, uint64_t ke, uint64_t e, int64_t r) {
     const double y = de ? x + lamb * (z1 - z2) : x;
-    const uint64_t e = (uint64_t)r * (uint64_t)d.Wg + (uint64_t)chain;
     const double u2 = 2.0 * rng_unit(rng_mix(ke + e)) - 1.0;
     const double eps = (d.S ? u2 * d.S[r] : u2) * sc;
     return y + eps;
+}
+__device__ __forceinline__ double dz_value(const DemcAccept& d, bool de, double x, double z1, double z2, double lamb,
+                                          double sc, uint64_t ke, int64_t r, int64_t chain) {
+    return dz_value_e(d, de, x, z1, z2, lamb, sc, ke, (uint64_t)r * (uint64_t)d.Wg + (uint64_t)chain, r);
+}
+
+// Per-well chains (DemczArgs::per_well), the proposal step of plans without a single-launch
+// instance: one thread per unit c = l W + w (theta's [L][W] order: the state / proposal
+// rows [P][L][W] are read and written coalesced), partners and random numbers of the unit's
+// own stream (dz_cid), history entries = P contiguous doubles of the unit-major history
+// [cap][W][L][P].  The arithmetic of dz_stage's per-well branch (bitwise).
+NGRTD_KLINK __global__ void __launch_bounds__(256) demcz_propose_pw_kernel(const DemczArgs d) {
+    const int64_t W = d.W, U = d.W * d.L;
+    const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (c >= U) return;
+    const int64_t l = c / W, w = c % W;
+    const int P = d.P;
+    const uint64_t cid = dz_cid(d.well0, l, d.Wg, d.chain0, w);
+    const size_t entry = (size_t)U * P, slot = ((size_t)w * d.L + l) * P;
+    double x[kRoleCount];
+    for (int p = 0; p < P; ++p) x[p] = d.x[(int64_t)p * U + c];
+    if (d.append_at >= 0)
+        for (int p = 0; p < P; ++p) d.hist[(size_t)d.append_at * entry + slot + p] = x[p];
+    if (!d.propose) return;
+    const bool de = d.it > 1;
+    int64_t e1 = -1, e2 = -1;
+    if (de) {
+        uint64_t iz1, iz2;
+        demcz_partners(d.key, cid, (uint64_t)d.it, iz1, iz2);
+        e1 = d.lo + (int64_t)iz1;
+        e2 = d.lo + (int64_t)iz2;
+    }
+    // an entry appended by this launch is the state itself
+    const bool c1 = e1 == d.append_at, c2 = e2 == d.append_at;
+    const double lamb = d.lamb[c], sc = d.scaling[c];
+    const uint64_t ke = rng_mix(d.key + 2);
+    for (int p = 0; p < P; ++p) {
+        const double z1 = de ? (c1 ? x[p] : d.hist[(size_t)e1 * entry + slot + p]) : 0.0;
+        const double z2 = de ? (c2 ? x[p] : d.hist[(size_t)e2 * entry + slot + p]) : 0.0;
+        const double v = dz_value_e(d, de, x[p], z1, z2, lamb, sc, ke, dz_pw_elem(cid, p), (int64_t)p * d.L + l);
+        d.prop[(int64_t)p * U + c] = v;
+        if (d.prop_x) d.prop_x[(int64_t)p * U + c] = pymc3_backward(d.tr_kind[p], d.tr_a[p], d.tr_b[p], v);
+    }
+}
+
+// Per-well chains, the accept step after the per-unit log-prob (ngrtd_logp_units): one
+// thread per unit c = l W + w decides its own chain and copies its P proposal rows.
+NGRTD_KLINK __global__ void __launch_bounds__(256) demc_accept_pw_kernel(const DemcAccept d,
+                                                                          const double* __restrict__ ulp, int64_t W) {
+    const int64_t U = W * d.L;
+    const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (c >= U) return;
+    const int64_t l = c / W, w = c % W;
+    if (demc_decide(d, c, dz_cid(d.well0, l, d.Wg, d.chain0, w), ulp[c], d.key, d.tune_now, 0)) {
+        for (int p = 0; p < d.P; ++p) d.x[(int64_t)p * U + c] = d.prop[(int64_t)p * U + c];
+        if (d.xu)
+            for (int p = 0; p < d.P; ++p) d.xu[(int64_t)p * U + c] = d.prop_u[(int64_t)p * U + c];
+    }
 }
 
 // Single-launch DEMetropolisZ step (logp_fused_kernel MIX bit 3), unit (walker w, well l)
@@ -1258,7 +1334,10 @@ __device__ __forceinline__ void dz_partners(const DemcAccept& d, const DzStep& s
 // chains'-space value in LDS row p of th for dz_commit.  (Reading the natural proposals
 // back from an LDS copy instead of d.dz_prop was slower: the extra uniform row indices
 // spilled SGPRs into the unit body.)
-template <int PMAX, bool TR>
+// PW (per-well chains, DemcAccept::per_well): the unit is the chain -- partners, lamb /
+// scaling and random numbers of its own (dz_cid), history entry = its P contiguous rows of
+// the unit-major history [cap][W][L][P].
+template <int PMAX, bool TR, bool PW = false>
 __device__ __forceinline__ void dz_stage(const DemcAccept& d, const DzStep& sj, int64_t U, int64_t u, int i, int64_t w,
                                          int l, int L, int64_t W, bool valid, double* th, int p0, double* pl) {
     const int64_t R = (int64_t)d.P * L;
@@ -1268,13 +1347,24 @@ __device__ __forceinline__ void dz_stage(const DemcAccept& d, const DzStep& sj, 
             d.dz_prop[(int64_t)p * U + u] = d.zx[(int64_t)p * U + u];
         return;
     }
-    int64_t e1, e2;
-    dz_partners(d, sj, w, e1, e2);
+    const uint64_t cid = PW ? dz_cid(d.well0, l, d.Wg, d.chain0, w) : 0;
+    int64_t e1 = -1, e2 = -1;
+    if (!PW) {
+        dz_partners(d, sj, w, e1, e2);
+    } else if (sj.it > 1) {
+        uint64_t iz1, iz2;
+        demcz_partners(sj.key, cid, (uint64_t)sj.it, iz1, iz2);
+        e1 = sj.lo + (int64_t)iz1;
+        e2 = sj.lo + (int64_t)iz2;
+    }
     if (d.dz_diag & 16) e1 = e2 = -1;   // timing diagnostics: no partner loads (noise only)
     const bool de = e1 >= 0;
-    const double* z1 = d.hist + ((size_t)(de ? e1 : 0) * W + w) * R + l;
-    const double* z2 = d.hist + ((size_t)(de ? e2 : 0) * W + w) * R + l;
-    const double lamb = d.lamb[w], sc = d.scaling[w];
+    // row p of entry e: joint chains at (e W + w) R + p L + l, per-well at (e W + w) R + l P + p
+    const int64_t roff = PW ? (int64_t)l * d.P : l, rst = PW ? 1 : L;
+    const double* z1 = d.hist + ((size_t)(de ? e1 : 0) * W + w) * R + roff;
+    const double* z2 = d.hist + ((size_t)(de ? e2 : 0) * W + w) * R + roff;
+    const int64_t ci = PW ? (int64_t)l * W + w : w;   // per-chain arrays: [L][W] per-well, [W] joint
+    const double lamb = d.lamb[ci], sc = d.scaling[ci];
     constexpr int KMAX = (PMAX + 1) / 2;
     double x[KMAX], a1[KMAX], a2[KMAX];
 #pragma unroll
@@ -1282,21 +1372,23 @@ __device__ __forceinline__ void dz_stage(const DemcAccept& d, const DzStep& sj, 
         const int p = p0 + 2 * k;
         if (p < d.P) {
             x[k] = d.zx[(int64_t)p * U + u];
-            a1[k] = de ? z1[(int64_t)p * L] : 0.0;
-            a2[k] = de ? z2[(int64_t)p * L] : 0.0;
+            a1[k] = de ? z1[(int64_t)p * rst] : 0.0;
+            a2[k] = de ? z2[(int64_t)p * rst] : 0.0;
         }
     }
     // an entry appended in this launch is the state itself (as demcz_propose_kernel)
     const bool c1 = e1 == sj.at, c2 = e2 == sj.at;
-    double* hrow = d.hist + ((size_t)(sj.at < 0 ? 0 : sj.at) * W + w) * R + l;
+    double* hrow = d.hist + ((size_t)(sj.at < 0 ? 0 : sj.at) * W + w) * R + roff;
     const uint64_t ke = rng_mix(sj.key + 2);
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
         const int p = p0 + 2 * k;
         if (p < d.P) {
-            if (sj.at >= 0 && !(d.dz_diag & 2)) hrow[(int64_t)p * L] = x[k];
-            double v = dz_value(d, de, x[k], c1 ? x[k] : a1[k], c2 ? x[k] : a2[k], lamb, sc, ke,
-                                (int64_t)p * L + l, d.chain0 + w);
+            if (sj.at >= 0 && !(d.dz_diag & 2)) hrow[(int64_t)p * rst] = x[k];
+            const uint64_t el = PW ? dz_pw_elem(cid, p) : (uint64_t)((int64_t)p * L + l) * (uint64_t)d.Wg +
+                                                          (uint64_t)(d.chain0 + w);
+            double v = dz_value_e(d, de, x[k], c1 ? x[k] : a1[k], c2 ? x[k] : a2[k], lamb, sc, ke, el,
+                                  (int64_t)p * L + l);
             // transformed chains: the natural-space value the log-prob reads (and v itself,
             // the chains'-space value, for dz_commit)
             if (TR) {
@@ -1580,6 +1672,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
                                                                               int32_t WB, double* __restrict__ logp,
                                                                               const DemcAccept dacc) {
     constexpr bool DZ = (MIX & 8) != 0;
+    constexpr bool PW = DZ && (MIX & 16) != 0;   // per-well chains: one Metropolis decision per unit
     static_assert(!DZ || (FULL && ROLES == 2), "the DEMetropolisZ step runs in the FULL role-split kernel");
     static_assert(kFusedUnitsDz == kFusedUnits, "DZ staging stride");
     const RtdArgs& a = ak;
@@ -1738,8 +1831,8 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         const int64_t log_off = (int64_t)js * W;
         // both roles stage: theta waves the even parameter rows, RTD waves the odd ones
         if (DZ)
-            dz_stage<kDzMaxP, (MIX & 4) != 0>(dk, sj, uk.U, mu, mi, w0 + mwl, ml, L, W, mvalid, thl,
-                                              do_theta ? 0 : 1, dk.prop_lds ? propl : nullptr);
+            dz_stage<kDzMaxP, (MIX & 4) != 0, PW>(dk, sj, uk.U, mu, mi, w0 + mwl, ml, L, W, mvalid, thl,
+                                                  do_theta ? 0 : 1, dk.prop_lds ? propl : nullptr);
         __syncthreads();
         NGRTD_PROBE(1);
         if (DZ && dk.prop_lds) {                              // the proposal's rows, from LDS
@@ -1838,9 +1931,19 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             __syncthreads();
             if (do_theta) part[pi] = th + part2[pi];          // th + like, as ROLES = 1
         }
+        if (!DZ && uk.unit_out) {   // ngrtd_logp_units: each unit's log-prob, no per-walker sum
+            if (do_theta && mvalid) uk.unit_out[mu] = part[pi];
+            return;
+        }
         NGRTD_PROBE(6);
         __syncthreads();
-        if (WB <= 64 && (WB & (WB - 1)) == 0) {
+        if (PW) {   // per-well chains: the unit's own Metropolis decision (its theta lane)
+            if (do_theta && mvalid) {
+                const int64_t wq = w0 + mwl;
+                dec[mi] = demc_decide(dk, (int64_t)ml * W + wq, dz_cid(dk.well0, ml, dk.Wg, dk.chain0, wq), part[pi],
+                                      sj.key, sj.tune_now, (int64_t)js * uk.U);
+            }
+        } else if (WB <= 64 && (WB & (WB - 1)) == 0) {
             if (wave == 0) {
                 const int G = 64 / WB;                        // well groups (power of two)
                 const int wl = lane % WB, g = lane / WB;
@@ -1856,7 +1959,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         }
         if (DZ) {
             __syncthreads();
-            if (mvalid && dec[mwl] && !(dk.dz_diag & 4))
+            if (mvalid && dec[PW ? mi : mwl] && !(dk.dz_diag & 4))
                 dz_commit<kDzMaxP, (MIX & 4) != 0>(dk, uk.U, mu, mi, thl, do_theta ? 0 : 1,
                                                    dk.prop_lds ? propl : nullptr);
         } else if (dk.lp) {   // DE-MC: accepted walkers take the proposal's theta rows of this unit

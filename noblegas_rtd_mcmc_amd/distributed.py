@@ -8,9 +8,9 @@ block with its own GPU plan and the per-block log-prob vectors are exchanged wit
 tests).  The payload is W_total float64 (16 KiB at 2048 walkers): latency-bound, so it is
 a single collective per step, never bucketed.
 
-``sharded_demcz`` runs the reference's sampler (DEMetropolisZ, one chain per walker) over
-the shards: its chains propose from their own histories, so sampling itself exchanges
-nothing; the trace's log-probs are gathered once at the end.
+``sharded_demcz`` runs the reference's sampler (DEMetropolisZ: one chain per (walker, well),
+or per walker) over the shards: its chains propose from their own histories, so sampling
+itself exchanges nothing; the trace's log-probs are gathered once at the end.
 """
 import torch
 import torch.distributed as dist
@@ -160,12 +160,15 @@ def sharded_demcz(log_prob, x_block, W_total, tune, draws, device_sampler=False,
         return res, res["logp"], res["accepted"]
     per = (int(W_total) + world - 1) // world
 
-    def gather(t, fill):
-        buf = torch.full((t.shape[0], per), fill, dtype=t.dtype, device=t.device)
-        buf[:, : t.shape[1]] = t
-        out = torch.empty((world * t.shape[0], per), dtype=t.dtype, device=t.device)
+    def gather(t, fill):      # [..., W_block] -> [..., W_total] (per-well logs: [draws][L][W])
+        lead = t.shape[:-1]
+        t2 = t.reshape(-1, t.shape[-1])
+        buf = torch.full((t2.shape[0], per), fill, dtype=t.dtype, device=t.device)
+        buf[:, : t2.shape[1]] = t2
+        out = torch.empty((world * t2.shape[0], per), dtype=t.dtype, device=t.device)
         all_gather_into(out, buf.contiguous(), group=group)
-        out = out.view(world, t.shape[0], per)
-        return torch.cat([out[r, :, : shard_walkers(int(W_total), r, world)[1] - shard_walkers(int(W_total), r, world)[0]]
-                          for r in range(world)], dim=1)
+        out = out.view(world, t2.shape[0], per)
+        g = torch.cat([out[r, :, : shard_walkers(int(W_total), r, world)[1] - shard_walkers(int(W_total), r, world)[0]]
+                       for r in range(world)], dim=1)
+        return g.reshape(lead + (int(W_total),))
     return res, gather(res["logp"], float("nan")), gather(res["accepted"].to(torch.float64), 0.0).to(torch.uint8)

@@ -150,6 +150,28 @@ class LogProb:
                                            res.ctypes.data_as(C.c_void_p), _lib.MEM_HOST), "ngrtd_logp")
         return res
 
+    def units(self, theta, soa=False, out=None):
+        """Per-(walker, well) log-probability [L][W] (ngrtd_logp_units): the log-prob of each
+        well's own model -- what the per-well sampler's chains target; ``__call__`` is its sum
+        over wells."""
+        L = self.spec.n_wells
+        if _is_torch(theta):
+            import torch
+            W = self._check_dev(theta)
+            if out is None:
+                out = torch.empty((L, W), dtype=torch.float64, device=theta.device)
+            elif out.dtype != torch.float64 or not out.is_cuda or not out.is_contiguous() or out.numel() != L * W:
+                raise ValueError("out must be a contiguous CUDA float64 tensor [L][W]")
+            self.ctx.check(self.lib.ngrtd_logp_units(self.plan, C.c_void_p(theta.data_ptr()), W,
+                                                     C.c_void_p(out.data_ptr()), _lib.MEM_DEVICE), "ngrtd_logp_units")
+            return out
+        t = self._host_soa(theta, soa)
+        W = t.shape[2]
+        res = np.empty((L, W), dtype=np.float64)
+        self.ctx.check(self.lib.ngrtd_logp_units(self.plan, t.ctypes.data_as(C.c_void_p), W,
+                                                 res.ctypes.data_as(C.c_void_p), _lib.MEM_HOST), "ngrtd_logp_units")
+        return res
+
     def bind(self, theta, out):
         """Fast path for repeated log-probs of the same device buffers: returns a no-argument
         callable that enqueues ngrtd_logp(theta -> out) on torch's current stream of the
@@ -213,20 +235,21 @@ class LogProb:
 
     def demcz(self, theta, logp, n_steps, state, accepted_log=None, logp_log=None, n_accepted=None):
         """n_steps device-resident DEMetropolisZ steps (ngrtd_demcz_run) of the chains theta
-        [P][L][W] (CUDA float64, logp [W] = their log-prob), updated in place on torch's
-        current stream.  state: sampler.ZState (its host counters advance).  accepted_log
-        (uint8) / logp_log (float64): optional CUDA [n_steps][W]; n_accepted: optional CUDA
-        int64 [1] counter."""
+        [P][L][W] (CUDA float64, logp = their log-prob: [W], or [L][W] for per-well chains),
+        updated in place on torch's current stream.  state: sampler.ZState (its host counters
+        advance).  accepted_log (uint8) / logp_log (float64): optional CUDA [n_steps][chains];
+        n_accepted: optional CUDA int64 [1] counter."""
         W = self._check_dev(theta)
-        if logp.dtype != torch_float64() or not logp.is_cuda or logp.numel() != W:
-            raise ValueError("logp must be a CUDA float64 tensor [W]")
+        nc = W * (self.spec.n_wells if state.per_well else 1)
+        if logp.dtype != torch_float64() or not logp.is_cuda or logp.numel() != nc or not logp.is_contiguous():
+            raise ValueError("logp must be a contiguous CUDA float64 tensor of %d chains" % nc)
         R = self.spec.n_params * self.spec.n_wells
         if state.W != W or state.R != R:
             raise ValueError("state was built for R=%d, W=%d" % (state.R, state.W))
         for name, t, dt in (("accepted_log", accepted_log, 1), ("logp_log", logp_log, 8)):
-            if t is not None and (not t.is_cuda or t.element_size() != dt or t.numel() < n_steps * W
+            if t is not None and (not t.is_cuda or t.element_size() != dt or t.numel() < n_steps * nc
                                   or not t.is_contiguous()):
-                raise ValueError("%s must be a contiguous CUDA tensor [n_steps][W]" % name)
+                raise ValueError("%s must be a contiguous CUDA tensor [n_steps][chains]" % name)
         self.ctx.check(self.lib.ngrtd_demcz_run(
             self.plan, C.c_void_p(theta.data_ptr()), C.c_void_p(logp.data_ptr()), W, int(n_steps),
             C.byref(state.c), C.c_void_p(accepted_log.data_ptr() if accepted_log is not None else 0),

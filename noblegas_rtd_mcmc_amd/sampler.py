@@ -178,15 +178,37 @@ def _result(hist, lp_log, acc_log, tune, draws, lamb, scaling, x, lp):
             "lamb": lamb, "scaling": scaling, "x": x, "lp": lp, "tuning_steps": tune}
 
 
+def pw_cid(well0, L, Wg, chain0, W, device):
+    """Per-well chains: the random-stream id of every unit [L][W] (= ngrtd_kernels.hpp dz_cid),
+    (well0 + l) Wg + chain0 + w -- the same in a run of all L wells and in a run of well l
+    alone (well0 = l), and in every walker-block shard (chain0)."""
+    l = torch.arange(L, device=device, dtype=torch.int64)[:, None] + int(well0)
+    w = torch.arange(W, device=device, dtype=torch.int64)[None, :] + int(chain0)
+    return l * int(Wg) + w
+
+
+PW_ROW_STRIDE = 32      # = ngrtd_kernels.hpp kPwRowStride: noise element cid * 32 + p
+
+
 class DEMetropolisZ:
     """PyMC3 DEMetropolisZ for the W chains of x0 [..., W] on torch ops (any device).
 
-    log_prob: callable theta [..., W] -> logp [W] (e.g. engine.LogProb, or a CPU oracle)."""
+    log_prob: callable theta [..., W] -> logp [W] (e.g. engine.LogProb, or a CPU oracle).
+
+    per_well=True: x0 is [P][L][W] and every (walker w, well l) is its own P-dimensional
+    chain -- the reference's structure, one PyMC3 model per well (run_age_mcmc.py:122-231,
+    noble_gas_mcmc.py:95-104).  log_prob must then return the per-unit log-prob [L][W]
+    (engine.LogProb.units); lamb (default 2.38 / sqrt(2 P)), scaling, the tuning counters,
+    the decisions and the logs are per unit ([L][W]); random streams are keyed by the unit's
+    pw_cid (well0: global index of well 0), the device sampler's streams bit for bit."""
 
     def __init__(self, log_prob, lamb=None, scaling=0.001, tune="lambda", tune_interval=100,
-                 tune_drop_fraction=0.9, seed=123423, chain0=0, n_chains_total=None, S=None, transform=None):
+                 tune_drop_fraction=0.9, seed=123423, chain0=0, n_chains_total=None, S=None, transform=None,
+                 per_well=False, well0=0):
         if tune not in (None, "none", "scaling", "lambda"):
             raise ValueError('tune must be None, "scaling" or "lambda" (pymc3 DEMetropolisZ)')
+        self.per_well = bool(per_well)
+        self.well0 = int(well0)
         self.transform = transform               # Transform: chains in PyMC3's transformed space
         self.S = S                               # proposal scale per parameter (x[..., 0] shape), None = ones
         self.chain0 = int(chain0)                # global index of chain 0 (walker-block shards)
@@ -205,6 +227,8 @@ class DEMetropolisZ:
         chains move in u = transform.forward(x0), log_prob must return the log-density of u
         (natural log-prob + log|Jacobian|, e.g. a LogProb of a spec with jacobian=True), and
         it is called on the natural values backward(u)."""
+        if self.per_well:
+            return self._run_per_well(x0, tune, draws)
         tf = self.transform
         u = tf.forward(x0) if tf is not None else x0.clone()
         x = u
@@ -274,17 +298,91 @@ class DEMetropolisZ:
         return _result(hist, lp_log, acc_log, tune, draws, lamb, scaling, x, lp)
 
 
+    def _run_per_well(self, x0, tune, draws):
+        """per_well=True: the chains are the units of x0 [P][L][W] (see the class doc)."""
+        tf = self.transform
+        x = tf.forward(x0) if tf is not None else x0.clone()
+        if x.dim() != 3:
+            raise ValueError("per-well chains need theta [P][L][W]")
+        P, L, W = x.shape
+        dev = x.device
+        lamb = torch.full((L, W), self.lamb if self.lamb is not None else default_lamb(P), dtype=torch.float64,
+                          device=dev)
+        scaling = torch.full((L, W), float(self.scaling), dtype=torch.float64, device=dev)
+        lp = self.log_prob(tf.backward(x) if tf is not None else x).clone()
+        if tuple(lp.shape) != (L, W):
+            raise ValueError("per-well chains need a per-unit log_prob [L][W] (engine.LogProb.units)")
+        if not bool(torch.isfinite(lp).all()):
+            raise ValueError("initial log-prob is not finite for every chain (pymc3: 'Initial evaluation of model "
+                             "at starting point failed')")
+        n = tune + draws
+        hist = torch.empty((n, P, L, W), dtype=x.dtype, device=dev)
+        lp_log = torch.empty((n, L, W), dtype=torch.float64, device=dev)
+        acc_log = torch.empty((n, L, W), dtype=torch.uint8, device=dev)
+        n_acc_tune = torch.zeros((L, W), dtype=torch.int32, device=dev)
+        hist_lo = 0
+        Wg = int(self.n_chains_total or W)
+        cid = pw_cid(self.well0, L, Wg, self.chain0, W, dev)                     # [L][W]
+        e_idx = cid[None] * PW_ROW_STRIDE + torch.arange(P, device=dev, dtype=torch.int64)[:, None, None]
+        li = torch.arange(L, device=dev)[:, None].expand(L, W)
+        wi = torch.arange(W, device=dev)[None, :].expand(L, W)
+        target = {"scaling": 1, "lambda": 2}.get(self.tune, 0)
+        S = None if self.S is None else torch.as_tensor(self.S, dtype=torch.float64, device=dev).reshape(P, L, 1)
+        for s in range(n):
+            if s == tune and tune > 0:                       # stop_tuning: drop the oldest entries
+                hist_lo += int(self.tune_drop_fraction * (s - hist_lo))
+            key = step_key(self.seed, s)
+            it = s - hist_lo
+            if it > 1:
+                hp = mix_t(cid + _s64(mix_int((key + 1) & _M64)))
+                iz1 = (_lsr(hp, 32) * it) >> 32
+                iz2 = ((hp & 0xFFFFFFFF) * (it - 1)) >> 32
+                iz2 = iz2 + (iz2 >= iz1).to(torch.int64)
+                z1 = hist[hist_lo + iz1, :, li, wi].permute(2, 0, 1)      # [P][L][W]
+                z2 = hist[hist_lo + iz2, :, li, wi].permute(2, 0, 1)
+                y = x + lamb * (z1 - z2)
+            else:
+                y = x
+            ke = _s64(mix_int((key + 2) & _M64))
+            u2 = 2.0 * unit_t(mix_t(e_idx + ke)) - 1.0
+            eps = (u2 if S is None else u2 * S) * scaling
+            prop = y + eps
+            lp_prop = self.log_prob(tf.backward(prop) if tf is not None else prop)
+            logu = torch.log(unit_t(mix_t(cid + _s64(mix_int((key + 3) & _M64)))))
+            mr = lp_prop - lp
+            acc = torch.isfinite(mr) & (logu < mr)
+            x = torch.where(acc, prop, x)
+            lp = torch.where(acc, lp_prop, lp)
+            n_acc_tune += acc.to(torch.int32)
+            if target and s + 1 < tune and (s + 1) % self.tune_interval == 0:
+                rate = n_acc_tune.to(torch.float64) / self.tune_interval
+                if target == 2:
+                    lamb = pymc3_tune(lamb, rate)
+                else:
+                    scaling = pymc3_tune(scaling, rate)
+                n_acc_tune.zero_()
+            hist[s] = x
+            lp_log[s] = lp
+            acc_log[s] = acc.to(torch.uint8)
+        if tf is not None:
+            hist = tf.backward(hist)
+            x = tf.backward(x)
+        return _result(hist, lp_log, acc_log, tune, draws, lamb, scaling, x, lp)
+
+
 class ZState:
     """Device state of a DEMetropolisZ run (ngrtd_demcz_state): per-chain lamb / scaling /
     tuning counters and the chain histories [cap][W][R] (chain-major: a chain's state is one
     contiguous run), which also hold the draws."""
 
     def __init__(self, R, W, hist_cap, device, lamb, scaling, n_tune, tune_interval, tune_target,
-                 drop_fraction, seed, chain0=0, n_chains_total=0, S=None):
+                 drop_fraction, seed, chain0=0, n_chains_total=0, S=None, per_well=False, L=1, well0=0):
         self.R, self.W = int(R), int(W)
-        self.lamb = torch.full((W,), float(lamb), dtype=torch.float64, device=device)
-        self.scaling = torch.full((W,), float(scaling), dtype=torch.float64, device=device)
-        self.n_acc_tune = torch.zeros(W, dtype=torch.int32, device=device)
+        self.per_well, self.L = bool(per_well), int(L)
+        shp = (self.L, W) if self.per_well else (W,)      # per-well chains: [L][W]
+        self.lamb = torch.full(shp, float(lamb), dtype=torch.float64, device=device)
+        self.scaling = torch.full(shp, float(scaling), dtype=torch.float64, device=device)
+        self.n_acc_tune = torch.zeros(shp, dtype=torch.int32, device=device)
         self.hist = torch.empty((int(hist_cap), W, self.R), dtype=torch.float64, device=device)
         self.u = None                     # transformed-space chains (set by DeviceDEMetropolisZ.start)
         self.S = (None if S is None else
@@ -295,10 +393,15 @@ class ZState:
                                  tune_interval=int(tune_interval), tune_target=int(tune_target),
                                  drop_fraction=float(drop_fraction), seed=int(seed) & _M64,
                                  chain0=int(chain0), n_chains_total=int(n_chains_total or 0),
-                                 S=self.S.data_ptr() if self.S is not None else None)
+                                 S=self.S.data_ptr() if self.S is not None else None,
+                                 per_well=int(self.per_well), well0=int(well0))
 
     def entries(self, lo, hi):
-        """History entries [lo, hi) as [hi - lo][R][W]."""
+        """History entries [lo, hi) as [hi - lo][R][W] (per-well chains: [hi - lo][P][L][W],
+        from the unit-major [cap][W][L][P] history)."""
+        if self.per_well:
+            P = self.R // self.L
+            return self.hist[lo:hi].reshape(hi - lo, self.W, self.L, P).permute(0, 3, 2, 1)
         return self.hist[lo:hi].permute(0, 2, 1)
 
 
@@ -310,12 +413,20 @@ class DeviceDEMetropolisZ:
 
     transformed: chains in PyMC3's transformed space (Transform.from_spec) -- the default
     when the plan's spec has jacobian=True (the log-prob is then the density of u); else
-    the natural space."""
+    the natural space.
+
+    per_well (default True): every (walker, well) unit is its own chain, as the reference
+    runs one PyMC3 model per well (the wells of every reference model share no parameter);
+    logp / lamb / scaling / the logs are then [L][W].  False: one chain per walker over all
+    its wells (one decision on the sum of the wells' log-probs)."""
 
     def __init__(self, logprob, lamb=None, scaling=0.001, tune="lambda", tune_interval=100,
-                 tune_drop_fraction=0.9, seed=123423, chain0=0, n_chains_total=None, S=None, transformed=None):
+                 tune_drop_fraction=0.9, seed=123423, chain0=0, n_chains_total=None, S=None, transformed=None,
+                 per_well=True, well0=0):
         if tune not in (None, "none", "scaling", "lambda"):
             raise ValueError('tune must be None, "scaling" or "lambda" (pymc3 DEMetropolisZ)')
+        self.per_well = bool(per_well)
+        self.well0 = int(well0)
         if transformed is None:
             transformed = bool(logprob.spec.jacobian)
         if transformed and not logprob.spec.jacobian:
@@ -340,13 +451,15 @@ class DeviceDEMetropolisZ:
         x = tf.backward(u).contiguous() if tf is not None else x0.clone().contiguous()
         W = x.shape[-1]
         R = int(x[..., 0].numel())
-        lp = self.lp(x).clone()
+        P, L = self.lp.spec.n_params, self.lp.spec.n_wells
+        lp = (self.lp.units(x) if self.per_well else self.lp(x)).clone()
         if not bool(torch.isfinite(lp).all()):
             raise ValueError("initial log-prob is not finite for every chain (pymc3: 'Initial evaluation of model "
                              "at starting point failed')")
-        z = ZState(R, W, hist_cap, x.device, self.lamb if self.lamb is not None else default_lamb(R), self.scaling,
+        lamb = self.lamb if self.lamb is not None else default_lamb(P if self.per_well else R)
+        z = ZState(R, W, hist_cap, x.device, lamb, self.scaling,
                    n_tune, self.tune_interval, _lib.TUNE_TARGET[self.tune], self.tune_drop_fraction, self.seed,
-                   self.chain0, self.n_chains_total, self.S)
+                   self.chain0, self.n_chains_total, self.S, per_well=self.per_well, L=L, well0=self.well0)
         if tf is not None:
             z.u = u
             z.c.theta_u = u.data_ptr()
@@ -356,9 +469,9 @@ class DeviceDEMetropolisZ:
     def run(self, x0, tune, draws):
         n = tune + draws
         x, lp, z = self.start(x0, tune, n)
-        W = x.shape[-1]
-        acc_log = torch.empty((n, W), dtype=torch.uint8, device=x.device)
-        lp_log = torch.empty((n, W), dtype=torch.float64, device=x.device)
+        shp = tuple(lp.shape)                   # [W], or [L][W] for per-well chains
+        acc_log = torch.empty((n,) + shp, dtype=torch.uint8, device=x.device)
+        lp_log = torch.empty((n,) + shp, dtype=torch.float64, device=x.device)
         self.lp.demcz(x, lp, n, z, accepted_log=acc_log, logp_log=lp_log)
         hist = z.entries(0, n).reshape((n,) + tuple(x.shape))
         if self.transform is not None:              # the histories hold u: report natural draws
@@ -367,10 +480,12 @@ class DeviceDEMetropolisZ:
 
 
 def sample_model(spec, max_walkers, device, x0, tune, draws, seed, tune_interval, sampler="device",
-                 space="transformed", cache=None):
+                 space="transformed", cache=None, per_well=True):
     """DEMetropolisZ on the log-prob of ``spec`` (the drivers' mc.sample replacement):
     space "transformed" samples PyMC3's free variables (a plan with the Jacobian),
-    "natural" theta itself.  ``cache``: a dict that keeps the sampling plan between calls."""
+    "natural" theta itself.  per_well: one chain per (walker, well), as the reference's one
+    model per well (logp / accepted [draws][L][W]); False: one chain per walker.
+    ``cache``: a dict that keeps the sampling plan between calls."""
     import dataclasses
     from .engine import LogProb
     if space not in ("transformed", "natural"):
@@ -386,10 +501,13 @@ def sample_model(spec, max_walkers, device, x0, tune, draws, seed, tune_interval
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     if sampler == "device":
-        res = DeviceDEMetropolisZ(lp, tune_interval=tune_interval, seed=seed, transformed=jac).run(x0, tune, draws)
+        res = DeviceDEMetropolisZ(lp, tune_interval=tune_interval, seed=seed, transformed=jac,
+                                  per_well=per_well).run(x0, tune, draws)
     else:
         tf = Transform.from_spec(spec) if jac else None
-        res = DEMetropolisZ(lambda th: lp(th), tune_interval=tune_interval, seed=seed, transform=tf).run(x0, tune, draws)
+        f = (lambda th: lp.units(th)) if per_well else (lambda th: lp(th))
+        res = DEMetropolisZ(f, tune_interval=tune_interval, seed=seed, transform=tf,
+                            per_well=per_well).run(x0, tune, draws)
     torch.cuda.synchronize()
     res["sampling_time"] = time.perf_counter() - t0          # PyMC3's trace attribute, seconds
     return res

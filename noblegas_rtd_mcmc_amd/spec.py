@@ -227,6 +227,18 @@ class ModelSpec:
     def n_params(self):
         return len(self.roles)
 
+    def well(self, l):
+        """The one-well model of well l (what the reference builds per well:
+        run_age_mcmc.py:122-231, noble_gas_mcmc.py:95-104)."""
+        import dataclasses
+        ce = rtd = None
+        if self.ce is not None:
+            ce = dataclasses.replace(self.ce, obs=self.ce.obs[l:l + 1], sd=self.ce.sd[l:l + 1],
+                                     E_min=self.ce.E_min[l:l + 1])
+        if self.rtd is not None:
+            rtd = dataclasses.replace(self.rtd, obs=self.rtd.obs[l:l + 1], sd=self.rtd.sd[l:l + 1])
+        return dataclasses.replace(self, n_wells=1, ce=ce, rtd=rtd, roles=list(self.roles))
+
     def role_index(self):
         idx = [-1] * len(ROLES)
         for i, r in enumerate(self.roles):

@@ -55,8 +55,10 @@ def inference_data(res, spec, sampling_time=None, wells=None, library="noblegas_
         for role, name in CE_NAMES.items():
             put(("ce_" + name) if (both and role == "nu_ce_beta") else name, by_role[role])
         Emin = np.asarray(c.E_min)[None, None, :]
-        put("Ae", 10 ** (by_role["Ae_beta"] * (c.logA_max - c.logA_min) + c.logA_min))
-        put("F", 10 ** (by_role["F_beta"] * (c.logF_max - c.logF_min) + c.logF_min))
+        # the reference's Deterministics 'Ae' / 'F' live in log10 space (par_bnd holds
+        # log10 bounds, noble_gas_mcmc.py:183-185, 229-230); ce_exc_wrapper takes 10** (:207)
+        put("Ae", by_role["Ae_beta"] * (c.logA_max - c.logA_min) + c.logA_min)
+        put("F", by_role["F_beta"] * (c.logF_max - c.logF_min) + c.logF_min)
         E = by_role["E_beta"] * (c.E_max - Emin) + Emin
         b = by_role["b_beta"] * (c.b_max - c.b_min) + c.b_min
         put("E", E)
@@ -76,13 +78,23 @@ def inference_data(res, spec, sampling_time=None, wells=None, library="noblegas_
             put("tau", by_role["f1"] * by_role["tau1"] + f2 * by_role["tau2"])
         if "thalf_cfc_beta" in by_role:
             put("thalf_cfc", by_role["thalf_cfc_beta"] * (r.thalf[1] - r.thalf[0]) + r.thalf[0])
-    lp = _np(res["logp"]).T                                  # [chain, draw]
-    acc = _np(res["accepted"]).T.astype(np.int8)
-    stats = {"lp": (("chain", "draw"), lp.astype(np.float64)),
-             "accepted": (("chain", "draw"), acc),
-             "tune": (("chain", "draw"), np.zeros_like(acc)),
-             "lambda": (("chain", "draw"), np.broadcast_to(_np(res["lamb"])[:, None], lp.shape).astype(np.float64)),
-             "scaling": (("chain", "draw"), np.broadcast_to(_np(res["scaling"])[:, None], lp.shape).astype(np.float64))}
+    # per-chain stats: [draw, chain] (one chain per walker) or [draw, L, chain] (per-well
+    # chains) -> [chain, draw(, well)]
+    def per_chain(a):
+        a = _np(a)
+        return a.T if a.ndim == 2 else np.moveaxis(a, (2, 0, 1), (0, 1, 2))
+    lp = per_chain(res["logp"]).astype(np.float64)
+    acc = per_chain(res["accepted"]).astype(np.int8)
+
+    def tuned(v):        # final lamb / scaling per chain, [W] or [L][W]
+        v = _np(v)
+        v = v[:, None] if v.ndim == 1 else v.T[:, None, :]
+        return np.broadcast_to(v, lp.shape).astype(np.float64)
+    sd = ("chain", "draw") if lp.ndim == 2 else ("chain", "draw", "well")
+    stats = {"lp": (sd, lp), "accepted": (sd, acc), "tune": (sd, np.zeros_like(acc)),
+             "lambda": (sd, tuned(res["lamb"])), "scaling": (sd, tuned(res["scaling"]))}
+    if lp.ndim == 3 and L == 1:
+        stats = {k: (("chain", "draw"), v[..., 0]) for k, (dims, v) in stats.items()}
     attrs = {"created_at": datetime.datetime.now(datetime.timezone.utc).isoformat(),
              "inference_library": library,
              "sampler": "DEMetropolisZ (pymc3 3.11.2 algorithm, device-resident)",

@@ -167,6 +167,14 @@ def log_prob(spec, theta_soa, walkers=None):
     return np.array(out)
 
 
+def log_prob_units(spec, theta_soa):
+    """Per-(walker, well) log-prob [L][W]: each well's own model (the reference builds one
+    PyMC3 model per well, run_age_mcmc.py:122-231); log_prob is its sum over wells."""
+    theta_soa = np.asarray(theta_soa, dtype=np.float64)
+    W = theta_soa.shape[2]
+    return np.array([[unit_logp(spec, theta_soa, w, l) for w in range(W)] for l in range(spec.n_wells)])
+
+
 def forward(spec, theta_soa, walkers=None):
     """Model outputs: CE conc [L][G][W'] and RTD conc [L][K][W'] (None where absent)."""
     theta_soa = np.asarray(theta_soa, dtype=np.float64)

@@ -40,8 +40,7 @@ def main():
         g1 = loop.step().clone()
         g2 = loop.run(3).clone()
         kw = dict(tune_interval=4, seed=2024)
-        if per_well:
-            kw["per_well"] = True
+        kw["per_well"] = bool(per_well)
         # the sampler in PyMC3's transformed space (a plan with the Jacobians)
         lpj = LogProb(dataclasses.replace(spec, jacobian=True), max_walkers=loop.hi - loop.lo, device=0)
         res, lp_tr, acc_tr = sharded_demcz(lpj, blk, W, tune=8, draws=6, device_sampler=True, **kw)

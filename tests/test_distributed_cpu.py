@@ -23,15 +23,18 @@ def _spec():
     return wl.c4_spec(L=2, N=120)
 
 
-def _oracle_eval(spec):
+def _oracle_eval(spec, per_well=False):
     import oracle.models as om
 
     def f(theta_block):
         return torch.from_numpy(om.log_prob(spec, theta_block.numpy()))
-    return f
+
+    def fu(theta_block):
+        return torch.from_numpy(om.log_prob_units(spec, theta_block.numpy()))
+    return fu if per_well else f
 
 
-def _worker(rank, world, port, W, outdir):
+def _worker(rank, world, port, W, outdir, per_well=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -43,7 +46,8 @@ def _worker(rank, world, port, W, outdir):
         blk = sh.block(full)
         lp_b, lp_full = sh(blk)
         pos = sh.gather_positions(blk)
-        res, lp_tr, acc_tr = sharded_demcz(_oracle_eval(spec), blk, W, tune=6, draws=4, seed=3, tune_interval=2)
+        res, lp_tr, acc_tr = sharded_demcz(_oracle_eval(spec, per_well), blk, W, tune=6, draws=4, seed=3,
+                                           tune_interval=2, per_well=per_well)
         np.savez(os.path.join(outdir, "r%d.npz" % rank), lp_full=lp_full.numpy(), pos=pos.numpy(),
                  lp_tr=lp_tr.numpy(), acc_tr=acc_tr.numpy(), x=res["x"].numpy(), lp=res["lp"].numpy(),
                  samples=res["samples"].numpy(), lo=sh.lo, hi=sh.hi)
@@ -51,16 +55,17 @@ def _worker(rank, world, port, W, outdir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("W", [9, 16])
-def test_walker_block_allgather_matches_single_process(tmp_path, W):
+@pytest.mark.parametrize("W,per_well", [(9, False), (16, False), (9, True)])
+def test_walker_block_allgather_matches_single_process(tmp_path, W, per_well):
     """Sharded DEMetropolisZ: the union of the two ranks' chains is bitwise the
     single-process run of the whole ensemble (chains draw the random numbers of their
-    global index), and the gathered trace log-probs are the same on both ranks."""
+    global index), and the gathered trace log-probs are the same on both ranks.  per_well:
+    every (walker, well) its own chain, per-unit log-probs [L][W] (oracle.log_prob_units)."""
     import oracle.models as om
     from noblegas_rtd_mcmc_amd import workloads as wl
     from noblegas_rtd_mcmc_amd.sampler import DEMetropolisZ
     port = _free_port()
-    mp.start_processes(_worker, args=(2, port, W, str(tmp_path)), nprocs=2, start_method="spawn")
+    mp.start_processes(_worker, args=(2, port, W, str(tmp_path), per_well), nprocs=2, start_method="spawn")
     r0, r1 = (np.load(tmp_path / ("r%d.npz" % r)) for r in (0, 1))
     spec = _spec()
     full = wl.sample_prior(spec, W, np.random.default_rng(5))
@@ -69,13 +74,15 @@ def test_walker_block_allgather_matches_single_process(tmp_path, W):
     assert np.array_equal(r0["pos"], full) and np.array_equal(r1["pos"], full)
     # blocks tile the ensemble
     assert int(r0["lo"]) == 0 and int(r0["hi"]) == int(r1["lo"]) and int(r1["hi"]) == W
-    one = DEMetropolisZ(_oracle_eval(spec), seed=3, tune_interval=2).run(torch.from_numpy(full), tune=6, draws=4)
+    one = DEMetropolisZ(_oracle_eval(spec, per_well), seed=3, tune_interval=2,
+                        per_well=per_well).run(torch.from_numpy(full), tune=6, draws=4)
     assert np.array_equal(np.concatenate([r0["x"], r1["x"]], axis=-1), one["x"].numpy())
     assert np.array_equal(np.concatenate([r0["samples"], r1["samples"]], axis=-1), one["samples"].numpy())
     assert np.array_equal(r0["lp_tr"], one["logp"].numpy()) and np.array_equal(r1["lp_tr"], one["logp"].numpy())
     assert np.array_equal(r0["acc_tr"], one["accepted"].numpy())
     # the final chain log-probs are consistent with the positions
-    assert np.allclose(om.log_prob(spec, r1["x"]), r1["lp"], rtol=1e-13)
+    f = om.log_prob_units if per_well else om.log_prob
+    assert np.allclose(f(spec, r1["x"]), r1["lp"], rtol=1e-13)
 
 
 def test_shard_walkers_partition():

@@ -15,9 +15,10 @@ def _same(a, b):
     return torch.equal(a, b) or bool(((a == b) | (torch.isnan(a) & torch.isnan(b))).all())
 
 
+@pytest.mark.parametrize("per_well", [True, False])
 @pytest.mark.parametrize("kind", ["joint", "ce_only", "joint_transformed", "bmm_transformed", "bmm", "epm",
                                   "epm_piston", "epm_transformed", "joint_c4_transformed", "joint_l3"])
-def test_device_demcz_matches_torch_bitwise(kind):
+def test_device_demcz_matches_torch_bitwise(kind, per_well):
     """Tuning (every 4 steps), stop_tuning's history drop and the draws: device chains ==
     torch chains, bit for bit.  joint / bmm / epm / epm_piston / joint_transformed /
     epm_transformed / joint_c4_transformed run one launch per step (logp_fused_kernel forms the
@@ -26,7 +27,10 @@ def test_device_demcz_matches_torch_bitwise(kind):
     *_transformed: PyMC3's logodds / interval / log space, the plan adds the Jacobian.
     joint_c4_transformed: the c4 shape (64 wells, 8 walkers per block), 520 chains: the last
     block is partial.  joint_l3: 3 wells, so a block holds 170 walkers (510 of its 512 unit
-    slots) and the walker-major unit mapping of the multi-step launch leaves a ragged tail."""
+    slots) and the walker-major unit mapping of the multi-step launch leaves a ragged tail.
+    per_well: every (walker, well) its own chain (the default; the per-unit decision inside
+    the multi-step launch, or the per-unit proposal / log-prob / accept kernels) or one chain
+    per walker."""
     import dataclasses
     import torch
     from noblegas_rtd_mcmc_amd import workloads as wl
@@ -57,17 +61,19 @@ def test_device_demcz_matches_torch_bitwise(kind):
     lp = LogProb(spec, max_walkers=W)
     x0 = torch.from_numpy(th0).cuda()
     kw = dict(tune_interval=4, seed=987654321)
-    dev = DeviceDEMetropolisZ(lp, **kw).run(x0, tune=12, draws=8)
+    dev = DeviceDEMetropolisZ(lp, per_well=per_well, **kw).run(x0, tune=12, draws=8)
     tf = Transform.from_spec(spec) if spec.jacobian else None
-    ref = DEMetropolisZ(lambda t: lp(t), transform=tf, **kw).run(x0, tune=12, draws=8)
+    f = (lambda t: lp.units(t)) if per_well else (lambda t: lp(t))
+    ref = DEMetropolisZ(f, transform=tf, per_well=per_well, **kw).run(x0, tune=12, draws=8)
     for k in ("x", "lp", "samples", "logp", "accepted", "lamb", "scaling"):
         assert _same(dev[k], ref[k]), k
     assert 0 < int(dev["accepted"].sum()) < dev["accepted"].numel()
     lp.close()
 
 
+@pytest.mark.parametrize("per_well", [True, False])
 @pytest.mark.parametrize("jac", [False, True])
-def test_device_demcz_step_modes_bitwise(jac):
+def test_device_demcz_step_modes_bitwise(jac, per_well):
     """Every device step schedule gives the same chains bit for bit at the c4 shape (520
     chains: 65 walker blocks, the last partial): the multi-step launch (default: up to 256
     steps per launch, each block running its chains through them), one step per launch
@@ -92,7 +98,7 @@ def test_device_demcz_step_modes_bitwise(jac):
         for mode, (m, ch) in modes.items():
             os.environ["NGRTD_DZ_MODE"] = m
             os.environ["NGRTD_DZ_CHUNK"] = ch
-            res[mode] = DeviceDEMetropolisZ(lp, tune_interval=4, seed=99).run(x0, tune=8, draws=6)
+            res[mode] = DeviceDEMetropolisZ(lp, tune_interval=4, seed=99, per_well=per_well).run(x0, tune=8, draws=6)
     finally:
         os.environ.pop("NGRTD_DZ_MODE", None)
         os.environ.pop("NGRTD_DZ_CHUNK", None)
@@ -145,7 +151,7 @@ def test_device_demcz_split_calls_and_shard_offsets():
     W = 64
     th0 = torch.from_numpy(wl.sample_prior(spec, W, np.random.default_rng(9))).cuda()
     lp = LogProb(spec, max_walkers=W)
-    s = DeviceDEMetropolisZ(lp, tune_interval=5, seed=11)
+    s = DeviceDEMetropolisZ(lp, tune_interval=5, seed=11, per_well=False)
     x, l, z = s.start(th0, 10, 20)
     lp.demcz(x, l, 20, z)
     x2, l2, z2 = s.start(th0, 10, 20)
@@ -155,7 +161,7 @@ def test_device_demcz_split_calls_and_shard_offsets():
     assert z.c.hist_len == 20 and z.c.steps_done == 20 and z.c.hist_lo == 9
     # shard [24, 64) of the same ensemble
     lpb = LogProb(spec, max_walkers=W)
-    sb = DeviceDEMetropolisZ(lpb, tune_interval=5, seed=11, chain0=24, n_chains_total=W)
+    sb = DeviceDEMetropolisZ(lpb, tune_interval=5, seed=11, chain0=24, n_chains_total=W, per_well=False)
     xb, lb, zb = sb.start(th0[..., 24:].contiguous(), 10, 20)
     lpb.demcz(xb, lb, 20, zb)
     assert torch.equal(xb, x[..., 24:]) and torch.equal(lb, l[24:])
@@ -163,6 +169,76 @@ def test_device_demcz_split_calls_and_shard_offsets():
         lp.demcz(x, l, 1, z)
     lp.close()
     lpb.close()
+
+
+def test_per_well_run_equals_single_well_runs():
+    """Per-well chains: a run of all L wells equals L independent runs of one well each
+    (ModelSpec.well(l), well0 = l), chain for chain and bit for bit -- the reference's
+    structure, one PyMC3 model per well (run_age_mcmc.py:122-231).  Also for a walker-block
+    shard (chain0) of the L-well run, and through the pair schedule."""
+    import dataclasses
+    import os
+    import torch
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+    from noblegas_rtd_mcmc_amd.sampler import DeviceDEMetropolisZ
+    L, W = 5, 96
+    spec = dataclasses.replace(wl.c4_spec(L=L, N=1200), jacobian=True)
+    x0 = torch.from_numpy(wl.sample_prior(spec, W, np.random.default_rng(31))).cuda()
+    kw = dict(tune_interval=4, seed=77)
+    lp = LogProb(spec, max_walkers=W)
+    full = DeviceDEMetropolisZ(lp, **kw).run(x0, tune=10, draws=6)
+    assert tuple(full["logp"].shape) == (6, L, W) and tuple(full["lamb"].shape) == (L, W)
+    for l in range(L):
+        lpl = LogProb(spec.well(l), max_walkers=W)
+        one = DeviceDEMetropolisZ(lpl, well0=l, **kw).run(x0[:, l:l + 1].contiguous(), tune=10, draws=6)
+        assert torch.equal(one["x"][:, 0], full["x"][:, l]), l
+        assert torch.equal(one["samples"][:, :, 0], full["samples"][:, :, l]), l
+        for k in ("logp", "accepted", "lp", "lamb", "scaling"):
+            assert torch.equal(one[k][..., 0, :] if one[k].dim() > 1 else one[k], full[k][..., l, :]), (l, k)
+        lpl.close()
+    # a walker-block shard of the L-well run
+    lpb = LogProb(spec, max_walkers=W)
+    sh = DeviceDEMetropolisZ(lpb, chain0=40, n_chains_total=W, **kw).run(x0[..., 40:].contiguous(), tune=10, draws=6)
+    assert torch.equal(sh["samples"], full["samples"][..., 40:]) and torch.equal(sh["logp"], full["logp"][..., 40:])
+    # the proposal / per-unit log-prob / accept kernels give the same chains
+    os.environ["NGRTD_DZ_MODE"] = "pair"
+    try:
+        pair = DeviceDEMetropolisZ(lp, **kw).run(x0, tune=10, draws=6)
+    finally:
+        os.environ.pop("NGRTD_DZ_MODE", None)
+    for k in ("x", "lp", "samples", "logp", "accepted", "lamb", "scaling"):
+        assert _same(pair[k], full[k]), k
+    assert 0 < int(full["accepted"].sum()) < full["accepted"].numel()
+    lp.close()
+    lpb.close()
+
+
+@pytest.mark.parametrize("L", [1, 3, 5, 7, 48, 100, 300])
+def test_ragged_walker_major_sweep(L):
+    """The multi-step launch's walker-major unit mapping over ragged blocks (WB = 512 // L
+    walkers per block, WB L < 512 unit slots used; W not a multiple of WB): device == torch
+    bit for bit for W in {1, 63, 65, 1025}, per-well chains in PyMC3's transformed space
+    and one chain per walker in the natural space -- the class of bug da34ef9 fixed (L = 3)."""
+    import dataclasses
+    import torch
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+    from noblegas_rtd_mcmc_amd.sampler import DEMetropolisZ, DeviceDEMetropolisZ, Transform
+    base = wl.c4_spec(L=L, N=300)
+    for per_well, jac in ((True, True), (False, False)):
+        spec = dataclasses.replace(base, jacobian=jac)
+        lp = LogProb(spec, max_walkers=1025)
+        tf = Transform.from_spec(spec) if jac else None
+        f = (lambda t: lp.units(t)) if per_well else (lambda t: lp(t))
+        for W in (1, 63, 65, 1025):
+            x0 = torch.from_numpy(wl.sample_prior(spec, W, np.random.default_rng(L * 1000 + W))).cuda()
+            kw = dict(tune_interval=3, seed=L + W, per_well=per_well)
+            dev = DeviceDEMetropolisZ(lp, **kw).run(x0, tune=6, draws=4)
+            ref = DEMetropolisZ(f, transform=tf, **kw).run(x0, tune=6, draws=4)
+            for k in ("x", "lp", "samples", "logp", "accepted", "lamb", "scaling"):
+                assert _same(dev[k], ref[k]), (L, W, per_well, k)
+        lp.close()
 
 
 def test_prior_only_recovers_analytic_moments():
@@ -220,7 +296,7 @@ def test_demcz_invariants_c4():
     W = 256
     th0 = torch.from_numpy(wl.sample_prior(spec, W, np.random.default_rng(6))).cuda()
     lp = LogProb(spec, max_walkers=W)
-    x, l, z = DeviceDEMetropolisZ(lp, lamb=0.0, scaling=0.0, tune=None, seed=1).start(th0, 0, 8)
+    x, l, z = DeviceDEMetropolisZ(lp, lamb=0.0, scaling=0.0, tune=None, seed=1, per_well=False).start(th0, 0, 8)
     l0 = l.clone()
     cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
     lp.demcz(x, l, 4, z, n_accepted=cnt)
@@ -229,11 +305,17 @@ def test_demcz_invariants_c4():
     # the Beta(2, 0.1) nu rows, which sit at ~1 - 1e-9, out of [0, 1]: nothing is accepted)
     import dataclasses
     lpj = LogProb(dataclasses.replace(spec, jacobian=True), max_walkers=W)
-    x, l, z = DeviceDEMetropolisZ(lpj, tune_interval=5, seed=2).start(th0, 10, 30)
+    x, l, z = DeviceDEMetropolisZ(lpj, tune_interval=5, seed=2, per_well=False).start(th0, 10, 30)
     cnt.zero_()
     lpj.demcz(x, l, 30, z, n_accepted=cnt)
     assert torch.equal(l, lpj(x))
     assert 0 < int(cnt.item()) < 30 * W
+    # per-well chains: the tracked per-unit log-probs equal a fresh ngrtd_logp_units
+    x, l, z = DeviceDEMetropolisZ(lpj, tune_interval=5, seed=2).start(th0, 10, 30)
+    cnt.zero_()
+    lpj.demcz(x, l, 30, z, n_accepted=cnt)
+    assert torch.equal(l, lpj.units(x)) and tuple(l.shape) == (8, W)
+    assert 0 < int(cnt.item()) < 30 * W * 8
     lp.close()
     lpj.close()
 

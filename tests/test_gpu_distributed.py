@@ -37,7 +37,7 @@ def _torchrun(args, timeout=300):
     return subprocess.run(cmd, check=True, timeout=timeout, env=env, capture_output=True, text=True, cwd=REPO)
 
 
-@pytest.mark.parametrize("W,L,per_well", [(2048, 64, 0), (130, 3, 0)])
+@pytest.mark.parametrize("W,L,per_well", [(2048, 64, 1), (2048, 64, 0), (130, 3, 1)])
 def test_two_ranks_on_gpu_equal_one_process(tmp_path, W, L, per_well):
     """Strong sharding of one seeded ensemble (c5's partition at N = 2; W = 130 at L = 3:
     ragged walker-major blocks): the gathered ensemble log-prob == the single-process
@@ -58,8 +58,7 @@ def test_two_ranks_on_gpu_equal_one_process(tmp_path, W, L, per_well):
         assert np.array_equal(r["ens"], ref, equal_nan=True)
         assert np.array_equal(r["g1"], r["g2"], equal_nan=True)
     kw = dict(tune_interval=4, seed=2024)
-    if per_well:
-        kw["per_well"] = True
+    kw["per_well"] = bool(per_well)
     lpj = LogProb(dataclasses.replace(spec, jacobian=True), max_walkers=W)
     one = DeviceDEMetropolisZ(lpj, **kw).run(full, tune=8, draws=6)
     cat = lambda k: np.concatenate([r0[k], r1[k]], axis=-1)   # noqa: E731

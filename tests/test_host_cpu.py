@@ -150,6 +150,38 @@ def test_demcz_tuning_and_history_drop():
     assert res["samples"].shape == (20, 3, 16) and res["accepted"].shape == (20, 16)
 
 
+def test_demcz_per_well_chains_are_independent():
+    """per_well=True: every (walker, well) unit is its own chain.  A 3-well run equals three
+    1-well runs (well0 = l) chain for chain, bit for bit, and each unit's decision only sees
+    its own log-prob (a well whose log-prob is -inf everywhere but the start never moves,
+    the others do)."""
+    from noblegas_rtd_mcmc_amd.sampler import DEMetropolisZ, default_lamb
+    rng = np.random.default_rng(2)
+    P, L, W = 3, 3, 10
+    x0 = torch.from_numpy(rng.normal(size=(P, L, W)))
+    scale = torch.tensor([1.0, 2.0, 0.5], dtype=torch.float64)[:, None]
+
+    def lpu(x):                                   # [P][L][W] -> [L][W], a different Gaussian per well
+        return -0.5 * (x ** 2).sum(0) / scale ** 2
+    full = DEMetropolisZ(lpu, tune_interval=5, seed=9, per_well=True).run(x0, tune=12, draws=8)
+    assert tuple(full["logp"].shape) == (8, L, W) and tuple(full["lamb"].shape) == (L, W)
+    for l in range(L):
+        one = DEMetropolisZ(lambda x, l=l: -0.5 * (x ** 2).sum(0) / scale[l] ** 2, tune_interval=5, seed=9,
+                            per_well=True, well0=l).run(x0[:, l:l + 1].clone(), tune=12, draws=8)
+        assert torch.equal(one["samples"][:, :, 0], full["samples"][:, :, l])
+        assert torch.equal(one["logp"][:, 0], full["logp"][:, l])
+    fixed = DEMetropolisZ(lpu, tune=None, seed=9, per_well=True).run(x0, tune=4, draws=4)
+    assert torch.equal(fixed["lamb"], torch.full((L, W), default_lamb(P), dtype=torch.float64))
+
+    def stuck(x):                                 # well 1 rejects every move
+        v = lpu(x)
+        v[1] = torch.where(torch.isclose(x[0, 1], x0[0, 1]), v[1], torch.full_like(v[1], -np.inf))
+        return v
+    st = DEMetropolisZ(stuck, tune_interval=5, seed=9, per_well=True).run(x0, tune=12, draws=8)
+    assert torch.equal(st["x"][:, 1], x0[:, 1]) and not torch.equal(st["x"][:, 0], x0[:, 0])
+    assert int(st["accepted"][:, 1].sum()) == 0 and int(st["accepted"][:, 0].sum()) > 0
+
+
 def test_ce_sampler_plumbing_with_cpu_logp():
     """c1 plumbing: DEMetropolisZ driving the CE log-prob (oracle as the CPU log-prob)."""
     import oracle.models as om
