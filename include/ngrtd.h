@@ -362,6 +362,9 @@ typedef struct {
     int32_t per_well;
     int32_t reserved0;
     int64_t well0;           /* global index of well 0 (per-well streams) */
+    /* Per call, like accepted_log: [n_steps][chains] PyMC3's `accept` sample stat,
+     * exp(logp(x*) - logp(x)) (DEMetropolisZ.astep), device memory; NULL = not logged. */
+    double* accept_log;
 } ngrtd_demcz_state;
 int ngrtd_demcz_run(ngrtd_plan* plan, double* theta, double* logp, int64_t W, int64_t n_steps,
                     ngrtd_demcz_state* state, uint8_t* accepted_log, double* logp_log,

@@ -46,7 +46,7 @@ class DemczState(C.Structure):
                 ("chain0", C.c_int64), ("n_chains_total", C.c_int64), ("S", C.c_void_p),
                 ("theta_u", C.c_void_p), ("tr_kind", C.c_int32 * ROLE_COUNT), ("tr_a", C.c_double * ROLE_COUNT),
                 ("tr_b", C.c_double * ROLE_COUNT), ("per_well", C.c_int32), ("reserved0", C.c_int32),
-                ("well0", C.c_int64)]
+                ("well0", C.c_int64), ("accept_log", C.c_void_p)]
 
 
 class ModelDesc(C.Structure):

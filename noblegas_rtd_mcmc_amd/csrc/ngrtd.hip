@@ -1722,6 +1722,7 @@ int ngrtd_demcz_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64
                       0, z->tune_target, z->tune_interval, accepted_log ? accepted_log + j * NC : nullptr,
                       logp_log ? logp_log + j * NC : nullptr, z->chain0, tr ? xw[1] : nullptr, nullptr};
         da.per_well = pw ? 1 : 0; da.well0 = z->well0;
+        da.ar_log = z->accept_log ? z->accept_log + j * NC : nullptr;
         da.zx = tr ? xw[1] : xw[0]; da.dz_prop = prop_x; da.hist = z->hist;
         da.Wg = Wg; da.S = z->S; da.L = p->desc.n_wells;
         da.dz_diag = dz_diag;
@@ -1771,6 +1772,7 @@ int ngrtd_demcz_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64
                       tune_now, z->tune_target, z->tune_interval,
                       accepted_log ? accepted_log + j * NC : nullptr, logp_log ? logp_log + j * NC : nullptr,
                       z->chain0, tr ? z->theta_u : nullptr, tr ? prop : nullptr};
+        da.ar_log = z->accept_log ? z->accept_log + j * NC : nullptr;
         if (pw) {   // per-unit log-probs of the proposal, then one decision per unit
             da.L = p->desc.n_wells; da.Wg = Wg; da.per_well = 1; da.well0 = z->well0;
             NG_CHECK(plan_run_units(p, prop_x, W, p->demc_lp.d()));

@@ -216,6 +216,7 @@ struct DemcAccept {
     // the history is unit-major [cap][W][L][P] (a chain's entry is P contiguous doubles).
     int32_t per_well;
     int64_t well0;
+    double* ar_log;         // [chains] this step's PyMC3 `accept` stat exp(mr) (null: not logged)
 };
 
 // One DEMetropolisZ step's schedule (ngrtd_demcz_run's host loop, restated so that a

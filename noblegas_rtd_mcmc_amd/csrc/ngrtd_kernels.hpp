@@ -1044,6 +1044,7 @@ __device__ __forceinline__ bool demc_decide(const DemcAccept& d, int64_t w, uint
     }
     if (d.acc_log) d.acc_log[log_off + w] = (uint8_t)acc;
     if (d.lp_log) d.lp_log[log_off + w] = acc ? lp_prop : cur;
+    if (d.ar_log) d.ar_log[log_off + w] = exp(mr);
     return acc;
 }
 __device__ __forceinline__ bool demc_decide(const DemcAccept& d, int64_t w, double lp_prop, uint64_t key,

@@ -233,12 +233,14 @@ class LogProb:
                                               _lib.MEM_HOST), "ngrtd_forward")
         return ce, rt
 
-    def demcz(self, theta, logp, n_steps, state, accepted_log=None, logp_log=None, n_accepted=None):
+    def demcz(self, theta, logp, n_steps, state, accepted_log=None, logp_log=None, n_accepted=None,
+              accept_log=None):
         """n_steps device-resident DEMetropolisZ steps (ngrtd_demcz_run) of the chains theta
         [P][L][W] (CUDA float64, logp = their log-prob: [W], or [L][W] for per-well chains),
         updated in place on torch's current stream.  state: sampler.ZState (its host counters
         advance).  accepted_log (uint8) / logp_log (float64): optional CUDA [n_steps][chains];
-        n_accepted: optional CUDA int64 [1] counter."""
+        n_accepted: optional CUDA int64 [1] counter; accept_log (float64, [n_steps][chains]):
+        PyMC3's `accept` stat exp(logp(x*) - logp(x)) per step."""
         W = self._check_dev(theta)
         nc = W * (self.spec.n_wells if state.per_well else 1)
         if logp.dtype != torch_float64() or not logp.is_cuda or logp.numel() != nc or not logp.is_contiguous():
@@ -246,10 +248,11 @@ class LogProb:
         R = self.spec.n_params * self.spec.n_wells
         if state.W != W or state.R != R:
             raise ValueError("state was built for R=%d, W=%d" % (state.R, state.W))
-        for name, t, dt in (("accepted_log", accepted_log, 1), ("logp_log", logp_log, 8)):
+        for name, t, dt in (("accepted_log", accepted_log, 1), ("logp_log", logp_log, 8), ("accept_log", accept_log, 8)):
             if t is not None and (not t.is_cuda or t.element_size() != dt or t.numel() < n_steps * nc
                                   or not t.is_contiguous()):
                 raise ValueError("%s must be a contiguous CUDA tensor [n_steps][chains]" % name)
+        state.c.accept_log = accept_log.data_ptr() if accept_log is not None else None
         self.ctx.check(self.lib.ngrtd_demcz_run(
             self.plan, C.c_void_p(theta.data_ptr()), C.c_void_p(logp.data_ptr()), W, int(n_steps),
             C.byref(state.c), C.c_void_p(accepted_log.data_ptr() if accepted_log is not None else 0),

@@ -91,8 +91,9 @@ class CEModel:
 
     def sample(self, nwalkers=100, tune=500, draws=500, seed=12345, tune_interval=100, sampler="device",
                space="transformed"):
-        """DEMetropolisZ, one chain per walker, on the GPU log-prob (replaces mc.sample,
-        :408-415).  sampler: "device" (ngrtd_demcz_run, device-resident) or "torch"
+        """DEMetropolisZ on the GPU log-prob (replaces mc.sample, :408-415): one chain per
+        (walker, well), each well its own model as the reference runs them (logp / accepted
+        [draws][L][W]).  sampler: "device" (ngrtd_demcz_run, device-resident) or "torch"
         (sampler.DEMetropolisZ on torch ops; same random stream).  space: "transformed"
         (PyMC3's: logodds for the Beta variables; the log-prob adds the Jacobian) or
         "natural"."""
@@ -104,7 +105,7 @@ class CEModel:
         res = sample_model(self.spec, self.max_walkers, self.device, x, tune, draws, seed, tune_interval, sampler,
                            space, cache=self.__dict__)
         from . import trace
-        res["idata"] = trace.inference_data(res, self.spec, wells=self.wells)   # az.from_pymc3 layout
+        res["idata"] = trace.inference_data(res, self.spec, wells=self.wells, observed=self.spec.ce.obs)
         res["samples"] = res["samples"].cpu().numpy()
         res["logp"] = res["logp"].cpu().numpy()
         return res

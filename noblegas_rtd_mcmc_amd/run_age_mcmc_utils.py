@@ -168,8 +168,8 @@ class conv_mcmc:
 
     def sample_mcmc(self, nwalkers=96, tune=10000, draws=10000, seed=123423, tune_interval=1000, sampler="device",
                     space="transformed"):
-        """DEMetropolisZ, one chain per walker, on the GPU log-prob (replaces mc.sample,
-        :407-429).  sampler: "device" (ngrtd_demcz_run, device-resident) or "torch"
+        """DEMetropolisZ, one chain per walker (the plan holds this one well), on the GPU
+        log-prob (replaces mc.sample, :407-429).  sampler: "device" (ngrtd_demcz_run, device-resident) or "torch"
         (sampler.DEMetropolisZ on torch ops; same random stream).  space: "transformed"
         (PyMC3's: logodds / interval / log; the log-prob adds the Jacobian) or "natural"."""
         import torch
@@ -181,7 +181,7 @@ class conv_mcmc:
         res = sample_model(lp.spec, self.max_walkers, self.device, x, tune, draws, seed, tune_interval, sampler,
                            space, cache=self.__dict__)
         from . import trace
-        idata = trace.inference_data(res, lp.spec, wells=[self.well])
+        idata = trace.inference_data(res, lp.spec, wells=[self.well], observed=lp.spec.rtd.obs)
         res = {k: (v.cpu().numpy() if hasattr(v, "cpu") else v) for k, v in res.items()}
         res["roles"] = list(lp.spec.roles)
         res["idata"] = idata

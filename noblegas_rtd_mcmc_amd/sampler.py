@@ -170,10 +170,11 @@ class Transform:
             c.tr_kind[p], c.tr_a[p], c.tr_b[p] = k, self.a[p], self.b[p]
 
 
-def _result(hist, lp_log, acc_log, tune, draws, lamb, scaling, x, lp):
+def _result(hist, lp_log, acc_log, tune, draws, lamb, scaling, x, lp, ar_log=None):
     acc = acc_log[tune:].to(torch.float64)
     return {"samples": hist[tune:tune + draws], "logp": lp_log[tune:tune + draws],
             "accepted": acc_log[tune:tune + draws], "accept_rate": float(acc.mean()) if draws else 0.0,
+            "accept": ar_log[tune:tune + draws] if ar_log is not None else None,   # PyMC3's exp(mr) stat
             "tune_accept_rate": float(acc_log[:tune].to(torch.float64).mean()) if tune else 0.0,
             "lamb": lamb, "scaling": scaling, "x": x, "lp": lp, "tuning_steps": tune}
 
@@ -246,6 +247,7 @@ class DEMetropolisZ:
         hist = torch.empty((n,) + tuple(x.shape), dtype=x.dtype, device=dev)
         lp_log = torch.empty((n, W), dtype=torch.float64, device=dev)
         acc_log = torch.empty((n, W), dtype=torch.uint8, device=dev)
+        ar_log = torch.empty((n, W), dtype=torch.float64, device=dev)
         n_acc_tune = torch.zeros(W, dtype=torch.int32, device=dev)
         hist_lo = 0
         w_loc = torch.arange(W, device=dev, dtype=torch.int64)
@@ -292,10 +294,11 @@ class DEMetropolisZ:
             hist[s] = x
             lp_log[s] = lp
             acc_log[s] = acc.to(torch.uint8)
+            ar_log[s] = torch.exp(mr)
         if tf is not None:
             hist = tf.backward(hist)
             x = tf.backward(x)
-        return _result(hist, lp_log, acc_log, tune, draws, lamb, scaling, x, lp)
+        return _result(hist, lp_log, acc_log, tune, draws, lamb, scaling, x, lp, ar_log)
 
 
     def _run_per_well(self, x0, tune, draws):
@@ -319,6 +322,7 @@ class DEMetropolisZ:
         hist = torch.empty((n, P, L, W), dtype=x.dtype, device=dev)
         lp_log = torch.empty((n, L, W), dtype=torch.float64, device=dev)
         acc_log = torch.empty((n, L, W), dtype=torch.uint8, device=dev)
+        ar_log = torch.empty((n, L, W), dtype=torch.float64, device=dev)
         n_acc_tune = torch.zeros((L, W), dtype=torch.int32, device=dev)
         hist_lo = 0
         Wg = int(self.n_chains_total or W)
@@ -364,10 +368,11 @@ class DEMetropolisZ:
             hist[s] = x
             lp_log[s] = lp
             acc_log[s] = acc.to(torch.uint8)
+            ar_log[s] = torch.exp(mr)
         if tf is not None:
             hist = tf.backward(hist)
             x = tf.backward(x)
-        return _result(hist, lp_log, acc_log, tune, draws, lamb, scaling, x, lp)
+        return _result(hist, lp_log, acc_log, tune, draws, lamb, scaling, x, lp, ar_log)
 
 
 class ZState:
@@ -472,11 +477,12 @@ class DeviceDEMetropolisZ:
         shp = tuple(lp.shape)                   # [W], or [L][W] for per-well chains
         acc_log = torch.empty((n,) + shp, dtype=torch.uint8, device=x.device)
         lp_log = torch.empty((n,) + shp, dtype=torch.float64, device=x.device)
-        self.lp.demcz(x, lp, n, z, accepted_log=acc_log, logp_log=lp_log)
+        ar_log = torch.empty((n,) + shp, dtype=torch.float64, device=x.device)
+        self.lp.demcz(x, lp, n, z, accepted_log=acc_log, logp_log=lp_log, accept_log=ar_log)
         hist = z.entries(0, n).reshape((n,) + tuple(x.shape))
         if self.transform is not None:              # the histories hold u: report natural draws
             hist = self.transform.backward(hist)
-        return _result(hist, lp_log, acc_log, tune, draws, z.lamb, z.scaling, x, lp)
+        return _result(hist, lp_log, acc_log, tune, draws, z.lamb, z.scaling, x, lp, ar_log)
 
 
 def sample_model(spec, max_walkers, device, x0, tune, draws, seed, tune_interval, sampler="device",

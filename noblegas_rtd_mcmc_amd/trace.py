@@ -1,23 +1,29 @@
-"""Posterior traces in ArviZ's InferenceData layout (the reference's az.to_netcdf).
+"""Posterior traces in ArviZ's InferenceData layout, in the reference's container.
 
 The reference saves every run with ``az.to_netcdf(az.from_pymc3(trace), trace_name)``
-(age_ens_runs_mcmc/run_age_mcmc_utils.py:420-425; ArviZ 0.11.4, PyMC3 3.11.2): a netCDF4
-file with a ``posterior`` group -- one variable per PyMC3 random variable AND
-deterministic, dims (chain, draw[, ...]) -- a ``sample_stats`` group (the step method's
-stats: lp, accepted, tune, scaling, lambda) and attributes (created_at,
-inference_library, sampling_time [s], tuning_steps).
+(age_ens_runs_mcmc/run_age_mcmc_utils.py:420-425, ng_interp/noble_gas_mcmc.py:422-447;
+ArviZ 0.11.4, PyMC3 3.11.2, netCDF 4.8.1): ONE netCDF-4 (HDF5) file with the groups
 
-netCDF4/HDF5 writers (h5py, netCDF4, xarray) are not available in this image, so
-``to_netcdf`` writes the SAME groups as one netCDF-3 file per group into a directory
-(``<trace>/posterior.nc``, ``<trace>/sample_stats.nc``, classic format through
-scipy.io.netcdf_file -- readable by xarray's scipy engine, hence by
-``az.InferenceData(posterior=xr.open_dataset(".../posterior.nc"), sample_stats=...)``),
-with the global attributes on every group file.  Variable names follow the reference
-models: CE (ng_interp/noble_gas_mcmc.py:216-267) Ae_beta, F_beta, E_beta, m, b_beta, nu_
-and the deterministics Ae, F, E, b, T, nu; RTD (run_age_mcmc_utils.py:286-344) tau1,
-nu_, nu, J, tau2, f1, f2, tau, eta1, eta2, D1, D2, thalf_cfc_, thalf_cfc, lamsf6.  A
-model with both blocks prefixes the CE nu variables with ``ce_``.  Walkers are chains;
-a model of several wells gets a trailing ``well`` dim.
+* ``posterior``: one variable per PyMC3 random variable and deterministic, dims (chain, draw);
+* ``sample_stats``: DEMetropolisZ's stats accept (exp(logp(x*) - logp(x))), accepted
+  (int8, ``dtype = "bool"``), lambda, scaling;
+* ``observed_data``: the likelihood's observations ``like`` (dim like_dim_0);
+
+each with the attributes created_at, arviz_version, inference_library,
+inference_library_version (+ sampling_time [s], tuning_steps on posterior / sample_stats).
+The reference reads it back with ``az.from_netcdf`` (run_age_mcmc_utils.py:434,
+run_age_mcmc.post_plots.comp.py:171, age_modeling_mcmc.post_plots.py:128).  ``to_netcdf``
+writes that file with h5lite (HDF5 written from the format specification; h5py / netCDF4 are
+not in this image): same groups, variable names, dims, dtypes, attributes, dimension scales
+and storage (one shuffle + deflate chunk per variable) as the shipped
+``conv_traces/*.netcdf``, which ``tests/test_trace_cpu.py`` reads and diffs against.
+
+Variable names follow the reference models: CE (noble_gas_mcmc.py:216-267) Ae_beta, F_beta,
+E_beta, m, b_beta, nu_ and the deterministics Ae, F (log10 values, as the model defines them:
+:229-230), E, b, T, nu; RTD (run_age_mcmc_utils.py:286-344) tau1, nu_, nu, J, tau2, f1, f2,
+tau, eta1, eta2, D1, D2, thalf_cfc_, thalf_cfc, lamsf6.  A model with both blocks prefixes the
+CE nu variables with ``ce_``.  Walkers are chains; a model of several wells (the reference
+writes one file per well) gets a trailing ``well`` dim.
 """
 import datetime
 import os
@@ -34,9 +40,13 @@ def _np(x):
     return x.detach().cpu().numpy() if hasattr(x, "detach") else np.asarray(x)
 
 
-def inference_data(res, spec, sampling_time=None, wells=None, library="noblegas_rtd_mcmc_amd"):
+LIBRARY_VERSION = "0.3"
+
+
+def inference_data(res, spec, sampling_time=None, wells=None, library="noblegas_rtd_mcmc_amd", observed=None):
     """Result of sampler.*DEMetropolisZ.run (samples [draw][P][L][chain]) -> dict with
-    'posterior' and 'sample_stats' ({name: (dims, array)}) and 'attrs'."""
+    'posterior' and 'sample_stats' ({name: (dims, array)}), 'observed' (the likelihood's
+    observations, az.from_pymc3's observed_data 'like'), 'attrs' and 'coords'."""
     s = _np(res["samples"])                                  # [draw, P, L, chain]
     D, P, L, W = s.shape
     by_role = {r: np.moveaxis(s[:, i], -1, 0) for i, r in enumerate(spec.roles)}   # [chain, draw, L]
@@ -83,66 +93,82 @@ def inference_data(res, spec, sampling_time=None, wells=None, library="noblegas_
     def per_chain(a):
         a = _np(a)
         return a.T if a.ndim == 2 else np.moveaxis(a, (2, 0, 1), (0, 1, 2))
-    lp = per_chain(res["logp"]).astype(np.float64)
+    # DEMetropolisZ's sample stats as az.from_pymc3 keeps them (the shipped traces'
+    # sample_stats: accept = exp(logp(x*) - logp(x)), accepted, lambda, scaling; 'tune' is
+    # dropped and DEMetropolisZ records no lp)
     acc = per_chain(res["accepted"]).astype(np.int8)
+    ar = res.get("accept")
+    ar = per_chain(ar).astype(np.float64) if ar is not None else np.full(acc.shape, np.nan)
 
     def tuned(v):        # final lamb / scaling per chain, [W] or [L][W]
         v = _np(v)
         v = v[:, None] if v.ndim == 1 else v.T[:, None, :]
-        return np.broadcast_to(v, lp.shape).astype(np.float64)
-    sd = ("chain", "draw") if lp.ndim == 2 else ("chain", "draw", "well")
-    stats = {"lp": (sd, lp), "accepted": (sd, acc), "tune": (sd, np.zeros_like(acc)),
-             "lambda": (sd, tuned(res["lamb"])), "scaling": (sd, tuned(res["scaling"]))}
-    if lp.ndim == 3 and L == 1:
+        return np.broadcast_to(v, acc.shape).astype(np.float64)
+    sd = ("chain", "draw") if acc.ndim == 2 else ("chain", "draw", "well")
+    stats = {"lambda": (sd, tuned(res["lamb"])), "accepted": (sd, acc), "accept": (sd, ar),
+             "scaling": (sd, tuned(res["scaling"]))}
+    if acc.ndim == 3 and L == 1:
         stats = {k: (("chain", "draw"), v[..., 0]) for k, (dims, v) in stats.items()}
     attrs = {"created_at": datetime.datetime.now(datetime.timezone.utc).isoformat(),
+             "arviz_version": "none (ArviZ 0.11.4 InferenceData layout, written by h5lite)",
              "inference_library": library,
+             "inference_library_version": LIBRARY_VERSION,
              "sampler": "DEMetropolisZ (pymc3 3.11.2 algorithm, device-resident)",
              "tuning_steps": int(res.get("tuning_steps", 0)),
              "sampling_time": float(sampling_time if sampling_time is not None else res.get("sampling_time", np.nan))}
     if wells is not None and L > 1:
         attrs["wells"] = ",".join(wells)
-    return {"posterior": post, "sample_stats": stats, "attrs": attrs,
+    obs = None if observed is None else np.asarray(observed, dtype=np.float64)
+    if obs is not None and obs.ndim == 2 and obs.shape[0] == 1:
+        obs = obs[0]
+    return {"posterior": post, "sample_stats": stats, "attrs": attrs, "observed": obs,
             "coords": {"chain": np.arange(W, dtype=np.int64), "draw": np.arange(D, dtype=np.int64),
                        "well": np.arange(L, dtype=np.int64)}}
 
 
 def to_netcdf(idata, path):
-    """Write the groups as <path>/<group>.nc (netCDF-3 classic, one file per group)."""
-    from scipy.io import netcdf_file
-    os.makedirs(path, exist_ok=True)
-    for group in ("posterior", "sample_stats"):
-        fn = os.path.join(path, group + ".nc")
-        with netcdf_file(fn, "w", version=2) as f:
-            for k, v in idata["attrs"].items():
-                setattr(f, k, v)
-            dims_used = set()
-            for dims, _ in idata[group].values():
-                dims_used.update(dims)
-            for d in ("chain", "draw", "well"):
-                if d in dims_used:
-                    f.createDimension(d, len(idata["coords"][d]))
-                    cv = f.createVariable(d, "i", (d,))
-                    cv[:] = idata["coords"][d].astype(np.int32)
-            for name, (dims, arr) in idata[group].items():
-                v = f.createVariable(name, "d" if arr.dtype.kind == "f" else "b", dims)
-                v[:] = arr
+    """Write ``idata`` as ONE netCDF-4 file at ``path`` (az.to_netcdf's layout)."""
+    from . import h5lite
+    attrs = idata["attrs"]
+    base = {k: attrs[k] for k in ("created_at", "arviz_version", "inference_library", "inference_library_version")}
+    run = dict(base, sampling_time=np.array([float(attrs["sampling_time"])]),
+               tuning_steps=np.array([int(attrs["tuning_steps"])], dtype=np.int64))
+    if "wells" in attrs:                  # several wells in one file (the reference: one file per well)
+        run["wells"] = attrs["wells"]
+    groups = {}
+    for gname in ("posterior", "sample_stats"):
+        g = idata[gname]
+        used = []
+        for dims, _ in g.values():
+            used += [d for d in dims if d not in used]
+        gv = {}
+        for name, (dims, arr) in g.items():
+            a = np.asarray(arr)
+            gv[name] = (dims, a, {"dtype": "bool"} if name == "accepted" else {})
+        groups[gname] = {"attrs": run, "dims": {d: idata["coords"][d].astype(np.int64) for d in used}, "vars": gv}
+    if idata.get("observed") is not None:
+        obs = np.asarray(idata["observed"], dtype=np.float64)
+        dims = tuple("like_dim_%d" % i for i in range(obs.ndim))
+        groups["observed_data"] = {"attrs": base, "dims": {d: np.arange(n, dtype=np.int64) for d, n in zip(dims, obs.shape)},
+                                   "vars": {"like": (dims, obs, {})}}
+    h5lite.write_netcdf4(path, groups)
     return path
 
 
 def from_netcdf(path):
-    """Read a trace written by to_netcdf back into the same dict layout."""
-    from scipy.io import netcdf_file
+    """Read a trace file (ours, or the reference's conv_traces/*.netcdf) into the dict layout
+    of ``inference_data``."""
+    from . import h5lite
+    f = h5lite.read_netcdf4(path)
     out = {"attrs": {}, "coords": {}}
-    for group in ("posterior", "sample_stats"):
-        with netcdf_file(os.path.join(path, group + ".nc"), "r", mmap=False) as f:
-            grp = {}
-            for name, v in f.variables.items():
-                if name in ("chain", "draw", "well"):
-                    out["coords"][name] = np.array(v[:])
-                    continue
-                grp[name] = (tuple(v.dimensions), np.array(v[:]))
-            out[group] = grp
-            for k, v in f._attributes.items():
-                out["attrs"][k] = v.decode() if isinstance(v, bytes) else v
+    for gname in ("posterior", "sample_stats", "observed_data"):
+        if gname not in f:
+            continue
+        g = f[gname]
+        for k, v in g["attrs"].items():
+            v = v[0] if isinstance(v, np.ndarray) and v.shape == (1,) else v
+            out["attrs"][k] = v.item() if isinstance(v, np.generic) else v
+        for d, c in g["dims"].items():
+            out["coords"][d] = c
+        out[gname] = {name: (dims, arr) for name, (dims, arr, _) in g["vars"].items()}
     return out

@@ -65,7 +65,7 @@ def test_device_demcz_matches_torch_bitwise(kind, per_well):
     tf = Transform.from_spec(spec) if spec.jacobian else None
     f = (lambda t: lp.units(t)) if per_well else (lambda t: lp(t))
     ref = DEMetropolisZ(f, transform=tf, per_well=per_well, **kw).run(x0, tune=12, draws=8)
-    for k in ("x", "lp", "samples", "logp", "accepted", "lamb", "scaling"):
+    for k in ("x", "lp", "samples", "logp", "accepted", "accept", "lamb", "scaling"):
         assert _same(dev[k], ref[k]), k
     assert 0 < int(dev["accepted"].sum()) < dev["accepted"].numel()
     lp.close()
@@ -103,7 +103,7 @@ def test_device_demcz_step_modes_bitwise(jac, per_well):
         os.environ.pop("NGRTD_DZ_MODE", None)
         os.environ.pop("NGRTD_DZ_CHUNK", None)
     for mode in ("pair", "chunk1", "chunk3"):
-        for k in ("x", "lp", "samples", "logp", "accepted", "lamb", "scaling"):
+        for k in ("x", "lp", "samples", "logp", "accepted", "accept", "lamb", "scaling"):
             assert _same(res[mode][k], res["fused"][k]), (mode, k)
     if jac:
         assert 0 < int(res["fused"]["accepted"].sum()) < res["fused"]["accepted"].numel()
@@ -131,7 +131,7 @@ def test_device_demcz_many_blocks_chunks_bitwise():
             res[ch] = DeviceDEMetropolisZ(lp, tune_interval=3, seed=5).run(x0, tune=4, draws=3)
     finally:
         os.environ.pop("NGRTD_DZ_CHUNK", None)
-    for k in ("x", "lp", "samples", "logp", "accepted", "lamb", "scaling"):
+    for k in ("x", "lp", "samples", "logp", "accepted", "accept", "lamb", "scaling"):
         assert _same(res["256"][k], res["1"][k]), k
     # the final state is the last draw, in the caller's layout
     assert _same(res["256"]["x"], res["256"]["samples"][-1])
@@ -194,7 +194,7 @@ def test_per_well_run_equals_single_well_runs():
         one = DeviceDEMetropolisZ(lpl, well0=l, **kw).run(x0[:, l:l + 1].contiguous(), tune=10, draws=6)
         assert torch.equal(one["x"][:, 0], full["x"][:, l]), l
         assert torch.equal(one["samples"][:, :, 0], full["samples"][:, :, l]), l
-        for k in ("logp", "accepted", "lp", "lamb", "scaling"):
+        for k in ("logp", "accepted", "accept", "lp", "lamb", "scaling"):
             assert torch.equal(one[k][..., 0, :] if one[k].dim() > 1 else one[k], full[k][..., l, :]), (l, k)
         lpl.close()
     # a walker-block shard of the L-well run
@@ -207,7 +207,7 @@ def test_per_well_run_equals_single_well_runs():
         pair = DeviceDEMetropolisZ(lp, **kw).run(x0, tune=10, draws=6)
     finally:
         os.environ.pop("NGRTD_DZ_MODE", None)
-    for k in ("x", "lp", "samples", "logp", "accepted", "lamb", "scaling"):
+    for k in ("x", "lp", "samples", "logp", "accepted", "accept", "lamb", "scaling"):
         assert _same(pair[k], full[k]), k
     assert 0 < int(full["accepted"].sum()) < full["accepted"].numel()
     lp.close()
@@ -236,7 +236,7 @@ def test_ragged_walker_major_sweep(L):
             kw = dict(tune_interval=3, seed=L + W, per_well=per_well)
             dev = DeviceDEMetropolisZ(lp, **kw).run(x0, tune=6, draws=4)
             ref = DEMetropolisZ(f, transform=tf, **kw).run(x0, tune=6, draws=4)
-            for k in ("x", "lp", "samples", "logp", "accepted", "lamb", "scaling"):
+            for k in ("x", "lp", "samples", "logp", "accepted", "accept", "lamb", "scaling"):
                 assert _same(dev[k], ref[k]), (L, W, per_well, k)
         lp.close()
 

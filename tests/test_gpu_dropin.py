@@ -210,7 +210,11 @@ def test_conv_mcmc_sample_writes_arviz_trace(tmp_path):
     assert m.trace_name.endswith("PLM1.CFC12.SF6.H3.He4_ter.exponential.1.netcdf")
     assert back["posterior"]["tau1"][1].shape == (12, 30) and "nu" in back["posterior"]
     assert back["attrs"]["tuning_steps"] == 60 and back["attrs"]["sampling_time"] > 0
-    assert np.array_equal(back["sample_stats"]["lp"][1], res["logp"][:, 0, :].T)   # per-well chains, 1 well
+    # ONE netCDF-4 file (az.to_netcdf's container), sample stats of per-well chains (1 well)
+    assert os.path.isfile(m.trace_name)
+    assert np.array_equal(back["sample_stats"]["accepted"][1], res["accepted"][:, 0, :].T)
+    assert np.array_equal(back["sample_stats"]["accept"][1], res["accept"][:, 0, :].T, equal_nan=True)
+    assert np.array_equal(back["observed_data"]["like"][1], m.build_mcmc_model_joint_sT().spec.rtd.obs[0])
 
 
 def _ref_summary(well):
@@ -228,27 +232,34 @@ def _ref_summary(well):
 
 def test_ce_posterior_matches_reference_summaries():
     """The CE model of PLM1, PLM6 and PLM7 (Ne, Ar, Kr, Xe; noble_gas_mcmc.py:216-267) sampled
-    with the device DEMetropolisZ as the reference samples it -- one chain per well (the
-    per-well chains of ONE 3-well plan), PyMC3's transformed space, tune 10 000 with
-    tune_interval 5000 -- against every row of the reference's summaries
-    (ng_opt{PLM1,PLM6,PLM7}.csv): the pooled posterior mean within
-    4 sqrt(mcse_ref^2 + mcse_build^2) and the sd within 4 sqrt(mcse_sd_ref^2 + mcse_sd_build^2),
-    mcse_build from the spread of the 1024 independent chains' means / sds (batch means with
-    one batch per chain).  PyMC3 is not installed here: this is the reference-held pin of the
-    sampler and of the transformed-space Jacobians (a statistical one; the draws themselves
-    are parity unpinned)."""
+    as the reference samples it (noble_gas_mcmc.py:408-415): DEMetropolisZ in PyMC3's
+    transformed space, one chain per well (the per-well chains of ONE 3-well plan), every
+    chain started at the model's test point (the prior means), tune 10 000 with
+    tune_interval 5000, then 50 000 draws.  Compared with every row of the reference's
+    summaries (ng_opt{PLM1,PLM6,PLM7}.csv, 4 such chains): the pooled mean within
+    4 sqrt(mcse_ref^2 + mcse_build^2), the pooled sd within 4 sqrt(mcse_sd_ref^2 +
+    mcse_sd_build^2), mcse_build by batch means over 16 groups of 32 independent chains.
+    The comparison is between two realisations of the same finite run: for Ae / F both
+    under-disperse the exact posterior by 5-20 % in sd (importance sampling from the prior,
+    tools/ce_posterior_check.py).  PyMC3 is not installed here: this is the
+    reference-held pin of the sampler and of the transformed-space Jacobians (statistical;
+    the draws themselves are parity unpinned)."""
     import torch
     from noblegas_rtd_mcmc_amd.noble_gas_mcmc import CEModel
     from noblegas_rtd_mcmc_amd.sampler import sample_model
-    from noblegas_rtd_mcmc_amd.workloads import field_data, sample_prior
+    from noblegas_rtd_mcmc_amd.workloads import field_data
     wells = ["PLM1", "PLM6", "PLM7"]
-    W, tune, draws = 1024, 10000, 4000
+    W, G, tune, draws, thin = 512, 16, 10000, 50000, 5
     m = CEModel(field_data()["obs"], wells, max_walkers=W)
-    x0 = torch.from_numpy(sample_prior(m.spec, W, np.random.default_rng(123423))).cuda()
+    c = m.spec.ce
+    # model.test_point: the Beta means and the Normal mean
+    tp = [c.beta_Ae[0] / sum(c.beta_Ae), c.beta_F[0] / sum(c.beta_F), c.beta_E[0] / sum(c.beta_E), c.m_mu,
+          c.beta_b[0] / sum(c.beta_b), c.beta_nu[0] / sum(c.beta_nu)]
+    x0 = torch.tensor(tp, dtype=torch.float64, device="cuda")[:, None, None].expand(6, len(wells), W).contiguous()
     res = sample_model(m.spec, W, 0, x0, tune, draws, seed=123423, tune_interval=5000)
     assert 0.05 < res["accept_rate"] < 0.9
-    s = res["samples"]                                    # [draws, 6, L, W] natural space
-    c = m.spec.ce
+    s = res["samples"][::thin]                            # [draws / thin, 6, L, W] natural space
+    del res
     Emin = torch.as_tensor(c.E_min, device=s.device)[:, None]
     v = {"m": s[:, 3], "Ae_beta": s[:, 0], "F_beta": s[:, 1], "E_beta": s[:, 2], "b_beta": s[:, 4], "nu_": s[:, 5]}
     v["Ae"] = 10 ** (v["Ae_beta"] * (c.logA_max - c.logA_min) + c.logA_min)
@@ -264,9 +275,9 @@ def test_ce_posterior_matches_reference_summaries():
         for name, r in ref.items():
             a = v[name][:, l, :]                          # [draws, chains]
             mean, sd = float(a.mean()), float(a.std())
-            cm, cs = a.mean(0), a.std(0)
-            mcse_m = float(cm.std()) / np.sqrt(W)
-            mcse_s = float(cs.std()) / np.sqrt(W)
+            grp = a.reshape(a.shape[0], G, W // G).permute(1, 0, 2).reshape(G, -1)
+            mcse_m = float(grp.mean(1).std()) / np.sqrt(G)
+            mcse_s = float(grp.std(1).std()) / np.sqrt(G)
             bm = 4 * np.hypot(r["mcse_mean"], mcse_m)
             bs = 4 * np.hypot(r["mcse_sd"], mcse_s)
             if not (abs(mean - r["mean"]) <= bm and abs(sd - r["sd"]) <= bs):

@@ -1,0 +1,141 @@
+"""The trace container (f4): the reference's runs are ONE netCDF-4 / HDF5 file each
+(az.to_netcdf, age_ens_runs_mcmc/run_age_mcmc_utils.py:425), read back by az.from_netcdf
+(:434, run_age_mcmc.post_plots.comp.py:171).  h5lite reads the reference's shipped
+conv_traces/*.netcdf (all 22 when /root/reference is present; the committed
+tests/golden/traces/PLM1.H3.exponential.0.netcdf always) and writes ours; the structure of our
+file is diffed against the frozen structure of
+conv_traces/PLM1.CFC12.SF6.H3.He4_ter.exponential.123.netcdf
+(tests/golden/make_trace_structure.py)."""
+import glob
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+REF = "/root/reference/age_ens_runs_mcmc/conv_traces"
+
+# sampling_time ranges per model family (s, all chains, tune included)
+RANGES = {"exponential.0": (67.0, 101.0), "exponential.123": (230.0, 241.0), "exp_pist_flow.123": (296.0, 324.0),
+          "exponential-piston.123": (401.0, 401.5), "exp_pist_flow-piston.123": (438.0, 494.0)}
+
+
+def _shipped():
+    paths = sorted(glob.glob(os.path.join(REF, "*.netcdf")))
+    return paths or [os.path.join(GOLD, "traces", "PLM1.H3.exponential.0.netcdf")]
+
+
+def test_lookup3_known_values():
+    """HDF5's metadata checksum (Jenkins lookup3 hashlittle, initval 0)."""
+    from noblegas_rtd_mcmc_amd.h5lite import lookup3
+    assert lookup3(b"") == 0xDEADBEEF
+    assert lookup3(b"Four score and seven years ago") == 0x17770551        # lookup3.c driver5
+    assert lookup3(b"Four score and seven years ago", 1) == 0xCD628161
+
+
+@pytest.mark.parametrize("path", _shipped(), ids=os.path.basename)
+def test_reader_decodes_shipped_trace(path):
+    """Every shipped trace decodes (superblock v2, dense link / attribute storage, chunked
+    shuffle + deflate datasets, global-heap DIMENSION_LIST): 3 chains x 10 000 draws per
+    posterior variable, finite, tau1 positive (the single-tracer runs of savenum 0 predate the
+    U(1, 1000) bounds of run_age_mcmc.py:145-146: their tau1 reaches 4400); accepted in {0, 1};
+    tuning_steps = 10 000 and sampling_time in SURVEY.md §6's range for its model."""
+    from noblegas_rtd_mcmc_amd import trace
+    t = trace.from_netcdf(path)
+    assert set(t) >= {"posterior", "sample_stats", "attrs", "coords"}
+    assert t["attrs"]["tuning_steps"] == 10000 and t["attrs"]["inference_library"] == "pymc3"
+    name = os.path.basename(path)
+    key = next(k for k in RANGES if name.endswith(k + ".netcdf") and not (k == "exponential.123" and "piston" in name))
+    lo, hi = RANGES[key]
+    assert lo <= t["attrs"]["sampling_time"] <= hi, (name, t["attrs"]["sampling_time"])
+    frozen = json.load(open(os.path.join(GOLD, "trace_attrs.json")))[name]
+    assert t["attrs"]["sampling_time"] == frozen["sampling_time"]
+    assert np.array_equal(t["coords"]["chain"], [0, 1, 2]) and np.array_equal(t["coords"]["draw"], np.arange(10000))
+    for v, (dims, a) in t["posterior"].items():
+        assert dims == ("chain", "draw") and a.shape == (3, 10000) and np.isfinite(a).all(), v
+    tau = t["posterior"]["tau1"][1]
+    assert (tau >= 1).all() and (tau <= 15000).all()
+    acc = t["sample_stats"]["accepted"][1]
+    assert set(np.unique(acc)) <= {0, 1} and 0 < acc.mean() < 1
+    assert set(t["sample_stats"]) == {"accept", "accepted", "lambda", "scaling"}
+
+
+def _norm(st):
+    """Structure without string lengths (values differ) and without the root provenance."""
+    s = json.loads(re.sub(r'"string\d+"', '"string"', json.dumps(st)))
+    s.pop("/", None)
+    return s
+
+
+def _our_trace(tmp_path, with_lp=False):
+    import torch
+    from noblegas_rtd_mcmc_amd import trace
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    from noblegas_rtd_mcmc_amd.spec import ModelSpec
+    base = wl.c4_spec(L=1, N=60, par_names=("tau1", "J", "thalf_cfc", "lamsf6"))
+    tr = [t for t in base.rtd.tracers if t.name in ("CFC12", "SF6", "H3", "He4_ter")]
+    import dataclasses
+    rtd = dataclasses.replace(base.rtd, tracers=tr, obs=base.rtd.obs[:, [0, 1, 2, 4]], sd=base.rtd.sd[:, [0, 1, 2, 4]])
+    spec = ModelSpec(n_wells=1, rtd=rtd)
+    D, W = 40, 3
+    rng = np.random.default_rng(3)
+    s = np.stack([wl.sample_prior(spec, W, rng) for _ in range(D)])
+    res = {"samples": torch.from_numpy(s), "logp": torch.from_numpy(rng.normal(size=(D, 1, W))),
+           "accepted": torch.from_numpy(rng.integers(0, 2, (D, 1, W)).astype(np.uint8)),
+           "accept": torch.from_numpy(rng.uniform(0, 2, (D, 1, W))),
+           "lamb": torch.full((1, W), 0.5, dtype=torch.float64), "scaling": torch.full((1, W), 1e-3, dtype=torch.float64),
+           "tuning_steps": 10000, "sampling_time": 12.5}
+    idata = trace.inference_data(res, spec, wells=["PLM1"], observed=spec.rtd.obs)
+    path = str(tmp_path / "PLM1.CFC12.SF6.H3.He4_ter.exponential.123.netcdf")
+    trace.to_netcdf(idata, path)
+    return idata, path
+
+
+def test_our_trace_structure_matches_reference(tmp_path):
+    """A trace of the same model (4 tracers, exponential, savenum 123: tau1, J, thalf_cfc,
+    lamsf6) written by trace.to_netcdf has the reference file's structure: groups, group
+    attributes, variables, dtypes, dimension names, per-variable attributes (netCDF's
+    _Netcdf4Dimid / _Netcdf4Coordinates, _FillValue, the dimension-scale CLASS / NAME /
+    REFERENCE_LIST, DIMENSION_LIST) and storage filters (shuffle, deflate)."""
+    from noblegas_rtd_mcmc_amd import h5lite
+    _, path = _our_trace(tmp_path)
+    ours = _norm(h5lite.structure(path))
+    ref = _norm(json.load(open(os.path.join(GOLD, "trace_structure_exponential_123.json"))))
+    assert set(ours) == set(ref)
+    for g in ref:
+        assert ours[g]["attrs"] == ref[g]["attrs"], g
+        assert set(ours[g]["vars"]) == set(ref[g]["vars"]), (g, set(ours[g]["vars"]) ^ set(ref[g]["vars"]))
+        for v in ref[g]["vars"]:
+            assert ours[g]["vars"][v] == ref[g]["vars"][v], (g, v, ours[g]["vars"][v], ref[g]["vars"][v])
+
+
+def test_our_trace_roundtrip(tmp_path):
+    """to_netcdf -> from_netcdf gives back every array bit for bit and the attributes."""
+    from noblegas_rtd_mcmc_amd import trace
+    idata, path = _our_trace(tmp_path)
+    back = trace.from_netcdf(path)
+    assert back["attrs"]["tuning_steps"] == 10000 and back["attrs"]["sampling_time"] == 12.5
+    for g in ("posterior", "sample_stats"):
+        assert set(back[g]) == set(idata[g])
+        for k, (dims, arr) in idata[g].items():
+            assert back[g][k][0] == dims and np.array_equal(back[g][k][1], arr), (g, k)
+    assert np.array_equal(back["observed_data"]["like"][1], idata["observed"])
+
+
+def test_writer_uncompressed_and_multiwell(tmp_path):
+    """Contiguous (unfiltered) datasets and a third (well) dimension read back as written."""
+    from noblegas_rtd_mcmc_amd import h5lite
+    groups = {"posterior": {"attrs": {"created_at": "x"},
+                            "dims": {"chain": np.arange(4), "draw": np.arange(7), "well": np.arange(3)},
+                            "vars": {"T": (("chain", "draw", "well"), np.random.default_rng(0).normal(size=(4, 7, 3)), {}),
+                                     "n": (("chain", "draw"), np.arange(28, dtype=np.int64).reshape(4, 7), {})}}}
+    p = str(tmp_path / "t.nc")
+    w = h5lite.H5Writer(compress=False)
+    h5lite.write_netcdf4(p, groups, compress=False)
+    back = h5lite.read_netcdf4(p)
+    for k, (dims, a, _) in groups["posterior"]["vars"].items():
+        d2, a2, _ = back["posterior"]["vars"][k]
+        assert d2 == dims and np.array_equal(a2, a)
+    assert w is not None
