@@ -3,7 +3,9 @@
 the single-launch step (NGRTD_DZ_DIAG selects timing-only variants, wrong results), and
 the plain log-prob on the state and on natural-space-noise proposals of it.  JSON line.
 
-    [NGRTD_DZ_DIAG=k] [DZ_JAC=1] python tools/dz_probe.py"""
+    [NGRTD_DZ_DIAG=k] [DZ_JAC=1] [DZ_PW=0] [DZ_MODEL=bmm|epm|epm_piston] python tools/dz_probe.py
+
+DZ_PW=0: one chain per walker over its wells (default: per-well chains)."""
 import json
 import os
 import sys
@@ -47,7 +49,9 @@ def main():
         spec = dataclasses.replace(spec, jacobian=True)
     x0 = torch.from_numpy(workloads.sample_prior(spec, W, np.random.default_rng(34568))).cuda()
     lp = LogProb(spec, max_walkers=W)
-    out = {"diag": os.environ.get("NGRTD_DZ_DIAG", "0"), "jacobian": jac, "model": model or "exponential"}
+    pw = os.environ.get("DZ_PW", "1") != "0"
+    out = {"diag": os.environ.get("NGRTD_DZ_DIAG", "0"), "jacobian": jac, "model": model or "exponential",
+           "per_well": pw}
     o = torch.empty(W, dtype=torch.float64, device="cuda")
     out["logp_state_us"] = ev_time(lp, lambda: lp(x0, out=o))
     g = torch.Generator(device="cuda").manual_seed(1)
@@ -58,7 +62,7 @@ def main():
     else:
         xn = (x0 + noise).contiguous()
     out["logp_noisy_us"] = ev_time(lp, lambda: lp(xn, out=o))
-    s = DeviceDEMetropolisZ(lp, seed=7, tune=None)
+    s = DeviceDEMetropolisZ(lp, seed=7, tune=None, per_well=pw)
     x, l, z = s.start(x0, 0, 400)
     lp.demcz(x, l, 10, z)
     # one launch runs K steps (NGRTD_DZ_CHUNK caps it): per-step time = launch time / K
