@@ -356,7 +356,8 @@ typedef struct {
      * its wells (0).  Per-well: every (walker w, well l) is a P-dimensional chain c = l W + w
      * with its own Metropolis decision, partners, lamb / scaling / n_acc_tune (PyMC3 default
      * lamb 2.38 / sqrt(2 P)); logp, lamb, scaling, n_acc_tune and the logs are [L][W] (the
-     * order of theta's rows); the history is unit-major [hist_cap][W][L][P]; random streams
+     * order of theta's rows); the history is unit-major [hist_cap][W][L][Ps], Ps = 4 ceil(P/4),
+     * row p of an entry at slot (p mod 2) Ps/2 + p div 2 (even rows, then odd rows); streams
      * are keyed by cid = (well0 + l) n_chains_total + chain0 + w, so a run of all L wells
      * equals L runs of one well each (well0 = l) chain for chain. */
     int32_t per_well;

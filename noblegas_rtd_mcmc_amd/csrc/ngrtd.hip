@@ -115,6 +115,7 @@ struct ngrtd_plan {
     DevBuf conc, ulogp, theta_stage, out_stage, ce_stage;
     DevBuf demc_prop[2], demc_lp, demc_acc, demc_cnt;   // ngrtd_demcz_run scratch
     DevBuf demc_xw[2];      // the multi-step launch's walker-major state [P][W][L] (natural, transformed)
+    DevBuf demc_pw;         // ... and per-well chains' lp, lamb, scaling [W][L] f64 + n_acc_tune [W][L] i32
 
     RtdArgs rtd{};
     UnitArgs unit{};
@@ -1716,9 +1717,27 @@ int ngrtd_demcz_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64
         if (tr) hipLaunchKernelGGL(dz_layout_kernel, g, dim3(256), 0, st, z->theta_u, xw[1], (int64_t)Lw, W);
         HIP_TRY(ctx, hipGetLastError());
     }
+    // per-well chains: their lp / lamb / scaling / tuning counters walker-major too ([W][L],
+    // the launch's unit order) for the whole call, so a wave's per-chain loads and stores are
+    // contiguous runs; the logs stay [n][L][W]
+    double* cl = logp;
+    double* clamb = z->lamb;
+    double* cscal = z->scaling;
+    int32_t* cnat = z->n_acc_tune;
+    const dim3 g1((unsigned)cdiv(W, 32), (unsigned)cdiv(Lw, 32), 1u), g1b((unsigned)cdiv(Lw, 32), (unsigned)cdiv(W, 32), 1u);
+    if (dzm >= 0 && pw) {
+        HIP_TRY(ctx, p->demc_pw.ensure((size_t)U * (3 * sizeof(double) + sizeof(int32_t))));
+        cl = p->demc_pw.d(); clamb = cl + U; cscal = clamb + U;
+        cnat = reinterpret_cast<int32_t*>(cscal + U);
+        hipLaunchKernelGGL(dz_layout_kernel, g1, dim3(256), 0, st, logp, cl, (int64_t)Lw, W);
+        hipLaunchKernelGGL(dz_layout_kernel, g1, dim3(256), 0, st, z->lamb, clamb, (int64_t)Lw, W);
+        hipLaunchKernelGGL(dz_layout_kernel, g1, dim3(256), 0, st, z->scaling, cscal, (int64_t)Lw, W);
+        hipLaunchKernelGGL(dz_layout_i32_kernel, g1, dim3(256), 0, st, z->n_acc_tune, cnat, (int64_t)Lw, W);
+        HIP_TRY(ctx, hipGetLastError());
+    }
     for (int64_t j = 0; dzm >= 0 && j < n_steps;) {
         const int64_t k = std::min(chunk, n_steps - j);
-        DemcAccept da{logp, acc, cnt, xw[0], nullptr, p->desc.n_params, 0, z->n_acc_tune, z->lamb, z->scaling,
+        DemcAccept da{cl, acc, cnt, xw[0], nullptr, p->desc.n_params, 0, cnat, clamb, cscal,
                       0, z->tune_target, z->tune_interval, accepted_log ? accepted_log + j * NC : nullptr,
                       logp_log ? logp_log + j * NC : nullptr, z->chain0, tr ? xw[1] : nullptr, nullptr};
         da.per_well = pw ? 1 : 0; da.well0 = z->well0;
@@ -1749,6 +1768,12 @@ int ngrtd_demcz_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64
         const dim3 g((unsigned)cdiv(Lw, 32), (unsigned)cdiv(W, 32), (unsigned)p->desc.n_params);
         hipLaunchKernelGGL(dz_layout_kernel, g, dim3(256), 0, st, xw[0], theta, W, (int64_t)Lw);
         if (tr) hipLaunchKernelGGL(dz_layout_kernel, g, dim3(256), 0, st, xw[1], z->theta_u, W, (int64_t)Lw);
+        if (pw) {
+            hipLaunchKernelGGL(dz_layout_kernel, g1b, dim3(256), 0, st, cl, logp, W, (int64_t)Lw);
+            hipLaunchKernelGGL(dz_layout_kernel, g1b, dim3(256), 0, st, clamb, z->lamb, W, (int64_t)Lw);
+            hipLaunchKernelGGL(dz_layout_kernel, g1b, dim3(256), 0, st, cscal, z->scaling, W, (int64_t)Lw);
+            hipLaunchKernelGGL(dz_layout_i32_kernel, g1b, dim3(256), 0, st, cnat, z->n_acc_tune, W, (int64_t)Lw);
+        }
         HIP_TRY(ctx, hipGetLastError());
     }
     for (int64_t j = 0; dzm < 0 && j < n_steps; ++j) {

@@ -1021,17 +1021,24 @@ __host__ __device__ __forceinline__ double pymc3_tune(double scale, double acc_r
 // acceptance rate, counter reset).  Returns the decision.
 // Chain index w of the per-chain arrays, random-stream id rid (joint chains: chain0 + w;
 // per-well chains: the unit's cid, dz_cid).
+// The acceptances of the calling lanes, counted with ONE atomic per wave (an integer count:
+// order-independent; one atomic per accepted per-well chain serialised ~10^5 atomics on one
+// address per step).
+__device__ __forceinline__ void count_accepts(unsigned long long* n, bool acc) {
+    const unsigned long long act = __ballot(1), m = __ballot(acc);
+    if (m && (int)__lane_id() == __ffsll((long long)act) - 1) atomicAdd(n, (unsigned long long)__popcll(m));
+}
+// li: the chain's index in the logs (log_off + li), which may differ from w (per-well chains
+// in the multi-step launch keep their state arrays walker-major).
 __device__ __forceinline__ bool demc_decide(const DemcAccept& d, int64_t w, uint64_t rid, double lp_prop,
-                                            uint64_t key, int32_t tune_now, int64_t log_off) {
+                                            uint64_t key, int32_t tune_now, int64_t log_off, int64_t li) {
     const double cur = d.lp[w];
     const double logu = log(rng_unit(rng_mix(rng_mix(key + 3) + rid)));
     const double mr = lp_prop - cur;
     const bool acc = __builtin_isfinite(mr) && logu < mr;
     d.acc[w] = acc;
-    if (acc) {
-        d.lp[w] = lp_prop;
-        atomicAdd(d.n_acc, 1ull);     // integer count: order-independent
-    }
+    if (acc) d.lp[w] = lp_prop;
+    count_accepts(d.n_acc, acc);
     if (d.n_acc_tune) {
         int32_t na = d.n_acc_tune[w] + (acc ? 1 : 0);
         if (tune_now) {
@@ -1042,10 +1049,14 @@ __device__ __forceinline__ bool demc_decide(const DemcAccept& d, int64_t w, uint
         }
         d.n_acc_tune[w] = na;
     }
-    if (d.acc_log) d.acc_log[log_off + w] = (uint8_t)acc;
-    if (d.lp_log) d.lp_log[log_off + w] = acc ? lp_prop : cur;
-    if (d.ar_log) d.ar_log[log_off + w] = exp(mr);
+    if (d.acc_log) d.acc_log[log_off + li] = (uint8_t)acc;
+    if (d.lp_log) d.lp_log[log_off + li] = acc ? lp_prop : cur;
+    if (d.ar_log) d.ar_log[log_off + li] = exp(mr);
     return acc;
+}
+__device__ __forceinline__ bool demc_decide(const DemcAccept& d, int64_t w, uint64_t rid, double lp_prop,
+                                            uint64_t key, int32_t tune_now, int64_t log_off) {
+    return demc_decide(d, w, rid, lp_prop, key, tune_now, log_off, w);
 }
 __device__ __forceinline__ bool demc_decide(const DemcAccept& d, int64_t w, double lp_prop, uint64_t key,
                                             int32_t tune_now, int64_t log_off) {
@@ -1059,6 +1070,11 @@ __device__ __forceinline__ bool demc_decide(const DemcAccept& d, int64_t w, doub
 __host__ __device__ __forceinline__ uint64_t dz_cid(int64_t well0, int64_t l, int64_t Wg, int64_t chain0, int64_t w) {
     return (uint64_t)(well0 + l) * (uint64_t)Wg + (uint64_t)(chain0 + w);
 }
+// Per-well history entry of one unit: Ps = 4 ceil(P / 4) doubles; row p at slot
+// pw_slot(p) = (p mod 2) Ps/2 + p div 2 -- the even rows (staged by the theta waves) then the
+// odd rows (RTD waves), each group 16-B aligned.
+__host__ __device__ __forceinline__ int pw_stride(int P) { return 4 * ((P + 3) / 4); }
+__host__ __device__ __forceinline__ int pw_slot(int p, int P) { return (p & 1) * (pw_stride(P) / 2) + (p >> 1); }
 // ... and the noise element of its parameter row p (rows of one chain are contiguous)
 constexpr int kPwRowStride = 32;   // >= NGRTD_ROLE_COUNT
 __host__ __device__ __forceinline__ uint64_t dz_pw_elem(uint64_t cid, int p) {
@@ -1220,15 +1236,16 @@ NGRTD_KLINK __global__ void __launch_bounds__(kZThreads) demcz_propose_kernel(co
 }
 
 // out[p][b][a] = in[p][a][b] for p < P (a < A, b < B): the caller's [P][L][W] state into the
-// multi-step DEMetropolisZ launch's walker-major [P][W][L] and back.  32 x 32 LDS tiles.
-NGRTD_KLINK __global__ void __launch_bounds__(256) dz_layout_kernel(const double* __restrict__ in,
-                                                                    double* __restrict__ out, int64_t A, int64_t B) {
-    __shared__ double t[32][33];
+// multi-step DEMetropolisZ launch's walker-major [P][W][L] and back (and, per-well chains,
+// the per-chain arrays [L][W] <-> [W][L]).  32 x 32 LDS tiles.
+template <class T>
+__device__ __forceinline__ void dz_layout_body(T (*t)[33], const T* __restrict__ in, T* __restrict__ out, int64_t A,
+                                               int64_t B) {
     const int64_t p = blockIdx.z;
     const int64_t a0 = (int64_t)blockIdx.y * 32, b0 = (int64_t)blockIdx.x * 32;
     const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-    const double* src = in + p * A * B;
-    double* dst = out + p * A * B;
+    const T* src = in + p * A * B;
+    T* dst = out + p * A * B;
 #pragma unroll
     for (int k = 0; k < 32; k += 8) {
         const int64_t a = a0 + ty + k, b = b0 + tx;
@@ -1240,6 +1257,16 @@ NGRTD_KLINK __global__ void __launch_bounds__(256) dz_layout_kernel(const double
         const int64_t b = b0 + ty + k, a = a0 + tx;
         if (a < A && b < B) dst[b * A + a] = t[tx][ty + k];
     }
+}
+NGRTD_KLINK __global__ void __launch_bounds__(256) dz_layout_kernel(const double* __restrict__ in,
+                                                                    double* __restrict__ out, int64_t A, int64_t B) {
+    __shared__ double t[32][33];
+    dz_layout_body<double>(t, in, out, A, B);
+}
+NGRTD_KLINK __global__ void __launch_bounds__(256) dz_layout_i32_kernel(const int32_t* __restrict__ in,
+                                                                        int32_t* __restrict__ out, int64_t A, int64_t B) {
+    __shared__ int32_t t[32][33];
+    dz_layout_body<int32_t>(t, in, out, A, B);
 }
 
 constexpr int kDzMaxP = 12;          // parameter rows of a single-launch DEMetropolisZ step
@@ -1265,8 +1292,8 @@ __device__ __forceinline__ double dz_value(const DemcAccept& d, bool de, double 
 // Per-well chains (DemczArgs::per_well), the proposal step of plans without a single-launch
 // instance: one thread per unit c = l W + w (theta's [L][W] order: the state / proposal
 // rows [P][L][W] are read and written coalesced), partners and random numbers of the unit's
-// own stream (dz_cid), history entries = P contiguous doubles of the unit-major history
-// [cap][W][L][P].  The arithmetic of dz_stage's per-well branch (bitwise).
+// own stream (dz_cid), history entries = pw_stride(P) doubles of the unit-major history
+// [cap][W][L][Ps] (rows at pw_slot).  The arithmetic of dz_stage's per-well branch (bitwise).
 NGRTD_KLINK __global__ void __launch_bounds__(256) demcz_propose_pw_kernel(const DemczArgs d) {
     const int64_t W = d.W, U = d.W * d.L;
     const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -1274,11 +1301,14 @@ NGRTD_KLINK __global__ void __launch_bounds__(256) demcz_propose_pw_kernel(const
     const int64_t l = c / W, w = c % W;
     const int P = d.P;
     const uint64_t cid = dz_cid(d.well0, l, d.Wg, d.chain0, w);
-    const size_t entry = (size_t)U * P, slot = ((size_t)w * d.L + l) * P;
+    const int Ps = pw_stride(P);
+    const size_t entry = (size_t)U * Ps, base = ((size_t)w * d.L + l) * Ps;
+    int sl[kRoleCount];
+    for (int p = 0; p < P; ++p) sl[p] = pw_slot(p, P);
     double x[kRoleCount];
     for (int p = 0; p < P; ++p) x[p] = d.x[(int64_t)p * U + c];
     if (d.append_at >= 0)
-        for (int p = 0; p < P; ++p) d.hist[(size_t)d.append_at * entry + slot + p] = x[p];
+        for (int p = 0; p < P; ++p) d.hist[(size_t)d.append_at * entry + base + sl[p]] = x[p];
     if (!d.propose) return;
     const bool de = d.it > 1;
     int64_t e1 = -1, e2 = -1;
@@ -1293,8 +1323,8 @@ NGRTD_KLINK __global__ void __launch_bounds__(256) demcz_propose_pw_kernel(const
     const double lamb = d.lamb[c], sc = d.scaling[c];
     const uint64_t ke = rng_mix(d.key + 2);
     for (int p = 0; p < P; ++p) {
-        const double z1 = de ? (c1 ? x[p] : d.hist[(size_t)e1 * entry + slot + p]) : 0.0;
-        const double z2 = de ? (c2 ? x[p] : d.hist[(size_t)e2 * entry + slot + p]) : 0.0;
+        const double z1 = de ? (c1 ? x[p] : d.hist[(size_t)e1 * entry + base + sl[p]]) : 0.0;
+        const double z2 = de ? (c2 ? x[p] : d.hist[(size_t)e2 * entry + base + sl[p]]) : 0.0;
         const double v = dz_value_e(d, de, x[p], z1, z2, lamb, sc, ke, dz_pw_elem(cid, p), (int64_t)p * d.L + l);
         d.prop[(int64_t)p * U + c] = v;
         if (d.prop_x) d.prop_x[(int64_t)p * U + c] = pymc3_backward(d.tr_kind[p], d.tr_a[p], d.tr_b[p], v);
@@ -1336,12 +1366,13 @@ __device__ __forceinline__ void dz_partners(const DemcAccept& d, const DzStep& s
 // back from an LDS copy instead of d.dz_prop was slower: the extra uniform row indices
 // spilled SGPRs into the unit body.)
 // PW (per-well chains, DemcAccept::per_well): the unit is the chain -- partners, lamb /
-// scaling and random numbers of its own (dz_cid), history entry = its P contiguous rows of
-// the unit-major history [cap][W][L][P].
+// scaling (walker-major scratch copies [W][L] inside the call) and random numbers of its own
+// (dz_cid); its history entry is Ps = pw_stride(P) contiguous doubles of the unit-major
+// history [cap][W][L][Ps] with the rows of each staging role adjacent (pw_slot): this lane
+// reads its role's rows of a partner as 16-B loads.
 template <int PMAX, bool TR, bool PW = false>
 __device__ __forceinline__ void dz_stage(const DemcAccept& d, const DzStep& sj, int64_t U, int64_t u, int i, int64_t w,
                                          int l, int L, int64_t W, bool valid, double* th, int p0, double* pl) {
-    const int64_t R = (int64_t)d.P * L;
     if (!valid || (d.dz_diag & 8)) return;
     if (d.dz_diag & 1) {   // timing diagnostics: the proposal is the state (no partners, no noise)
         for (int p = p0; p < d.P; p += 2)
@@ -1360,32 +1391,51 @@ __device__ __forceinline__ void dz_stage(const DemcAccept& d, const DzStep& sj, 
     }
     if (d.dz_diag & 16) e1 = e2 = -1;   // timing diagnostics: no partner loads (noise only)
     const bool de = e1 >= 0;
-    // row p of entry e: joint chains at (e W + w) R + p L + l, per-well at (e W + w) R + l P + p
-    const int64_t roff = PW ? (int64_t)l * d.P : l, rst = PW ? 1 : L;
-    const double* z1 = d.hist + ((size_t)(de ? e1 : 0) * W + w) * R + roff;
-    const double* z2 = d.hist + ((size_t)(de ? e2 : 0) * W + w) * R + roff;
-    const int64_t ci = PW ? (int64_t)l * W + w : w;   // per-chain arrays: [L][W] per-well, [W] joint
-    const double lamb = d.lamb[ci], sc = d.scaling[ci];
     constexpr int KMAX = (PMAX + 1) / 2;
     double x[KMAX], a1[KMAX], a2[KMAX];
+    // joint chains: row p of entry e at (e W + w) R + p L + l (R = P L); per-well chains: slot
+    // pw_slot(p) of the unit's entry ((e W + w) L + l) Ps
+    const int Ps = pw_stride(d.P), half = Ps / 2;
+    const int64_t ent = PW ? (int64_t)L * Ps : (int64_t)d.P * L;          // doubles per chain entry
+    const int64_t roff = PW ? (int64_t)l * Ps + p0 * half : l, rst = PW ? 1 : L;
+    const double* z1 = d.hist + ((size_t)(de ? e1 : 0) * W + w) * ent + roff;
+    const double* z2 = d.hist + ((size_t)(de ? e2 : 0) * W + w) * ent + roff;
+    const int64_t ci = PW ? w * (int64_t)L + l : w;   // per-chain arrays: walker-major [W][L] / [W]
+    const double lamb = d.lamb[ci], sc = d.scaling[ci];
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
         const int p = p0 + 2 * k;
-        if (p < d.P) {
-            x[k] = d.zx[(int64_t)p * U + u];
-            a1[k] = de ? z1[(int64_t)p * rst] : 0.0;
-            a2[k] = de ? z2[(int64_t)p * rst] : 0.0;
+        if (p < d.P) x[k] = d.zx[(int64_t)p * U + u];
+    }
+    if (PW) {       // this role's rows of each partner: adjacent slots, 16-B aligned (half even)
+#pragma unroll
+        for (int k = 0; k < KMAX; k += 2) {
+            if (p0 + 2 * k < d.P) {
+                const double2 v1 = de ? *reinterpret_cast<const double2*>(z1 + k) : double2{0.0, 0.0};
+                const double2 v2 = de ? *reinterpret_cast<const double2*>(z2 + k) : double2{0.0, 0.0};
+                a1[k] = v1.x; a2[k] = v2.x;
+                if (k + 1 < KMAX) { a1[k + 1] = v1.y; a2[k + 1] = v2.y; }
+            }
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k) {
+            const int p = p0 + 2 * k;
+            if (p < d.P) {
+                a1[k] = de ? z1[(int64_t)p * rst] : 0.0;
+                a2[k] = de ? z2[(int64_t)p * rst] : 0.0;
+            }
         }
     }
     // an entry appended in this launch is the state itself (as demcz_propose_kernel)
     const bool c1 = e1 == sj.at, c2 = e2 == sj.at;
-    double* hrow = d.hist + ((size_t)(sj.at < 0 ? 0 : sj.at) * W + w) * R + roff;
+    double* hrow = d.hist + ((size_t)(sj.at < 0 ? 0 : sj.at) * W + w) * ent + roff;
     const uint64_t ke = rng_mix(sj.key + 2);
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
         const int p = p0 + 2 * k;
         if (p < d.P) {
-            if (sj.at >= 0 && !(d.dz_diag & 2)) hrow[(int64_t)p * rst] = x[k];
+            if (sj.at >= 0 && !(d.dz_diag & 2)) hrow[PW ? k : (int64_t)p * rst] = x[k];
             const uint64_t el = PW ? dz_pw_elem(cid, p) : (uint64_t)((int64_t)p * L + l) * (uint64_t)d.Wg +
                                                           (uint64_t)(d.chain0 + w);
             double v = dz_value_e(d, de, x[k], c1 ? x[k] : a1[k], c2 ? x[k] : a2[k], lamb, sc, ke, el,
@@ -1941,8 +1991,8 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         if (PW) {   // per-well chains: the unit's own Metropolis decision (its theta lane)
             if (do_theta && mvalid) {
                 const int64_t wq = w0 + mwl;
-                dec[mi] = demc_decide(dk, (int64_t)ml * W + wq, dz_cid(dk.well0, ml, dk.Wg, dk.chain0, wq), part[pi],
-                                      sj.key, sj.tune_now, (int64_t)js * uk.U);
+                dec[mi] = demc_decide(dk, wq * (int64_t)L + ml, dz_cid(dk.well0, ml, dk.Wg, dk.chain0, wq), part[pi],
+                                      sj.key, sj.tune_now, (int64_t)js * uk.U, (int64_t)ml * W + wq);
             }
         } else if (WB <= 64 && (WB & (WB - 1)) == 0) {
             if (wave == 0) {

@@ -191,6 +191,16 @@ def pw_cid(well0, L, Wg, chain0, W, device):
 PW_ROW_STRIDE = 32      # = ngrtd_kernels.hpp kPwRowStride: noise element cid * 32 + p
 
 
+def pw_stride(P):
+    """Doubles per per-well history entry (ngrtd_kernels.hpp pw_stride): 4 ceil(P / 4)."""
+    return 4 * ((P + 3) // 4)
+
+
+def pw_slot(p, P):
+    """Slot of row p in a per-well history entry: the even rows, then the odd rows."""
+    return (p & 1) * (pw_stride(P) // 2) + (p >> 1)
+
+
 class DEMetropolisZ:
     """PyMC3 DEMetropolisZ for the W chains of x0 [..., W] on torch ops (any device).
 
@@ -388,7 +398,11 @@ class ZState:
         self.lamb = torch.full(shp, float(lamb), dtype=torch.float64, device=device)
         self.scaling = torch.full(shp, float(scaling), dtype=torch.float64, device=device)
         self.n_acc_tune = torch.zeros(shp, dtype=torch.int32, device=device)
-        self.hist = torch.empty((int(hist_cap), W, self.R), dtype=torch.float64, device=device)
+        # per-well chains: unit-major entries of pw_stride(P) doubles (row p at pw_slot(p))
+        self.P = self.R // self.L
+        self.Ps = pw_stride(self.P)
+        ent = self.L * self.Ps if self.per_well else self.R
+        self.hist = torch.empty((int(hist_cap), W, ent), dtype=torch.float64, device=device)
         self.u = None                     # transformed-space chains (set by DeviceDEMetropolisZ.start)
         self.S = (None if S is None else
                   torch.as_tensor(S, dtype=torch.float64).reshape(self.R).contiguous().to(device))
@@ -405,8 +419,9 @@ class ZState:
         """History entries [lo, hi) as [hi - lo][R][W] (per-well chains: [hi - lo][P][L][W],
         from the unit-major [cap][W][L][P] history)."""
         if self.per_well:
-            P = self.R // self.L
-            return self.hist[lo:hi].reshape(hi - lo, self.W, self.L, P).permute(0, 3, 2, 1)
+            sl = torch.tensor([pw_slot(p, self.P) for p in range(self.P)], device=self.hist.device)
+            h = self.hist[lo:hi].reshape(hi - lo, self.W, self.L, self.Ps).index_select(3, sl)
+            return h.permute(0, 3, 2, 1)
         return self.hist[lo:hi].permute(0, 2, 1)
 
 
