@@ -354,12 +354,14 @@ typedef struct {
      * per well (age_ens_runs_mcmc/run_age_mcmc.py:122-231 loops `for ww in wells`;
      * ng_interp/noble_gas_mcmc.py:95-104 runs one well) -- or one chain per walker over all
      * its wells (0).  Per-well: every (walker w, well l) is a P-dimensional chain c = l W + w
-     * with its own Metropolis decision, partners, lamb / scaling / n_acc_tune (PyMC3 default
-     * lamb 2.38 / sqrt(2 P)); logp, lamb, scaling, n_acc_tune and the logs are [L][W] (the
-     * order of theta's rows); the history is unit-major [hist_cap][W][L][Ps], Ps = 4 ceil(P/4),
-     * row p of an entry at slot (p mod 2) Ps/2 + p div 2 (even rows, then odd rows); streams
-     * are keyed by cid = (well0 + l) n_chains_total + chain0 + w, so a run of all L wells
-     * equals L runs of one well each (well0 = l) chain for chain. */
+     * with its own Metropolis decision, lamb / scaling / n_acc_tune (PyMC3 default lamb
+     * 2.38 / sqrt(2 P)); logp, lamb, scaling, n_acc_tune and the logs are [L][W] (the order
+     * of theta's rows).  The proposal noise and the accept draw of a unit are keyed by
+     * cid = (well0 + l) n_chains_total + chain0 + w; the history partner indices by the
+     * walker chain0 + w (the wells of a walker draw the same indices, each into its own
+     * history, which keeps the joint chains' history layout and its 512-B loads; every
+     * well's chain is still exactly a DEMetropolisZ chain).  So a run of all L wells equals
+     * L runs of one well each (well0 = l) chain for chain. */
     int32_t per_well;
     int32_t reserved0;
     int64_t well0;           /* global index of well 0 (per-well streams) */

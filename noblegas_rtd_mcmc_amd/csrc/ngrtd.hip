@@ -271,7 +271,6 @@ static double cheb_build(const std::vector<std::vector<double>>& cols, int C, do
             if (!(v >= 0.0) || !std::isfinite(v)) return HUGE_VAL;
     const long double PI = 3.14159265358979323846264338327950288L;
     const long double dd = d01;
-    std::vector<long double> f(n), ch(n);
     // power-basis coefficients of T_j: T_0 = 1, T_1 = x, T_{j+1} = 2x T_j - T_{j-1} (exact)
     std::vector<std::vector<long double>> Tm(n, std::vector<long double>(n, 0.0L));
     Tm[0][0] = 1.0L;
@@ -279,64 +278,78 @@ static double cheb_build(const std::vector<std::vector<double>>& cols, int C, do
     for (int j = 2; j < n; ++j)
         for (int k = 0; k < n; ++k)
             Tm[j][k] = (k > 0 ? 2.0L * Tm[j - 1][k - 1] : 0.0L) - Tm[j - 2][k];
-    for (int p = p_lo; p < p_hi; ++p) {
-        for (int c = 0; c <= C; ++c) {
-            const std::vector<double>& col = cols[c < C ? c : 0];
-            for (int k = 0; k < n; ++k) {
-                const long double xk = cosl(PI * (k + 0.5L) / n);
-                long double sv;
+    long double cs[kChebN][kChebN], xn[kChebN];   // cos(pi j (k + 1/2) / n), the nodes
+    for (int k = 0; k < n; ++k) {
+        xn[k] = cosl(PI * (k + 0.5L) / n);
+        for (int j = 0; j < n; ++j) cs[j][k] = cosl(PI * j * (k + 0.5L) / n);
+    }
+    // pieces split over host threads: fit, then validate (each piece's own coefficients)
+    std::vector<double> worst_t(64, 0.0);
+    auto work = [&](int t, int nt) {
+        std::vector<long double> f(n), ch(n);
+        double worst = 0.0;
+        for (int p = p_lo + t; p < p_hi; p += nt) {
+            for (int c = 0; c <= C; ++c) {
+                const std::vector<double>& col = cols[c < C ? c : 0];
+                for (int k = 0; k < n; ++k) {
+                    long double sv;
+                    if (p < kChebBinPieces) {
+                        const int e = kChebOct0 + p / kChebSub, j = p % kChebSub;
+                        sv = 1.0L / ldexpl(1.125L + 0.25L * j + xn[k] / 8.0L, e);
+                    } else {
+                        sv = 0.5L * (long double)kChebSHi * (1.0L + xn[k]);
+                    }
+                    f[k] = cheb_exact(col, sv, dd, c == C);
+                }
+                for (int j = 0; j < n; ++j) {
+                    long double acc = 0.0L;
+                    for (int k = 0; k < n; ++k) acc += f[k] * cs[j][k];
+                    ch[j] = acc * (j == 0 ? 1.0L : 2.0L) / n;
+                }
+                // Chebyshev -> monomial coefficients in the piece's local x (long double): the
+                // kernel evaluates one FMA per coefficient by Horner.  The coefficients decay
+                // like rho^-j with rho ~ 25 (the strip |Im log tau| < pi/2 over half-width 1/8),
+                // far above 1 + sqrt 2, so the monomial form amplifies rounding by ~1.1 only.
+                for (int k = 0; k < n; ++k) {
+                    long double m = 0.0L;
+                    for (int j = k; j < n; ++j) m += ch[j] * Tm[j][k];
+                    coef[((size_t)p * n + k) * CP + c] = (double)m;
+                }
+            }
+            const int M = 24;
+            for (int i = 0; i <= M + 1; ++i) {
+                double tau;
                 if (p < kChebBinPieces) {
                     const int e = kChebOct0 + p / kChebSub, j = p % kChebSub;
-                    sv = 1.0L / ldexpl(1.125L + 0.25L * j + xk / 8.0L, e);
+                    const long double tt = (i == 0) ? 0.0L : (i == M + 1) ? 1.0L - 1e-12L : (i - 0.5L) / M;
+                    tau = (double)ldexpl(1.0L + 0.25L * (j + tt), e);
                 } else {
-                    sv = 0.5L * (long double)kChebSHi * (1.0L + xk);
+                    const long double sv = (long double)kChebSHi * (i / (long double)(M + 1));
+                    tau = (sv == 0.0L) ? HUGE_VAL : (double)(1.0L / sv);
                 }
-                f[k] = cheb_exact(col, sv, dd, c == C);
-            }
-            for (int j = 0; j < n; ++j) {
-                long double acc = 0.0L;
-                for (int k = 0; k < n; ++k) acc += f[k] * cosl(PI * j * (k + 0.5L) / n);
-                acc *= 2.0L / n;
-                if (j == 0) acc *= 0.5L;
-                ch[j] = acc;
-            }
-            // Chebyshev -> monomial coefficients in the piece's local x (long double): the
-            // kernel evaluates one FMA per coefficient by Horner.  The coefficients decay
-            // like rho^-j with rho ~ 25 (the strip |Im log tau| < pi/2 over half-width 1/8),
-            // far above 1 + sqrt 2, so the monomial form amplifies rounding by ~1.1 only.
-            for (int k = 0; k < n; ++k) {
-                long double m = 0.0L;
-                for (int j = k; j < n; ++j) m += ch[j] * Tm[j][k];
-                coef[((size_t)p * n + k) * CP + c] = (double)m;
+                double x = 0.0;
+                const int pp = cheb_piece(tau, x);
+                if (pp != p) { worst = HUGE_VAL; continue; }
+                const long double sv = 1.0L / (long double)tau;
+                for (int c = 0; c <= C; ++c) {
+                    double y = 0.0;
+                    cheb_sums<1>(coef.data() + (size_t)pp * n * CP + c, CP, x, &y);
+                    const long double ex = cheb_exact(cols[c < C ? c : 0], sv, dd, c == C);
+                    const double e = (ex > 0) ? (double)(fabsl((long double)y - ex) / ex) : (y == 0.0 ? 0.0 : HUGE_VAL);
+                    if (!(e <= worst)) worst = e;   // NaN -> worst = NaN
+                }
             }
         }
-    }
+        worst_t[t] = worst;
+    };
+    const int nt = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(work, t, nt);
+    work(0, nt);
+    for (auto& t : th) t.join();
     double worst = 0.0;
-    const int M = 24;
-    for (int p = p_lo; p < p_hi; ++p) {
-        for (int i = 0; i <= M + 1; ++i) {
-            double tau;
-            if (p < kChebBinPieces) {
-                const int e = kChebOct0 + p / kChebSub, j = p % kChebSub;
-                const long double t = (i == 0) ? 0.0L : (i == M + 1) ? 1.0L - 1e-12L : (i - 0.5L) / M;
-                tau = (double)ldexpl(1.0L + 0.25L * (j + t), e);
-            } else {
-                const long double sv = (long double)kChebSHi * (i / (long double)(M + 1));
-                tau = (sv == 0.0L) ? HUGE_VAL : (double)(1.0L / sv);
-            }
-            double x = 0.0;
-            const int pp = cheb_piece(tau, x);
-            if (pp < 0) return HUGE_VAL;
-            const long double sv = 1.0L / (long double)tau;
-            for (int c = 0; c <= C; ++c) {
-                double y = 0.0;
-                cheb_sums<1>(coef.data() + (size_t)pp * n * CP + c, CP, x, &y);
-                const long double ex = cheb_exact(cols[c < C ? c : 0], sv, dd, c == C);
-                const double e = (ex > 0) ? (double)(fabsl((long double)y - ex) / ex) : (y == 0.0 ? 0.0 : HUGE_VAL);
-                if (!(e <= worst)) worst = e;   // NaN -> worst = NaN
-            }
-        }
-    }
+    for (int t = 0; t < nt; ++t)
+        if (!(worst_t[t] <= worst)) worst = worst_t[t];
     return worst;
 }
 
@@ -356,43 +369,118 @@ static int cheb_prepare(ngrtd_ctx* ctx, TableDev& tab, double d01) {
     return NGRTD_OK;
 }
 
-// exp_pist_flow block-tail surrogates: for b = 1.. while b S < N, the columns
-// A_c[b S - 1 ...] (so that the surrogate's sum_{j>=0} cols[1 + j] e^{-j/tau'} is
-// T_b = sum_{k >= b S} A_{c,k} e^{-(k - b S)/tau'}), with s01 = 1 (d01 = 0), fitted and
-// validated over the pieces [p_lo, p_hi) only, one thread per table.  Used only if every
-// table validates to kChebTol (else the plan keeps the multi-kernel EPM path).
+// exp_pist_flow block-tail surrogates: for every block b = 1.. with b S < N, per channel c
+//   T_b,c(tau') = sum_{k >= b S} A_{c,k} e^{-(k - b S) / tau'}     (and the normaliser, A = 1)
+// over the pieces [p_lo, p_hi) of epm_piece.  At one tau' ALL blocks' values come from one
+// backward recursion over the series, R_k = A_k + q R_{k+1} (q = e^{-1/tau'}, long double),
+// T_b = R_{b S}: the fit needs kChebN such passes per piece and the validation 26, instead of
+// one sum per block and point.  The Chebyshev interpolant of each (block, piece, channel) is
+// turned into monomial form (long double) and every piece is validated at 26 points through
+// epm_piece + cheb_sums, the kernel's own code, at the plan tolerance kChebTol.  Threads split
+// the pieces.  Used only if every table validates (else the plan keeps the multi-kernel path).
 static int epm_prepare(ngrtd_ctx* ctx, TableDev& tab, int N, int p_lo, int p_hi) {
     tab.epm_ok = false;
-    const int C = tab.C, CP = cheb_cp(C), S = kEpmBlock;
-    if (C < 1 || C > 5 || tab.cols_host.empty() || N <= S + 1 || p_lo < 0 || p_hi > kChebPieces || p_hi <= p_lo)
+    const int C = tab.C, CP = cheb_cp(C), S = kEpmBlock, n = kChebN;
+    if (C < 1 || C > 5 || tab.cols_host.empty() || N <= S + 1 || p_lo < 0 || p_hi > kEpmPieces || p_hi <= p_lo)
         return NGRTD_OK;
+    for (int c = 0; c < C; ++c)
+        for (double v : tab.cols_host[c])
+            if (!(v >= 0.0) || !std::isfinite(v)) return NGRTD_OK;   // the relative bound needs A >= 0
     const int nb = (N - 1) / S;                    // b S < N for b = 1..nb
-    std::vector<std::vector<double>> coefs((size_t)nb);
-    std::vector<double> errs((size_t)nb, HUGE_VAL);
-    auto work = [&](int b0, int stride) {
-        for (int b = b0; b <= nb; b += stride) {
-            std::vector<std::vector<double>> cols((size_t)C);
-            for (int c = 0; c < C; ++c)
-                cols[c].assign(tab.cols_host[c].begin() + ((size_t)b * S - 1), tab.cols_host[c].end());
-            errs[b - 1] = cheb_build(cols, C, 0.0, coefs[b - 1], p_lo, p_hi);
+    const int np = p_hi - p_lo;
+    const size_t per = (size_t)n * CP;
+    std::vector<double> h((size_t)nb * np * per, 0.0);
+    const long double PI = 3.14159265358979323846264338327950288L;
+    std::vector<std::vector<long double>> Tm(n, std::vector<long double>(n, 0.0L));
+    Tm[0][0] = 1.0L;
+    Tm[1][1] = 1.0L;
+    for (int j = 2; j < n; ++j)
+        for (int k = 0; k < n; ++k)
+            Tm[j][k] = (k > 0 ? 2.0L * Tm[j - 1][k - 1] : 0.0L) - Tm[j - 2][k];
+    // tail values of every block at s = 1/tau': out[(b - 1) (C + 1) + c]
+    auto tails = [&](long double sv, std::vector<long double>& out) {
+        const long double q = expl(-sv);
+        out.assign((size_t)nb * (C + 1), 0.0L);
+        for (int c = 0; c <= C; ++c) {
+            long double r = 0.0L;
+            for (int k = N - 1; k >= S; --k) {
+                r = r * q + (c < C ? (long double)tab.cols_host[c][k] : 1.0L);
+                if (k % S == 0) out[(size_t)(k / S - 1) * (C + 1) + c] = r;
+            }
         }
+    };
+    auto s_of = [&](int p, long double x) {       // s = 1/tau' at local x of piece p
+        if (p < kEpmBinPieces) {
+            const int e = kEpmOct0 + p / kChebSub, j = p % kChebSub;
+            return 1.0L / ldexpl(1.125L + 0.25L * j + x / 8.0L, e);
+        }
+        return 0.5L * (long double)kChebSHi * (1.0L + x);
+    };
+    long double cs[kChebN][kChebN], xn[kChebN];   // cos(pi j (k + 1/2) / n), the nodes
+    for (int k = 0; k < n; ++k) {
+        xn[k] = cosl(PI * (k + 0.5L) / n);
+        for (int j = 0; j < n; ++j) cs[j][k] = cosl(PI * j * (k + 0.5L) / n);
+    }
+    std::vector<double> worst_t(64, 0.0);
+    auto work = [&](int t, int nt) {
+        std::vector<long double> f((size_t)n * nb * (C + 1)), v;
+        double worst = 0.0;
+        for (int p = p_lo + t; p < p_hi; p += nt) {
+            for (int k = 0; k < n; ++k) {          // values at the Chebyshev nodes
+                tails(s_of(p, xn[k]), v);
+                std::copy(v.begin(), v.end(), f.begin() + (size_t)k * nb * (C + 1));
+            }
+            for (int b = 0; b < nb; ++b)
+                for (int c = 0; c <= C; ++c) {
+                    long double ch[kChebN];
+                    for (int j = 0; j < n; ++j) {
+                        long double acc = 0.0L;
+                        for (int k = 0; k < n; ++k)
+                            acc += f[((size_t)k * nb + b) * (C + 1) + c] * cs[j][k];
+                        ch[j] = acc * (j == 0 ? 1.0L : 2.0L) / n;
+                    }
+                    for (int k = 0; k < n; ++k) {
+                        long double m = 0.0L;
+                        for (int j = k; j < n; ++j) m += ch[j] * Tm[j][k];
+                        h[(((size_t)b * np + (p - p_lo)) * n + k) * CP + c] = (double)m;
+                    }
+                }
+            const int M = 24;                        // validation: 26 points per piece
+            for (int i = 0; i <= M + 1; ++i) {
+                double taup;
+                if (p < kEpmBinPieces) {
+                    const int e = kEpmOct0 + p / kChebSub, j = p % kChebSub;
+                    const long double tt = (i == 0) ? 0.0L : (i == M + 1) ? 1.0L - 1e-12L : (i - 0.5L) / M;
+                    taup = (double)ldexpl(1.0L + 0.25L * (j + tt), e);
+                } else {
+                    const long double sv = (long double)kChebSHi * (i / (long double)(M + 1));
+                    taup = (sv == 0.0L) ? HUGE_VAL : (double)(1.0L / sv);
+                }
+                double x = 0.0;
+                if (epm_piece(taup, x) != p) { worst = HUGE_VAL; continue; }
+                tails(1.0L / (long double)taup, v);
+                for (int b = 0; b < nb; ++b)
+                    for (int c = 0; c <= C; ++c) {
+                        double y = 0.0;
+                        cheb_sums<1>(h.data() + ((size_t)b * np + (p - p_lo)) * per + c, CP, x, &y);
+                        const long double ex = v[(size_t)b * (C + 1) + c];
+                        const double e = (ex > 0) ? (double)(fabsl((long double)y - ex) / ex) : (y == 0.0 ? 0.0 : HUGE_VAL);
+                        if (!(e <= worst)) worst = e;   // NaN -> worst = NaN
+                    }
+            }
+        }
+        worst_t[t] = worst;
     };
     const int nt = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     std::vector<std::thread> th;
-    for (int t = 1; t < nt && t <= nb; ++t) th.emplace_back(work, 1 + t, nt);
-    work(1, nt);
+    for (int t = 1; t < nt; ++t) th.emplace_back(work, t, nt);
+    work(0, nt);
     for (auto& t : th) t.join();
     double worst = 0.0;
-    for (double e : errs)
-        if (!(e <= worst)) worst = e;
+    for (int t = 0; t < nt; ++t)
+        if (!(worst_t[t] <= worst)) worst = worst_t[t];
     tab.epm_err = worst;
     if (!(worst <= kChebTol)) return NGRTD_OK;
-    const int np = p_hi - p_lo;
-    const size_t per = (size_t)kChebN * CP;
-    std::vector<double> h((size_t)nb * np * per);
-    for (int b = 0; b < nb; ++b)
-        std::copy(coefs[b].begin() + (size_t)p_lo * per, coefs[b].begin() + (size_t)p_hi * per,
-                  h.begin() + (size_t)b * np * per);
     HIP_TRY(ctx, tab.epm.ensure(h.size() * sizeof(double)));
     HIP_TRY(ctx, hipMemcpy(tab.epm.p, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
     tab.epm_ok = true;
@@ -549,7 +637,7 @@ static void launch_mfma(const RtdArgs& a, const UnitArgs& u, int32_t fuse, hipSt
 // packed per-well data (ce obs, 1/sd^2, sums of 0.5 log 1/sd^2, E_min; rtd obs, 1/sd^2,
 // sums; the Student-t normaliser table).
 static size_t fused_lds(const RtdArgs& a, const UnitArgs& u, int dz_p = 0) {
-    const size_t epm_tab = a.mod[0] == MOD_EPM ? (size_t)a.N * a.CP : 0;   // EPM: the channel table
+    const size_t epm_tab = a.mod[0] == MOD_EPM ? (size_t)epm_lds_doubles(a.N, a.CP) : 0;   // EPM: the channel table
     const size_t dz = (size_t)dz_p * kFusedUnits;                          // DZ step: the proposals
     return (size_t)(2 * kFusedUnits + kFusedUnits / 2 + a.cheb_np * cheb_lds_stride(a.C) + epm_tab + u.wd_n + dz) *
            sizeof(double);
@@ -1300,12 +1388,12 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
         }
         if (a.mod[0] == MOD_EPM && (a.mod[1] == MOD_NONE || a.mod[1] == MOD_PISTON) && !any_lamw &&
             p->table.C <= 5 && p->dtp >= 0.0 && !(d->flags & NGRTD_EXACT_RTD) && ri[NGRTD_ROLE_ETA1] >= 0) {
-            // block-tail surrogates over every tau' = tau / eta >= 1/2 (down to the priors'
-            // lower end when it is higher); lanes below sum their short tails exactly
+            // block-tail surrogates over every tau' = tau / eta >= the priors' lower end (the
+            // table reaches 2^kEpmOct0); lanes below it or NaN sum their tails exactly
             static const bool disabled = std::getenv("NGRTD_NO_CHEB") != nullptr;
             double x;
-            const double lo = std::max(kChebTauLo, d->tau1_lo / d->eta1_hi);
-            const int pa = cheb_piece(lo, x), pb = kChebPieces - 1;
+            const double lo = std::max(1.0 / (1 << -kEpmOct0), d->tau1_lo / d->eta1_hi);
+            const int pa = epm_piece(lo, x), pb = kEpmPieces - 1;
             if (!disabled && pa >= 0 && pb >= pa) {
                 NG_CHECK(epm_prepare(ctx, p->table, p->N, pa, pb + 1));
                 if (p->table.epm_ok) {

@@ -76,6 +76,15 @@ constexpr int kChebBinPieces = kChebSub * kChebOcts;
 constexpr int kChebPieces = kChebBinPieces + 1;
 constexpr double kChebTauLo = 0.5;
 constexpr double kChebSHi = 0x1p-18;               // the tail: s = 1/tau in [0, 2^-18]
+// The exp_pist_flow block-tail surrogates (ngrtd.hip epm_prepare) use the same pieces over
+// a wider range, tau' = tau / eta down to 2^kEpmOct0 (the priors reach tau' = 1 / 5): a
+// Chebyshev piece [a, 1.25 a] converges as fast at any scale (each term e^(-j / tau') is
+// analytic in log tau' over |Im| < pi/2), so no lane of the priors' support sums its tail
+// exactly.  Same tail piece (s = 1/tau' in [0, kChebSHi]).
+constexpr int kEpmOct0 = -4;
+constexpr int kEpmOcts = kChebOct0 + kChebOcts - kEpmOct0;   // up to 2^18 as well
+constexpr int kEpmBinPieces = kChebSub * kEpmOcts;
+constexpr int kEpmPieces = kEpmBinPieces + 1;
 // surrogate table row length for C channels: C numerator sums + the normaliser, even
 __host__ __device__ constexpr int cheb_cp(int C) { return (C + 2) & ~1; }
 
@@ -188,7 +197,7 @@ struct DemcAccept {
     int32_t L;
     int32_t dz_diag;        // timing diagnostics only (NGRTD_DZ_DIAG, tools/dz_probe.py): bit 0: proposal =
                             // state, 1: no history store, 2: no commit, 3: no staging, 4: no partner
-                            // loads (noise-only proposals) (wrong results)
+                            // loads (noise-only proposals), 5: no per-well decision (wrong results)
     int32_t tr_kind[NGRTD_ROLE_COUNT];
     double tr_a[NGRTD_ROLE_COUNT], tr_b[NGRTD_ROLE_COUNT];
     // Multi-step launch (MIX bit 3): the block runs n_steps consecutive steps of its own

@@ -744,19 +744,30 @@ struct MfmaWave {
 // ---------------------------------------------- Chebyshev surrogate (see ngrtd_device.hpp)
 // Piece of tau and its local coordinate x in [-1, 1]; -1 when tau is not covered (tau < 1/2
 // or NaN).  Host and device run this same code (the host validates the table with it).
-__host__ __device__ __forceinline__ int cheb_piece(double tau, double& x) {
-    if (!(tau >= kChebTauLo)) return -1;
+// OCT0 / OCTS: the binary octaves [2^OCT0, 2^(OCT0 + OCTS)) the pieces split, then the tail.
+template <int OCT0, int OCTS>
+__host__ __device__ __forceinline__ int cheb_piece_t(double tau, double& x) {
+    static_assert(OCT0 + OCTS == kChebOct0 + kChebOcts, "one tail piece for every table");
+    constexpr double lo = OCT0 >= 0 ? (double)(1ull << OCT0) : 1.0 / (double)(1ull << -OCT0);
+    if (!(tau >= lo)) return -1;
     const unsigned hi = fm_hi(tau);
-    const int e = (int)(hi >> 20) - 1023;          // tau >= 1/2: sign bit clear
-    if (e >= kChebOct0 + kChebOcts) {              // tau >= 2^18, inf
+    const int e = (int)(hi >> 20) - 1023;          // tau > 0: sign bit clear
+    if (e >= OCT0 + OCTS) {                        // tau >= 2^18, inf
         const double sv = 1.0 / tau;
         x = sv * (2.0 / kChebSHi) - 1.0;
-        return kChebBinPieces;
+        return kChebSub * OCTS;
     }
     const int j = (int)((hi >> 18) & 3u);
     const double m = fm_with_hi(tau, (hi & 0x000FFFFFu) | 0x3FF00000u);
     x = (m - (1.125 + 0.25 * j)) * 8.0;
-    return (e - kChebOct0) * kChebSub + j;
+    return (e - OCT0) * kChebSub + j;
+}
+__host__ __device__ __forceinline__ int cheb_piece(double tau, double& x) {
+    return cheb_piece_t<kChebOct0, kChebOcts>(tau, x);
+}
+// the exp_pist_flow block-tail tables: tau' >= 2^kEpmOct0 (ngrtd_device.hpp)
+__host__ __device__ __forceinline__ int epm_piece(double tau, double& x) {
+    return cheb_piece_t<kEpmOct0, kEpmOcts>(tau, x);
 }
 
 // Surrogate sums of C channels at x from one piece's coefficients [kChebN][CP]: the
@@ -1066,15 +1077,13 @@ __device__ __forceinline__ bool demc_decide(const DemcAccept& d, int64_t w, doub
     return demc_decide(d, w, lp_prop, d.key, d.tune_now, 0);
 }
 // Per-well chains: the random-stream id of unit (walker w, well l) -- the same in a run of
-// all L wells and in a run of well l alone (well0 = l), and in any walker-block shard.
+// all L wells and in a run of well l alone (well0 = l), and in any walker-block shard.  It
+// keys the unit's proposal noise and its accept draw; the partner indices are keyed by the
+// walker (every well of a walker draws the same indices, each into its own history), so
+// each well's chain is still exactly a DEMetropolisZ chain.
 __host__ __device__ __forceinline__ uint64_t dz_cid(int64_t well0, int64_t l, int64_t Wg, int64_t chain0, int64_t w) {
     return (uint64_t)(well0 + l) * (uint64_t)Wg + (uint64_t)(chain0 + w);
 }
-// Per-well history entry of one unit: Ps = 4 ceil(P / 4) doubles; row p at slot
-// pw_slot(p) = (p mod 2) Ps/2 + p div 2 -- the even rows (staged by the theta waves) then the
-// odd rows (RTD waves), each group 16-B aligned.
-__host__ __device__ __forceinline__ int pw_stride(int P) { return 4 * ((P + 3) / 4); }
-__host__ __device__ __forceinline__ int pw_slot(int p, int P) { return (p & 1) * (pw_stride(P) / 2) + (p >> 1); }
 // ... and the noise element of its parameter row p (rows of one chain are contiguous)
 constexpr int kPwRowStride = 32;   // >= NGRTD_ROLE_COUNT
 __host__ __device__ __forceinline__ uint64_t dz_pw_elem(uint64_t cid, int p) {
@@ -1291,9 +1300,9 @@ __device__ __forceinline__ double dz_value(const DemcAccept& d, bool de, double 
 
 // Per-well chains (DemczArgs::per_well), the proposal step of plans without a single-launch
 // instance: one thread per unit c = l W + w (theta's [L][W] order: the state / proposal
-// rows [P][L][W] are read and written coalesced), partners and random numbers of the unit's
-// own stream (dz_cid), history entries = pw_stride(P) doubles of the unit-major history
-// [cap][W][L][Ps] (rows at pw_slot).  The arithmetic of dz_stage's per-well branch (bitwise).
+// rows [P][L][W] are read and written coalesced), noise and accept draws of the unit's
+// own stream (dz_cid), partner indices of the walker, the joint chains' history layout.  The
+// arithmetic of dz_stage's per-well branch (bitwise).
 NGRTD_KLINK __global__ void __launch_bounds__(256) demcz_propose_pw_kernel(const DemczArgs d) {
     const int64_t W = d.W, U = d.W * d.L;
     const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -1301,20 +1310,18 @@ NGRTD_KLINK __global__ void __launch_bounds__(256) demcz_propose_pw_kernel(const
     const int64_t l = c / W, w = c % W;
     const int P = d.P;
     const uint64_t cid = dz_cid(d.well0, l, d.Wg, d.chain0, w);
-    const int Ps = pw_stride(P);
-    const size_t entry = (size_t)U * Ps, base = ((size_t)w * d.L + l) * Ps;
-    int sl[kRoleCount];
-    for (int p = 0; p < P; ++p) sl[p] = pw_slot(p, P);
+    // the joint chains' history layout: entry e of walker w at (e W + w) R, row p L + l
+    const size_t entry = (size_t)U * P, base = (size_t)w * P * d.L + l;
     double x[kRoleCount];
     for (int p = 0; p < P; ++p) x[p] = d.x[(int64_t)p * U + c];
     if (d.append_at >= 0)
-        for (int p = 0; p < P; ++p) d.hist[(size_t)d.append_at * entry + base + sl[p]] = x[p];
+        for (int p = 0; p < P; ++p) d.hist[(size_t)d.append_at * entry + base + (size_t)p * d.L] = x[p];
     if (!d.propose) return;
     const bool de = d.it > 1;
     int64_t e1 = -1, e2 = -1;
-    if (de) {
+    if (de) {            // partners keyed by the walker (as dz_stage)
         uint64_t iz1, iz2;
-        demcz_partners(d.key, cid, (uint64_t)d.it, iz1, iz2);
+        demcz_partners(d.key, (uint64_t)(d.chain0 + w), (uint64_t)d.it, iz1, iz2);
         e1 = d.lo + (int64_t)iz1;
         e2 = d.lo + (int64_t)iz2;
     }
@@ -1323,8 +1330,8 @@ NGRTD_KLINK __global__ void __launch_bounds__(256) demcz_propose_pw_kernel(const
     const double lamb = d.lamb[c], sc = d.scaling[c];
     const uint64_t ke = rng_mix(d.key + 2);
     for (int p = 0; p < P; ++p) {
-        const double z1 = de ? (c1 ? x[p] : d.hist[(size_t)e1 * entry + base + sl[p]]) : 0.0;
-        const double z2 = de ? (c2 ? x[p] : d.hist[(size_t)e2 * entry + base + sl[p]]) : 0.0;
+        const double z1 = de ? (c1 ? x[p] : d.hist[(size_t)e1 * entry + base + (size_t)p * d.L]) : 0.0;
+        const double z2 = de ? (c2 ? x[p] : d.hist[(size_t)e2 * entry + base + (size_t)p * d.L]) : 0.0;
         const double v = dz_value_e(d, de, x[p], z1, z2, lamb, sc, ke, dz_pw_elem(cid, p), (int64_t)p * d.L + l);
         d.prop[(int64_t)p * U + c] = v;
         if (d.prop_x) d.prop_x[(int64_t)p * U + c] = pymc3_backward(d.tr_kind[p], d.tr_a[p], d.tr_b[p], v);
@@ -1365,11 +1372,10 @@ __device__ __forceinline__ void dz_partners(const DemcAccept& d, const DzStep& s
 // chains'-space value in LDS row p of th for dz_commit.  (Reading the natural proposals
 // back from an LDS copy instead of d.dz_prop was slower: the extra uniform row indices
 // spilled SGPRs into the unit body.)
-// PW (per-well chains, DemcAccept::per_well): the unit is the chain -- partners, lamb /
-// scaling (walker-major scratch copies [W][L] inside the call) and random numbers of its own
-// (dz_cid); its history entry is Ps = pw_stride(P) contiguous doubles of the unit-major
-// history [cap][W][L][Ps] with the rows of each staging role adjacent (pw_slot): this lane
-// reads its role's rows of a partner as 16-B loads.
+// PW (per-well chains, DemcAccept::per_well): the unit is the chain -- lamb / scaling
+// (walker-major scratch copies [W][L] inside the call), proposal noise and accept draw of
+// its own (dz_cid); the partner indices are the walker's, so the history layout and its
+// loads are the joint chains' ones.
 template <int PMAX, bool TR, bool PW = false>
 __device__ __forceinline__ void dz_stage(const DemcAccept& d, const DzStep& sj, int64_t U, int64_t u, int i, int64_t w,
                                          int l, int L, int64_t W, bool valid, double* th, int p0, double* pl) {
@@ -1380,62 +1386,40 @@ __device__ __forceinline__ void dz_stage(const DemcAccept& d, const DzStep& sj, 
         return;
     }
     const uint64_t cid = PW ? dz_cid(d.well0, l, d.Wg, d.chain0, w) : 0;
-    int64_t e1 = -1, e2 = -1;
-    if (!PW) {
-        dz_partners(d, sj, w, e1, e2);
-    } else if (sj.it > 1) {
-        uint64_t iz1, iz2;
-        demcz_partners(sj.key, cid, (uint64_t)sj.it, iz1, iz2);
-        e1 = sj.lo + (int64_t)iz1;
-        e2 = sj.lo + (int64_t)iz2;
-    }
+    // partner entries: keyed by the walker (chain0 + w) for joint and per-well chains alike --
+    // the wells of one walker draw the same history indices (each from its own history), so
+    // a wave (one walker's wells) reads two contiguous entries, as the joint chains do
+    int64_t e1, e2;
+    dz_partners(d, sj, w, e1, e2);
     if (d.dz_diag & 16) e1 = e2 = -1;   // timing diagnostics: no partner loads (noise only)
     const bool de = e1 >= 0;
     constexpr int KMAX = (PMAX + 1) / 2;
     double x[KMAX], a1[KMAX], a2[KMAX];
-    // joint chains: row p of entry e at (e W + w) R + p L + l (R = P L); per-well chains: slot
-    // pw_slot(p) of the unit's entry ((e W + w) L + l) Ps
-    const int Ps = pw_stride(d.P), half = Ps / 2;
-    const int64_t ent = PW ? (int64_t)L * Ps : (int64_t)d.P * L;          // doubles per chain entry
-    const int64_t roff = PW ? (int64_t)l * Ps + p0 * half : l, rst = PW ? 1 : L;
-    const double* z1 = d.hist + ((size_t)(de ? e1 : 0) * W + w) * ent + roff;
-    const double* z2 = d.hist + ((size_t)(de ? e2 : 0) * W + w) * ent + roff;
+    // row p of entry e at (e W + w) R + p L + l (R = P L), per-well chains too: a wave (one
+    // walker's wells) reads 512-B runs of the walker's two partner entries
+    const int64_t R = (int64_t)d.P * L;
+    const double* z1 = d.hist + ((size_t)(de ? e1 : 0) * W + w) * R + l;
+    const double* z2 = d.hist + ((size_t)(de ? e2 : 0) * W + w) * R + l;
     const int64_t ci = PW ? w * (int64_t)L + l : w;   // per-chain arrays: walker-major [W][L] / [W]
     const double lamb = d.lamb[ci], sc = d.scaling[ci];
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
         const int p = p0 + 2 * k;
-        if (p < d.P) x[k] = d.zx[(int64_t)p * U + u];
-    }
-    if (PW) {       // this role's rows of each partner: adjacent slots, 16-B aligned (half even)
-#pragma unroll
-        for (int k = 0; k < KMAX; k += 2) {
-            if (p0 + 2 * k < d.P) {
-                const double2 v1 = de ? *reinterpret_cast<const double2*>(z1 + k) : double2{0.0, 0.0};
-                const double2 v2 = de ? *reinterpret_cast<const double2*>(z2 + k) : double2{0.0, 0.0};
-                a1[k] = v1.x; a2[k] = v2.x;
-                if (k + 1 < KMAX) { a1[k + 1] = v1.y; a2[k + 1] = v2.y; }
-            }
-        }
-    } else {
-#pragma unroll
-        for (int k = 0; k < KMAX; ++k) {
-            const int p = p0 + 2 * k;
-            if (p < d.P) {
-                a1[k] = de ? z1[(int64_t)p * rst] : 0.0;
-                a2[k] = de ? z2[(int64_t)p * rst] : 0.0;
-            }
+        if (p < d.P) {
+            x[k] = d.zx[(int64_t)p * U + u];
+            a1[k] = de ? z1[(int64_t)p * L] : 0.0;
+            a2[k] = de ? z2[(int64_t)p * L] : 0.0;
         }
     }
     // an entry appended in this launch is the state itself (as demcz_propose_kernel)
     const bool c1 = e1 == sj.at, c2 = e2 == sj.at;
-    double* hrow = d.hist + ((size_t)(sj.at < 0 ? 0 : sj.at) * W + w) * ent + roff;
+    double* hrow = d.hist + ((size_t)(sj.at < 0 ? 0 : sj.at) * W + w) * R + l;
     const uint64_t ke = rng_mix(sj.key + 2);
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
         const int p = p0 + 2 * k;
         if (p < d.P) {
-            if (sj.at >= 0 && !(d.dz_diag & 2)) hrow[PW ? k : (int64_t)p * rst] = x[k];
+            if (sj.at >= 0 && !(d.dz_diag & 2)) hrow[(int64_t)p * L] = x[k];
             const uint64_t el = PW ? dz_pw_elem(cid, p) : (uint64_t)((int64_t)p * L + l) * (uint64_t)d.Wg +
                                                           (uint64_t)(d.chain0 + w);
             double v = dz_value_e(d, de, x[k], c1 ? x[k] : a1[k], c2 ? x[k] : a2[k], lamb, sc, ke, el,
@@ -1541,6 +1525,29 @@ __device__ __forceinline__ void fused_exact(const RtdArgs& a, const UnitArgs& ul
     }
 }
 
+// The EPM channel table in LDS: blocks of kEpmBlock rows of CP doubles, each block padded by
+// 2 doubles.  Every head-loop iteration reads row r of its OWN block in every lane, so with
+// unpadded blocks (16 CP doubles = a multiple of 64 banks apart) all lanes hit the same banks;
+// the pad rotates consecutive blocks by 4 banks, so the 16 lanes of a ds_read_b128 group
+// spread over all 64 banks unless their blocks coincide modulo 16.
+__host__ __device__ constexpr int epm_blk_stride(int CP) { return kEpmBlock * CP + 2; }
+__host__ __device__ constexpr int epm_lds_doubles(int N, int CP) {
+    return (N + kEpmBlock - 1) / kEpmBlock * epm_blk_stride(CP);
+}
+__device__ __forceinline__ int epm_row(int k, int CP) { return (k / kEpmBlock) * epm_blk_stride(CP) + (k % kEpmBlock) * CP; }
+// One table row's C channels: CP / 2 16-B loads (rows are 16-B aligned: CP even, stride even).
+template <int C>
+__device__ __forceinline__ void epm_row_load(const double* row, double* v) {
+    constexpr int CP = cheb_cp(C);
+    const double2* r2 = reinterpret_cast<const double2*>(row);
+#pragma unroll
+    for (int i = 0; i < CP / 2; ++i) {
+        const double2 t = r2[i];
+        if (2 * i < C) v[2 * i] = t.x;
+        if (2 * i + 1 < C) v[2 * i + 1] = t.y;
+    }
+}
+
 // exp_pist_flow channel sums of one unit (numerators num_c and normaliser den, as
 // rtd_conc_kernel's EPM finalise: conc = (A + J B) / den):
 //   f = first unmasked age (epm_first, the exact mask of :189), m = max(f, 1),
@@ -1569,17 +1576,18 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
     for (int i = 0; i < nhead; ++i) {                  // head, top-down Horner (predicated)
         const int k = kt - i;
         const bool on = k >= m;
-        const double* row = tabl + (on ? k : 0) * CP;
+        double rv[C];
+        epm_row_load<C>(tabl + epm_row(on ? k : 0, CP), rv);
 #pragma unroll
         for (int c = 0; c < C; ++c) {
-            const double t = fma(y[c], q, row[c]);
+            const double t = fma(y[c], q, rv[c]);
             y[c] = on ? t : y[c];
         }
     }
     const bool tail = B < N;
     double ex = 0.0;
     const double taup = 1.0 / beta;
-    int pc = (tail && a.epm) ? cheb_piece(taup, ex) - a.epm_p0 : -1;
+    int pc = (tail && a.epm) ? epm_piece(taup, ex) - a.epm_p0 : -1;
     pc = (unsigned)pc < (unsigned)a.epm_np ? pc : -1;
     const bool bad = mvalid && tail && pc < 0;
     double tl[C];
@@ -1590,12 +1598,13 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
         cheb_sums<C>(pt, CP, ex, tl);
     }
     if (__any(bad) && !(a.epm_diag & 4)) {              // exact tails of the uncovered lanes
-        // tau' < 1/2 (q < e^-2): the tail's terms fall below 2e-56 of its first after 64
-        // ages, so it is summed over [B, B + 64) only -- 64 iterations over each lane's own
+        // tau' below the table (q < e^-16): the tail's terms fall below 1e-400 of its first
+        // after 64 ages, so it is summed over [B, B + 64) only -- 64 iterations over each lane's own
         // LDS rows, whatever the spread of B across the wave; other uncovered tau' (NaN,
         // <= 0, beyond the table) over the whole series, the wave's union of those ranges.
         // Both are the same top-down Horner as before per lane (same bits).
-        const bool shortq = taup > 0.0 && taup < kChebTauLo;
+        constexpr double kEpmTauLo = 1.0 / (double)(1 << -kEpmOct0);
+        const bool shortq = taup > 0.0 && taup < kEpmTauLo;
         const bool sb = bad && shortq, lb = bad && !shortq;
         double te[C];
 #pragma unroll
@@ -1605,10 +1614,11 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
             for (int j = 63; j >= 0; --j) {
                 const int k = B + j;
                 const bool on = sb && k <= N - 1;
-                const double* row = tabl + (on ? k : 0) * CP;
+                double rv[C];
+                epm_row_load<C>(tabl + epm_row(on ? k : 0, CP), rv);
 #pragma unroll
                 for (int c = 0; c < C; ++c) {
-                    const double t = fma(te[c], q, row[c]);
+                    const double t = fma(te[c], q, rv[c]);
                     te[c] = on ? t : te[c];
                 }
             }
@@ -1624,10 +1634,11 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
 #pragma unroll 8
             for (int k = kmax; k >= bmin; --k) {
                 const bool on = lb && k >= B;
-                const double* row = tabl + k * CP;
+                double rv[C];
+                epm_row_load<C>(tabl + epm_row(k, CP), rv);
 #pragma unroll
                 for (int c = 0; c < C; ++c) {
-                    const double t = fma(te[c], q, row[c]);
+                    const double t = fma(te[c], q, rv[c]);
                     te[c] = on ? t : te[c];
                 }
             }
@@ -1773,8 +1784,8 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     // per-well observation data -> LDS (read per lane by the likelihood blocks): all loads
     // issued before any store, so the prologue pays one memory latency
     constexpr bool EPM = (MIX & 2) != 0;
-    double* tabl = cheb + a.cheb_np * PST;                // EPM: the channel table [N][CP]
-    double* wd = tabl + (EPM ? a.N * CP : 0);
+    double* tabl = cheb + a.cheb_np * PST;                // EPM: the channel table (epm_row)
+    double* wd = tabl + (EPM ? epm_lds_doubles(a.N, CP) : 0);
     constexpr int kWdRegs = (4 * 64 * kFusedWaves + NTH - 1) / NTH;
     double wv[kWdRegs];
 #pragma unroll
@@ -1799,7 +1810,8 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     if (EPM) {   // channel table -> LDS (rows of CP doubles, CP even: 16-B copies)
         const double2* src = reinterpret_cast<const double2*>(a.tab);
         double2* dst = reinterpret_cast<double2*>(tabl);
-        for (int i = tid; i < a.N * CP / 2; i += NTH) dst[i] = src[i];
+        constexpr int RB = kEpmBlock * CP / 2, SB = epm_blk_stride(CP) / 2;   // double2 per block / padded
+        for (int i = tid; i < a.N * CP / 2; i += NTH) dst[(i / RB) * SB + i % RB] = src[i];
     }
 #pragma unroll
     for (int r = 0; r < kWdRegs; ++r) {
@@ -1857,7 +1869,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         // zero partial sums land on no walker's slots
         const int pi = (DZ && mwl >= WB) ? mi : ml * WB + mwl;
         double* tabl = cheb + a.cheb_np * PST;
-        double* wd = tabl + (EPM ? a.N * CP : 0);
+        double* wd = tabl + (EPM ? epm_lds_doubles(a.N, CP) : 0);
         double* thl = wd + uk.wd_n;
         double* propl = thl + (((MIX & 4) && DZ) ? dk.P * kFusedUnits : 0);   // DZ: [P][512] proposals
         UnitArgs ul = uk;
@@ -1989,7 +2001,9 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         NGRTD_PROBE(6);
         __syncthreads();
         if (PW) {   // per-well chains: the unit's own Metropolis decision (its theta lane)
-            if (do_theta && mvalid) {
+            if (dk.dz_diag & 32) {              // timing diagnostics: no decision (all rejected)
+                if (do_theta) dec[mi] = 0;
+            } else if (do_theta && mvalid) {
                 const int64_t wq = w0 + mwl;
                 dec[mi] = demc_decide(dk, wq * (int64_t)L + ml, dz_cid(dk.well0, ml, dk.Wg, dk.chain0, wq), part[pi],
                                       sj.key, sj.tune_now, (int64_t)js * uk.U, (int64_t)ml * W + wq);

@@ -191,15 +191,6 @@ def pw_cid(well0, L, Wg, chain0, W, device):
 PW_ROW_STRIDE = 32      # = ngrtd_kernels.hpp kPwRowStride: noise element cid * 32 + p
 
 
-def pw_stride(P):
-    """Doubles per per-well history entry (ngrtd_kernels.hpp pw_stride): 4 ceil(P / 4)."""
-    return 4 * ((P + 3) // 4)
-
-
-def pw_slot(p, P):
-    """Slot of row p in a per-well history entry: the even rows, then the odd rows."""
-    return (p & 1) * (pw_stride(P) // 2) + (p >> 1)
-
 
 class DEMetropolisZ:
     """PyMC3 DEMetropolisZ for the W chains of x0 [..., W] on torch ops (any device).
@@ -210,8 +201,10 @@ class DEMetropolisZ:
     chain -- the reference's structure, one PyMC3 model per well (run_age_mcmc.py:122-231,
     noble_gas_mcmc.py:95-104).  log_prob must then return the per-unit log-prob [L][W]
     (engine.LogProb.units); lamb (default 2.38 / sqrt(2 P)), scaling, the tuning counters,
-    the decisions and the logs are per unit ([L][W]); random streams are keyed by the unit's
-    pw_cid (well0: global index of well 0), the device sampler's streams bit for bit."""
+    the decisions and the logs are per unit ([L][W]); the proposal noise and the accept
+    draws are keyed by the unit's pw_cid (well0: global index of well 0), the history
+    partner indices by the walker (each well reading its own history), the device sampler's
+    streams bit for bit."""
 
     def __init__(self, log_prob, lamb=None, scaling=0.001, tune="lambda", tune_interval=100,
                  tune_drop_fraction=0.9, seed=123423, chain0=0, n_chains_total=None, S=None, transform=None,
@@ -337,6 +330,7 @@ class DEMetropolisZ:
         hist_lo = 0
         Wg = int(self.n_chains_total or W)
         cid = pw_cid(self.well0, L, Wg, self.chain0, W, dev)                     # [L][W]
+        wkey = (torch.arange(W, device=dev, dtype=torch.int64) + self.chain0)[None, :].expand(L, W)
         e_idx = cid[None] * PW_ROW_STRIDE + torch.arange(P, device=dev, dtype=torch.int64)[:, None, None]
         li = torch.arange(L, device=dev)[:, None].expand(L, W)
         wi = torch.arange(W, device=dev)[None, :].expand(L, W)
@@ -347,8 +341,8 @@ class DEMetropolisZ:
                 hist_lo += int(self.tune_drop_fraction * (s - hist_lo))
             key = step_key(self.seed, s)
             it = s - hist_lo
-            if it > 1:
-                hp = mix_t(cid + _s64(mix_int((key + 1) & _M64)))
+            if it > 1:              # partner indices keyed by the walker (every well alike)
+                hp = mix_t(wkey + _s64(mix_int((key + 1) & _M64)))
                 iz1 = (_lsr(hp, 32) * it) >> 32
                 iz2 = ((hp & 0xFFFFFFFF) * (it - 1)) >> 32
                 iz2 = iz2 + (iz2 >= iz1).to(torch.int64)
@@ -398,11 +392,8 @@ class ZState:
         self.lamb = torch.full(shp, float(lamb), dtype=torch.float64, device=device)
         self.scaling = torch.full(shp, float(scaling), dtype=torch.float64, device=device)
         self.n_acc_tune = torch.zeros(shp, dtype=torch.int32, device=device)
-        # per-well chains: unit-major entries of pw_stride(P) doubles (row p at pw_slot(p))
         self.P = self.R // self.L
-        self.Ps = pw_stride(self.P)
-        ent = self.L * self.Ps if self.per_well else self.R
-        self.hist = torch.empty((int(hist_cap), W, ent), dtype=torch.float64, device=device)
+        self.hist = torch.empty((int(hist_cap), W, self.R), dtype=torch.float64, device=device)
         self.u = None                     # transformed-space chains (set by DeviceDEMetropolisZ.start)
         self.S = (None if S is None else
                   torch.as_tensor(S, dtype=torch.float64).reshape(self.R).contiguous().to(device))
@@ -416,12 +407,9 @@ class ZState:
                                  per_well=int(self.per_well), well0=int(well0))
 
     def entries(self, lo, hi):
-        """History entries [lo, hi) as [hi - lo][R][W] (per-well chains: [hi - lo][P][L][W],
-        from the unit-major [cap][W][L][P] history)."""
+        """History entries [lo, hi) as [hi - lo][R][W] (per-well chains: [hi - lo][P][L][W])."""
         if self.per_well:
-            sl = torch.tensor([pw_slot(p, self.P) for p in range(self.P)], device=self.hist.device)
-            h = self.hist[lo:hi].reshape(hi - lo, self.W, self.L, self.Ps).index_select(3, sl)
-            return h.permute(0, 3, 2, 1)
+            return self.hist[lo:hi].reshape(hi - lo, self.W, self.P, self.L).permute(0, 2, 3, 1)
         return self.hist[lo:hi].permute(0, 2, 1)
 
 
