@@ -113,7 +113,7 @@ struct ngrtd_plan {
     double tp0 = 1e-5, dtp = 0.0;
     // workspaces
     DevBuf conc, ulogp, theta_stage, out_stage, ce_stage;
-    DevBuf demc_prop[2], demc_lp, demc_acc, demc_cnt;   // ngrtd_demcz_run scratch
+    DevBuf demc_prop[2], demc_lp, demc_acc;   // ngrtd_demcz_run scratch
     DevBuf demc_xw[2];      // the multi-step launch's walker-major state [P][W][L] (natural, transformed)
     DevBuf demc_pw;         // ... and per-well chains' lp, lamb, scaling [W][L] f64 + n_acc_tune [W][L] i32
 
@@ -639,7 +639,7 @@ static void launch_mfma(const RtdArgs& a, const UnitArgs& u, int32_t fuse, hipSt
 static size_t fused_lds(const RtdArgs& a, const UnitArgs& u, int dz_p = 0) {
     const size_t epm_tab = a.mod[0] == MOD_EPM ? (size_t)epm_lds_doubles(a.N, a.CP) : 0;   // EPM: the channel table
     const size_t dz = (size_t)dz_p * kFusedUnits;                          // DZ step: the proposals
-    return (size_t)(2 * kFusedUnits + kFusedUnits / 2 + a.cheb_np * cheb_lds_stride(a.C) + epm_tab + u.wd_n + dz) *
+    return (size_t)(kFusedHdr + a.cheb_np * cheb_lds_stride(a.C) + epm_tab + u.wd_n + dz) *
            sizeof(double);
 }
 // Surrogate pieces the fused kernel stages: when the unit's log-prob carries the tau1
@@ -1749,11 +1749,8 @@ int ngrtd_demcz_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64
     HIP_TRY(ctx, p->demc_prop[0].ensure((size_t)E * sizeof(double)));
     HIP_TRY(ctx, p->demc_lp.ensure((size_t)NC * sizeof(double)));
     HIP_TRY(ctx, p->demc_acc.ensure((size_t)NC * sizeof(int32_t)));
+    // acceptances are counted only on request (n_accepted NULL: no atomics at all)
     unsigned long long* cnt = reinterpret_cast<unsigned long long*>(n_accepted);
-    if (!cnt) {
-        HIP_TRY(ctx, p->demc_cnt.ensure(sizeof(unsigned long long)));
-        cnt = static_cast<unsigned long long*>(p->demc_cnt.p);
-    }
     int32_t* acc = static_cast<int32_t*>(p->demc_acc.p);
     const bool tr = z->theta_u != nullptr;
     if (tr && !(p->desc.flags & NGRTD_WANT_JACOBIAN))

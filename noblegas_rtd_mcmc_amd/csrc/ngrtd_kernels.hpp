@@ -1041,15 +1041,19 @@ __device__ __forceinline__ void count_accepts(unsigned long long* n, bool acc) {
 }
 // li: the chain's index in the logs (log_off + li), which may differ from w (per-well chains
 // in the multi-step launch keep their state arrays walker-major).
+// count: add the decision to d.n_acc here (per wave); the per-well multi-step launch counts
+// per block itself (one atomic per block: same-address atomics serialise in L2, and one per
+// wave cost ~10 us per c4 step).
 __device__ __forceinline__ bool demc_decide(const DemcAccept& d, int64_t w, uint64_t rid, double lp_prop,
-                                            uint64_t key, int32_t tune_now, int64_t log_off, int64_t li) {
+                                            uint64_t key, int32_t tune_now, int64_t log_off, int64_t li,
+                                            bool count = true) {
     const double cur = d.lp[w];
     const double logu = log(rng_unit(rng_mix(rng_mix(key + 3) + rid)));
     const double mr = lp_prop - cur;
     const bool acc = __builtin_isfinite(mr) && logu < mr;
     d.acc[w] = acc;
     if (acc) d.lp[w] = lp_prop;
-    count_accepts(d.n_acc, acc);
+    if (count && d.n_acc) count_accepts(d.n_acc, acc);
     if (d.n_acc_tune) {
         int32_t na = d.n_acc_tune[w] + (acc ? 1 : 0);
         if (tune_now) {
@@ -1698,6 +1702,9 @@ __device__ __forceinline__ T opaque_s(T x) {
 
 constexpr int kFusedWaves = 8;                 // waves of units per block (512 units)
 constexpr int kFusedUnits = 64 * kFusedWaves;
+// LDS doubles ahead of the tables: per-unit partial sums [2][512], decisions [512] int, per-
+// wave accept counts [16] int (8 doubles, padded to keep the tables 16-B aligned)
+constexpr int kFusedHdr = 2 * kFusedUnits + kFusedUnits / 2 + 16;
 constexpr int kFusedPrefetch = 6;   // double2 per thread (512 threads): covers kChebPieces*kChebN*6 doubles
 // LDS stride of one surrogate piece: kChebN*CP doubles + 2 of padding, so that consecutive
 // pieces start 16-B slots an ODD number apart -- lanes gathering different pieces with
@@ -1751,7 +1758,8 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     double* part = lds;                                   // [512] per-unit log-prob
     double* part2 = lds + kFusedUnits;                    // [512] RTD likelihood (ROLES = 2)
     int* dec = reinterpret_cast<int*>(lds + 2 * kFusedUnits);   // [512] DE-MC decisions per walker
-    double* cheb = lds + 2 * kFusedUnits + kFusedUnits / 2;   // [kChebPieces][kChebN][CP]
+    int* wcnt = reinterpret_cast<int*>(lds + 2 * kFusedUnits + kFusedUnits / 2);   // [16] per-wave accept counts
+    double* cheb = lds + kFusedHdr;                       // [kChebPieces][kChebN][CP]
     NGRTD_PROBE(0);
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
@@ -2001,12 +2009,18 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         NGRTD_PROBE(6);
         __syncthreads();
         if (PW) {   // per-well chains: the unit's own Metropolis decision (its theta lane)
+            int a = 0;
             if (dk.dz_diag & 32) {              // timing diagnostics: no decision (all rejected)
                 if (do_theta) dec[mi] = 0;
             } else if (do_theta && mvalid) {
                 const int64_t wq = w0 + mwl;
-                dec[mi] = demc_decide(dk, wq * (int64_t)L + ml, dz_cid(dk.well0, ml, dk.Wg, dk.chain0, wq), part[pi],
-                                      sj.key, sj.tune_now, (int64_t)js * uk.U, (int64_t)ml * W + wq);
+                a = demc_decide(dk, wq * (int64_t)L + ml, dz_cid(dk.well0, ml, dk.Wg, dk.chain0, wq), part[pi],
+                                sj.key, sj.tune_now, (int64_t)js * uk.U, (int64_t)ml * W + wq, false);
+                dec[mi] = a;
+            }
+            if (do_theta && dk.n_acc) {        // the wave's accept count -> LDS (summed after the barrier)
+                const unsigned long long m = __ballot(a != 0);
+                if (lane == 0) wcnt[uw] = __popcll(m);
             }
         } else if (WB <= 64 && (WB & (WB - 1)) == 0) {
             if (wave == 0) {
@@ -2024,6 +2038,12 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         }
         if (DZ) {
             __syncthreads();
+            if (PW && dk.n_acc && tid == 0) {  // one accept-count atomic per block and step
+                int n = 0;
+#pragma unroll
+                for (int i = 0; i < kFusedWaves; ++i) n += wcnt[i];
+                if (n) atomicAdd(dk.n_acc, (unsigned long long)n);
+            }
             if (mvalid && dec[PW ? mi : mwl] && !(dk.dz_diag & 4))
                 dz_commit<kDzMaxP, (MIX & 4) != 0>(dk, uk.U, mu, mi, thl, do_theta ? 0 : 1,
                                                    dk.prop_lds ? propl : nullptr);

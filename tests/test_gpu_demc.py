@@ -313,9 +313,11 @@ def test_demcz_invariants_c4():
     # per-well chains: the tracked per-unit log-probs equal a fresh ngrtd_logp_units
     x, l, z = DeviceDEMetropolisZ(lpj, tune_interval=5, seed=2).start(th0, 10, 30)
     cnt.zero_()
-    lpj.demcz(x, l, 30, z, n_accepted=cnt)
+    alog = torch.zeros((30, 8 * W), dtype=torch.uint8, device="cuda")
+    lpj.demcz(x, l, 30, z, accepted_log=alog, n_accepted=cnt)
     assert torch.equal(l, lpj.units(x)) and tuple(l.shape) == (8, W)
-    assert 0 < int(cnt.item()) < 30 * W * 8
+    # the per-block accept count (one atomic per block and step) equals the decisions logged
+    assert 0 < int(cnt.item()) < 30 * W * 8 and int(cnt.item()) == int(alog.sum())
     lp.close()
     lpj.close()
 
