@@ -748,9 +748,14 @@ static int launch_fused_dz(ngrtd_ctx* ctx, const RtdArgs& a0, const UnitArgs& u,
     // the natural proposal rows in LDS too where they fit (not next to the EPM channel
     // table); NGRTD_DZ_PROP_GLOBAL=1 reads them back from dz_prop instead (A/B runs)
     DemcAccept d = da;
+    // first the chains' state for the whole launch (DemcAccept::state_lds: rows [P][512] and
+    // 3.5 per-chain doubles per slot; NGRTD_DZ_STATE_GLOBAL=1 keeps it in global memory, A/B)
+    const size_t sb = ((size_t)da.P * kFusedUnits + 3 * kFusedUnits + kFusedUnits / 2) * sizeof(double);
+    d.state_lds = (lds + sb <= kFusedMaxLds && !std::getenv("NGRTD_DZ_STATE_GLOBAL")) ? 1 : 0;
     const size_t pb = (size_t)da.P * kFusedUnits * sizeof(double);
-    d.prop_lds = (lds + pb <= kFusedMaxLds && !std::getenv("NGRTD_DZ_PROP_GLOBAL")) ? 1 : 0;
+    d.prop_lds = (lds + pb + (d.state_lds ? sb : 0) <= kFusedMaxLds && !std::getenv("NGRTD_DZ_PROP_GLOBAL")) ? 1 : 0;
     if (d.prop_lds) lds += pb;
+    if (d.state_lds) lds += sb;   // after the proposal rows (logp_fused_kernel's carve-up)
     if (!fused_dz_instance_exists(mix)) return set_err(ctx, NGRTD_EINVAL, "no single-launch DEMetropolisZ instance %d", mix);
     HIP_TRY(ctx, launch_fused_dz_instance(mix, a, u, WB, W, logp, d, lds, kFusedMaxLds, st));
     return NGRTD_OK;

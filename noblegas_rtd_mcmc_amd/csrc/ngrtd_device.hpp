@@ -209,6 +209,12 @@ struct DemcAccept {
     // transformed rows): dz_stage writes them there as well as to dz_prop, and the step's
     // own theta loads and commit read them from LDS instead of back from L2
     int32_t prop_lds;
+    // 1: the block keeps its chains' state in LDS for the whole launch -- the state rows in
+    // the chains' space [P][512] and the per-chain lp / lamb / scaling / tuning counter [512]
+    // (per-well chains: slot = unit; joint chains: slot = walker) -- loaded once before the
+    // first step and written back (x, xu for the chains that moved; the per-chain arrays)
+    // after the last: per step no state loads, no commit stores, no per-chain round trips
+    int32_t state_lds;
     struct Sched {
         uint64_t seed;
         int64_t s0;         // steps_done at the launch's first step
@@ -221,8 +227,8 @@ struct DemcAccept {
     // Per-well chains (ngrtd_demcz_state.per_well): every (walker w, well l) unit is its own
     // chain -- the reference runs one PyMC3 model per well (run_age_mcmc.py:122-231,
     // noble_gas_mcmc.py:95-104).  Chain c = l W + w: lp / acc / n_acc_tune / lamb / scaling
-    // and the logs are [L][W]; random streams are keyed by cid = (well0 + l) Wg + chain0 + w;
-    // the history is unit-major [cap][W][L][P] (a chain's entry is P contiguous doubles).
+    // and the logs are [L][W]; proposal noise and accept draws are keyed by cid = (well0 + l)
+    // Wg + chain0 + w, the partner indices by the walker; the history layout is the joint one.
     int32_t per_well;
     int64_t well0;
     double* ar_log;         // [chains] this step's PyMC3 `accept` stat exp(mr) (null: not logged)

@@ -54,3 +54,12 @@ hipError_t launch_fused_dz_instance(int mix, const RtdArgs& a, const UnitArgs& u
 }
 
 }  // namespace ngrtd
+
+#ifdef NGRTD_SECTION_PROBE
+// this translation unit's probe buffer (the DZ instances stamp it; tools/section_probe.py)
+extern "C" int ngrtd_probe_read_dz(unsigned long long* dst, int64_t n) {
+    using ngrtd::g_probe;
+    if (n > (int64_t)(sizeof(g_probe) / sizeof(g_probe[0]))) n = sizeof(g_probe) / sizeof(g_probe[0]);
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_probe), (size_t)n * sizeof(unsigned long long)) == hipSuccess ? 0 : -2;
+}
+#endif

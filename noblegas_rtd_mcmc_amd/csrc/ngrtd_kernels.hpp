@@ -42,13 +42,14 @@ namespace ngrtd {
 // -DNGRTD_SECTION_PROBE): lane 0 of every wave of logp_fused_kernel records the shader
 // clock (s_memtime) at fixed points.  Compiled out of the product library.
 #ifdef NGRTD_SECTION_PROBE
-constexpr int kProbeSlots = 8;
+// slots 0-7: the log-prob sections; 8-12: a DEMetropolisZ step's (the last step of a launch)
+constexpr int kProbeSlots = 16;
 __device__ unsigned long long g_probe[8192 * kProbeSlots];
 #define NGRTD_PROBE(k)                                                                        \
     do {                                                                                     \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                          \
         if ((threadIdx.x & 63) == 0)                                                          \
-            g_probe[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * kProbeSlots + (k)] = \
-                __builtin_amdgcn_s_memtime();                                                \
+            g_probe[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * kProbeSlots + (k)] = t_; \
     } while (0)
 #else
 #define NGRTD_PROBE(k) do {} while (0)
@@ -1044,30 +1045,41 @@ __device__ __forceinline__ void count_accepts(unsigned long long* n, bool acc) {
 // count: add the decision to d.n_acc here (per wave); the per-well multi-step launch counts
 // per block itself (one atomic per block: same-address atomics serialise in L2, and one per
 // wave cost ~10 us per c4 step).
-__device__ __forceinline__ bool demc_decide(const DemcAccept& d, int64_t w, uint64_t rid, double lp_prop,
-                                            uint64_t key, int32_t tune_now, int64_t log_off, int64_t li,
-                                            bool count = true) {
-    const double cur = d.lp[w];
+// The chain's lp / lamb / scaling / tuning counter at index w of the arrays given (d's own
+// global arrays, or the multi-step launch's LDS copies, DemcAccept::state_lds; the tuning
+// state exists iff d.n_acc_tune does); acc_out: the decision array, stored iff store_acc.
+// (Flags rather than null tests: a null test of an LDS-derived generic pointer miscompiles.)
+__device__ __forceinline__ bool demc_decide_at(const DemcAccept& d, double* lpa, double* lamb, double* scal,
+                                               int32_t* nat, int32_t* acc_out, bool store_acc, int64_t w,
+                                               uint64_t rid, double lp_prop, uint64_t key, int32_t tune_now,
+                                               int64_t log_off, int64_t li, bool count) {
+    const double cur = lpa[w];
     const double logu = log(rng_unit(rng_mix(rng_mix(key + 3) + rid)));
     const double mr = lp_prop - cur;
     const bool acc = __builtin_isfinite(mr) && logu < mr;
-    d.acc[w] = acc;
-    if (acc) d.lp[w] = lp_prop;
+    if (store_acc) acc_out[w] = acc;
+    if (acc) lpa[w] = lp_prop;
     if (count && d.n_acc) count_accepts(d.n_acc, acc);
     if (d.n_acc_tune) {
-        int32_t na = d.n_acc_tune[w] + (acc ? 1 : 0);
+        int32_t na = nat[w] + (acc ? 1 : 0);
         if (tune_now) {
             const double rate = (double)na / (double)d.tune_interval;
-            if (d.tune_target == 2) d.lamb[w] = pymc3_tune(d.lamb[w], rate);
-            else if (d.tune_target == 1) d.scaling[w] = pymc3_tune(d.scaling[w], rate);
+            if (d.tune_target == 2) lamb[w] = pymc3_tune(lamb[w], rate);
+            else if (d.tune_target == 1) scal[w] = pymc3_tune(scal[w], rate);
             na = 0;
         }
-        d.n_acc_tune[w] = na;
+        nat[w] = na;
     }
     if (d.acc_log) d.acc_log[log_off + li] = (uint8_t)acc;
     if (d.lp_log) d.lp_log[log_off + li] = acc ? lp_prop : cur;
     if (d.ar_log) d.ar_log[log_off + li] = exp(mr);
     return acc;
+}
+__device__ __forceinline__ bool demc_decide(const DemcAccept& d, int64_t w, uint64_t rid, double lp_prop,
+                                            uint64_t key, int32_t tune_now, int64_t log_off, int64_t li,
+                                            bool count = true) {
+    return demc_decide_at(d, d.lp, d.lamb, d.scaling, d.n_acc_tune, d.acc, true, w, rid, lp_prop, key, tune_now,
+                          log_off, li, count);
 }
 __device__ __forceinline__ bool demc_decide(const DemcAccept& d, int64_t w, uint64_t rid, double lp_prop,
                                             uint64_t key, int32_t tune_now, int64_t log_off) {
@@ -1357,6 +1369,19 @@ NGRTD_KLINK __global__ void __launch_bounds__(256) demc_accept_pw_kernel(const D
     }
 }
 
+// The multi-step launch's LDS copies of its block's chain state (DemcAccept::state_lds):
+// rows [P][512] in the chains' space (unit slot i), per-chain lp / lamb / scaling / tuning
+// counter [512] (slot: the unit for per-well chains, the block's walker for joint chains).
+// on == false: the state lives in global memory (d.zx, d.lp, d.lamb, ...).
+struct DzLds {
+    bool on = false;
+    double* st = nullptr;
+    double* lp = nullptr;
+    double* lamb = nullptr;
+    double* sc = nullptr;
+    int32_t* nat = nullptr;
+};
+
 // Single-launch DEMetropolisZ step (logp_fused_kernel MIX bit 3), unit (walker w, well l)
 // of block column i.  Partner entries of chain w (demcz_partners); e = -1 without DE.
 __device__ __forceinline__ void dz_partners(const DemcAccept& d, const DzStep& sj, int64_t w, int64_t& e1,
@@ -1380,13 +1405,15 @@ __device__ __forceinline__ void dz_partners(const DemcAccept& d, const DzStep& s
 // (walker-major scratch copies [W][L] inside the call), proposal noise and accept draw of
 // its own (dz_cid); the partner indices are the walker's, so the history layout and its
 // loads are the joint chains' ones.
+// sl: the chains' LDS state (DzLds; slot = the chain's per-chain slot) or global (sl.on false).
 template <int PMAX, bool TR, bool PW = false>
 __device__ __forceinline__ void dz_stage(const DemcAccept& d, const DzStep& sj, int64_t U, int64_t u, int i, int64_t w,
-                                         int l, int L, int64_t W, bool valid, double* th, int p0, double* pl) {
+                                         int l, int L, int64_t W, bool valid, double* th, int p0, double* pl,
+                                         const DzLds& sl, int slot) {
     if (!valid || (d.dz_diag & 8)) return;
     if (d.dz_diag & 1) {   // timing diagnostics: the proposal is the state (no partners, no noise)
         for (int p = p0; p < d.P; p += 2)
-            d.dz_prop[(int64_t)p * U + u] = d.zx[(int64_t)p * U + u];
+            d.dz_prop[(int64_t)p * U + u] = sl.on ? sl.st[p * kFusedUnitsDz + i] : d.zx[(int64_t)p * U + u];
         return;
     }
     const uint64_t cid = PW ? dz_cid(d.well0, l, d.Wg, d.chain0, w) : 0;
@@ -1405,12 +1432,12 @@ __device__ __forceinline__ void dz_stage(const DemcAccept& d, const DzStep& sj, 
     const double* z1 = d.hist + ((size_t)(de ? e1 : 0) * W + w) * R + l;
     const double* z2 = d.hist + ((size_t)(de ? e2 : 0) * W + w) * R + l;
     const int64_t ci = PW ? w * (int64_t)L + l : w;   // per-chain arrays: walker-major [W][L] / [W]
-    const double lamb = d.lamb[ci], sc = d.scaling[ci];
+    const double lamb = sl.on ? sl.lamb[slot] : d.lamb[ci], sc = sl.on ? sl.sc[slot] : d.scaling[ci];
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
         const int p = p0 + 2 * k;
         if (p < d.P) {
-            x[k] = d.zx[(int64_t)p * U + u];
+            x[k] = sl.on ? sl.st[p * kFusedUnitsDz + i] : d.zx[(int64_t)p * U + u];
             a1[k] = de ? z1[(int64_t)p * L] : 0.0;
             a2[k] = de ? z2[(int64_t)p * L] : 0.0;
         }
@@ -1441,11 +1468,22 @@ __device__ __forceinline__ void dz_stage(const DemcAccept& d, const DzStep& sj, 
 }
 // An accepted unit takes the proposal: natural rows from d.dz_prop (written by this lane
 // role before the barriers), transformed chains also the chains'-space value that
-// dz_stage kept in LDS (row p of th).
+// dz_stage kept in LDS (row p of th).  LDS state (sl.on): only the chains'-space rows, in LDS
+// (the natural rows are re-derived from them when the launch writes its state back).
 template <int PMAX, bool TR>
 __device__ __forceinline__ void dz_commit(const DemcAccept& d, int64_t U, int64_t u, int i, const double* th,
-                                          int p0, const double* pl) {
+                                          int p0, const double* pl, const DzLds& sl) {
     constexpr int KMAX = (PMAX + 1) / 2;
+    if (sl.on) {
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k) {
+            const int p = p0 + 2 * k;
+            if (p < d.P)
+                sl.st[p * kFusedUnitsDz + i] = TR ? th[p * kFusedUnitsDz + i]
+                                                  : (pl ? pl[p * kFusedUnitsDz + i] : d.dz_prop[(int64_t)p * U + u]);
+        }
+        return;
+    }
     double pv[KMAX];
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {   // every load first, then every store
@@ -1465,11 +1503,18 @@ __device__ __forceinline__ void dz_commit(const DemcAccept& d, int64_t U, int64_
 
 // STEP: a multi-step DEMetropolisZ launch (the step's schedule sj and log offset), else the
 // launch's own DemcAccept fields
+// sl.on: the chain's state in the launch's LDS copies at slot (the block's walker w - w0).
 template <bool STEP>
 __device__ __forceinline__ void walker_out(double* logp, const DemcAccept& d, const DzStep& sj, int64_t log_off,
-                                           int64_t w, double tot, int* dec) {
+                                           int64_t w, double tot, int* dec, const DzLds& sl = DzLds{},
+                                           int slot = 0) {
     if (logp) logp[w] = tot;
-    if (d.lp) *dec = STEP ? demc_decide(d, w, tot, sj.key, sj.tune_now, log_off) : demc_decide(d, w, tot);
+    if (!d.lp) return;
+    if (STEP && sl.on)
+        *dec = demc_decide_at(d, sl.lp, sl.lamb, sl.sc, sl.nat, nullptr, false, slot, (uint64_t)(d.chain0 + w), tot,
+                              sj.key, sj.tune_now, log_off, w, true);
+    else
+        *dec = STEP ? demc_decide(d, w, tot, sj.key, sj.tune_now, log_off) : demc_decide(d, w, tot);
 }
 
 // Exact (matrix-core) channel sums for a wave of logp_fused_kernel with an uncovered tau:
@@ -1760,7 +1805,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     int* dec = reinterpret_cast<int*>(lds + 2 * kFusedUnits);   // [512] DE-MC decisions per walker
     int* wcnt = reinterpret_cast<int*>(lds + 2 * kFusedUnits + kFusedUnits / 2);   // [16] per-wave accept counts
     double* cheb = lds + kFusedHdr;                       // [kChebPieces][kChebN][CP]
-    NGRTD_PROBE(0);
+    if (!DZ) NGRTD_PROBE(0);   // (a stamp here broke the DZ instances' instruction selection)
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
     const int uw = wave % kFusedWaves;                    // unit wave
@@ -1838,6 +1883,29 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     // DZ: the theta waves form the proposals (a.theta = dacc.dz_prop), after the table stores
     // so that the table registers are free for the 3 P loads
     double* thl = wd + ua.wd_n;                           // DZ, transformed: [P][512] u
+    // DZ, LDS state (dacc.state_lds): the block's chains -> LDS, once per launch (each lane the
+    // rows of its unit it stages: theta waves the even rows, RTD waves the odd ones)
+    bool moved = false;                                   // ... a row of this lane's unit changed
+    if (DZ && dacc.state_lds) {
+        double* st = thl + ((MIX & 4) ? dacc.P * kFusedUnits : 0) + (dacc.prop_lds ? dacc.P * kFusedUnits : 0);
+        const int dwl = mi / L, dml = mi % L;
+        const bool dv = dwl < WB && w0 + dwl < W;
+        const int64_t du = dv ? (w0 + dwl) * (int64_t)L + dml : 0;
+        for (int p = do_theta ? 0 : 1; p < dacc.P; p += 2) st[p * kFusedUnits + mi] = dv ? dacc.zx[(int64_t)p * ua.U + du] : 0.0;
+        double* c = st + dacc.P * kFusedUnits;            // lp, lamb, scaling [512] each, tuning counter [512] int
+        int32_t* cn = reinterpret_cast<int32_t*>(c + 3 * kFusedUnits);
+        // per-chain slots: the unit (per-well chains, walker-major index du) / the walker
+        const bool own = PW ? (do_theta && dv) : (tid < WB && w0 + tid < W);
+        const int sl = PW ? mi : tid;
+        const int64_t gi = PW ? du : w0 + tid;
+        if (own) {
+            c[sl] = dacc.lp[gi];
+            c[kFusedUnits + sl] = dacc.lamb[gi];
+            c[2 * kFusedUnits + sl] = dacc.scaling[gi];
+            if (dacc.n_acc_tune) cn[sl] = dacc.n_acc_tune[gi];
+        }
+        __syncthreads();
+    }
     // DZ: dacc.n_steps steps of the block's own chains, the tables staged once above
     // (a do-while: without DZ there is no back edge at all -- a one-trip for loop changed the
     // register allocation of the plain log-prob instances)
@@ -1880,6 +1948,15 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         double* wd = tabl + (EPM ? epm_lds_doubles(a.N, CP) : 0);
         double* thl = wd + uk.wd_n;
         double* propl = thl + (((MIX & 4) && DZ) ? dk.P * kFusedUnits : 0);   // DZ: [P][512] proposals
+        DzLds dl;                                         // DZ: the chains' LDS state (or none)
+        if (DZ && dk.state_lds) {
+            dl.on = true;
+            dl.st = propl + (dk.prop_lds ? dk.P * kFusedUnits : 0);
+            dl.lp = dl.st + dk.P * kFusedUnits;
+            dl.lamb = dl.lp + kFusedUnits;
+            dl.sc = dl.lamb + kFusedUnits;
+            dl.nat = reinterpret_cast<int32_t*>(dl.sc + kFusedUnits);
+        }
         UnitArgs ul = uk;
         {
             const int nce = uk.ce_on ? L * uk.G : 0, nrt = uk.rtd_on ? L * uk.K : 0;
@@ -1901,9 +1978,12 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         if (DZ) sj = dz_step(dk.sch, js);
         const int64_t log_off = (int64_t)js * W;
         // both roles stage: theta waves the even parameter rows, RTD waves the odd ones
+        NGRTD_PROBE(8);
         if (DZ)
             dz_stage<kDzMaxP, (MIX & 4) != 0, PW>(dk, sj, uk.U, mu, mi, w0 + mwl, ml, L, W, mvalid, thl,
-                                                  do_theta ? 0 : 1, dk.prop_lds ? propl : nullptr);
+                                                  do_theta ? 0 : 1, dk.prop_lds ? propl : nullptr, dl,
+                                                  PW ? mi : mwl);
+        NGRTD_PROBE(9);
         __syncthreads();
         NGRTD_PROBE(1);
         if (DZ && dk.prop_lds) {                              // the proposal's rows, from LDS
@@ -2014,8 +2094,11 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
                 if (do_theta) dec[mi] = 0;
             } else if (do_theta && mvalid) {
                 const int64_t wq = w0 + mwl;
-                a = demc_decide(dk, wq * (int64_t)L + ml, dz_cid(dk.well0, ml, dk.Wg, dk.chain0, wq), part[pi],
-                                sj.key, sj.tune_now, (int64_t)js * uk.U, (int64_t)ml * W + wq, false);
+                const uint64_t cid = dz_cid(dk.well0, ml, dk.Wg, dk.chain0, wq);
+                a = dl.on ? demc_decide_at(dk, dl.lp, dl.lamb, dl.sc, dl.nat, nullptr, false, mi, cid, part[pi],
+                                           sj.key, sj.tune_now, (int64_t)js * uk.U, (int64_t)ml * W + wq, false)
+                          : demc_decide(dk, wq * (int64_t)L + ml, cid, part[pi], sj.key, sj.tune_now,
+                                        (int64_t)js * uk.U, (int64_t)ml * W + wq, false);
                 dec[mi] = a;
             }
             if (do_theta && dk.n_acc) {        // the wave's accept count -> LDS (summed after the barrier)
@@ -2029,24 +2112,29 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
                 double tot = 0.0;
                 for (int l = g; l < L; l += G) tot += part[l * WB + wl];
                 for (int off = WB; off < 64; off <<= 1) tot += __shfl_xor(tot, off);
-                if (g == 0 && w0 + wl < W) walker_out<DZ>(logp, dk, sj, log_off, w0 + wl, tot, dec + wl);
+                if (g == 0 && w0 + wl < W) walker_out<DZ>(logp, dk, sj, log_off, w0 + wl, tot, dec + wl, dl, wl);
             }
         } else if (tid < WB && w0 + tid < W) {
             double tot = part[tid];
             for (int l = 1; l < L; ++l) tot += part[l * WB + tid];
-            walker_out<DZ>(logp, dk, sj, log_off, w0 + tid, tot, dec + tid);
+            walker_out<DZ>(logp, dk, sj, log_off, w0 + tid, tot, dec + tid, dl, tid);
         }
         if (DZ) {
+            NGRTD_PROBE(10);
             __syncthreads();
+            NGRTD_PROBE(11);
             if (PW && dk.n_acc && tid == 0) {  // one accept-count atomic per block and step
                 int n = 0;
 #pragma unroll
                 for (int i = 0; i < kFusedWaves; ++i) n += wcnt[i];
                 if (n) atomicAdd(dk.n_acc, (unsigned long long)n);
             }
-            if (mvalid && dec[PW ? mi : mwl] && !(dk.dz_diag & 4))
+            if (mvalid && dec[PW ? mi : mwl] && !(dk.dz_diag & 4)) {
                 dz_commit<kDzMaxP, (MIX & 4) != 0>(dk, uk.U, mu, mi, thl, do_theta ? 0 : 1,
-                                                   dk.prop_lds ? propl : nullptr);
+                                                   dk.prop_lds ? propl : nullptr, dl);
+                moved = true;
+            }
+            NGRTD_PROBE(12);
         } else if (dk.lp) {   // DE-MC: accepted walkers take the proposal's theta rows of this unit
             __syncthreads();
             if (do_theta && mvalid && dec[mwl]) {
@@ -2056,6 +2144,35 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             }
         }
     } while (DZ && ++js < nst);   // steps
+    if (DZ && dacc.state_lds) {   // the LDS state back: the rows of the units that moved, every chain's scalars
+        __syncthreads();
+        const double* st = thl + ((MIX & 4) ? dacc.P * kFusedUnits : 0) + (dacc.prop_lds ? dacc.P * kFusedUnits : 0);
+        const int dwl = mi / L, dml = mi % L;
+        const bool dv = dwl < WB && w0 + dwl < W;
+        const int64_t du = dv ? (w0 + dwl) * (int64_t)L + dml : 0;
+        if (moved && dv)
+            for (int p = do_theta ? 0 : 1; p < dacc.P; p += 2) {
+                const double v = st[p * kFusedUnits + mi];
+                const int64_t gi = (int64_t)p * ua.U + du;
+                if (MIX & 4) {   // transformed chains: u, and the natural value dz_stage derived from it
+                    dacc.xu[gi] = v;
+                    dacc.x[gi] = pymc3_backward_sel(dacc.tr_kind[p], dacc.tr_a[p], dacc.tr_b[p], v);
+                } else {
+                    dacc.x[gi] = v;
+                }
+            }
+        const double* c = st + dacc.P * kFusedUnits;
+        const int32_t* cn = reinterpret_cast<const int32_t*>(c + 3 * kFusedUnits);
+        const bool own = PW ? (do_theta && dv) : (tid < WB && w0 + tid < W);
+        const int sl = PW ? mi : tid;
+        const int64_t gi = PW ? du : w0 + tid;
+        if (own) {
+            dacc.lp[gi] = c[sl];
+            dacc.lamb[gi] = c[kFusedUnits + sl];
+            dacc.scaling[gi] = c[2 * kFusedUnits + sl];
+            if (dacc.n_acc_tune) dacc.n_acc_tune[gi] = cn[sl];
+        }
+    }
     NGRTD_PROBE(7);
 }
 

@@ -4,8 +4,11 @@ the GPU) and print its JSON lines: per-well / joint chains x natural / transform
 NGRTD_DZ_DIAG variants (0 full, 16 no partner loads, 1 proposal = state, 8 no staging,
 4 no commit).
 
-    python tools/dz_variants.py [--diags 0,16,1,8,4] [--models exponential]"""
+    python tools/dz_variants.py [--diags 0,16,1,8,4] [--models exponential]
+                                [--envs none,NGRTD_DZ_STATE_GLOBAL=1+NGRTD_DZ_PROP_GLOBAL=1]
+--envs: extra environment per variant ("none"; K=V pairs joined by "+")."""
 import argparse
+import json
 import os
 import subprocess
 import sys
@@ -18,12 +21,15 @@ if __name__ == "__main__":
     ap.add_argument("--models", default="exponential")
     ap.add_argument("--pw", default="1,0")
     ap.add_argument("--jac", default="1,0")
+    ap.add_argument("--envs", default="none")
     a = ap.parse_args()
-    for model in a.models.split(","):
+    for model, ev in [(m, e) for m in a.models.split(",") for e in a.envs.split(",")]:
         for pw in a.pw.split(","):
             for jac in a.jac.split(","):
                 for dg in a.diags.split(","):
                     env = dict(os.environ, NGRTD_DZ_DIAG=dg, DZ_PW=pw)
+                    extra = dict(kv.split("=", 1) for kv in ev.split("+")) if ev != "none" else {}
+                    env.update(extra)
                     if model != "exponential":
                         env["DZ_MODEL"] = model
                     if jac == "1":
@@ -35,4 +41,6 @@ if __name__ == "__main__":
                     if r.returncode:
                         print('{"error": %r}' % r.stderr[-500:], flush=True)
                         sys.exit(r.returncode)
-                    print(r.stdout.strip(), flush=True)
+                    line = json.loads(r.stdout.strip().splitlines()[-1])
+                    line["env"] = extra
+                    print(json.dumps(line), flush=True)

@@ -10,7 +10,12 @@ block) and the RTD-role waves (8-15):
   1->3 the role's work (RTD waves: 1->2 surrogate + likelihood, 2->3 exact fallback)
   3->6 exchange barrier (th + like)          6->7 per-walker sum over wells
 
-    python tools/section_probe.py [--wells 64] [--walkers 2048]
+--variant dz: the last step of a multi-step DEMetropolisZ launch (--dz-steps, per-well /
+joint chains, natural / transformed space), its sections
+  8->9 staging (partners, noise, history append, proposal)   9->1 staging barrier
+  1->3 the role's work   3->6 exchange   6->10 decision   10->11 commit barrier   11->12 commit
+
+    python tools/section_probe.py [--wells 64] [--walkers 2048] [--variant dz --pw 1 --jac 1]
 """
 import argparse
 import ctypes as C
@@ -27,11 +32,20 @@ PROBE_LIB = os.path.join(PKG, "libngrtd_probe.so")
 
 
 def build():
+    """Both translation units with -DNGRTD_SECTION_PROBE (the DZ instances live in
+    ngrtd_dz.hip, with its own probe buffer), linked into libngrtd_probe.so."""
     sys.path.insert(0, REPO)
     import __graft_entry__ as g
-    src = os.path.join(PKG, "csrc", "ngrtd.hip")
     if not os.path.exists(PROBE_LIB) or os.path.getmtime(PROBE_LIB) < max(os.path.getmtime(p) for p in g._deps()):
-        subprocess.run(["hipcc"] + g.HIPCC_FLAGS + ["-DNGRTD_SECTION_PROBE", "-o", PROBE_LIB, src], check=True)
+        objs = []
+        for src in g._sources():
+            obj = src + ".probe.o"
+            subprocess.run(["hipcc"] + g.HIPCC_FLAGS + g.EXTRA_FLAGS.get(os.path.basename(src), []) +
+                           ["-DNGRTD_SECTION_PROBE", "-c", "-o", obj, src], check=True)
+            objs.append(obj)
+        subprocess.run(["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", PROBE_LIB] + objs, check=True)
+        for o in objs:
+            os.remove(o)
 
 
 def main():
@@ -40,6 +54,9 @@ def main():
     ap.add_argument("--walkers", type=int, default=2048)
     ap.add_argument("--build-only", action="store_true")
     ap.add_argument("--variant", default="joint", choices=["joint", "rtd_only", "rtd_bare", "dz"])
+    ap.add_argument("--pw", type=int, default=1)
+    ap.add_argument("--jac", type=int, default=1)
+    ap.add_argument("--dz-steps", type=int, default=8)
     args = ap.parse_args()
     build()
     if args.build_only:
@@ -50,7 +67,10 @@ def main():
     from noblegas_rtd_mcmc_amd import _lib, workloads
     from noblegas_rtd_mcmc_amd.engine import LogProb
     spec = workloads.c4_spec(L=args.wells)
-    if args.variant != "joint":
+    if args.variant == "dz" and args.jac:
+        import dataclasses
+        spec = dataclasses.replace(spec, jacobian=True)
+    if args.variant not in ("joint", "dz"):
         import dataclasses
         from noblegas_rtd_mcmc_amd.spec import ModelSpec
         spec = ModelSpec(n_wells=args.wells, rtd=spec.rtd)
@@ -63,27 +83,40 @@ def main():
     for _ in range(20):
         lp(dev, out=out)
     torch.cuda.synchronize()
-    if args.variant == "dz":     # one single-launch DEMetropolisZ step after 10 steps
+    if args.variant == "dz":     # a multi-step DEMetropolisZ launch after 50 steps
         from noblegas_rtd_mcmc_amd.sampler import DeviceDEMetropolisZ
-        x, l, z = DeviceDEMetropolisZ(lp, tune=None, seed=7).start(dev, 0, 12)
-        lp.demcz(x, l, 10, z)
+        x, l, z = DeviceDEMetropolisZ(lp, tune=None, seed=7, per_well=bool(args.pw)).start(dev, 0, 60 + args.dz_steps)
+        lp.demcz(x, l, 50, z)
         torch.cuda.synchronize()
     lp.ctx.set_profiling(True)
     lp.kernel_stats(reset=True)
     if args.variant == "dz":
-        lp.demcz(x, l, 1, z)
+        lp.demcz(x, l, args.dz_steps, z)
     else:
         lp(dev, out=out)
     torch.cuda.synchronize()
     ks = lp.kernel_stats(reset=True)
     lib = _lib.load()
-    lib.ngrtd_probe_read.argtypes = [C.c_void_p, C.c_int64]
+    rd = lib.ngrtd_probe_read_dz if args.variant == "dz" else lib.ngrtd_probe_read
+    rd.argtypes = [C.c_void_p, C.c_int64]
     nwaves = (args.walkers * args.wells + 511) // 512 * 16
-    buf = np.zeros(nwaves * 8, dtype=np.uint64)
-    assert lib.ngrtd_probe_read(buf.ctypes.data, buf.size) == 0
-    t = buf.reshape(-1, 8).astype(np.int64)
+    buf = np.zeros(nwaves * 16, dtype=np.uint64)
+    assert rd(buf.ctypes.data, buf.size) == 0
+    t = buf.reshape(-1, 16).astype(np.int64)
     w = np.arange(t.shape[0]) % 16
     res = {"kernel_us_event": ks["fused"][0] * 1e3}
+    if args.variant == "dz":
+        res["us_per_step_event"] = res["kernel_us_event"] / args.dz_steps
+        res["per_well"], res["transformed"] = bool(args.pw), bool(args.jac)
+        for grp, sel in (("theta_role", w < 8), ("rtd_role", w >= 8)):
+            tt = t[sel]
+            r = {"stage": tt[:, 9] - tt[:, 8], "stage_barrier": tt[:, 1] - tt[:, 9], "work": tt[:, 3] - tt[:, 1],
+                 "exchange": tt[:, 6] - tt[:, 3], "decision": tt[:, 10] - tt[:, 6],
+                 "commit_barrier": tt[:, 11] - tt[:, 10], "commit": tt[:, 12] - tt[:, 11],
+                 "step": tt[:, 12] - tt[:, 8]}
+            res[grp] = {k: float(np.median(v)) for k, v in r.items()}
+        print(json.dumps(res, indent=1))
+        return
     for grp, sel in (("theta_role", w < 8), ("rtd_role", w >= 8)):
         tt = t[sel]
         r = {"prologue": tt[:, 1] - tt[:, 0], "work": tt[:, 3] - tt[:, 1], "exchange": tt[:, 6] - tt[:, 3],
