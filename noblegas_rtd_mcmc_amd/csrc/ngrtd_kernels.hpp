@@ -1049,10 +1049,11 @@ __device__ __forceinline__ void count_accepts(unsigned long long* n, bool acc) {
 // global arrays, or the multi-step launch's LDS copies, DemcAccept::state_lds; the tuning
 // state exists iff d.n_acc_tune does); acc_out: the decision array, stored iff store_acc.
 // (Flags rather than null tests: a null test of an LDS-derived generic pointer miscompiles.)
-__device__ __forceinline__ bool demc_decide_at(const DemcAccept& d, double* lpa, double* lamb, double* scal,
-                                               int32_t* nat, int32_t* acc_out, bool store_acc, int64_t w,
-                                               uint64_t rid, double lp_prop, uint64_t key, int32_t tune_now,
-                                               int64_t log_off, int64_t li, bool count) {
+template <class F64P, class I32P>
+__device__ __forceinline__ bool demc_decide_at(const DemcAccept& d, F64P lpa, F64P lamb, F64P scal, I32P nat,
+                                               int32_t* acc_out, bool store_acc, int64_t w, uint64_t rid,
+                                               double lp_prop, uint64_t key, int32_t tune_now, int64_t log_off,
+                                               int64_t li, bool count) {
     const double cur = lpa[w];
     const double logu = log(rng_unit(rng_mix(rng_mix(key + 3) + rid)));
     const double mr = lp_prop - cur;
@@ -1301,13 +1302,19 @@ constexpr int kFusedUnitsDz = 512;   // = kFusedUnits (units per logp_fused_kern
 // x + lamb (z1 - z2) + eps, eps = U(-1, 1) S_r scaling from the (row, global chain) stream.
 // e: the noise element (row-major (row, global chain) for joint chains, dz_pw_elem for
 // per-well chains); r: the theta row p L + l (the index of S).
+// x* = x + lamb (z1 - z2) + U(-1, 1) S_r scaling (no DE term while the history has < 2
+// entries); sr = S_r when has_s.
+__device__ __forceinline__ double dz_value_core(bool de, double x, double z1, double z2, double lamb, double sc,
+                                               uint64_t ke, uint64_t e, bool has_s, double sr) {
+    const double y = de ? x + lamb * (z1 - z2) : x;
+    const double u2 = 2.0 * rng_unit(rng_mix(ke + e)) - 1.0;
+    const double eps = (has_s ? u2 * sr : u2) * sc;
+    return y + eps;
+}
 template <class A>
 __device__ __forceinline__ double dz_value_e(const A& d, bool de, double x, double z1, double z2, double lamb,
                                             double sc, uint64_t ke, uint64_t e, int64_t r) {
-    const double y = de ? x + lamb * (z1 - z2) : x;
-    const double u2 = 2.0 * rng_unit(rng_mix(ke + e)) - 1.0;
-    const double eps = (d.S ? u2 * d.S[r] : u2) * sc;
-    return y + eps;
+    return dz_value_core(de, x, z1, z2, lamb, sc, ke, e, d.S != nullptr, d.S ? d.S[r] : 1.0);
 }
 __device__ __forceinline__ double dz_value(const DemcAccept& d, bool de, double x, double z1, double z2, double lamb,
                                           double sc, uint64_t ke, int64_t r, int64_t chain) {
@@ -1373,13 +1380,18 @@ NGRTD_KLINK __global__ void __launch_bounds__(256) demc_accept_pw_kernel(const D
 // rows [P][512] in the chains' space (unit slot i), per-chain lp / lamb / scaling / tuning
 // counter [512] (slot: the unit for per-well chains, the block's walker for joint chains).
 // on == false: the state lives in global memory (d.zx, d.lp, d.lamb, ...).
+// LDS-qualified pointers (address space 3): held in a struct, plain pointers lose the
+// address space and every access became a flat load (which waits behind the vector-memory
+// queue, here the partner loads).
+typedef __attribute__((address_space(3))) double lds_f64;
+typedef __attribute__((address_space(3))) int32_t lds_i32;
 struct DzLds {
     bool on = false;
-    double* st = nullptr;
-    double* lp = nullptr;
-    double* lamb = nullptr;
-    double* sc = nullptr;
-    int32_t* nat = nullptr;
+    lds_f64* st = nullptr;
+    lds_f64* lp = nullptr;
+    lds_f64* lamb = nullptr;
+    lds_f64* sc = nullptr;
+    lds_i32* nat = nullptr;
 };
 
 // Single-launch DEMetropolisZ step (logp_fused_kernel MIX bit 3), unit (walker w, well l)
@@ -1416,52 +1428,70 @@ __device__ __forceinline__ void dz_stage(const DemcAccept& d, const DzStep& sj, 
             d.dz_prop[(int64_t)p * U + u] = sl.on ? sl.st[p * kFusedUnitsDz + i] : d.zx[(int64_t)p * U + u];
         return;
     }
-    const uint64_t cid = PW ? dz_cid(d.well0, l, d.Wg, d.chain0, w) : 0;
+    // every field of d into a local before the first store: d is read through an opaque
+    // kernarg pointer that a store may alias, so a field read after a store is re-loaded and
+    // waited for; the role's row parity made wave-uniform so that the per-row kernarg reads
+    // (transform kinds and bounds) stay scalar
+    const int P = d.P, dg = d.dz_diag;
+    const int q0 = __builtin_amdgcn_readfirstlane(p0);
+    const double* const S = d.S;
+    const double* const zx = d.zx;
+    double* const hist = d.hist;
+    double* const prop = d.dz_prop;
+    const int64_t Wg = d.Wg, ch0 = d.chain0;
+    const uint64_t cid = PW ? dz_cid(d.well0, l, Wg, ch0, w) : 0;
     // partner entries: keyed by the walker (chain0 + w) for joint and per-well chains alike --
     // the wells of one walker draw the same history indices (each from its own history), so
     // a wave (one walker's wells) reads two contiguous entries, as the joint chains do
     int64_t e1, e2;
     dz_partners(d, sj, w, e1, e2);
-    if (d.dz_diag & 16) e1 = e2 = -1;   // timing diagnostics: no partner loads (noise only)
+    if (dg & 16) e1 = e2 = -1;   // timing diagnostics: no partner loads (noise only)
     const bool de = e1 >= 0;
     constexpr int KMAX = (PMAX + 1) / 2;
-    double x[KMAX], a1[KMAX], a2[KMAX];
+    double x[KMAX], a1[KMAX], a2[KMAX], sr[KMAX], ta[KMAX], tb[KMAX];
+    int tk[KMAX];
     // row p of entry e at (e W + w) R + p L + l (R = P L), per-well chains too: a wave (one
     // walker's wells) reads 512-B runs of the walker's two partner entries
-    const int64_t R = (int64_t)d.P * L;
-    const double* z1 = d.hist + ((size_t)(de ? e1 : 0) * W + w) * R + l;
-    const double* z2 = d.hist + ((size_t)(de ? e2 : 0) * W + w) * R + l;
+    const int64_t R = (int64_t)P * L;
+    const double* z1 = hist + ((size_t)(de ? e1 : 0) * W + w) * R + l;
+    const double* z2 = hist + ((size_t)(de ? e2 : 0) * W + w) * R + l;
     const int64_t ci = PW ? w * (int64_t)L + l : w;   // per-chain arrays: walker-major [W][L] / [W]
     const double lamb = sl.on ? sl.lamb[slot] : d.lamb[ci], sc = sl.on ? sl.sc[slot] : d.scaling[ci];
 #pragma unroll
-    for (int k = 0; k < KMAX; ++k) {
-        const int p = p0 + 2 * k;
-        if (p < d.P) {
-            x[k] = sl.on ? sl.st[p * kFusedUnitsDz + i] : d.zx[(int64_t)p * U + u];
+    for (int k = 0; k < KMAX; ++k) {   // every load first
+        const int p = q0 + 2 * k;
+        if (p < P) {
+            x[k] = sl.on ? sl.st[p * kFusedUnitsDz + i] : zx[(int64_t)p * U + u];
             a1[k] = de ? z1[(int64_t)p * L] : 0.0;
             a2[k] = de ? z2[(int64_t)p * L] : 0.0;
+            sr[k] = S ? S[(int64_t)p * L + l] : 1.0;
+            if (TR) {
+                tk[k] = d.tr_kind[p];
+                ta[k] = d.tr_a[p];
+                tb[k] = d.tr_b[p];
+            }
         }
     }
     // an entry appended in this launch is the state itself (as demcz_propose_kernel)
     const bool c1 = e1 == sj.at, c2 = e2 == sj.at;
-    double* hrow = d.hist + ((size_t)(sj.at < 0 ? 0 : sj.at) * W + w) * R + l;
+    double* hrow = hist + ((size_t)(sj.at < 0 ? 0 : sj.at) * W + w) * R + l;
     const uint64_t ke = rng_mix(sj.key + 2);
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
-        const int p = p0 + 2 * k;
-        if (p < d.P) {
-            if (sj.at >= 0 && !(d.dz_diag & 2)) hrow[(int64_t)p * L] = x[k];
-            const uint64_t el = PW ? dz_pw_elem(cid, p) : (uint64_t)((int64_t)p * L + l) * (uint64_t)d.Wg +
-                                                          (uint64_t)(d.chain0 + w);
-            double v = dz_value_e(d, de, x[k], c1 ? x[k] : a1[k], c2 ? x[k] : a2[k], lamb, sc, ke, el,
-                                  (int64_t)p * L + l);
+        const int p = q0 + 2 * k;
+        if (p < P) {
+            if (sj.at >= 0 && !(dg & 2)) hrow[(int64_t)p * L] = x[k];
+            const uint64_t el = PW ? dz_pw_elem(cid, p) : (uint64_t)((int64_t)p * L + l) * (uint64_t)Wg +
+                                                          (uint64_t)(ch0 + w);
+            double v = dz_value_core(de, x[k], c1 ? x[k] : a1[k], c2 ? x[k] : a2[k], lamb, sc, ke, el, S != nullptr,
+                                     sr[k]);
             // transformed chains: the natural-space value the log-prob reads (and v itself,
             // the chains'-space value, for dz_commit)
             if (TR) {
                 th[p * kFusedUnitsDz + i] = v;
-                v = pymc3_backward_sel(d.tr_kind[p], d.tr_a[p], d.tr_b[p], v);
+                v = pymc3_backward_sel(tk[k], ta[k], tb[k], v);
             }
-            d.dz_prop[(int64_t)p * U + u] = v;
+            prop[(int64_t)p * U + u] = v;
             if (pl) pl[p * kFusedUnitsDz + i] = v;
         }
     }
@@ -1951,11 +1981,11 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         DzLds dl;                                         // DZ: the chains' LDS state (or none)
         if (DZ && dk.state_lds) {
             dl.on = true;
-            dl.st = propl + (dk.prop_lds ? dk.P * kFusedUnits : 0);
+            dl.st = (lds_f64*)(propl + (dk.prop_lds ? dk.P * kFusedUnits : 0));
             dl.lp = dl.st + dk.P * kFusedUnits;
             dl.lamb = dl.lp + kFusedUnits;
             dl.sc = dl.lamb + kFusedUnits;
-            dl.nat = reinterpret_cast<int32_t*>(dl.sc + kFusedUnits);
+            dl.nat = (lds_i32*)(dl.sc + kFusedUnits);
         }
         UnitArgs ul = uk;
         {
