@@ -1642,30 +1642,52 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
     constexpr int CP = cheb_cp(C), S = kEpmBlock;
     const int N = a.N;
     const double beta = eta / tau;
-    const int f = epm_first(tau * (1 - (1 / eta)), a.tp0, a.dtp, N);
+    const double ie = 1 / eta;                          // the mask's 1/eta (:189), also tau' = tau / eta
+    const int f = epm_first(tau * (1 - ie), a.tp0, a.dtp, N);
     const int m = f > 1 ? f : 1;
     const int blk = m / S + 1, B = blk * S;
     const double q = fexp(-beta);
     double y[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) y[c] = 0.0;
-    const int kt = (B < N ? B : N) - 1;
-    const int nhead = (a.epm_diag & 1) ? 0 : S;
-#pragma unroll 8
-    for (int i = 0; i < nhead; ++i) {                  // head, top-down Horner (predicated)
-        const int k = kt - i;
-        const bool on = k >= m;
-        double rv[C];
-        epm_row_load<C>(tabl + epm_row(on ? k : 0, CP), rv);
+    // head: the S rows of m's block [B - S, B), bottom-up with the weight w = q^(k - m) for
+    // k >= m and 0 below (rows past N are zeros in LDS): one select per row instead of one
+    // per channel, and the rows at fixed offsets from the block's base (no per-row index
+    // arithmetic).  A wave holding a q > 1 or NaN (beta < 0: tau or eta outside every
+    // prior) runs the top-down predicated Horner instead, whose inf / NaN results the
+    // reference's overflowing weights give (w = inf times a zero row would be NaN).
+    if (!(a.epm_diag & 1)) {
+        if (__all(q <= 1.0)) {
+            const double* hb = tabl + epm_row(B - S, CP);
+            double w = 0.0;
 #pragma unroll
-        for (int c = 0; c < C; ++c) {
-            const double t = fma(y[c], q, rv[c]);
-            y[c] = on ? t : y[c];
+            for (int i = 0; i < S; ++i) {
+                const int k = B - S + i;
+                w = k == m ? 1.0 : w * q;
+                double rv[C];
+                epm_row_load<C>(hb + i * CP, rv);
+#pragma unroll
+                for (int c = 0; c < C; ++c) y[c] = fma(rv[c], w, y[c]);
+            }
+        } else {
+            const int kt = (B < N ? B : N) - 1;
+#pragma unroll 4
+            for (int i = 0; i < S; ++i) {
+                const int k = kt - i;
+                const bool on = k >= m;
+                double rv[C];
+                epm_row_load<C>(tabl + epm_row(on ? k : 0, CP), rv);
+#pragma unroll
+                for (int c = 0; c < C; ++c) {
+                    const double t = fma(y[c], q, rv[c]);
+                    y[c] = on ? t : y[c];
+                }
+            }
         }
     }
     const bool tail = B < N;
     double ex = 0.0;
-    const double taup = 1.0 / beta;
+    const double taup = tau * ie;
     int pc = (tail && a.epm) ? epm_piece(taup, ex) - a.epm_p0 : -1;
     pc = (unsigned)pc < (unsigned)a.epm_np ? pc : -1;
     const bool bad = mvalid && tail && pc < 0;
@@ -1894,7 +1916,10 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         const double2* src = reinterpret_cast<const double2*>(a.tab);
         double2* dst = reinterpret_cast<double2*>(tabl);
         constexpr int RB = kEpmBlock * CP / 2, SB = epm_blk_stride(CP) / 2;   // double2 per block / padded
-        for (int i = tid; i < a.N * CP / 2; i += NTH) dst[(i / RB) * SB + i % RB] = src[i];
+        // whole blocks: the rows past N of the last block are zeros (epm_sums reads every row
+        // of a unit's head block, weighting the ones before its first age by 0)
+        const int n2 = (a.N + kEpmBlock - 1) / kEpmBlock * RB, nv = a.N * CP / 2;
+        for (int i = tid; i < n2; i += NTH) dst[(i / RB) * SB + i % RB] = i < nv ? src[i] : double2{0.0, 0.0};
     }
 #pragma unroll
     for (int r = 0; r < kWdRegs; ++r) {
