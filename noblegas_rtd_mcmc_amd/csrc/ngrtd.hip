@@ -380,7 +380,7 @@ static int cheb_prepare(ngrtd_ctx* ctx, TableDev& tab, double d01) {
 // the pieces.  Used only if every table validates (else the plan keeps the multi-kernel path).
 static int epm_prepare(ngrtd_ctx* ctx, TableDev& tab, int N, int p_lo, int p_hi) {
     tab.epm_ok = false;
-    const int C = tab.C, CP = cheb_cp(C), S = kEpmBlock, n = kChebN;
+    const int C = tab.C, S = kEpmBlock, n = kChebN;
     if (C < 1 || C > 5 || tab.cols_host.empty() || N <= S + 1 || p_lo < 0 || p_hi > kEpmPieces || p_hi <= p_lo)
         return NGRTD_OK;
     for (int c = 0; c < C; ++c)
@@ -388,7 +388,9 @@ static int epm_prepare(ngrtd_ctx* ctx, TableDev& tab, int N, int p_lo, int p_hi)
             if (!(v >= 0.0) || !std::isfinite(v)) return NGRTD_OK;   // the relative bound needs A >= 0
     const int nb = (N - 1) / S;                    // b S < N for b = 1..nb
     const int np = p_hi - p_lo;
-    const size_t per = (size_t)n * CP;
+    // the C channel columns only (the kernel sums the normaliser's tail in closed form), rows
+    // packed: a piece is kChebN * C contiguous doubles, read with 16-B loads (kChebN even)
+    const size_t per = (size_t)n * C;
     std::vector<double> h((size_t)nb * np * per, 0.0);
     const long double PI = 3.14159265358979323846264338327950288L;
     std::vector<std::vector<long double>> Tm(n, std::vector<long double>(n, 0.0L));
@@ -397,15 +399,15 @@ static int epm_prepare(ngrtd_ctx* ctx, TableDev& tab, int N, int p_lo, int p_hi)
     for (int j = 2; j < n; ++j)
         for (int k = 0; k < n; ++k)
             Tm[j][k] = (k > 0 ? 2.0L * Tm[j - 1][k - 1] : 0.0L) - Tm[j - 2][k];
-    // tail values of every block at s = 1/tau': out[(b - 1) (C + 1) + c]
+    // tail values of every block at s = 1/tau': out[(b - 1) C + c]
     auto tails = [&](long double sv, std::vector<long double>& out) {
         const long double q = expl(-sv);
-        out.assign((size_t)nb * (C + 1), 0.0L);
-        for (int c = 0; c <= C; ++c) {
+        out.assign((size_t)nb * C, 0.0L);
+        for (int c = 0; c < C; ++c) {
             long double r = 0.0L;
             for (int k = N - 1; k >= S; --k) {
-                r = r * q + (c < C ? (long double)tab.cols_host[c][k] : 1.0L);
-                if (k % S == 0) out[(size_t)(k / S - 1) * (C + 1) + c] = r;
+                r = r * q + (long double)tab.cols_host[c][k];
+                if (k % S == 0) out[(size_t)(k / S - 1) * C + c] = r;
             }
         }
     };
@@ -423,26 +425,26 @@ static int epm_prepare(ngrtd_ctx* ctx, TableDev& tab, int N, int p_lo, int p_hi)
     }
     std::vector<double> worst_t(64, 0.0);
     auto work = [&](int t, int nt) {
-        std::vector<long double> f((size_t)n * nb * (C + 1)), v;
+        std::vector<long double> f((size_t)n * nb * C), v;
         double worst = 0.0;
         for (int p = p_lo + t; p < p_hi; p += nt) {
             for (int k = 0; k < n; ++k) {          // values at the Chebyshev nodes
                 tails(s_of(p, xn[k]), v);
-                std::copy(v.begin(), v.end(), f.begin() + (size_t)k * nb * (C + 1));
+                std::copy(v.begin(), v.end(), f.begin() + (size_t)k * nb * C);
             }
             for (int b = 0; b < nb; ++b)
-                for (int c = 0; c <= C; ++c) {
+                for (int c = 0; c < C; ++c) {
                     long double ch[kChebN];
                     for (int j = 0; j < n; ++j) {
                         long double acc = 0.0L;
                         for (int k = 0; k < n; ++k)
-                            acc += f[((size_t)k * nb + b) * (C + 1) + c] * cs[j][k];
+                            acc += f[((size_t)k * nb + b) * C + c] * cs[j][k];
                         ch[j] = acc * (j == 0 ? 1.0L : 2.0L) / n;
                     }
                     for (int k = 0; k < n; ++k) {
                         long double m = 0.0L;
                         for (int j = k; j < n; ++j) m += ch[j] * Tm[j][k];
-                        h[(((size_t)b * np + (p - p_lo)) * n + k) * CP + c] = (double)m;
+                        h[(((size_t)b * np + (p - p_lo)) * n + k) * C + c] = (double)m;
                     }
                 }
             const int M = 24;                        // validation: 26 points per piece
@@ -460,10 +462,10 @@ static int epm_prepare(ngrtd_ctx* ctx, TableDev& tab, int N, int p_lo, int p_hi)
                 if (epm_piece(taup, x) != p) { worst = HUGE_VAL; continue; }
                 tails(1.0L / (long double)taup, v);
                 for (int b = 0; b < nb; ++b)
-                    for (int c = 0; c <= C; ++c) {
+                    for (int c = 0; c < C; ++c) {
                         double y = 0.0;
-                        cheb_sums<1>(h.data() + ((size_t)b * np + (p - p_lo)) * per + c, CP, x, &y);
-                        const long double ex = v[(size_t)b * (C + 1) + c];
+                        cheb_sums<1>(h.data() + ((size_t)b * np + (p - p_lo)) * per + c, C, x, &y);
+                        const long double ex = v[(size_t)b * C + c];
                         const double e = (ex > 0) ? (double)(fabsl((long double)y - ex) / ex) : (y == 0.0 ? 0.0 : HUGE_VAL);
                         if (!(e <= worst)) worst = e;   // NaN -> worst = NaN
                     }

@@ -1627,6 +1627,36 @@ __device__ __forceinline__ void epm_row_load(const double* row, double* v) {
     }
 }
 
+// The block-tail surrogate of one piece: kChebN rows of C packed channel coefficients
+// (C kChebN doubles, 16-B aligned), read as 16-B chunks in descending order as Horner
+// consumes the rows (top row first).
+template <int C>
+__device__ __forceinline__ void epm_tail_sums(const double* pt, double x, double* y) {
+    constexpr int NF = kChebN * C;
+    static_assert(NF % 2 == 0, "pieces of whole 16-B chunks");
+    const double2* p2 = reinterpret_cast<const double2*>(pt);
+    double f[NF];
+    int next = NF / 2 - 1;                              // next chunk to load (descending)
+#pragma unroll
+    for (int k = kChebN - 1; k >= 0; --k) {
+#pragma unroll
+        for (int i = NF / 2 - 1; i >= 0; --i)
+            if (i <= next && 2 * i + 1 >= k * C) {       // compile-time after unrolling
+                const double2 t = p2[i];
+                f[2 * i] = t.x;
+                f[2 * i + 1] = t.y;
+            }
+        next = (k * C) / 2 - 1 < next ? (k * C) / 2 - 1 : next;
+        if (k == kChebN - 1) {
+#pragma unroll
+            for (int c = 0; c < C; ++c) y[c] = f[k * C + c];
+        } else {
+#pragma unroll
+            for (int c = 0; c < C; ++c) y[c] = fma(y[c], x, f[k * C + c]);
+        }
+    }
+}
+
 // exp_pist_flow channel sums of one unit (numerators num_c and normaliser den, as
 // rtd_conc_kernel's EPM finalise: conc = (A + J B) / den):
 //   f = first unmasked age (epm_first, the exact mask of :189), m = max(f, 1),
@@ -1695,8 +1725,8 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
 #pragma unroll
     for (int c = 0; c < C; ++c) tl[c] = 0.0;
     if (tail && !(a.epm_diag & 2)) {
-        const double* pt = a.epm + ((size_t)(blk - 1) * a.epm_np + (pc < 0 ? 0 : pc)) * (size_t)(kChebN * CP);
-        cheb_sums<C>(pt, CP, ex, tl);
+        const double* pt = a.epm + ((size_t)(blk - 1) * a.epm_np + (pc < 0 ? 0 : pc)) * (size_t)(kChebN * C);
+        epm_tail_sums<C>(pt, ex, tl);
     }
     if (__any(bad) && !(a.epm_diag & 4)) {              // exact tails of the uncovered lanes
         // tau' below the table (q < e^-16): the tail's terms fall below 1e-400 of its first
