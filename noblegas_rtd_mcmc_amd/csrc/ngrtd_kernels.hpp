@@ -1657,18 +1657,19 @@ __device__ __forceinline__ void epm_tail_sums(const double* pt, double x, double
     }
 }
 
-// exp_pist_flow channel sums of one unit (numerators num_c and normaliser den, as
+// exp_pist_flow channel sums of one unit (numerators num_c and normaliser den = dn / dd, as
 // rtd_conc_kernel's EPM finalise: conc = (A + J B) / den):
 //   f = first unmasked age (epm_first, the exact mask of :189), m = max(f, 1),
 //   Y_c = sum_{k >= m} A_{c,k} q^(k - m), q = exp(-beta), beta = eta / tau
 //       = head (ages [m, min(B, N)), Horner over the LDS table, B = (m / S + 1) S)
 //         + q^(B - m) T_{B/S}(1 / beta)        (block-tail surrogate, validated per plan)
-//   f >= 1: num = Y, den = G = sum_{j < N - m} q^j;  f = 0: num = A_0 + s01 Y, den = 1 + s01 G.
+//   f >= 1: num = Y, den = G = sum_{j < N - m} q^j;  f = 0: num = A_0 + s01 Y, den = 1 + s01 G,
+//   den returned as dn / dd (dd = e^(-beta) - 1) for the caller's batched reciprocal.
 // Lanes whose tau' = 1 / beta the surrogate does not cover (or NaN) sum their tail exactly;
 // the loop is wave-uniform and runs only when some lane needs it.
 template <int C>
 __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, bool mvalid, double tau, double eta,
-                                         double* num, double& den) {
+                                         double* num, double& dn, double& dd) {
     constexpr int CP = cheb_cp(C), S = kEpmBlock;
     const int N = a.N;
     const double beta = eta / tau;
@@ -1686,6 +1687,7 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
     // arithmetic).  A wave holding a q > 1 or NaN (beta < 0: tau or eta outside every
     // prior) runs the top-down predicated Horner instead, whose inf / NaN results the
     // reference's overflowing weights give (w = inf times a zero row would be NaN).
+    double qB = -1.0;                                   // q^(B - m) from the head's weights (fast path)
     if (!(a.epm_diag & 1)) {
         if (__all(q <= 1.0)) {
             const double* hb = tabl + epm_row(B - S, CP);
@@ -1699,6 +1701,7 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
 #pragma unroll
                 for (int c = 0; c < C; ++c) y[c] = fma(rv[c], w, y[c]);
             }
+            qB = w * q;                                 // w = q^(B - 1 - m) after the last row
         } else {
             const int kt = (B < N ? B : N) - 1;
 #pragma unroll 4
@@ -1778,22 +1781,25 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
         for (int c = 0; c < C; ++c) tl[c] = bad ? te[c] : tl[c];
     }
     if (tail) {
-        const double qB = fexp(-beta * (double)(B - m));
+        if (qB < 0.0) qB = fexp(-beta * (double)(B - m));
 #pragma unroll
         for (int c = 0; c < C; ++c) y[c] = fma(qB, tl[c], y[c]);
     }
+    // the normaliser as a fraction den = dn / dd (the caller's one batched reciprocal
+    // takes 1 / dn): G = (e^(-beta n) - 1) / (e^(-beta) - 1) over the n = N - m unmasked ages
     const int n = N - m;
-    const double G = (n > 0) ? fexpm1(-beta * (double)n) / fexpm1(-beta) : 0.0;
+    const double e1 = n > 0 ? fexpm1(-beta * (double)n) : 0.0, e2 = n > 0 ? fexpm1(-beta) : 1.0;
     if (f == 0) {
         const double s01 = fexp(-beta * ((1.0 + a.dtp) - a.tp0));
 #pragma unroll
         for (int c = 0; c < C; ++c) num[c] = a.tab0[c] + s01 * y[c];
-        den = 1.0 + s01 * G;
+        dn = fma(s01, e1, e2);                          // (1 + s01 G) e2
     } else {
 #pragma unroll
         for (int c = 0; c < C; ++c) num[c] = y[c];
-        den = G;
+        dn = e1;                                        // G e2
     }
+    dd = e2;
 }
 
 // A kernel argument read through a pointer the compiler cannot see through (an empty asm
@@ -2096,14 +2102,14 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         if (EPM && do_rtd) {
             double conc[kMaxTracer];
             {
-                double num[C], den;
-                epm_sums<C>(a, tabl, mvalid, tau, eta, num, den);
-                const double dr[2] = {den, tp.nub * (uk.rnu_max - uk.rnu_min) + uk.rnu_min};
+                double num[C], dn, dd;
+                epm_sums<C>(a, tabl, mvalid, tau, eta, num, dn, dd);
+                const double dr[2] = {dn, tp.nub * (uk.rnu_max - uk.rnu_min) + uk.rnu_min};
                 double rr[2];
                 batch_recip<2>(dr, rr);
                 double num2[C];
                 if (MIX & 1) piston_num<C>(a, mu, num2);
-                unit_conc<C>(a, mu, num, rr[0], conc, (MIX & 1) ? num2 : nullptr);
+                unit_conc<C>(a, mu, num, dd * rr[0], conc, (MIX & 1) ? num2 : nullptr);
                 like = mvalid ? unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL, &rr[1]) : 0.0;
             }
             if (!FULL && a.conc && mvalid)                        // forward(): model concentrations
