@@ -33,6 +33,20 @@ __device__ __forceinline__ void fm_lds_init() {
 #endif
 }
 
+// a * b + c for a compile-time constant c (the addend of a Horner step).  On the device
+// the constant goes to an SGPR pair (s_mov) and the step is one VOP3 v_fma_f64 reading it;
+// left to the compiler, the addend was materialised into the destination VGPRs (2 v_mov
+// per step, full-rate VALU work) for a v_fmac_f64.  Same IEEE fma either way.
+NGRTD_FM double fma_k(double a, double b, double c) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(NGRTD_NO_FMA_K)   // (NGRTD_NO_FMA_K: A/B builds)
+    double r;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+    return r;
+#else
+    return fma(a, b, c);
+#endif
+}
+
 NGRTD_FM unsigned fm_hi(double x) {
     unsigned long long b;
     __builtin_memcpy(&b, &x, 8);
@@ -60,10 +74,10 @@ NGRTD_FM double fexp(double x) {
     double r = fma(-kd, L2HI, xc);
     r = fma(-kd, L2LO, r);
     double q = 1.0 / 720.0;
-    q = fma(q, r, 1.0 / 120.0);
-    q = fma(q, r, 1.0 / 24.0);
-    q = fma(q, r, 1.0 / 6.0);
-    q = fma(q, r, 0.5);
+    q = fma_k(q, r, 1.0 / 120.0);
+    q = fma_k(q, r, 1.0 / 24.0);
+    q = fma_k(q, r, 1.0 / 6.0);
+    q = fma_k(q, r, 0.5);
     const double p = fma(r * r, q, r);                   // e^r - 1
     const int k = (int)kd;
     const int j = k & 63;
@@ -90,11 +104,11 @@ NGRTD_FM double fexp10(double y) {
     double r = fma(-kd, L2HI, ph);
     r = fma(-kd, L2LO, r) + pl;
     double q = 1.0 / 5040.0;
-    q = fma(q, r, 1.0 / 720.0);
-    q = fma(q, r, 1.0 / 120.0);
-    q = fma(q, r, 1.0 / 24.0);
-    q = fma(q, r, 1.0 / 6.0);
-    q = fma(q, r, 0.5);
+    q = fma_k(q, r, 1.0 / 720.0);
+    q = fma_k(q, r, 1.0 / 120.0);
+    q = fma_k(q, r, 1.0 / 24.0);
+    q = fma_k(q, r, 1.0 / 6.0);
+    q = fma_k(q, r, 0.5);
     const double p = fma(r * r, q, r);                   // e^r - 1
     const int k = (int)kd;
     const int j = k & 63;
@@ -124,12 +138,12 @@ NGRTD_FM double flog(double x) {
     const double f = m - ci;
     const double r = f * NGRTD_FMT[2 * kFmExpN + 3 * i];
     double q = -0.125;
-    q = fma(q, r, 1.0 / 7.0);
-    q = fma(q, r, -1.0 / 6.0);
-    q = fma(q, r, 0.2);
-    q = fma(q, r, -0.25);
-    q = fma(q, r, 1.0 / 3.0);
-    q = fma(q, r, -0.5);
+    q = fma_k(q, r, 1.0 / 7.0);
+    q = fma_k(q, r, -1.0 / 6.0);
+    q = fma_k(q, r, 0.2);
+    q = fma_k(q, r, -0.25);
+    q = fma_k(q, r, 1.0 / 3.0);
+    q = fma_k(q, r, -0.5);
     const double l1p = fma(r * r, q, r);
     const double ed = (double)e;
     const double t1 = fma(ed, LN2_HI, NGRTD_FMT[2 * kFmExpN + 3 * i + 1]);
@@ -153,18 +167,18 @@ NGRTD_FM double fexpm1(double x) {
     double r = fma(-kd, LN2_HI, x);
     r = fma(-kd, LN2_LO, r);
     double p = 1.0 / 87178291200.0;
-    p = fma(p, r, 1.0 / 6227020800.0);
-    p = fma(p, r, 1.0 / 479001600.0);
-    p = fma(p, r, 1.0 / 39916800.0);
-    p = fma(p, r, 1.0 / 3628800.0);
-    p = fma(p, r, 1.0 / 362880.0);
-    p = fma(p, r, 1.0 / 40320.0);
-    p = fma(p, r, 1.0 / 5040.0);
-    p = fma(p, r, 1.0 / 720.0);
-    p = fma(p, r, 1.0 / 120.0);
-    p = fma(p, r, 1.0 / 24.0);
-    p = fma(p, r, 1.0 / 6.0);
-    p = fma(p, r, 0.5);
+    p = fma_k(p, r, 1.0 / 6227020800.0);
+    p = fma_k(p, r, 1.0 / 479001600.0);
+    p = fma_k(p, r, 1.0 / 39916800.0);
+    p = fma_k(p, r, 1.0 / 3628800.0);
+    p = fma_k(p, r, 1.0 / 362880.0);
+    p = fma_k(p, r, 1.0 / 40320.0);
+    p = fma_k(p, r, 1.0 / 5040.0);
+    p = fma_k(p, r, 1.0 / 720.0);
+    p = fma_k(p, r, 1.0 / 120.0);
+    p = fma_k(p, r, 1.0 / 24.0);
+    p = fma_k(p, r, 1.0 / 6.0);
+    p = fma_k(p, r, 0.5);
     const double em = fma(r * r, p, r);                     // e^r - 1
     const double t = ldexp(1.0, (int)kd);                   // exact, |kd| <= 58
     double res = (kd == 0.0) ? em : fma(t, em, t - 1.0);

@@ -65,15 +65,15 @@ NGRTD_HD double lapse_rate_fast(double E) {
     const double x = (E - 2000.0) * (1.0 / 2500.0);
     if (fabs(x) <= 1.0) {
         double b = 0x1.009c0d260cdd0p-48;
-        b = fma(b, x, 0x1.bd2da15efea83p-43);
-        b = fma(b, x, 0x1.0de2196582d5ep-36);
-        b = fma(b, x, 0x1.4ff1690d5a15dp-29);
-        b = fma(b, x, -0x1.0449a1098ab8bp-20);
-        b = fma(b, x, 0x1.121ddef15cb4bp-14);
-        b = fma(b, x, -0x1.0128f0b9dc6d6p-9);
-        b = fma(b, x, 0x1.f57ab080e12f8p-6);
-        b = fma(b, x, -0x1.f2c43bdf3c9eep-3);
-        b = fma(b, x, 0x1.91b05cf635860p-1);
+        b = fma_k(b, x, 0x1.bd2da15efea83p-43);
+        b = fma_k(b, x, 0x1.0de2196582d5ep-36);
+        b = fma_k(b, x, 0x1.4ff1690d5a15dp-29);
+        b = fma_k(b, x, -0x1.0449a1098ab8bp-20);
+        b = fma_k(b, x, 0x1.121ddef15cb4bp-14);
+        b = fma_k(b, x, -0x1.0128f0b9dc6d6p-9);
+        b = fma_k(b, x, 0x1.f57ab080e12f8p-6);
+        b = fma_k(b, x, -0x1.f2c43bdf3c9eep-3);
+        b = fma_k(b, x, 0x1.91b05cf635860p-1);
         return b * 0.000101325;
     }
     return fexp(5.2561 * flog(1 - E * (.0065 / 288.15))) * 0.000101325;
@@ -321,7 +321,7 @@ NGRTD_HD int c0_piece(double nu, int e0, int np, double& x) {
 NGRTD_HD double c0_poly(const double* t, double x) {
     double b = t[kC0N - 1];
 #pragma unroll
-    for (int k = kC0N - 2; k >= 0; --k) b = fma(b, x, t[k]);
+    for (int k = kC0N - 2; k >= 0; --k) b = fma_k(b, x, t[k]);
     return b;
 }
 // table view: t = [np][kC0N] coefficients (null: exact everywhere)
