@@ -1603,12 +1603,18 @@ static int plan_run(ngrtd_plan* p, const double* theta, int64_t W, double* logp,
             NG_CHECK(timed_end(p, prof, st, 2, ev));
         }
     } else if (logp && p->desc.n_wells <= 512) {
-        // per-unit log-prob + per-walker sum over wells, one launch
+        // per-unit log-prob + per-walker sum over wells, one launch.  Blocks of one wave
+        // while the grid would not cover the CUs at 512 threads (the c2 CE plan: 2048
+        // walkers x 3 wells are 16 blocks of 512 threads on 16 CUs, 128 one-wave blocks
+        // on 128): each lane runs one unit's long dependent chain, so spreading the waves
+        // over the CUs is what shortens the launch.
         int LS = 1;
         while (LS < p->desc.n_wells) LS *= 2;
-        const int WB = 512 / LS;
+        int TB = 512;
+        while (TB > 64 && TB > LS && cdiv(W, (int64_t)(TB / LS)) < 256) TB /= 2;
+        const int WB = TB / LS;
         NG_CHECK(timed_begin(p, prof, st, &ev));
-        hipLaunchKernelGGL(unit_walker_kernel, dim3((unsigned)cdiv(W, WB)), dim3(512), (size_t)512 * sizeof(double),
+        hipLaunchKernelGGL(unit_walker_kernel, dim3((unsigned)cdiv(W, WB)), dim3(TB), (size_t)TB * sizeof(double),
                            st, u, WB, LS, logp);
         HIP_TRY(ctx, hipGetLastError());
         NG_CHECK(timed_end(p, prof, st, 1, ev));
