@@ -1548,10 +1548,12 @@ __device__ __forceinline__ void walker_out(double* logp, const DemcAccept& d, co
 }
 
 // Exact (matrix-core) channel sums for a wave of logp_fused_kernel with an uncovered tau:
-// its 64 units as 4 tiles of 16, then this lane's concentrations and RTD likelihood.
+// its 64 units as 4 tiles of 16, then the concentrations and RTD likelihood of the lanes
+// that need them (mine = valid and uncovered): a covered lane keeps its surrogate result, so
+// no lane's value depends on which units share its wave.
 template <int C, bool FULL, bool SEQ, int MIX>
 __device__ __forceinline__ void fused_exact(const RtdArgs& a, const UnitArgs& ul, int WB, int64_t w0, int uw,
-                                            bool mvalid, int64_t mu, int ml, double nub, double* conc,
+                                            bool mine, int64_t mu, int ml, double nub, double* conc,
                                             double& like) {
     constexpr int NT = mfma_tiles(C);
     const int col = threadIdx.x & 15;
@@ -1594,7 +1596,7 @@ __device__ __forceinline__ void fused_exact(const RtdArgs& a, const UnitArgs& ul
         mw.finish(a, y);
         mfma_pick_tile<C>(y, mw.beta, yy, bu);   // tile tq holds this lane's unit
     }
-    if (mvalid) {
+    if (mine) {
         ThetaPre tp;
         tp.nub = nub;
         double num2[C];
@@ -1684,38 +1686,46 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
     // head: the S rows of m's block [B - S, B), bottom-up with the weight w = q^(k - m) for
     // k >= m and 0 below (rows past N are zeros in LDS): one select per row instead of one
     // per channel, and the rows at fixed offsets from the block's base (no per-row index
-    // arithmetic).  A wave holding a q > 1 or NaN (beta < 0: tau or eta outside every
-    // prior) runs the top-down predicated Horner instead, whose inf / NaN results the
-    // reference's overflowing weights give (w = inf times a zero row would be NaN).
+    // arithmetic).  Lanes with q > 1 or NaN (beta < 0: tau or eta outside every prior) take
+    // the top-down predicated Horner instead, whose inf / NaN results the reference's
+    // overflowing weights give (w = inf times a zero row would be NaN); it runs only in
+    // waves holding such a lane and replaces only those lanes' sums, so every lane's result
+    // is its own whatever its wave-mates are (the multi-step sampler's walker-major waves
+    // and the log-prob kernel's well-major waves give the same bits).
     double qB = -1.0;                                   // q^(B - m) from the head's weights (fast path)
     if (!(a.epm_diag & 1)) {
-        if (__all(q <= 1.0)) {
-            const double* hb = tabl + epm_row(B - S, CP);
-            double w = 0.0;
+        const bool qok = q <= 1.0;
+        const double* hb = tabl + epm_row(B - S, CP);
+        double w = 0.0;
 #pragma unroll
-            for (int i = 0; i < S; ++i) {
-                const int k = B - S + i;
-                w = k == m ? 1.0 : w * q;
-                double rv[C];
-                epm_row_load<C>(hb + i * CP, rv);
+        for (int i = 0; i < S; ++i) {
+            const int k = B - S + i;
+            w = k == m ? 1.0 : w * q;
+            double rv[C];
+            epm_row_load<C>(hb + i * CP, rv);
 #pragma unroll
-                for (int c = 0; c < C; ++c) y[c] = fma(rv[c], w, y[c]);
-            }
-            qB = w * q;                                 // w = q^(B - 1 - m) after the last row
-        } else {
+            for (int c = 0; c < C; ++c) y[c] = fma(rv[c], w, y[c]);
+        }
+        qB = qok ? w * q : -1.0;                        // w = q^(B - 1 - m) after the last row
+        if (__any(!qok)) {
             const int kt = (B < N ? B : N) - 1;
+            double yt[C];
+#pragma unroll
+            for (int c = 0; c < C; ++c) yt[c] = 0.0;
 #pragma unroll 4
             for (int i = 0; i < S; ++i) {
                 const int k = kt - i;
-                const bool on = k >= m;
+                const bool on = !qok && k >= m;
                 double rv[C];
                 epm_row_load<C>(tabl + epm_row(on ? k : 0, CP), rv);
 #pragma unroll
                 for (int c = 0; c < C; ++c) {
-                    const double t = fma(y[c], q, rv[c]);
-                    y[c] = on ? t : y[c];
+                    const double t = fma(yt[c], q, rv[c]);
+                    yt[c] = on ? t : yt[c];
                 }
             }
+#pragma unroll
+            for (int c = 0; c < C; ++c) y[c] = qok ? y[c] : yt[c];
         }
     }
     const bool tail = B < N;
@@ -2159,7 +2169,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             NGRTD_PROBE(2);
             if (__any(bad)) {                                     // wave-uniform: exact channel sums
                 // ROLES = 2: one tile per pass keeps the exact path inside the 128-VGPR budget
-                fused_exact<C, FULL, ROLES == 2, MIX>(a, ul, WB, w0, uw, mvalid, mu, ml, tp.nub, conc, like);
+                fused_exact<C, FULL, ROLES == 2, MIX>(a, ul, WB, w0, uw, mvalid && bad, mu, ml, tp.nub, conc, like);
             }
             if (!FULL && a.conc && mvalid)                        // forward(): model concentrations
                 for (int t = 0; t < a.K; ++t) a.conc[(int64_t)t * a.U + mu] = conc[t];
