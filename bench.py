@@ -198,67 +198,27 @@ def main():
     loop.evaluate = lambda out: fast()
     loop.evaluate_n = lambda out, k: fast_n(k)     # N = 1: the K steps in one native call
 
-    # which kernels does one step launch? (one profiled step, before the warm-up so that the
-    # warm-up steps run right up to the timed region's synchronisation)
+    # which kernels does one step launch? (one profiled step)
     lp.ctx.set_profiling(True)
     lp.kernel_stats(reset=True)
     loop.step()
     lp.ctx.set_profiling(False)
     kinds = {k for k, v in lp.kernel_stats(reset=True).items() if v[1]}
     single_kernel = kinds == {"fused"}
-    for _ in range(args.warmup):
-        loop.step()
-    torch.cuda.synchronize()
-    # the ensemble vector of an untimed step: the timed steps must reproduce it bit for bit
-    ref_ens = loop.step().clone() if world > 1 else loop.out.clone()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    # timed region.  Kernel time for the roofline, measured live with HIP events on the
-    # launch stream (torch's current stream, which the plan enqueues on):
-    #  * N = 1 and one kernel per step: one event pair around the whole region, so
-    #    region / steps is that kernel's average duration back to back (as rocprofv3
-    #    --kernel-trace sees it);
-    #  * otherwise the kernels of every k-th step get their own event pairs (read back
-    #    after the region, no host syncs inside it).
-    lp.kernel_stats(reset=True)
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    per_step_events = world > 1 or not single_kernel
-    t0 = time.perf_counter()
-    ev0.record()
-    if per_step_events:
-        for i in range(args.steps):
-            sample = i % args.event_every == 0
-            if sample:
-                lp.ctx.set_profiling(True)
-            loop.step()
-            if sample:
-                lp.ctx.set_profiling(False)
-    else:
-        loop.run(args.steps)
-    ev1.record()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    ks = dict(lp.kernel_stats(reset=True))
-    if not per_step_events:
-        ks["fused"] = (ev0.elapsed_time(ev1), args.steps)
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX) if args.backend == "nccl" else _host_max(t)
-        dt = float(t.item())
-    last = loop.gathered if world > 1 else loop.out
-    if not torch.equal(last.nan_to_num(), ref_ens.nan_to_num()) or \
-            not torch.equal(torch.isnan(last), torch.isnan(ref_ens)):
-        raise SystemExit("bench: the timed steps' log-probs differ from an untimed evaluation")
-    finite_frac = float(torch.isfinite(loop.ensemble()).double().mean())
-    if not finite_frac > 0.5:
-        raise SystemExit("bench: only %.3f of the ensemble log-probs are finite" % finite_frac)
 
+    # the side lines (outside the timed region, reported beside the headline, never as it)
+    # run BEFORE it: the headline region then starts on a GPU that has been busy for
+    # seconds, at the clock a long sampling run holds (a 20-step region
+    # started from an idle GPU measured slower per launch)
+    side = {}
+    if world == 1 and not args.no_exact and spec.rtd.mod_type1 == "exponential" and not spec.rtd.mod_type2 \
+            and lp.info(Wb).get("surrogate"):
+        side.update(exact_line(args, spec, theta, Wb, lp.info(Wb)["channels"], spec.rtd.n_ages))
+    if world == 1 and not args.no_models:
+        try:
+            side["models"] = model_lines(args, gpu)
+        except Exception as e:        # noqa: BLE001
+            side["models"] = {"error": repr(e)}
     # device DEMetropolisZ on every rank (its own chains: no collective), max over ranks
     samp = None
     if not args.no_sampler:
@@ -278,8 +238,58 @@ def main():
                 e["chain_steps_per_s"] = e["walker_steps_per_s"] * e["chains"] / Wb
         if "transformed" in samp:
             samp["us_per_step"] = samp["transformed"]["us_per_step"]
+
+    for _ in range(args.warmup):
+        loop.step()
+    torch.cuda.synchronize()
+    # the ensemble vector of an untimed step: the timed steps must reproduce it bit for bit
+    ref_ens = loop.step().clone() if world > 1 else loop.out.clone()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    # timed region.  Kernel time for the roofline, measured live with HIP events on the
+    # launch stream:
+    #  * N = 1 and one kernel per step: the event pair ngrtd_logp_n records around its K
+    #    launches (LogProb.region_ms), so region / steps is that kernel's average duration
+    #    back to back (as rocprofv3 --kernel-trace sees it);
+    #  * otherwise the kernels of every k-th step get their own event pairs (read back
+    #    after the region, no host syncs inside it).
+    lp.kernel_stats(reset=True)
+    per_step_events = world > 1 or not single_kernel
+    t0 = time.perf_counter()
+    if per_step_events:
+        for i in range(args.steps):
+            sample = i % args.event_every == 0
+            if sample:
+                lp.ctx.set_profiling(True)
+            loop.step()
+            if sample:
+                lp.ctx.set_profiling(False)
+    else:
+        loop.run(args.steps)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    ks = dict(lp.kernel_stats(reset=True))
+    if not per_step_events:
+        ks["fused"] = (lp.region_ms(), args.steps)
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX) if args.backend == "nccl" else _host_max(t)
+        dt = float(t.item())
+    last = loop.gathered if world > 1 else loop.out
+    if not torch.equal(last.nan_to_num(), ref_ens.nan_to_num()) or \
+            not torch.equal(torch.isnan(last), torch.isnan(ref_ens)):
+        raise SystemExit("bench: the timed steps' log-probs differ from an untimed evaluation")
+    finite_frac = float(torch.isfinite(loop.ensemble()).double().mean())
+    if not finite_frac > 0.5:
+        raise SystemExit("bench: only %.3f of the ensemble log-probs are finite" % finite_frac)
+
     if rank == 0:
-        line = report(args, spec, lp, ks, dt, world, W_total, Wb, plan_build_ms, theta, theta_h)
+        line = report(args, spec, lp, ks, dt, world, W_total, Wb, plan_build_ms, theta, theta_h, side)
         line["ensemble_finite_frac"] = finite_frac
         if samp is not None:
             line["sampler"] = samp
@@ -314,7 +324,7 @@ def pmc_summary(kfull, instance=None):
     return {}, None
 
 
-def report(args, spec, lp, ks, dt, world, W_total, Wb, plan_build_ms, theta, theta_h):
+def report(args, spec, lp, ks, dt, world, W_total, Wb, plan_build_ms, theta, theta_h, side):
     import torch
     from noblegas_rtd_mcmc_amd.engine import LogProb
     info = lp.info(Wb)
@@ -332,7 +342,6 @@ def report(args, spec, lp, ks, dt, world, W_total, Wb, plan_build_ms, theta, the
         instance = "logp_fused_kernel<%d, %s, 2, %d>" % (C, "true" if full else "false", mix)
     pmc, pmc_path = pmc_summary(kfull, instance)
     traffic = pmc.get("hbm_bytes_per_launch")        # FETCH_SIZE x 2 (calibrated) + WRITE_SIZE
-    exp_single = spec.rtd.mod_type1 == "exponential" and not spec.rtd.mod_type2
     if info.get("surrogate") and pmc.get("fp64_flop_per_unit"):
         # FP64 work of the launch: PMC-counted FP64 FLOPs per (walker, well) unit of this
         # kernel (SQ_INSTS_VALU_FLOPS_FP64 x 64 lanes, fma = 2) x units
@@ -388,17 +397,13 @@ def report(args, spec, lp, ks, dt, world, W_total, Wb, plan_build_ms, theta, the
         "kernels_ms": {k: v[0] / max(v[1], 1) for k, v in ks.items()},
         "geometry": info,
     }
-    if world == 1 and exp_single and info.get("surrogate") and not args.no_exact:
-        line.update(exact_line(args, spec, theta, Wb, C, N))
+    line.update({k: v for k, v in side.items() if k != "models"})
     # the reference's run length (run_age_mcmc_utils.py:412-417: tune 10 000 + draws 10 000)
     # with the plan build paid once: W S / (S t_step + plan_build)
     S20k = 20000
     line["value_amortized_20k"] = W_total * S20k / (S20k * dt / args.steps + plan_build_ms * 1e-3)
-    if world == 1 and not args.no_models:
-        try:
-            line["models"] = model_lines(args, theta.device.index)
-        except Exception as e:        # noqa: BLE001
-            line["models"] = {"error": repr(e)}
+    if "models" in side:
+        line["models"] = side["models"]
     # PCIe-inclusive rate: theta handed over as host memory (staged H2D per call, results
     # copied back) -- reported beside `value`, never as it
     hs = max(5, args.steps // 20)

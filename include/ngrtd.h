@@ -268,6 +268,11 @@ int ngrtd_logp(ngrtd_plan* plan, const double* theta, int64_t W, double* logp, i
  * holds the last one.  Used by bench.py (N = 1) via distributed.LogpStepLoop.run. */
 int ngrtd_logp_n(ngrtd_plan* plan, const double* theta, int64_t W, double* logp, int64_t n);
 
+/* Device time (ms) between two events the last ngrtd_logp_n call recorded on the plan's
+ * stream before its first and after its last launch (waits for the second).  bench.py's
+ * kernel time for the roofline: the n launches back to back, as rocprofv3 sees them. */
+int ngrtd_plan_region_ms(ngrtd_plan* plan, float* ms);
+
 /* Forward model outputs of the plan (posterior predictive, run_age_mcmc.py:251-319,
  * noble_gas_mcmc.py:645-653): ce_out [G][L][W] (may be NULL), rtd_out [K][L][W]
  * (may be NULL).                                                                     */

@@ -102,6 +102,7 @@ PROTOTYPES = {
     "ngrtd_plan_destroy": (C.c_int, [C.c_void_p]),
     "ngrtd_logp": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int32]),
     "ngrtd_logp_n": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64]),
+    "ngrtd_plan_region_ms": (C.c_int, [C.c_void_p, C.POINTER(C.c_float)]),
     "ngrtd_forward": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int32]),
     "ngrtd_plan_kernel_stats": (C.c_int, [C.c_void_p, _dp, _i64p, C.c_int32, C.c_int32]),
     "ngrtd_plan_info": (C.c_int, [C.c_void_p, C.c_int64, _i64p, C.c_int32]),

@@ -121,6 +121,8 @@ struct ngrtd_plan {
     UnitArgs unit{};
     LaunchStats stats;
     std::vector<PendingTiming> pending;   // event pairs not yet read back (no host sync per launch)
+    hipEvent_t region[2] = {nullptr, nullptr};   // around the last ngrtd_logp_n call's launches
+    bool region_set = false;
 };
 
 static int drain_timings(ngrtd_plan* p);
@@ -1509,6 +1511,8 @@ int ngrtd_plan_destroy(ngrtd_plan* p) {
     if (!p) return NGRTD_ESTATE;
     (void)hipStreamSynchronize(p->ctx->stream);
     (void)drain_timings(p);
+    for (hipEvent_t e : p->region)
+        if (e) p->ctx->event_pool.push_back(e);
     delete p;
     return NGRTD_OK;
 }
@@ -1656,7 +1660,23 @@ int ngrtd_logp_n(ngrtd_plan* p, const double* theta, int64_t W, double* logp, in
     if (!theta || !logp || W < 0 || W > p->max_w || n < 0)
         return set_err(ctx, NGRTD_EINVAL, "bad theta/logp/W (max %lld)/n", (long long)p->max_w);
     if (W == 0) return NGRTD_OK;
+    // one event pair around the n launches (ngrtd_plan_region_ms): the launches' device
+    // time back to back, recorded here so that the caller's timed region pays no
+    // event-object round trips of its own
+    for (hipEvent_t& e : p->region)
+        if (!e) e = ctx->take_event();
+    HIP_TRY(ctx, hipEventRecord(p->region[0], S(ctx)));
     for (int64_t i = 0; i < n; ++i) NG_CHECK(plan_run(p, theta, W, logp, nullptr, nullptr));
+    HIP_TRY(ctx, hipEventRecord(p->region[1], S(ctx)));
+    p->region_set = true;
+    return NGRTD_OK;
+}
+
+int ngrtd_plan_region_ms(ngrtd_plan* p, float* ms) {
+    if (!p || !ms) return NGRTD_EINVAL;
+    if (!p->region_set) return set_err(p->ctx, NGRTD_ESTATE, "no ngrtd_logp_n call to time");
+    HIP_TRY(p->ctx, hipEventSynchronize(p->region[1]));
+    HIP_TRY(p->ctx, hipEventElapsedTime(ms, p->region[0], p->region[1]));
     return NGRTD_OK;
 }
 

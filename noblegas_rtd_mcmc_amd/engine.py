@@ -208,6 +208,13 @@ class LogProb:
             return keep[1]
         return run
 
+    def region_ms(self):
+        """Device time (ms) of the last ``bind_n`` call's launches, back to back: the event
+        pair ngrtd_logp_n recorded around them on the plan's stream (waits for the end)."""
+        ms = C.c_float()
+        self.ctx.check(self.lib.ngrtd_plan_region_ms(self.plan, C.byref(ms)), "ngrtd_plan_region_ms")
+        return float(ms.value)
+
     def forward(self, theta, soa=False):
         """Model outputs: (ce [G][L][W] or None, rtd [K][L][W] or None)."""
         spec = self.spec

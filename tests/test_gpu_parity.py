@@ -500,3 +500,42 @@ def test_full_instance_exact_fallback_in_support():
     assert np.isfinite(ref).all()
     assert close(got[walkers], ref, 1e-12, 1e-9).all(), (got[walkers], ref)
     lp.close()
+
+
+@pytest.mark.parametrize("model", ["exponential", "exp_pist_flow", "exp_pist_flow-piston"])
+def test_unit_logp_independent_of_wave_mates(model):
+    """A unit's log-prob is its own whatever units share its wave: the EPM head's top-down
+    fallback (q > 1: tau or eta < 0) and the exact MFMA fallback replace only their own
+    lanes.  Walkers permuted (so different walkers share each 64-lane wave), with q > 1,
+    NaN and out-of-support tau / eta mixed in: per-unit log-probs permute with them, bit
+    for bit.  (The multi-step sampler maps one walker's wells to a wave, the log-prob
+    kernel one well's walkers: test_gpu_demc's bitwise checks rely on this.)"""
+    import torch
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+    m1, _, m2 = model.partition("-")
+    pn = ["tau1"] + (["tau2", "f1"] if m2 else []) + (["eta1"] if m1 == "exp_pist_flow" else [])
+    spec = wl.c4_spec(L=4, N=1200, mod_type1=m1, mod_type2=m2 or None, par_names=tuple(pn))
+    W = 256
+    th = wl.sample_prior(spec, W, np.random.default_rng(71))
+    rng = np.random.default_rng(72)
+    r_tau = spec.roles.index("tau1")
+    bad = rng.choice(W, 40, replace=False)
+    th[r_tau, :, bad[:10]] = -rng.uniform(1, 50, (10, spec.n_wells))
+    th[r_tau, :, bad[10:15]] = np.nan
+    th[r_tau, :, bad[15:25]] = rng.uniform(1e3, 1e5, (10, spec.n_wells))
+    if m1 == "exp_pist_flow":
+        r_eta = spec.roles.index("eta1")
+        th[r_eta, :, bad[25:35]] = -rng.uniform(0.1, 3, (10, spec.n_wells))
+        th[r_eta, :, bad[35:]] = rng.uniform(1e-3, 0.5, (5, spec.n_wells))
+    lp = LogProb(spec, max_walkers=W)
+    dev = torch.from_numpy(th).cuda()
+    u0 = lp.units(dev).cpu()
+    for seed in (1, 2, 3):
+        perm = torch.from_numpy(np.random.default_rng(seed).permutation(W))
+        u1 = lp.units(dev[:, :, perm.cuda()].contiguous()).cpu()
+        ref = u0[:, perm]
+        same = (u1 == ref) | (torch.isnan(u1) & torch.isnan(ref))
+        assert bool(same.all()), (seed, torch.nonzero(~same)[:8])
+    assert bool(torch.isfinite(u0).any()) and not bool(torch.isfinite(u0).all())
+    lp.close()
