@@ -742,6 +742,13 @@ static int dz_mix(const RtdArgs& a0, const UnitArgs& u, int P, bool transformed)
     if (a.mod[1] == MOD_NONE) return 8 | 4 | mix;   // 12 (exponential), 14 (exp_pist_flow)
     return -1;
 }
+// Every theta row a single-launch step reads is one of ThetaPre's (the 6 CE rows, tau1,
+// nu_rtd: the joint exponential plan), all of them staged in the LDS proposal rows: no
+// second RTD component, eta, D, f1, J, half-life or SF6 rows, no further Beta rows.
+static bool dz_theta_all_lds(const RtdArgs& a, const UnitArgs& u, int P) {
+    return P == 8 && a.row_tau[1] < 0 && a.row_eta[0] < 0 && a.row_eta[1] < 0 && a.row_D[0] < 0 && a.row_D[1] < 0 &&
+           a.row_f1 < 0 && a.row_J < 0 && a.row_thalf < 0 && a.row_lamsf6 < 0 && u.bt_n <= 6;
+}
 static int launch_fused_dz(ngrtd_ctx* ctx, const RtdArgs& a0, const UnitArgs& u, int64_t W, int L, double* logp,
                            hipStream_t st, const DemcAccept& da, int mix) {
     const int WB = kFusedUnits / L;
@@ -760,6 +767,8 @@ static int launch_fused_dz(ngrtd_ctx* ctx, const RtdArgs& a0, const UnitArgs& u,
     d.prop_lds = (lds + pb + (d.state_lds ? sb : 0) <= kFusedMaxLds && !std::getenv("NGRTD_DZ_PROP_GLOBAL")) ? 1 : 0;
     if (d.prop_lds) lds += pb;
     if (d.state_lds) lds += sb;   // after the proposal rows (logp_fused_kernel's carve-up)
+    // no global proposal rows when nothing reads them (NGRTD_DZ_PROP_WRITE=1 writes them, A/B)
+    d.prop_skip = (d.prop_lds && dz_theta_all_lds(a, u, da.P) && !std::getenv("NGRTD_DZ_PROP_WRITE")) ? 1 : 0;
     if (!fused_dz_instance_exists(mix)) return set_err(ctx, NGRTD_EINVAL, "no single-launch DEMetropolisZ instance %d", mix);
     HIP_TRY(ctx, launch_fused_dz_instance(mix, a, u, WB, W, logp, d, lds, kFusedMaxLds, st));
     return NGRTD_OK;

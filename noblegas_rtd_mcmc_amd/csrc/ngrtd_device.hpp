@@ -215,6 +215,11 @@ struct DemcAccept {
     // first step and written back (x, xu for the chains that moved; the per-chain arrays)
     // after the last: per step no state loads, no commit stores, no per-chain round trips
     int32_t state_lds;
+    // 1 (with prop_lds): every theta row the launch reads is one of the LDS proposal rows
+    // (the joint exponential plan: 6 CE rows, tau1, nu_rtd), so dz_stage does not write the
+    // proposals to dz_prop (a state-sized store stream per step) and the exact fallback reads
+    // tau from LDS too
+    int32_t prop_skip;
     struct Sched {
         uint64_t seed;
         int64_t s0;         // steps_done at the launch's first step

@@ -42,7 +42,7 @@ namespace ngrtd {
 // -DNGRTD_SECTION_PROBE): lane 0 of every wave of logp_fused_kernel records the shader
 // clock (s_memtime) at fixed points.  Compiled out of the product library.
 #ifdef NGRTD_SECTION_PROBE
-// slots 0-7: the log-prob sections; 8-12: a DEMetropolisZ step's (the last step of a launch)
+// slots 0-7: the log-prob sections; 8-13: a DEMetropolisZ step's (the last step of a launch)
 constexpr int kProbeSlots = 16;
 __device__ unsigned long long g_probe[8192 * kProbeSlots];
 #define NGRTD_PROBE(k)                                                                        \
@@ -688,11 +688,18 @@ struct MfmaWave {
     ngrtd_v4d acc[NT][R];
 
     __device__ __forceinline__ void init(const RtdArgs& a, const int64_t* uoff) {
-        const int tq = (threadIdx.x & 63) >> 4;
         const double* tau_row = a.theta + (int64_t)a.row_tau[0] * a.U;
+        double tau[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) tau[t] = tau_row[uoff[t]];
+        init_tau(tau);
+    }
+    // ... from the tiles' tau values (the column's unit, tile t)
+    __device__ __forceinline__ void init_tau(const double* tau) {
+        const int tq = (threadIdx.x & 63) >> 4;
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
-            beta[t] = 1. / tau_row[uoff[t]];
+            beta[t] = 1. / tau[t];
             const double q = fexp(-beta[t]);
             const double q2 = q * q;
             q4[t] = q2 * q2;
@@ -1296,6 +1303,15 @@ NGRTD_KLINK __global__ void __launch_bounds__(256) dz_layout_i32_kernel(const in
 }
 
 constexpr int kDzMaxP = 12;          // parameter rows of a single-launch DEMetropolisZ step
+#ifndef NGRTD_DZ_PREFETCH
+#define NGRTD_DZ_PREFETCH 1
+#endif
+constexpr bool kDzPrefetch = NGRTD_DZ_PREFETCH != 0;   // partner rows one step ahead (dz_partner_rows)
+#ifndef NGRTD_DZ_PF_STEP
+#define NGRTD_DZ_PF_STEP 2
+#endif
+// 2: each role prefetches and stages its parity's rows; 1: the theta lanes all of them
+constexpr int kDzPfStep = NGRTD_DZ_PF_STEP;
 constexpr int kFusedUnitsDz = 512;   // = kFusedUnits (units per logp_fused_kernel block)
 
 // One element of a DEMetropolisZ proposal, the arithmetic of demcz_propose_kernel (bitwise):
@@ -1418,6 +1434,100 @@ __device__ __forceinline__ void dz_partners(const DemcAccept& d, const DzStep& s
 // its own (dz_cid); the partner indices are the walker's, so the history layout and its
 // loads are the joint chains' ones.
 // sl: the chains' LDS state (DzLds; slot = the chain's per-chain slot) or global (sl.on false).
+// The unit's partner rows of step sj, rows q0, q0 + STEP, ... (a1 / a2; zeros without a DE
+// term or when !valid): loads only.  The multi-step launch issues step j + 1's rows (every
+// row, STEP = 1, from the unit's theta lane) at the end of step j's log-prob body, so that
+// their HBM latency passes behind the role exchange, the decision and the commit instead of
+// opening step j + 1 (dz_stage_all then reads no partner rows itself).  The entry step j + 1
+// appends (sj.at: the state after step j's commit) is not in memory when they are issued;
+// dz_stage_all substitutes the state for it, as dz_stage does.  Every other entry was appended
+// by this same lane in an earlier step or earlier in this one, so its stores precede these
+// loads in the lane's own order.  Every element is assigned, so that nothing stays live
+// from before the call (the loop-carried registers would otherwise span the log-prob body).
+template <int PMAX, int STEP>
+__device__ __forceinline__ void dz_partner_rows(const DemcAccept& d, const DzStep& sj, int64_t w, int l, int L,
+                                                int64_t W, bool valid, int q0, double* a1, double* a2) {
+    constexpr int KMAX = (PMAX + STEP - 1) / STEP;
+    int64_t e1, e2;
+    dz_partners(d, sj, w, e1, e2);
+    if (d.dz_diag & 16) e1 = e2 = -1;
+    const bool de = valid && e1 >= 0;
+    const int P = d.P;
+    const int64_t R = (int64_t)P * L;
+    const double* z1 = d.hist + ((size_t)(de ? e1 : 0) * W + w) * R + l;
+    const double* z2 = d.hist + ((size_t)(de ? e2 : 0) * W + w) * R + l;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+        const int p = q0 + STEP * k;
+        a1[k] = (de && p < P) ? z1[(int64_t)p * L] : 0.0;
+        a2[k] = (de && p < P) ? z2[(int64_t)p * L] : 0.0;
+    }
+}
+
+// dz_stage with the partner rows prefetched (kDzPrefetch): the lane stages its unit's rows
+// q0, q0 + STEP, ... (STEP = 2: each role its parity's rows, as dz_stage; STEP = 1: every
+// row) from the prefetched partners pf1 / pf2 (dz_partner_rows<PMAX, STEP>, same rows), row
+// by row, the same arithmetic as dz_stage (bitwise); every kernel-argument read before the
+// first store (as dz_stage).
+template <int PMAX, int STEP, bool TR, bool PW>
+__device__ __forceinline__ void dz_stage_all(const DemcAccept& d, const DzStep& sj, int64_t U, int64_t u, int i,
+                                             int64_t w, int l, int L, int64_t W, bool valid, double* th, double* pl,
+                                             const DzLds& sl, int slot, int q0, const double* pf1, const double* pf2) {
+    constexpr int KMAX = (PMAX + STEP - 1) / STEP;
+    if (!valid || (d.dz_diag & 8)) return;
+    const int P = d.P, dg = d.dz_diag;
+    if (dg & 1) {   // timing diagnostics: the proposal is the state (no partners, no noise)
+        for (int p = q0; p < P; p += STEP)
+            d.dz_prop[(int64_t)p * U + u] = sl.on ? sl.st[p * kFusedUnitsDz + i] : d.zx[(int64_t)p * U + u];
+        return;
+    }
+    const double* const S = d.S;
+    const double* const zx = d.zx;
+    double* const hist = d.hist;
+    double* const prop = d.dz_prop;
+    const bool skip_g = d.prop_skip != 0;
+    const int64_t Wg = d.Wg, ch0 = d.chain0;
+    const uint64_t cid = PW ? dz_cid(d.well0, l, Wg, ch0, w) : 0;
+    int64_t e1, e2;
+    dz_partners(d, sj, w, e1, e2);
+    if (dg & 16) e1 = e2 = -1;
+    const bool de = e1 >= 0;
+    const int64_t R = (int64_t)P * L;
+    const int64_t ci = PW ? w * (int64_t)L + l : w;
+    const double lamb = sl.on ? sl.lamb[slot] : d.lamb[ci], sc = sl.on ? sl.sc[slot] : d.scaling[ci];
+    const bool c1 = e1 == sj.at, c2 = e2 == sj.at;   // an entry appended in this launch is the state
+    const uint64_t ke = rng_mix(sj.key + 2);
+    double v[KMAX], vu[TR ? KMAX : 1];
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+        const int p = q0 + STEP * k;
+        if (p < P) {
+            const double x = sl.on ? sl.st[p * kFusedUnitsDz + i] : zx[(int64_t)p * U + u];
+            const double sr = S ? S[(int64_t)p * L + l] : 1.0;
+            const uint64_t el = PW ? dz_pw_elem(cid, p) : (uint64_t)((int64_t)p * L + l) * (uint64_t)Wg +
+                                                          (uint64_t)(ch0 + w);
+            double vv = dz_value_core(de, x, c1 ? x : pf1[k], c2 ? x : pf2[k], lamb, sc, ke, el, S != nullptr, sr);
+            if (TR) {
+                vu[TR ? k : 0] = vv;
+                vv = pymc3_backward_sel(d.tr_kind[p], d.tr_a[p], d.tr_b[p], vv);
+            }
+            v[k] = vv;
+        }
+    }
+    const bool app = sj.at >= 0 && !(dg & 2);
+    double* hrow = hist + ((size_t)(sj.at < 0 ? 0 : sj.at) * W + w) * R + l;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+        const int p = q0 + STEP * k;
+        if (p < P) {
+            if (app) hrow[(int64_t)p * L] = sl.on ? sl.st[p * kFusedUnitsDz + i] : zx[(int64_t)p * U + u];
+            if (TR) th[p * kFusedUnitsDz + i] = vu[TR ? k : 0];
+            if (!skip_g) prop[(int64_t)p * U + u] = v[k];
+            if (pl) pl[p * kFusedUnitsDz + i] = v[k];
+        }
+    }
+}
+
 template <int PMAX, bool TR, bool PW = false>
 __device__ __forceinline__ void dz_stage(const DemcAccept& d, const DzStep& sj, int64_t U, int64_t u, int i, int64_t w,
                                          int l, int L, int64_t W, bool valid, double* th, int p0, double* pl,
@@ -1433,6 +1543,7 @@ __device__ __forceinline__ void dz_stage(const DemcAccept& d, const DzStep& sj, 
     // waited for; the role's row parity made wave-uniform so that the per-row kernarg reads
     // (transform kinds and bounds) stay scalar
     const int P = d.P, dg = d.dz_diag;
+    const bool skip_g = d.prop_skip != 0;
     const int q0 = __builtin_amdgcn_readfirstlane(p0);
     const double* const S = d.S;
     const double* const zx = d.zx;
@@ -1491,7 +1602,7 @@ __device__ __forceinline__ void dz_stage(const DemcAccept& d, const DzStep& sj, 
                 th[p * kFusedUnitsDz + i] = v;
                 v = pymc3_backward_sel(tk[k], ta[k], tb[k], v);
             }
-            prop[(int64_t)p * U + u] = v;
+            if (!skip_g) prop[(int64_t)p * U + u] = v;
             if (pl) pl[p * kFusedUnitsDz + i] = v;
         }
     }
@@ -2012,6 +2123,8 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     // register allocation of the plain log-prob instances)
     const int nst = DZ ? dacc.n_steps : 1;
     int js = 0;
+    // DZ: the next step's partner rows, issued at the end of this step's log-prob body
+    double pf1[(kDzMaxP + kDzPfStep - 1) / kDzPfStep], pf2[(kDzMaxP + kDzPfStep - 1) / kDzPfStep];
     do {
         ThetaPre tp = tp0;                                // DZ: loaded per step below
         double tau = tau0, eta = eta0;
@@ -2080,10 +2193,21 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         const int64_t log_off = (int64_t)js * W;
         // both roles stage: theta waves the even parameter rows, RTD waves the odd ones
         NGRTD_PROBE(8);
-        if (DZ)
+        if (DZ && kDzPrefetch) {
+            // each role stages its rows of the unit from partner rows loaded one step ahead
+            // (the first step of the launch loads its own here)
+            if (js == 0)
+                dz_partner_rows<kDzMaxP, kDzPfStep>(dk, sj, w0 + mwl, ml, L, W, mvalid && (kDzPfStep == 2 || do_theta),
+                                                    do_theta ? 0 : 1, pf1, pf2);
+            if (kDzPfStep == 2 || do_theta)
+                dz_stage_all<kDzMaxP, kDzPfStep, (MIX & 4) != 0, PW>(dk, sj, uk.U, mu, mi, w0 + mwl, ml, L, W, mvalid,
+                                                                     thl, dk.prop_lds ? propl : nullptr, dl,
+                                                                     PW ? mi : mwl, do_theta ? 0 : 1, pf1, pf2);
+        } else if (DZ) {
             dz_stage<kDzMaxP, (MIX & 4) != 0, PW>(dk, sj, uk.U, mu, mi, w0 + mwl, ml, L, W, mvalid, thl,
                                                   do_theta ? 0 : 1, dk.prop_lds ? propl : nullptr, dl,
                                                   PW ? mi : mwl);
+        }
         NGRTD_PROBE(9);
         __syncthreads();
         NGRTD_PROBE(1);
@@ -2168,6 +2292,13 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             }
             NGRTD_PROBE(2);
             if (__any(bad)) {                                     // wave-uniform: exact channel sums
+                if (DZ && dk.prop_skip) {
+                    // the step wrote no global proposal rows: the exact path reads its 64 units'
+                    // tau (all of them this wave's lanes) from a.theta = dz_prop, so the lanes put
+                    // them there first
+                    if (mvalid) const_cast<double*>(a.theta)[(int64_t)a.row_tau[0] * a.U + mu] = tau;
+                    __threadfence_block();
+                }
                 // ROLES = 2: one tile per pass keeps the exact path inside the 128-VGPR budget
                 fused_exact<C, FULL, ROLES == 2, MIX>(a, ul, WB, w0, uw, mvalid && bad, mu, ml, tp.nub, conc, like);
             }
@@ -2175,6 +2306,12 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
                 for (int t = 0; t < a.K; ++t) a.conc[(int64_t)t * a.U + mu] = conc[t];
         }
         NGRTD_PROBE(3);
+        if (DZ && kDzPrefetch)   // the next step's partner rows, theta lanes (loads only; zeros elsewhere and
+                                 // after the last step: unconditional, so no earlier value stays live)
+            dz_partner_rows<kDzMaxP, kDzPfStep>(dk, dz_step(dk.sch, js + 1), w0 + mwl, ml, L, W,
+                                                mvalid && (kDzPfStep == 2 || do_theta) && js + 1 < nst,
+                                                do_theta ? 0 : 1, pf1, pf2);
+        if (DZ) NGRTD_PROBE(13);
         if (!logp && !dk.lp) return;                        // forward() launch: no log-prob
         if (ROLES == 1) {
             part[pi] = th + like;

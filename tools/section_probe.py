@@ -13,7 +13,8 @@ block) and the RTD-role waves (8-15):
 --variant dz: the last step of a multi-step DEMetropolisZ launch (--dz-steps, per-well /
 joint chains, natural / transformed space), its sections
   8->9 staging (partners, noise, history append, proposal)   9->1 staging barrier
-  1->3 the role's work   3->6 exchange   6->10 decision   10->11 commit barrier   11->12 commit
+  1->3 the role's work   3->13 the next step's partner-row loads issued (kDzPrefetch builds)
+  13->6 exchange   6->10 decision   10->11 commit barrier   11->12 commit
 
     python tools/section_probe.py [--wells 64] [--walkers 2048] [--variant dz --pw 1 --jac 1]
 """
@@ -31,19 +32,27 @@ PKG = os.path.join(REPO, "noblegas_rtd_mcmc_amd")
 PROBE_LIB = os.path.join(PKG, "libngrtd_probe.so")
 
 
-def build():
+def probe_lib(defines):
+    return PROBE_LIB if not defines else PROBE_LIB.replace(".so", "_" + "_".join(
+        d.replace("=", "").lower() for d in defines) + ".so")
+
+
+def build(defines=()):
     """Both translation units with -DNGRTD_SECTION_PROBE (the DZ instances live in
-    ngrtd_dz.hip, with its own probe buffer), linked into libngrtd_probe.so."""
+    ngrtd_dz.hip, with its own probe buffer) and any --define, linked into
+    libngrtd_probe[_<defines>].so."""
     sys.path.insert(0, REPO)
     import __graft_entry__ as g
-    if not os.path.exists(PROBE_LIB) or os.path.getmtime(PROBE_LIB) < max(os.path.getmtime(p) for p in g._deps()):
+    lib = probe_lib(defines)
+    if not os.path.exists(lib) or os.path.getmtime(lib) < max(os.path.getmtime(p) for p in g._deps()):
         objs = []
         for src in g._sources():
-            obj = src + ".probe.o"
+            obj = src + ".probe%d.o" % os.getpid()
             subprocess.run(["hipcc"] + g.HIPCC_FLAGS + g.EXTRA_FLAGS.get(os.path.basename(src), []) +
-                           ["-DNGRTD_SECTION_PROBE", "-c", "-o", obj, src], check=True)
+                           ["-DNGRTD_SECTION_PROBE"] + ["-D" + d for d in defines] + ["-c", "-o", obj, src],
+                           check=True)
             objs.append(obj)
-        subprocess.run(["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", PROBE_LIB] + objs, check=True)
+        subprocess.run(["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", lib] + objs, check=True)
         for o in objs:
             os.remove(o)
 
@@ -57,11 +66,12 @@ def main():
     ap.add_argument("--pw", type=int, default=1)
     ap.add_argument("--jac", type=int, default=1)
     ap.add_argument("--dz-steps", type=int, default=8)
+    ap.add_argument("--define", action="append", default=[], help="extra -D for the probe build (A/B)")
     args = ap.parse_args()
-    build()
+    build(args.define)
     if args.build_only:
         return
-    os.environ["NGRTD_LIB"] = PROBE_LIB
+    os.environ["NGRTD_LIB"] = probe_lib(args.define)
     sys.path.insert(0, REPO)
     import torch
     from noblegas_rtd_mcmc_amd import _lib, workloads
@@ -111,7 +121,8 @@ def main():
         for grp, sel in (("theta_role", w < 8), ("rtd_role", w >= 8)):
             tt = t[sel]
             r = {"stage": tt[:, 9] - tt[:, 8], "stage_barrier": tt[:, 1] - tt[:, 9], "work": tt[:, 3] - tt[:, 1],
-                 "exchange": tt[:, 6] - tt[:, 3], "decision": tt[:, 10] - tt[:, 6],
+                 "prefetch_issue": tt[:, 13] - tt[:, 3], "exchange": tt[:, 6] - tt[:, 13],
+                 "decision": tt[:, 10] - tt[:, 6],
                  "commit_barrier": tt[:, 11] - tt[:, 10], "commit": tt[:, 12] - tt[:, 11],
                  "step": tt[:, 12] - tt[:, 8]}
             res[grp] = {k: float(np.median(v)) for k, v in r.items()}
