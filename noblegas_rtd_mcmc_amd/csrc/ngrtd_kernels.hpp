@@ -867,11 +867,14 @@ __device__ __forceinline__ void unit_conc(const RtdArgs& a, int64_t u, const dou
 // Piston second component (BMM, convolution_integral_utils.py:178-181): the channel-table
 // row at the FIRST argmin |tp - tau2| -- a lookup, no age loop.
 template <int C>
-__device__ __forceinline__ void piston_num(const RtdArgs& a, int64_t u, double* num2) {
-    const double tau2 = a.theta[(int64_t)a.row_tau[1] * a.U + u];
+__device__ __forceinline__ void piston_num_tau(const RtdArgs& a, double tau2, double* num2) {
     const int ix = piston_index(tau2, a.tp0, a.dtp, a.N);
 #pragma unroll
     for (int c = 0; c < C; ++c) num2[c] = a.tab[(int64_t)ix * a.CP + c];
+}
+template <int C>
+__device__ __forceinline__ void piston_num(const RtdArgs& a, int64_t u, double* num2) {
+    piston_num_tau<C>(a, a.theta[(int64_t)a.row_tau[1] * a.U + u], num2);
 }
 
 // The reference's exponential weights g = (1/tau) exp(-tp/tau) / sum(...) (:184, :270)
@@ -1743,9 +1746,20 @@ __device__ __forceinline__ void epm_row_load(const double* row, double* v) {
 // The block-tail surrogate of one piece: kChebN rows of C packed channel coefficients
 // (C kChebN doubles, 16-B aligned), read as 16-B chunks in descending order as Horner
 // consumes the rows (top row first).
+// The first kEpmTailPre chunks Horner reads (the top ones), loaded ahead by the caller --
+// before the head loop, so that their L2 latency passes behind it.
+constexpr int kEpmTailPre = 8;
+__host__ __device__ constexpr int epm_tail_pre_n(int C) { return kEpmTailPre < kChebN * C / 2 ? kEpmTailPre : kChebN * C / 2; }
 template <int C>
-__device__ __forceinline__ void epm_tail_sums(const double* pt, double x, double* y) {
-    constexpr int NF = kChebN * C;
+__device__ __forceinline__ void epm_tail_pre(const double* pt, bool on, double2* pre) {
+    constexpr int NF = kChebN * C, NP = epm_tail_pre_n(C);
+    const double2* p2 = reinterpret_cast<const double2*>(pt);
+#pragma unroll
+    for (int j = 0; j < NP; ++j) pre[j] = on ? p2[NF / 2 - 1 - j] : double2{0.0, 0.0};
+}
+template <int C>
+__device__ __forceinline__ void epm_tail_sums(const double* pt, double x, double* y, const double2* pre) {
+    constexpr int NF = kChebN * C, NP = epm_tail_pre_n(C);
     static_assert(NF % 2 == 0, "pieces of whole 16-B chunks");
     const double2* p2 = reinterpret_cast<const double2*>(pt);
     double f[NF];
@@ -1755,7 +1769,7 @@ __device__ __forceinline__ void epm_tail_sums(const double* pt, double x, double
 #pragma unroll
         for (int i = NF / 2 - 1; i >= 0; --i)
             if (i <= next && 2 * i + 1 >= k * C) {       // compile-time after unrolling
-                const double2 t = p2[i];
+                const double2 t = (i >= NF / 2 - NP) ? pre[NF / 2 - 1 - i] : p2[i];
                 f[2 * i] = t.x;
                 f[2 * i + 1] = t.y;
             }
@@ -1791,6 +1805,16 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
     const int m = f > 1 ? f : 1;
     const int blk = m / S + 1, B = blk * S;
     const double q = fexp(-beta);
+    // the block tail's surrogate piece first: its top chunks are loaded before the head loop
+    const bool tail = B < N;
+    double ex = 0.0;
+    const double taup = tau * ie;
+    int pc = (tail && a.epm) ? epm_piece(taup, ex) - a.epm_p0 : -1;
+    pc = (unsigned)pc < (unsigned)a.epm_np ? pc : -1;
+    const bool tail_on = tail && !(a.epm_diag & 2);
+    const double* pt = a.epm + ((size_t)(tail_on ? blk - 1 : 0) * a.epm_np + (pc < 0 ? 0 : pc)) * (size_t)(kChebN * C);
+    double2 tpre[epm_tail_pre_n(C)];
+    epm_tail_pre<C>(pt, tail_on, tpre);
     double y[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) y[c] = 0.0;
@@ -1839,19 +1863,11 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
             for (int c = 0; c < C; ++c) y[c] = qok ? y[c] : yt[c];
         }
     }
-    const bool tail = B < N;
-    double ex = 0.0;
-    const double taup = tau * ie;
-    int pc = (tail && a.epm) ? epm_piece(taup, ex) - a.epm_p0 : -1;
-    pc = (unsigned)pc < (unsigned)a.epm_np ? pc : -1;
     const bool bad = mvalid && tail && pc < 0;
     double tl[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) tl[c] = 0.0;
-    if (tail && !(a.epm_diag & 2)) {
-        const double* pt = a.epm + ((size_t)(blk - 1) * a.epm_np + (pc < 0 ? 0 : pc)) * (size_t)(kChebN * C);
-        epm_tail_sums<C>(pt, ex, tl);
-    }
+    if (tail_on) epm_tail_sums<C>(pt, ex, tl, tpre);
     if (__any(bad) && !(a.epm_diag & 4)) {              // exact tails of the uncovered lanes
         // tau' below the table (q < e^-16): the tail's terms fall below 1e-400 of its first
         // after 64 ages, so it is summed over [B, B + 64) only -- 64 iterations over each lane's own
@@ -2060,12 +2076,13 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     // wait only for those) so that their HBM latency overlaps the prologue's barrier
     // (A/B against loading them after the barrier: 11.87 vs 11.95 us, tools/gpu_ab_libs.sh)
     ThetaPre tp0{};
-    double tau0 = 1.0, eta0 = 1.0;
+    double tau0 = 1.0, eta0 = 1.0, tau20 = 1.0;
     if (!DZ) {
         if (do_theta) theta_preload(ua, mu, tp0);
         if (do_rtd) {
             tau0 = mvalid ? a.theta[(int64_t)a.row_tau[0] * a.U + mu] : 1.0;
             if (EPM) eta0 = mvalid ? a.theta[(int64_t)a.row_eta[0] * a.U + mu] : 1.0;
+            if (MIX & 1) tau20 = mvalid ? a.theta[(int64_t)a.row_tau[1] * a.U + mu] : 1.0;
             tp0.nub = (FULL || ua.rtd_on) ? a.theta[(int64_t)ua.row_nu * a.U + mu] : 0.0;
         }
     }
@@ -2127,7 +2144,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     double pf1[(kDzMaxP + kDzPfStep - 1) / kDzPfStep], pf2[(kDzMaxP + kDzPfStep - 1) / kDzPfStep];
     do {
         ThetaPre tp = tp0;                                // DZ: loaded per step below
-        double tau = tau0, eta = eta0;
+        double tau = tau0, eta = eta0, tau2 = tau20;
         // DZ: the argument structs through an opaque kernarg pointer per step, so that the
         // compiler re-reads their fields where they are used instead of hoisting every field
         // out of the step loop into registers (which spilled to scratch)
@@ -2221,6 +2238,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             if (do_rtd) {
                 tau = mvalid ? propl[a.row_tau[0] * kFusedUnits + mi] : 1.0;
                 if (EPM) eta = mvalid ? propl[a.row_eta[0] * kFusedUnits + mi] : 1.0;
+                if (MIX & 1) tau2 = mvalid ? propl[a.row_tau[1] * kFusedUnits + mi] : 1.0;
                 tp.nub = propl[uk.row_nu * kFusedUnits + mi];
             }
         } else if (DZ) {                                      // the proposal's rows
@@ -2228,6 +2246,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             if (do_rtd) {
                 tau = mvalid ? a.theta[(int64_t)a.row_tau[0] * a.U + mu] : 1.0;
                 if (EPM) eta = mvalid ? a.theta[(int64_t)a.row_eta[0] * a.U + mu] : 1.0;
+                if (MIX & 1) tau2 = mvalid ? a.theta[(int64_t)a.row_tau[1] * a.U + mu] : 1.0;
                 tp.nub = a.theta[(int64_t)uk.row_nu * a.U + mu];
             }
         }
@@ -2242,7 +2261,10 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
                 double rr[2];
                 batch_recip<2>(dr, rr);
                 double num2[C];
-                if (MIX & 1) piston_num<C>(a, mu, num2);
+                if (MIX & 1) {                  // the piston row from the LDS channel table
+                    const int ix = piston_index(tau2, a.tp0, a.dtp, a.N);
+                    epm_row_load<C>(tabl + epm_row(ix, CP), num2);
+                }
                 unit_conc<C>(a, mu, num, dd * rr[0], conc, (MIX & 1) ? num2 : nullptr);
                 like = mvalid ? unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL, &rr[1]) : 0.0;
             }
@@ -2284,7 +2306,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
                 double rr[2];
                 batch_recip<2>(dr, rr);
                 double num2[C];
-                if (MIX & 1) piston_num<C>(a, mu, num2);
+                if (MIX & 1) piston_num_tau<C>(a, tau2, num2);
                 unit_conc<C>(a, mu, num, rr[0], conc, (MIX & 1) ? num2 : nullptr);
                 if (cnan)
                     for (int t = 0; t < a.K; ++t) conc[t] = __builtin_nan("");
@@ -2325,7 +2347,9 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             return;
         }
         NGRTD_PROBE(6);
-        __syncthreads();
+        // per-well chains decide on their own unit's sum (the theta lane's own part[pi]): no
+        // cross-lane read before the decision, so no barrier (the commit barrier follows it)
+        if (!PW) __syncthreads();
         if (PW) {   // per-well chains: the unit's own Metropolis decision (its theta lane)
             int a = 0;
             if (dk.dz_diag & 32) {              // timing diagnostics: no decision (all rejected)

@@ -21,7 +21,7 @@ def main():
     import __graft_entry__ as g
     flags = g.HIPCC_FLAGS + g.EXTRA_FLAGS.get(os.path.basename(args.source), []) + ["-D" + d for d in args.D]
     out = subprocess.run(["hipcc"] + flags + ["-Rpass-analysis=kernel-resource-usage", "-c", "-o", "/dev/null",
-                                              args.source], capture_output=True, text=True, cwd="/tmp")
+                                              os.path.abspath(args.source)], capture_output=True, text=True, cwd="/tmp")
     rows, cur = [], None
     for line in out.stderr.splitlines():
         m = re.search(r"remark:\s+(Function Name|VGPRs|AGPRs|SGPRs|SGPRs Spill|VGPRs Spill|ScratchSize \[bytes/lane\]|"
