@@ -1748,7 +1748,10 @@ __device__ __forceinline__ void epm_row_load(const double* row, double* v) {
 // consumes the rows (top row first).
 // The first kEpmTailPre chunks Horner reads (the top ones), loaded ahead by the caller --
 // before the head loop, so that their L2 latency passes behind it.
-constexpr int kEpmTailPre = 8;
+#ifndef NGRTD_EPM_TAIL_PRE
+#define NGRTD_EPM_TAIL_PRE 12
+#endif
+constexpr int kEpmTailPre = NGRTD_EPM_TAIL_PRE;
 __host__ __device__ constexpr int epm_tail_pre_n(int C) { return kEpmTailPre < kChebN * C / 2 ? kEpmTailPre : kChebN * C / 2; }
 template <int C>
 __device__ __forceinline__ void epm_tail_pre(const double* pt, bool on, double2* pre) {
