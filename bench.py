@@ -193,9 +193,9 @@ def main():
     torch.cuda.synchronize()
     plan_build_ms = (time.perf_counter() - t0) * 1e3
     loop = LogpStepLoop(None, W_total, dev)
-    fast = lp.bind(theta, loop.out)
+    fasts = {o.data_ptr(): lp.bind(theta, o) for o in loop.outs}   # one bound launch per block buffer
     fast_n = lp.bind_n(theta, loop.out)
-    loop.evaluate = lambda out: fast()
+    loop.evaluate = lambda out: fasts[out.data_ptr()]()
     loop.evaluate_n = lambda out, k: fast_n(k)     # N = 1: the K steps in one native call
 
     # which kernels does one step launch? (one profiled step)
@@ -259,13 +259,10 @@ def main():
     per_step_events = world > 1 or not single_kernel
     t0 = time.perf_counter()
     if per_step_events:
-        for i in range(args.steps):
-            sample = i % args.event_every == 0
-            if sample:
-                lp.ctx.set_profiling(True)
-            loop.step()
-            if sample:
-                lp.ctx.set_profiling(False)
+        def hook(i, before):
+            if i % args.event_every == 0:
+                lp.ctx.set_profiling(before)
+        loop.run(args.steps, hook=hook)
     else:
         loop.run(args.steps)
     torch.cuda.synchronize()

@@ -46,8 +46,10 @@ class LogpStepLoop:
 
     ``evaluate(out)`` writes the block's log-probs into ``out`` (a contiguous prefix of a
     block buffer padded to the largest block, so uneven shards gather with one collective).
-    Both the block buffer and the gathered vector are allocated once.  ``step()`` returns
-    the gathered [per * world] vector; ``ensemble()`` the unpadded [W_total] view.
+    Two block buffers and two gathered vectors are allocated once (``outs``, ``gathers``):
+    ``run`` alternates them so that a step's all-gather overlaps the next step's
+    evaluation.  ``step()`` uses buffer 0 and returns the gathered [per * world] vector;
+    ``ensemble()`` the unpadded [W_total] view of the latest one.
 
     The same function runs under torchrun (RCCL) and in the world-size-2 gloo tests
     (tests/test_distributed_cpu.py), so the bench's multi-GPU step has no untested branch.
@@ -62,25 +64,60 @@ class LogpStepLoop:
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.lo, self.hi = shard_walkers(self.W_total, self.rank, self.world)
         self.per = (self.W_total + self.world - 1) // self.world
-        self.buf = torch.full((self.per,), float("nan"), dtype=dtype, device=device)
-        self.out = self.buf[: self.hi - self.lo]
-        self.gathered = (torch.empty(self.per * self.world, dtype=dtype, device=device)
-                         if self.world > 1 else self.buf)
+        nb = 2 if self.world > 1 else 1
+        self.bufs = [torch.full((self.per,), float("nan"), dtype=dtype, device=device) for _ in range(nb)]
+        self.outs = [b[: self.hi - self.lo] for b in self.bufs]
+        self.gathers = ([torch.empty(self.per * self.world, dtype=dtype, device=device) for _ in range(nb)]
+                        if self.world > 1 else self.bufs)
+        self.buf, self.out, self.gathered = self.bufs[0], self.outs[0], self.gathers[0]
 
     def step(self):
-        self.evaluate(self.out)
+        self.evaluate(self.outs[0])
         if self.world > 1:
-            all_gather_into(self.gathered, self.buf, group=self.group)
+            all_gather_into(self.gathers[0], self.bufs[0], group=self.group)
+        self.gathered = self.gathers[0]
         return self.gathered
 
-    def run(self, k):
-        """k steps.  World 1 with ``evaluate_n``: one call enqueues the k evaluations (no
-        collective to interleave, so no host round trip per step); else k ``step()``s."""
-        if self.world == 1 and self.evaluate_n is not None:
-            self.evaluate_n(self.out, int(k))
-        else:
-            for _ in range(int(k)):
-                self.step()
+    def run(self, k, hook=None):
+        """k steps.  World 1 with ``evaluate_n`` (and no per-step hook): one call enqueues the
+        k evaluations.  World > 1 with device-side collectives: two steps in flight -- step i
+        evaluates into block buffer i % 2 while step i - 1's all-gather (async_op, the
+        collective's own stream) still runs; step i's gather starts once its evaluation has
+        (the collective waits on the current stream), and step i + 2's evaluation waits for it
+        (``work.wait()``: a stream dependency, no host sync) because it reuses the buffer.
+        Otherwise (host-staged gloo rehearsals) k sequential ``step()``s.  ``hook(i, before)``
+        runs around step i's evaluation (bench.py's event sampling)."""
+        k = int(k)
+        if self.world == 1 and self.evaluate_n is not None and hook is None:
+            self.evaluate_n(self.out, k)
+            return self.gathered
+        if self.world == 1 or host_staged(self.group, self.bufs[0]):
+            for i in range(k):
+                if hook:
+                    hook(i, True)
+                self.evaluate(self.outs[0])
+                if hook:
+                    hook(i, False)
+                if self.world > 1:
+                    all_gather_into(self.gathers[0], self.bufs[0], group=self.group)
+            self.gathered = self.gathers[0]
+            return self.gathered
+        works = [None, None]
+        for i in range(k):
+            s = i & 1
+            if works[s] is not None:
+                works[s].wait()
+            if hook:
+                hook(i, True)
+            self.evaluate(self.outs[s])
+            if hook:
+                hook(i, False)
+            works[s] = dist.all_gather_into_tensor(self.gathers[s], self.bufs[s], group=self.group, async_op=True)
+        for w in works:
+            if w is not None:
+                w.wait()
+        if k:
+            self.gathered = self.gathers[(k - 1) & 1]
         return self.gathered
 
     def ensemble(self):

@@ -115,6 +115,16 @@ def _step_loop_worker(rank, world, port, W_total, outdir):
         g2 = loop.step().clone()
         loop.evaluate_n = lambda out, k: (_ for _ in ()).throw(AssertionError("world > 1 must gather per step"))
         assert torch.equal(loop.run(2).nan_to_num(), g1.nan_to_num())   # (padding is NaN)
+        # run()'s two-deep pipeline (CPU tensors on gloo: async all-gathers, not host-staged):
+        # the block buffers alternate, every step evaluates and gathers, the hook brackets each
+        # evaluation, and the latest gathered vector is the ensemble's
+        seen, hooks = [], []
+        loop.evaluate = lambda out: seen.append(out.data_ptr()) or evaluate(out)
+        last = loop.run(5, hook=lambda i, before: hooks.append((i, before)))
+        assert seen == [loop.outs[i % 2].data_ptr() for i in range(5)] and loop.outs[0].data_ptr() != loop.outs[1].data_ptr()
+        assert hooks == [(i, b) for i in range(5) for b in (True, False)]
+        assert last is loop.gathers[0] and torch.equal(loop.gathers[1].nan_to_num(), g1.nan_to_num())
+        assert torch.equal(last.nan_to_num(), g1.nan_to_num())
         np.savez(os.path.join(outdir, "s%d.npz" % rank), ens=loop.ensemble().numpy(), g1=g1.numpy(),
                  g2=g2.numpy(), lo=loop.lo, hi=loop.hi, per=loop.per)
     finally:
