@@ -42,7 +42,7 @@ namespace ngrtd {
 // -DNGRTD_SECTION_PROBE): lane 0 of every wave of logp_fused_kernel records the shader
 // clock (s_memtime) at fixed points.  Compiled out of the product library.
 #ifdef NGRTD_SECTION_PROBE
-// slots 0-7: the log-prob sections; 8-13: a DEMetropolisZ step's (the last step of a launch)
+// slots 0-7: the log-prob sections; 8-15: a DEMetropolisZ step's (the last step of a launch)
 constexpr int kProbeSlots = 16;
 __device__ unsigned long long g_probe[8192 * kProbeSlots];
 #define NGRTD_PROBE(k)                                                                        \
@@ -1500,6 +1500,7 @@ __device__ __forceinline__ void dz_stage_all(const DemcAccept& d, const DzStep& 
     const double lamb = sl.on ? sl.lamb[slot] : d.lamb[ci], sc = sl.on ? sl.sc[slot] : d.scaling[ci];
     const bool c1 = e1 == sj.at, c2 = e2 == sj.at;   // an entry appended in this launch is the state
     const uint64_t ke = rng_mix(sj.key + 2);
+    NGRTD_PROBE(14);
     double v[KMAX], vu[TR ? KMAX : 1];
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
@@ -1517,6 +1518,7 @@ __device__ __forceinline__ void dz_stage_all(const DemcAccept& d, const DzStep& 
             v[k] = vv;
         }
     }
+    NGRTD_PROBE(15);
     const bool app = sj.at >= 0 && !(dg & 2);
     double* hrow = hist + ((size_t)(sj.at < 0 ? 0 : sj.at) * W + w) * R + l;
 #pragma unroll

@@ -12,7 +12,8 @@ block) and the RTD-role waves (8-15):
 
 --variant dz: the last step of a multi-step DEMetropolisZ launch (--dz-steps, per-well /
 joint chains, natural / transformed space), its sections
-  8->9 staging (partners, noise, history append, proposal)   9->1 staging barrier
+  8->9 staging (partners, noise, history append, proposal): 8->14 arguments and partner
+  indices, 14->15 the proposal values, 15->9 the stores   9->1 staging barrier
   1->3 the role's work   3->13 the next step's partner-row loads issued (kDzPrefetch builds)
   13->6 exchange   6->10 decision   10->11 commit barrier   11->12 commit
 
@@ -120,7 +121,9 @@ def main():
         res["per_well"], res["transformed"] = bool(args.pw), bool(args.jac)
         for grp, sel in (("theta_role", w < 8), ("rtd_role", w >= 8)):
             tt = t[sel]
-            r = {"stage": tt[:, 9] - tt[:, 8], "stage_barrier": tt[:, 1] - tt[:, 9], "work": tt[:, 3] - tt[:, 1],
+            r = {"stage": tt[:, 9] - tt[:, 8], "stage_args": tt[:, 14] - tt[:, 8], "stage_values": tt[:, 15] - tt[:, 14],
+                 "stage_stores": tt[:, 9] - tt[:, 15],
+                 "stage_barrier": tt[:, 1] - tt[:, 9], "work": tt[:, 3] - tt[:, 1],
                  "prefetch_issue": tt[:, 13] - tt[:, 3], "exchange": tt[:, 6] - tt[:, 13],
                  "decision": tt[:, 10] - tt[:, 6],
                  "commit_barrier": tt[:, 11] - tt[:, 10], "commit": tt[:, 12] - tt[:, 11],
