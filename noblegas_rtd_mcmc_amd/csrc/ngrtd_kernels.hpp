@@ -1059,13 +1059,17 @@ __device__ __forceinline__ void count_accepts(unsigned long long* n, bool acc) {
 // global arrays, or the multi-step launch's LDS copies, DemcAccept::state_lds; the tuning
 // state exists iff d.n_acc_tune does); acc_out: the decision array, stored iff store_acc.
 // (Flags rather than null tests: a null test of an LDS-derived generic pointer miscompiles.)
+// The accept draw's log: log(u) of the (key, rid) stream (a function of the step and the
+// chain only, so the multi-step launch takes it before the step's log-prob is known).
+__device__ __forceinline__ double demc_logu(uint64_t key, uint64_t rid) {
+    return log(rng_unit(rng_mix(rng_mix(key + 3) + rid)));
+}
 template <class F64P, class I32P>
-__device__ __forceinline__ bool demc_decide_at(const DemcAccept& d, F64P lpa, F64P lamb, F64P scal, I32P nat,
-                                               int32_t* acc_out, bool store_acc, int64_t w, uint64_t rid,
-                                               double lp_prop, uint64_t key, int32_t tune_now, int64_t log_off,
-                                               int64_t li, bool count) {
+__device__ __forceinline__ bool demc_decide_at_u(const DemcAccept& d, F64P lpa, F64P lamb, F64P scal, I32P nat,
+                                                 int32_t* acc_out, bool store_acc, int64_t w, double logu,
+                                                 double lp_prop, int32_t tune_now, int64_t log_off, int64_t li,
+                                                 bool count) {
     const double cur = lpa[w];
-    const double logu = log(rng_unit(rng_mix(rng_mix(key + 3) + rid)));
     const double mr = lp_prop - cur;
     const bool acc = __builtin_isfinite(mr) && logu < mr;
     if (store_acc) acc_out[w] = acc;
@@ -1085,6 +1089,14 @@ __device__ __forceinline__ bool demc_decide_at(const DemcAccept& d, F64P lpa, F6
     if (d.lp_log) d.lp_log[log_off + li] = acc ? lp_prop : cur;
     if (d.ar_log) d.ar_log[log_off + li] = exp(mr);
     return acc;
+}
+template <class F64P, class I32P>
+__device__ __forceinline__ bool demc_decide_at(const DemcAccept& d, F64P lpa, F64P lamb, F64P scal, I32P nat,
+                                               int32_t* acc_out, bool store_acc, int64_t w, uint64_t rid,
+                                               double lp_prop, uint64_t key, int32_t tune_now, int64_t log_off,
+                                               int64_t li, bool count) {
+    return demc_decide_at_u(d, lpa, lamb, scal, nat, acc_out, store_acc, w, demc_logu(key, rid), lp_prop, tune_now,
+                            log_off, li, count);
 }
 __device__ __forceinline__ bool demc_decide(const DemcAccept& d, int64_t w, uint64_t rid, double lp_prop,
                                             uint64_t key, int32_t tune_now, int64_t log_off, int64_t li,
@@ -1754,17 +1766,22 @@ __device__ __forceinline__ void epm_row_load(const double* row, double* v) {
 #define NGRTD_EPM_TAIL_PRE 12
 #endif
 constexpr int kEpmTailPre = NGRTD_EPM_TAIL_PRE;
-__host__ __device__ constexpr int epm_tail_pre_n(int C) { return kEpmTailPre < kChebN * C / 2 ? kEpmTailPre : kChebN * C / 2; }
-template <int C>
+// the DEMetropolisZ instances carry the step's state in registers too: fewer chunks ahead
+#ifndef NGRTD_EPM_TAIL_PRE_DZ
+#define NGRTD_EPM_TAIL_PRE_DZ 4
+#endif
+constexpr int kEpmTailPreDz = NGRTD_EPM_TAIL_PRE_DZ;
+__host__ __device__ constexpr int epm_tail_pre_n(int C, int want) { return want < kChebN * C / 2 ? want : kChebN * C / 2; }
+template <int C, int NPW>
 __device__ __forceinline__ void epm_tail_pre(const double* pt, bool on, double2* pre) {
-    constexpr int NF = kChebN * C, NP = epm_tail_pre_n(C);
+    constexpr int NF = kChebN * C, NP = epm_tail_pre_n(C, NPW);
     const double2* p2 = reinterpret_cast<const double2*>(pt);
 #pragma unroll
     for (int j = 0; j < NP; ++j) pre[j] = on ? p2[NF / 2 - 1 - j] : double2{0.0, 0.0};
 }
-template <int C>
+template <int C, int NPW>
 __device__ __forceinline__ void epm_tail_sums(const double* pt, double x, double* y, const double2* pre) {
-    constexpr int NF = kChebN * C, NP = epm_tail_pre_n(C);
+    constexpr int NF = kChebN * C, NP = epm_tail_pre_n(C, NPW);
     static_assert(NF % 2 == 0, "pieces of whole 16-B chunks");
     const double2* p2 = reinterpret_cast<const double2*>(pt);
     double f[NF];
@@ -1799,7 +1816,7 @@ __device__ __forceinline__ void epm_tail_sums(const double* pt, double x, double
 //   den returned as dn / dd (dd = e^(-beta) - 1) for the caller's batched reciprocal.
 // Lanes whose tau' = 1 / beta the surrogate does not cover (or NaN) sum their tail exactly;
 // the loop is wave-uniform and runs only when some lane needs it.
-template <int C>
+template <int C, int NPW = kEpmTailPre>
 __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, bool mvalid, double tau, double eta,
                                          double* num, double& dn, double& dd) {
     constexpr int CP = cheb_cp(C), S = kEpmBlock;
@@ -1818,8 +1835,8 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
     pc = (unsigned)pc < (unsigned)a.epm_np ? pc : -1;
     const bool tail_on = tail && !(a.epm_diag & 2);
     const double* pt = a.epm + ((size_t)(tail_on ? blk - 1 : 0) * a.epm_np + (pc < 0 ? 0 : pc)) * (size_t)(kChebN * C);
-    double2 tpre[epm_tail_pre_n(C)];
-    epm_tail_pre<C>(pt, tail_on, tpre);
+    double2 tpre[epm_tail_pre_n(C, NPW) > 0 ? epm_tail_pre_n(C, NPW) : 1];
+    epm_tail_pre<C, NPW>(pt, tail_on, tpre);
     double y[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) y[c] = 0.0;
@@ -1872,7 +1889,7 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
     double tl[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) tl[c] = 0.0;
-    if (tail_on) epm_tail_sums<C>(pt, ex, tl, tpre);
+    if (tail_on) epm_tail_sums<C, NPW>(pt, ex, tl, tpre);
     if (__any(bad) && !(a.epm_diag & 4)) {              // exact tails of the uncovered lanes
         // tau' below the table (q < e^-16): the tail's terms fall below 1e-400 of its first
         // after 64 ages, so it is summed over [B, B + 64) only -- 64 iterations over each lane's own
@@ -2261,7 +2278,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             double conc[kMaxTracer];
             {
                 double num[C], dn, dd;
-                epm_sums<C>(a, tabl, mvalid, tau, eta, num, dn, dd);
+                epm_sums<C, DZ ? kEpmTailPreDz : kEpmTailPre>(a, tabl, mvalid, tau, eta, num, dn, dd);
                 const double dr[2] = {dn, tp.nub * (uk.rnu_max - uk.rnu_min) + uk.rnu_min};
                 double rr[2];
                 batch_recip<2>(dr, rr);
