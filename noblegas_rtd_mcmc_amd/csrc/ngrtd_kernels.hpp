@@ -1322,6 +1322,9 @@ constexpr int kDzMaxP = 12;          // parameter rows of a single-launch DEMetr
 #define NGRTD_DZ_PREFETCH 1
 #endif
 constexpr bool kDzPrefetch = NGRTD_DZ_PREFETCH != 0;   // partner rows one step ahead (dz_partner_rows)
+#ifndef NGRTD_DZ_TR_BRANCH
+#define NGRTD_DZ_TR_BRANCH 1
+#endif
 #ifndef NGRTD_DZ_PF_STEP
 #define NGRTD_DZ_PF_STEP 2
 #endif
@@ -1525,7 +1528,13 @@ __device__ __forceinline__ void dz_stage_all(const DemcAccept& d, const DzStep& 
             double vv = dz_value_core(de, x, c1 ? x : pf1[k], c2 ? x : pf2[k], lamb, sc, ke, el, S != nullptr, sr);
             if (TR) {
                 vu[TR ? k : 0] = vv;
+#if NGRTD_DZ_TR_BRANCH
+                // the row's transform kind is wave-uniform (a kernel argument of a compile-time
+                // row): branch on it instead of computing every kind and selecting
+                vv = pymc3_backward(d.tr_kind[p], d.tr_a[p], d.tr_b[p], vv);
+#else
                 vv = pymc3_backward_sel(d.tr_kind[p], d.tr_a[p], d.tr_b[p], vv);
+#endif
             }
             v[k] = vv;
         }
