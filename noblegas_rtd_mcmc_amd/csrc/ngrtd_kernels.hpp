@@ -1772,7 +1772,7 @@ __device__ __forceinline__ void epm_row_load(const double* row, double* v) {
 // The first kEpmTailPre chunks Horner reads (the top ones), loaded ahead by the caller --
 // before the head loop, so that their L2 latency passes behind it.
 #ifndef NGRTD_EPM_TAIL_PRE
-#define NGRTD_EPM_TAIL_PRE 12
+#define NGRTD_EPM_TAIL_PRE 14
 #endif
 constexpr int kEpmTailPre = NGRTD_EPM_TAIL_PRE;
 // the DEMetropolisZ instances carry the step's state in registers too: fewer chunks ahead
