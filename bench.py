@@ -61,6 +61,8 @@ def parse():
                     help="skip the published-model / c2 / c3 side lines (N = 1)")
     ap.add_argument("--sampler-steps", type=int, default=256,
                     help="steps of the timed device DEMetropolisZ call (one multi-step launch chunk)")
+    ap.add_argument("--sampler-tune", type=int, default=1000,
+                    help="untimed tuning steps before the sampler's timed window (its draw phase)")
     ap.add_argument("--event-every", type=int, default=8,
                     help="bracket the kernels of every k-th timed step with HIP events (multi-kernel / N > 1)")
     ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
@@ -420,7 +422,8 @@ def report(args, spec, lp, ks, dt, world, W_total, Wb, plan_build_ms, theta, the
 def sampler_line(args, spec, lp, theta, gpu):
     """The device DEMetropolisZ (ngrtd_demcz_run) on the same walkers, outside the timed
     region: per-step time of ONE call of --sampler-steps steps (the multi-step launch; the
-    call's two layout transposes included) after a 10-step warm-up.  Primary: PyMC3's
+    call's two layout transposes included) in the draw phase, after --sampler-tune (1000)
+    tuning steps and stop_tuning: the stationary regime of a reference-length run.  Primary: PyMC3's
     transformed space (a plan with the Jacobians -- the space the reference samples in);
     beside it the natural space on the headline plan.  Reported beside the headline, never
     as it.  Returns (fields, {space: us per step}) -- the caller takes the max over ranks."""
@@ -437,11 +440,14 @@ def sampler_line(args, spec, lp, theta, gpu):
     torch.cuda.synchronize()
     build_ms = (time.perf_counter() - t0) * 1e3
     L = spec.n_wells
+    tune = max(0, args.sampler_tune)
     for name, plan, pw in (("transformed", lpj, True), ("natural", lp, True), ("transformed_joint", lpj, False)):
         s = DeviceDEMetropolisZ(plan, tune_interval=100, seed=7, transformed=plan is lpj, per_well=pw)
-        x, l, z = s.start(theta, 50, 10 + n)
+        # the timed window is the draw phase after `tune` tuning steps (stop_tuning included),
+        # the stationary regime of a reference-length run, not the first steps of fresh chains
+        x, l, z = s.start(theta, tune, tune + n + 1)
         cnt = torch.zeros(1, dtype=torch.int64, device=theta.device)
-        plan.demcz(x, l, 10, z)
+        plan.demcz(x, l, tune, z)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         plan.demcz(x, l, n, z, n_accepted=cnt)
@@ -450,7 +456,8 @@ def sampler_line(args, spec, lp, theta, gpu):
         us[name] = dt * 1e6
         nch = W * (L if pw else 1)
         out[name] = {"us_per_step": dt * 1e6, "chains": nch, "chain_steps_per_s": nch / dt,
-                     "walker_steps_per_s": W / dt, "steps": n, "accept_rate": int(cnt.item()) / float(n * nch),
+                     "walker_steps_per_s": W / dt, "steps": n, "after_tune_steps": tune,
+                     "accept_rate": int(cnt.item()) / float(n * nch),
                      "chain": "one per (walker, well)" if pw else "one per walker over its %d wells" % L}
         del x, l, z
     out["transformed"]["plan_build_ms"] = build_ms

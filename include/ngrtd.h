@@ -368,7 +368,11 @@ typedef struct {
      * well's chain is still exactly a DEMetropolisZ chain).  So a run of all L wells equals
      * L runs of one well each (well0 = l) chain for chain. */
     int32_t per_well;
-    int32_t reserved0;
+    /* Wells of the whole run whose streams this call's wells [well0, well0 + L) are part of:
+     * ngrtd_demcz_run rejects well0 + L > n_wells_total, so that two calls never share a
+     * well's random streams by accident.  0: unchecked (the caller keeps well0 ranges
+     * disjoint). */
+    int32_t n_wells_total;
     int64_t well0;           /* global index of well 0 (per-well streams) */
     /* Per call, like accepted_log: [n_steps][chains] PyMC3's `accept` sample stat,
      * exp(logp(x*) - logp(x)) (DEMetropolisZ.astep), device memory; NULL = not logged. */

@@ -45,7 +45,7 @@ class DemczState(C.Structure):
                 ("tune_target", C.c_int32), ("drop_fraction", C.c_double), ("seed", C.c_uint64),
                 ("chain0", C.c_int64), ("n_chains_total", C.c_int64), ("S", C.c_void_p),
                 ("theta_u", C.c_void_p), ("tr_kind", C.c_int32 * ROLE_COUNT), ("tr_a", C.c_double * ROLE_COUNT),
-                ("tr_b", C.c_double * ROLE_COUNT), ("per_well", C.c_int32), ("reserved0", C.c_int32),
+                ("tr_b", C.c_double * ROLE_COUNT), ("per_well", C.c_int32), ("n_wells_total", C.c_int32),
                 ("well0", C.c_int64), ("accept_log", C.c_void_p)]
 
 

@@ -1777,8 +1777,11 @@ int ngrtd_demcz_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64
         z->hist_lo < 0 || z->hist_lo > z->hist_len || z->steps_done < 0 || z->tune_interval < 1 ||
         z->tune_target < 0 || z->tune_target > 2 || !(z->drop_fraction >= 0.0 && z->drop_fraction <= 1.0) ||
         z->chain0 < 0 || (z->n_chains_total != 0 && z->chain0 + W > z->n_chains_total) ||
-        (z->per_well != 0 && z->per_well != 1) || z->well0 < 0)
+        (z->per_well != 0 && z->per_well != 1) || z->well0 < 0 || z->n_wells_total < 0)
         return set_err(ctx, NGRTD_EINVAL, "bad DEMetropolisZ state");
+    if (z->n_wells_total > 0 && z->well0 + p->desc.n_wells > z->n_wells_total)
+        return set_err(ctx, NGRTD_EINVAL, "wells [%lld, %lld) outside the run's %d wells", (long long)z->well0,
+                       (long long)(z->well0 + p->desc.n_wells), z->n_wells_total);
     const bool pw = z->per_well != 0;
     const int64_t Wg = z->n_chains_total ? z->n_chains_total : W;
     if (z->hist_len + n_steps > z->hist_cap)

@@ -176,15 +176,17 @@ class ShardedLogProb:
         return torch.cat(parts, dim=-1)
 
 
-def sharded_demcz(log_prob, x_block, W_total, tune, draws, device_sampler=False, group=None, **kw):
+def sharded_demcz(log_prob, x_block, W_total, tune, draws, *, per_well, device_sampler=False, group=None, **kw):
     """DEMetropolisZ over an ensemble sharded in walker blocks: every rank runs the chains
     of its block (sampler.DEMetropolisZ on a batched log_prob, or DeviceDEMetropolisZ on an
     engine.LogProb), each chain drawing the random numbers of its GLOBAL index, so the
     union of the shards is bitwise the single-process run of the whole ensemble.  Chains
     are independent (each proposes from its own history), so sampling needs no
     collective at all; the per-draw log-probs and decisions are all-gathered once, at
-    the end, for the trace.  Returns (result of this rank's block, logp [draws, W_total],
-    accepted [draws, W_total])."""
+    the end, for the trace.  ``per_well`` (required, so that the chain structure never
+    depends on which backend is picked): True = one chain per (walker, well) (log_prob
+    returns [L][W]), False = one chain per walker ([W]).  Returns (result of this rank's
+    block, logp [draws, (L,) W_total], accepted [draws, (L,) W_total])."""
     from .sampler import DEMetropolisZ, DeviceDEMetropolisZ
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -192,7 +194,7 @@ def sharded_demcz(log_prob, x_block, W_total, tune, draws, device_sampler=False,
     if x_block.shape[-1] != hi - lo:
         raise ValueError("rank %d owns walkers [%d, %d), got a block of %d" % (rank, lo, hi, x_block.shape[-1]))
     cls = DeviceDEMetropolisZ if device_sampler else DEMetropolisZ
-    res = cls(log_prob, chain0=lo, n_chains_total=int(W_total), **kw).run(x_block, tune, draws)
+    res = cls(log_prob, chain0=lo, n_chains_total=int(W_total), per_well=bool(per_well), **kw).run(x_block, tune, draws)
     if world == 1:
         return res, res["logp"], res["accepted"]
     per = (int(W_total) + world - 1) // world

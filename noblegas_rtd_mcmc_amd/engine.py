@@ -255,10 +255,14 @@ class LogProb:
         R = self.spec.n_params * self.spec.n_wells
         if state.W != W or state.R != R:
             raise ValueError("state was built for R=%d, W=%d" % (state.R, state.W))
-        for name, t, dt in (("accepted_log", accepted_log, 1), ("logp_log", logp_log, 8), ("accept_log", accept_log, 8)):
-            if t is not None and (not t.is_cuda or t.element_size() != dt or t.numel() < n_steps * nc
-                                  or not t.is_contiguous()):
-                raise ValueError("%s must be a contiguous CUDA tensor [n_steps][chains]" % name)
+        import torch
+        for name, t, dt in (("accepted_log", accepted_log, torch.uint8), ("logp_log", logp_log, torch.float64),
+                            ("accept_log", accept_log, torch.float64)):
+            if t is not None and (not t.is_cuda or t.dtype != dt or t.numel() < n_steps * nc or not t.is_contiguous()):
+                raise ValueError("%s must be a contiguous CUDA %s tensor [n_steps][chains]" % (name, dt))
+        if n_accepted is not None and (not n_accepted.is_cuda or n_accepted.dtype != torch.int64
+                                       or n_accepted.numel() < 1):
+            raise ValueError("n_accepted must be a CUDA int64 tensor [1]")
         state.c.accept_log = accept_log.data_ptr() if accept_log is not None else None
         self.ctx.check(self.lib.ngrtd_demcz_run(
             self.plan, C.c_void_p(theta.data_ptr()), C.c_void_p(logp.data_ptr()), W, int(n_steps),

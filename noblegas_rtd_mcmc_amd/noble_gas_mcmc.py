@@ -78,7 +78,10 @@ class CEModel:
         return self.logp(theta)
 
     def deterministics(self, theta_soa):
-        """Ae, F, E, b, T, nu of theta SoA [6][L][W] (the mc.Deterministic nodes, :229-250)."""
+        """E, b, T, nu of theta SoA [6][L][W] (the mc.Deterministic nodes, :229-250) and Ae, F
+        as LINEAR values -- 10 ** the reference's log10 Deterministics 'Ae' / 'F' (:229-230), i.e.
+        what ce_exc_wrapper feeds the model (:207) and what the reference's plots convert
+        them to (:281-283, :438-440).  The trace keeps the log10 values (trace.py)."""
         c = self.spec.ce
         t = np.asarray(theta_soa)
         Ae = 10 ** (t[0] * (c.logA_max - c.logA_min) + c.logA_min)
@@ -90,7 +93,7 @@ class CEModel:
         return {"Ae": Ae, "F": F, "E": E, "b": b, "m": t[3], "T": T, "nu": nu}
 
     def sample(self, nwalkers=100, tune=500, draws=500, seed=12345, tune_interval=100, sampler="device",
-               space="transformed"):
+               space="transformed", prior_samples=10000):
         """DEMetropolisZ on the GPU log-prob (replaces mc.sample, :408-415): one chain per
         (walker, well), each well its own model as the reference runs them (logp / accepted
         [draws][L][W]).  sampler: "device" (ngrtd_demcz_run, device-resident) or "torch"
@@ -105,7 +108,23 @@ class CEModel:
         res = sample_model(self.spec, self.max_walkers, self.device, x, tune, draws, seed, tune_interval, sampler,
                            space, cache=self.__dict__)
         from . import trace
-        res["idata"] = trace.inference_data(res, self.spec, wells=self.wells, observed=self.spec.ce.obs)
+        idd = trace.inference_data(res, self.spec, wells=self.wells, observed=self.spec.ce.obs)
         res["samples"] = res["samples"].cpu().numpy()
         res["logp"] = res["logp"].cpu().numpy()
+        res["idata"] = trace.InferenceData.from_dict(idd, prior=self.prior_checks(prior_samples))
         return res
+
+    def prior_checks(self, samples=10000, seed=10):
+        """The prior group az.from_pymc3(trace, prior=prior_checks) stores (:276-283, :419):
+        ``samples`` prior draws of every variable and deterministic (one chain), with Ae / F
+        converted to linear values as the reference does before storing them (:281-283).
+        Draws from NumPy's generator (seed 10), not PyMC3's stream (not installed here); the
+        likelihood's prior-predictive 'like' draws are not included."""
+        from . import trace
+        from .workloads import sample_prior
+        th = sample_prior(self.spec, int(samples), np.random.default_rng(seed))
+        g = trace.prior_group(self.spec, th)
+        for p in ("Ae", "F"):
+            dims, a = g[p]
+            g[p] = (dims, 10 ** a)
+        return g

@@ -7,8 +7,9 @@
 * ``conv_mcmc(well, tracer, obs_kwgs, conv_kwgs, prior_kwgs, savedir, savenum)`` --
   :189-462.  ``build_mcmc_model_joint_sT()`` returns the batched log-prob (ModelSpec
   compiled on the GPU) of the same priors / obs statistics / StudentT likelihood;
-  ``sample_mcmc()`` runs DEMetropolisZ (one chain per walker) on the GPU instead of PyMC3
-  and saves the trace in ArviZ's group layout (trace.py).
+  ``sample_mcmc()`` runs DEMetropolisZ (one chain per walker) on the GPU instead of PyMC3,
+  saves the trace in ArviZ's group layout (trace.py) and returns it as the InferenceData
+  the reference's caller indexes (trace.InferenceData).
 """
 import copy
 import os
@@ -121,7 +122,7 @@ class conv_mcmc:
         self._lp = None
         tl = '.'.join(self.tracer)
         mt = '{}-{}'.format(self.mod_type1, self.mod_type2) if self.mod_type2 else self.mod_type1
-        # :255 -- a directory of per-group netCDF-3 files here (trace.to_netcdf)
+        # :255 -- ONE netCDF-4 (HDF5) file, az.to_netcdf's container (trace.to_netcdf)
         self.trace_name = os.path.join(savedir, '{}.{}.{}.{}.netcdf'.format(well, tl, mt, savenum))
 
     def frombeta(self, betaval, low, high):
@@ -166,30 +167,39 @@ class conv_mcmc:
             self._lp = LogProb(self.spec(), self.max_walkers, self.device)
         return self._lp
 
-    def sample_mcmc(self, nwalkers=96, tune=10000, draws=10000, seed=123423, tune_interval=1000, sampler="device",
-                    space="transformed"):
-        """DEMetropolisZ, one chain per walker (the plan holds this one well), on the GPU
-        log-prob (replaces mc.sample, :407-429).  sampler: "device" (ngrtd_demcz_run, device-resident) or "torch"
-        (sampler.DEMetropolisZ on torch ops; same random stream).  space: "transformed"
-        (PyMC3's: logodds / interval / log; the log-prob adds the Jacobian) or "natural"."""
+    def sample_mcmc(self, chains=3, tune=10000, draws=10000, seed=123423, tune_interval=1000, sampler="device",
+                    space="transformed", nwalkers=None):
+        """DEMetropolisZ on the GPU log-prob (replaces mc.sample, :407-429, with its
+        arguments as defaults: 3 chains, tune 10 000, draws 10 000, seed 123423,
+        tune_interval 1000), one chain per walker of this one well.  sampler: "device"
+        (ngrtd_demcz_run, device-resident) or "torch" (sampler.DEMetropolisZ on torch ops;
+        same random stream).  space: "transformed" (PyMC3's: logodds / interval / log; the
+        log-prob adds the Jacobian) or "natural".  ``nwalkers``: alias of ``chains``.
+
+        Returns what the reference returns, the InferenceData of the run
+        (trace.InferenceData: ``out['posterior'][v]`` is [chain, draw], the indexing of
+        run_age_mcmc.py:251-276), with the sampler's own result fields (samples, logp,
+        accepted, lamb, scaling, roles, ...) beside the groups."""
         import torch
         from .sampler import sample_model
         from .workloads import sample_prior
+        if nwalkers is not None:
+            chains = nwalkers
         lp = self.build_mcmc_model_joint_sT()
-        x0 = sample_prior(lp.spec, nwalkers, np.random.default_rng(seed))
+        x0 = sample_prior(lp.spec, chains, np.random.default_rng(seed))
         x = torch.from_numpy(x0).to("cuda:%d" % self.device)
         res = sample_model(lp.spec, self.max_walkers, self.device, x, tune, draws, seed, tune_interval, sampler,
                            space, cache=self.__dict__)
         from . import trace
-        idata = trace.inference_data(res, lp.spec, wells=[self.well], observed=lp.spec.rtd.obs)
-        res = {k: (v.cpu().numpy() if hasattr(v, "cpu") else v) for k, v in res.items()}
-        res["roles"] = list(lp.spec.roles)
-        res["idata"] = idata
+        idd = trace.inference_data(res, lp.spec, wells=[self.well], observed=lp.spec.rtd.obs)
+        raw = {k: (v.cpu().numpy() if hasattr(v, "cpu") else v) for k, v in res.items()}
+        raw["roles"] = list(lp.spec.roles)
+        out = trace.InferenceData.from_dict(idd, raw=raw)
         if self.savedir:
             # az.to_netcdf(idata, self.trace_name) (:425): same groups / names / attrs
-            trace.to_netcdf(idata, self.trace_name)
-        self.idata = res
-        return res
+            trace.to_netcdf(out, self.trace_name)
+        self.idata = out
+        return out
 
 
 def deepcopy_kwargs(kw):

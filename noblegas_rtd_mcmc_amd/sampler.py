@@ -385,7 +385,8 @@ class ZState:
     contiguous run), which also hold the draws."""
 
     def __init__(self, R, W, hist_cap, device, lamb, scaling, n_tune, tune_interval, tune_target,
-                 drop_fraction, seed, chain0=0, n_chains_total=0, S=None, per_well=False, L=1, well0=0):
+                 drop_fraction, seed, chain0=0, n_chains_total=0, S=None, per_well=False, L=1, well0=0,
+                 n_wells_total=0):
         self.R, self.W = int(R), int(W)
         self.per_well, self.L = bool(per_well), int(L)
         shp = (self.L, W) if self.per_well else (W,)      # per-well chains: [L][W]
@@ -404,7 +405,8 @@ class ZState:
                                  drop_fraction=float(drop_fraction), seed=int(seed) & _M64,
                                  chain0=int(chain0), n_chains_total=int(n_chains_total or 0),
                                  S=self.S.data_ptr() if self.S is not None else None,
-                                 per_well=int(self.per_well), well0=int(well0))
+                                 per_well=int(self.per_well), well0=int(well0),
+                                 n_wells_total=int(n_wells_total or 0))
 
     def entries(self, lo, hi):
         """History entries [lo, hi) as [hi - lo][R][W] (per-well chains: [hi - lo][P][L][W])."""
@@ -430,11 +432,14 @@ class DeviceDEMetropolisZ:
 
     def __init__(self, logprob, lamb=None, scaling=0.001, tune="lambda", tune_interval=100,
                  tune_drop_fraction=0.9, seed=123423, chain0=0, n_chains_total=None, S=None, transformed=None,
-                 per_well=True, well0=0):
+                 per_well=True, well0=0, n_wells_total=None):
         if tune not in (None, "none", "scaling", "lambda"):
             raise ValueError('tune must be None, "scaling" or "lambda" (pymc3 DEMetropolisZ)')
         self.per_well = bool(per_well)
         self.well0 = int(well0)
+        # the run's total wells: the device rejects a well range [well0, well0 + L) beyond it
+        # (streams keyed by the global well index must not collide between calls); None = unchecked
+        self.n_wells_total = n_wells_total
         if transformed is None:
             transformed = bool(logprob.spec.jacobian)
         if transformed and not logprob.spec.jacobian:
@@ -467,7 +472,8 @@ class DeviceDEMetropolisZ:
         lamb = self.lamb if self.lamb is not None else default_lamb(P if self.per_well else R)
         z = ZState(R, W, hist_cap, x.device, lamb, self.scaling,
                    n_tune, self.tune_interval, _lib.TUNE_TARGET[self.tune], self.tune_drop_fraction, self.seed,
-                   self.chain0, self.n_chains_total, self.S, per_well=self.per_well, L=L, well0=self.well0)
+                   self.chain0, self.n_chains_total, self.S, per_well=self.per_well, L=L, well0=self.well0,
+                   n_wells_total=self.n_wells_total)
         if tf is not None:
             z.u = u
             z.c.theta_u = u.data_ptr()

@@ -126,9 +126,130 @@ def inference_data(res, spec, sampling_time=None, wells=None, library="noblegas_
                        "well": np.arange(L, dtype=np.int64)}}
 
 
+def prior_group(spec, theta_soa):
+    """The ``prior`` group az.from_pymc3(trace, prior=prior_checks) adds
+    (ng_interp/noble_gas_mcmc.py:402-419: mc.sample_prior_predictive draws; the plotting at
+    :544 reads idata.prior[v]): the same variable names and deterministics as the posterior
+    (inference_data), dims (chain = 1, draw), from prior draws theta SoA [P][L][draws]."""
+    th = np.asarray(theta_soa, dtype=np.float64)
+    res = {"samples": np.moveaxis(th, -1, 0)[:, :, :, None],           # [draw, P, L, chain = 1]
+           "accepted": np.zeros((th.shape[-1], 1), dtype=np.uint8), "lamb": np.zeros(1), "scaling": np.zeros(1)}
+    return inference_data(res, spec)["posterior"]
+
+
+class Dataset(dict):
+    """One InferenceData group, the access patterns the reference's scripts use on an
+    xarray Dataset: ``ds[name]`` and ``ds.name`` give the variable as a numpy array
+    (``np.asarray(ds[name])`` is [chain, draw(, well)], as run_age_mcmc.py:251-276 indexes
+    it), ``ds.dims[name]`` its dimension names, ``ds.attrs`` the group attributes."""
+
+    def __init__(self, variables=None, attrs=None):
+        super().__init__()
+        self.var_dims = {}
+        self.attrs = dict(attrs or {})
+        for name, (dims, arr) in (variables or {}).items():
+            self[name] = np.asarray(arr)
+            self.var_dims[name] = tuple(dims)
+
+    @property
+    def data_vars(self):
+        return list(self.keys())
+
+    def __getattr__(self, name):
+        try:
+            return self[name]
+        except KeyError:
+            raise AttributeError(name) from None
+
+    def copy(self):
+        d = Dataset(attrs=self.attrs)
+        for k, v in self.items():
+            d[k] = v.copy()
+            d.var_dims[k] = self.var_dims[k]
+        return d
+
+
+class InferenceData(dict):
+    """What the reference's ``conv_mcmc.sample_mcmc`` returns (``az.from_pymc3(trace)``,
+    run_age_mcmc_utils.py:407-429) in the form its caller consumes: groups ``posterior``,
+    ``sample_stats``, ``observed_data`` (and ``prior`` when given) as :class:`Dataset`, read
+    as ``mc_out['posterior'][v]`` / ``mc_out.posterior[v]`` (run_age_mcmc.py:231-276) and
+    ``mc_out.copy()``.  ``raw`` extra keys (the sampler's own result: samples, logp,
+    accepted, lamb, scaling, ...) sit beside the groups under their own names."""
+
+    GROUPS = ("posterior", "sample_stats", "observed_data", "prior")
+
+    @classmethod
+    def from_dict(cls, idata, raw=None, prior=None):
+        """``inference_data()``'s dict (+ the sampler result ``raw``, + a prior group dict
+        {name: (dims, array)}) -> InferenceData."""
+        out = cls()
+        attrs = dict(idata.get("attrs", {}))
+        out["posterior"] = Dataset(idata["posterior"], attrs)
+        out["sample_stats"] = Dataset(idata["sample_stats"], attrs)
+        if idata.get("observed") is not None:
+            obs = np.asarray(idata["observed"])
+            out["observed_data"] = Dataset({"like": (tuple("like_dim_%d" % i for i in range(obs.ndim)), obs)})
+        if prior is not None:
+            out["prior"] = Dataset(prior, attrs)
+        out.attrs = attrs
+        out.coords = dict(idata.get("coords", {}))
+        for k, v in (raw or {}).items():
+            if k not in cls.GROUPS:
+                out[k] = v
+        return out
+
+    def __getattr__(self, name):
+        try:
+            return self[name]
+        except KeyError:
+            raise AttributeError(name) from None
+
+    def groups(self):
+        return [g for g in self.GROUPS if g in self]
+
+    def copy(self):
+        out = InferenceData()
+        for k, v in self.items():
+            out[k] = v.copy() if hasattr(v, "copy") else v
+        out.attrs = dict(getattr(self, "attrs", {}))
+        out.coords = dict(getattr(self, "coords", {}))
+        return out
+
+    def to_dict(self):
+        """Back to ``inference_data()``'s dict layout (what ``to_netcdf`` writes)."""
+        d = {g: {n: (self[g].var_dims[n], a) for n, a in self[g].items()} for g in ("posterior", "sample_stats")}
+        d["attrs"] = dict(self.attrs)
+        d["coords"] = dict(self.coords)
+        d["observed"] = self["observed_data"]["like"] if "observed_data" in self else None
+        if "prior" in self:
+            d["prior"] = {n: (self["prior"].var_dims[n], a) for n, a in self["prior"].items()}
+        return d
+
+
+def summary(idata, round_to=None, hdi_prob=0.94):
+    """The columns of ``az.summary`` the reference's scripts read (run_age_mcmc.py:232 prints
+    it and takes ``list(trace_summary.index)`` as the variable list of the posterior
+    predictive loop): one row per posterior variable, mean, sd and the equal-tailed
+    interval of ``hdi_prob`` over all chains and draws (ArviZ's HDI is the narrowest such
+    interval; here the central one -- ArviZ is not installed)."""
+    import pandas as pd
+    post = idata["posterior"]
+    rows = {}
+    lo_q, hi_q = (1 - hdi_prob) / 2, 1 - (1 - hdi_prob) / 2
+    for name in post:
+        a = np.asarray(post[name], dtype=np.float64).ravel()
+        rows[name] = {"mean": a.mean(), "sd": a.std(ddof=0),
+                      "hdi_%g%%" % (100 * lo_q): np.quantile(a, lo_q), "hdi_%g%%" % (100 * hi_q): np.quantile(a, hi_q)}
+    df = pd.DataFrame.from_dict(rows, orient="index")
+    return df.round(round_to) if round_to is not None else df
+
+
 def to_netcdf(idata, path):
     """Write ``idata`` as ONE netCDF-4 file at ``path`` (az.to_netcdf's layout)."""
     from . import h5lite
+    if isinstance(idata, InferenceData):
+        idata = idata.to_dict()
     attrs = idata["attrs"]
     base = {k: attrs[k] for k in ("created_at", "arviz_version", "inference_library", "inference_library_version")}
     run = dict(base, sampling_time=np.array([float(attrs["sampling_time"])]),
@@ -136,6 +257,14 @@ def to_netcdf(idata, path):
     if "wells" in attrs:                  # several wells in one file (the reference: one file per well)
         run["wells"] = attrs["wells"]
     groups = {}
+    if idata.get("prior") is not None:    # az.from_pymc3(trace, prior=...) (noble_gas_mcmc.py:419)
+        g = idata["prior"]
+        used = []
+        for dims, _ in g.values():
+            used += [d for d in dims if d not in used]
+        n = {d: next(a.shape[i] for dims, a in g.values() for i, dd in enumerate(dims) if dd == d) for d in used}
+        groups["prior"] = {"attrs": base, "dims": {d: np.arange(n[d], dtype=np.int64) for d in used},
+                           "vars": {name: (dims, np.asarray(arr), {}) for name, (dims, arr) in g.items()}}
     for gname in ("posterior", "sample_stats"):
         g = idata[gname]
         used = []
@@ -161,14 +290,15 @@ def from_netcdf(path):
     from . import h5lite
     f = h5lite.read_netcdf4(path)
     out = {"attrs": {}, "coords": {}}
-    for gname in ("posterior", "sample_stats", "observed_data"):
+    for gname in ("posterior", "sample_stats", "observed_data", "prior"):
         if gname not in f:
             continue
         g = f[gname]
-        for k, v in g["attrs"].items():
-            v = v[0] if isinstance(v, np.ndarray) and v.shape == (1,) else v
-            out["attrs"][k] = v.item() if isinstance(v, np.generic) else v
-        for d, c in g["dims"].items():
-            out["coords"][d] = c
+        if gname != "prior":              # the prior's own (chain, draw) sizes stay in its group
+            for k, v in g["attrs"].items():
+                v = v[0] if isinstance(v, np.ndarray) and v.shape == (1,) else v
+                out["attrs"][k] = v.item() if isinstance(v, np.generic) else v
+            for d, c in g["dims"].items():
+                out["coords"][d] = c
         out[gname] = {name: (dims, arr) for name, (dims, arr, _) in g["vars"].items()}
     return out

@@ -68,22 +68,34 @@ def convolve_batch(t, tau, mod_type, lamba, eta=None, D=None, J=None):
         return g @ np.flip(C)
 
 
+def _beta(x, ab, jac):
+    """Beta prior (+ the logodds transform's log|J| for the transformed-space log-prob, as
+    models._beta_lp)."""
+    return _st.beta_logp(x, ab[0], ab[1]) + (_st.jac_logodds(x) if jac else 0.0)
+
+
+def _unif(x, lohi, jac):
+    return _st.uniform_logp(x, lohi[0], lohi[1]) + (_st.jac_interval(x, lohi[0], lohi[1]) if jac else 0.0)
+
+
 def log_prob_vec(spec, theta_soa):
-    """Per-walker log-prob for theta SoA [P][L][W], vectorised over walkers."""
+    """Per-walker log-prob for theta SoA [P][L][W], vectorised over walkers (with the PyMC3
+    transform Jacobians when spec.jacobian, as models.log_prob)."""
     theta_soa = np.asarray(theta_soa, dtype=np.float64)
     P, L, W = theta_soa.shape
+    jac = spec.jacobian
     lp = np.zeros(W)
     for l in range(L):
         p = {role: theta_soa[i, l] for i, role in enumerate(spec.roles)}
         if spec.ce is not None:
             c = spec.ce
             if spec.include_prior:
-                lp = lp + _st.beta_logp(p["Ae_beta"], *c.beta_Ae)
-                lp = lp + _st.beta_logp(p["F_beta"], *c.beta_F)
-                lp = lp + _st.beta_logp(p["E_beta"], *c.beta_E)
+                lp = lp + _beta(p["Ae_beta"], c.beta_Ae, jac)
+                lp = lp + _beta(p["F_beta"], c.beta_F, jac)
+                lp = lp + _beta(p["E_beta"], c.beta_E, jac)
                 lp = lp + _st.normal_logp(p["m"], c.m_mu, c.m_sd)
-                lp = lp + _st.beta_logp(p["b_beta"], *c.beta_b)
-                lp = lp + _st.beta_logp(p["nu_ce_beta"], *c.beta_nu)
+                lp = lp + _beta(p["b_beta"], c.beta_b, jac)
+                lp = lp + _beta(p["nu_ce_beta"], c.beta_nu, jac)
             if spec.include_like:
                 Ae = p["Ae_beta"] * (c.logA_max - c.logA_min) + c.logA_min
                 F = p["F_beta"] * (c.logF_max - c.logF_min) + c.logF_min
@@ -98,17 +110,17 @@ def log_prob_vec(spec, theta_soa):
             r = spec.rtd
             names = r.par_names
             if spec.include_prior:
-                lp = lp + _st.uniform_logp(p["tau1"], *r.tau1)
-                lp = lp + _st.beta_logp(p["nu_rtd_beta"], *r.beta_nu)
+                lp = lp + _unif(p["tau1"], r.tau1, jac)
+                lp = lp + _beta(p["nu_rtd_beta"], r.beta_nu, jac)
                 for nm in ("tau2", "f1", "eta1", "eta2", "D1", "D2"):
                     if nm in names:
-                        lp = lp + _st.uniform_logp(p[nm], *getattr(r, nm))
+                        lp = lp + _unif(p[nm], getattr(r, nm), jac)
                 if "J" in names:
                     lp = lp + _st.normal_logp(p["J"], r.J_mu, r.J_sd)
                 if "thalf_cfc" in names:
-                    lp = lp + _st.beta_logp(p["thalf_cfc_beta"], *r.beta_thalf)
+                    lp = lp + _beta(p["thalf_cfc_beta"], r.beta_thalf, jac)
                 if "lamsf6" in names:
-                    lp = lp + _st.halfnormal_logp(p["lamsf6"], r.lamsf6_sd)
+                    lp = lp + _st.halfnormal_logp(p["lamsf6"], r.lamsf6_sd) + (_st.jac_log(p["lamsf6"]) if jac else 0.0)
             if spec.include_like:
                 nu = p["nu_rtd_beta"] * (r.nu_max - r.nu_min) + r.nu_min
                 f1 = p["f1"] if "f1" in names else 1.0

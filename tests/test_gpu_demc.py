@@ -191,11 +191,15 @@ def test_per_well_run_equals_single_well_runs():
     assert tuple(full["logp"].shape) == (6, L, W) and tuple(full["lamb"].shape) == (L, W)
     for l in range(L):
         lpl = LogProb(spec.well(l), max_walkers=W)
-        one = DeviceDEMetropolisZ(lpl, well0=l, **kw).run(x0[:, l:l + 1].contiguous(), tune=10, draws=6)
+        one = DeviceDEMetropolisZ(lpl, well0=l, n_wells_total=L, **kw).run(x0[:, l:l + 1].contiguous(), tune=10,
+                                                                           draws=6)
         assert torch.equal(one["x"][:, 0], full["x"][:, l]), l
         assert torch.equal(one["samples"][:, :, 0], full["samples"][:, :, l]), l
         for k in ("logp", "accepted", "accept", "lp", "lamb", "scaling"):
             assert torch.equal(one[k][..., 0, :] if one[k].dim() > 1 else one[k], full[k][..., l, :]), (l, k)
+        if l == L - 1:      # a well range past the run's wells is refused (streams would collide)
+            with pytest.raises(Exception, match="outside the run"):
+                DeviceDEMetropolisZ(lpl, well0=L, n_wells_total=L, **kw).run(x0[:, l:l + 1].contiguous(), 2, 1)
         lpl.close()
     # a walker-block shard of the L-well run
     lpb = LogProb(spec, max_walkers=W)

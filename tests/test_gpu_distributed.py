@@ -30,42 +30,46 @@ def _port():
     return p
 
 
-def _torchrun(args, timeout=300):
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+def _torchrun(args, timeout=300, nproc=2):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
            "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args
-    env = dict(os.environ, OMP_NUM_THREADS="4")
+    env = dict(os.environ, OMP_NUM_THREADS=str(max(1, 8 // nproc)))
     return subprocess.run(cmd, check=True, timeout=timeout, env=env, capture_output=True, text=True, cwd=REPO)
 
 
-@pytest.mark.parametrize("W,L,per_well", [(2048, 64, 1), (2048, 64, 0), (130, 3, 1)])
-def test_two_ranks_on_gpu_equal_one_process(tmp_path, W, L, per_well):
-    """Strong sharding of one seeded ensemble (c5's partition at N = 2; W = 130 at L = 3:
-    ragged walker-major blocks): the gathered ensemble log-prob == the single-process
-    log-prob, and the ranks' device DEMetropolisZ chains == the same chains of the
-    single-process device run, bit for bit."""
+@pytest.mark.parametrize("W,L,per_well,nproc", [(2048, 64, 1, 2), (2048, 64, 0, 2), (130, 3, 1, 2),
+                                                 (2048, 64, 1, 8)])
+def test_ranks_on_gpu_equal_one_process(tmp_path, W, L, per_well, nproc):
+    """Strong sharding of one seeded ensemble (c5's partition at N = 2, and c5's exact
+    partition: 8 ranks x 256 walkers x 64 wells; W = 130 at L = 3: ragged walker-major
+    blocks): the gathered ensemble log-prob == the single-process log-prob, and the ranks'
+    device DEMetropolisZ chains == the same chains of the single-process device run, bit for
+    bit.  All ranks share the box's one GPU (gloo, host-staged all-gathers)."""
     import torch
     from noblegas_rtd_mcmc_amd import workloads as wl
     from noblegas_rtd_mcmc_amd.engine import LogProb
     from noblegas_rtd_mcmc_amd.sampler import DeviceDEMetropolisZ
-    _torchrun([os.path.join(REPO, "tests", "dist_gpu_worker.py"), str(tmp_path), str(W), str(L), str(per_well)])
-    r0, r1 = (np.load(tmp_path / ("rank%d.npz" % r)) for r in (0, 1))
+    _torchrun([os.path.join(REPO, "tests", "dist_gpu_worker.py"), str(tmp_path), str(W), str(L), str(per_well)],
+              nproc=nproc)
+    rs = [np.load(tmp_path / ("rank%d.npz" % r)) for r in range(nproc)]
     spec = wl.c4_spec(L=L, N=1200)
     full = torch.from_numpy(wl.sample_prior(spec, W, np.random.default_rng(34568))).cuda()
     lp = LogProb(spec, max_walkers=W)
     ref = lp(full).cpu().numpy()
-    assert int(r0["lo"]) == 0 and int(r0["hi"]) == int(r1["lo"]) and int(r1["hi"]) == W
-    for r in (r0, r1):
+    assert int(rs[0]["lo"]) == 0 and int(rs[-1]["hi"]) == W
+    assert all(int(a["hi"]) == int(b["lo"]) for a, b in zip(rs, rs[1:]))
+    for r in rs:
         assert np.array_equal(r["ens"], ref, equal_nan=True)
         assert np.array_equal(r["g1"], r["g2"], equal_nan=True)
     kw = dict(tune_interval=4, seed=2024)
     kw["per_well"] = bool(per_well)
     lpj = LogProb(dataclasses.replace(spec, jacobian=True), max_walkers=W)
     one = DeviceDEMetropolisZ(lpj, **kw).run(full, tune=8, draws=6)
-    cat = lambda k: np.concatenate([r0[k], r1[k]], axis=-1)   # noqa: E731
+    cat = lambda k: np.concatenate([r[k] for r in rs], axis=-1)   # noqa: E731
     assert np.array_equal(cat("x"), one["x"].cpu().numpy())
     assert np.array_equal(cat("lp"), one["lp"].cpu().numpy())
     assert np.array_equal(cat("samples"), one["samples"].cpu().numpy())
-    for r in (r0, r1):
+    for r in rs:
         assert np.array_equal(r["lp_tr"], one["logp"].cpu().numpy())
         assert np.array_equal(r["acc_tr"], one["accepted"].cpu().numpy())
     assert 0 < int(one["accepted"].sum()) < one["accepted"].numel()
@@ -73,14 +77,16 @@ def test_two_ranks_on_gpu_equal_one_process(tmp_path, W, L, per_well):
     lpj.close()
 
 
-def test_bench_two_ranks_one_gpu():
+@pytest.mark.parametrize("nproc", [2, 8])
+def test_bench_ranks_one_gpu(nproc):
     """bench.py's N > 1 branch (LogpStepLoop + all-gather, max-over-ranks timing, the
-    sampler leg on every rank) end to end on the one GPU: a valid JSON line."""
-    r = _torchrun(["bench.py", "--gpus", "2", "--steps", "10", "--warmup", "2", "--scaling", "strong",
-                   "--backend", "gloo", "--one-device", "--sampler-steps", "16", "--no-cpu-baseline"])
+    sampler leg on every rank) end to end on the one GPU: a valid JSON line; nproc = 8 is
+    c5's strong partition (8 x 256 walkers of the 2048-walker ensemble)."""
+    r = _torchrun(["bench.py", "--gpus", str(nproc), "--steps", "10", "--warmup", "2", "--scaling", "strong",
+                   "--backend", "gloo", "--one-device", "--sampler-steps", "16", "--no-cpu-baseline"], nproc=nproc)
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:] + r.stderr[-2000:]
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["walkers_per_gpu"] == 1024
+    assert d["n_gpus"] == nproc and d["value"] > 0 and d["config"]["walkers_per_gpu"] == 2048 // nproc
     assert d["config"]["one_device"] is True and d["ensemble_finite_frac"] > 0.5
     assert "error" not in d["sampler"] and d["sampler"]["transformed"]["us_per_step"] > 0

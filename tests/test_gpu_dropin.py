@@ -205,7 +205,12 @@ def test_conv_mcmc_sample_writes_arviz_trace(tmp_path):
             ckw[t]["t_half"] = 12.34
     pkw = {"tau1_low": 1.0, "tau1_high": 1000.0, "J_mu": -10.42, "J_sd": 0.33, "par_names": ["tau1", "J"]}
     m = conv_mcmc("PLM1", tracers, okw, ckw, pkw, str(tmp_path), 1)
-    res = m.sample_mcmc(nwalkers=12, tune=60, draws=30, tune_interval=20)
+    res = m.sample_mcmc(chains=12, tune=60, draws=30, tune_interval=20)
+    # the reference returns the InferenceData; its caller reads np.asarray(out['posterior'][v])
+    # as [chain, draw] (run_age_mcmc.py:251-276)
+    assert isinstance(res, trace.InferenceData) and np.asarray(res["posterior"]["tau1"]).shape == (12, 30)
+    i = list(res["roles"]).index("tau1")
+    assert np.array_equal(np.asarray(res.copy()["posterior"]["tau1"]), res["samples"][:, i, 0, :].T)
     back = trace.from_netcdf(m.trace_name)
     assert m.trace_name.endswith("PLM1.CFC12.SF6.H3.He4_ter.exponential.1.netcdf")
     assert back["posterior"]["tau1"][1].shape == (12, 30) and "nu" in back["posterior"]

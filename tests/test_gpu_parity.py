@@ -215,12 +215,15 @@ def test_published_models_c4_shape_vs_oracle(model):
     lp.close()
 
 
-@pytest.mark.parametrize("model", ["exponential", "exp_pist_flow", "exponential-piston"])
+@pytest.mark.parametrize("model", ["exponential", "exp_pist_flow", "exponential-piston", "exp_pist_flow-piston"])
 def test_jacobian_plans_c4_shape_vs_oracle(model):
     """Plans with the PyMC3 transform Jacobians (the transformed-space sampler's log-prob;
     the joint single-component ones run the FULL + Jacobian kernel instances) at the c4
-    shape vs the per-walker oracle."""
+    shape: 264 walkers across every block / wave boundary vs the vectorised oracle, 5 vs the
+    per-walker loop, and the per-unit log-probs (what the per-well sampler's chains target)
+    summed over wells equal the per-walker ones."""
     import dataclasses
+    import torch
     import oracle.models as om
     from noblegas_rtd_mcmc_amd import workloads as wl
     from noblegas_rtd_mcmc_amd.engine import LogProb
@@ -234,6 +237,12 @@ def test_jacobian_plans_c4_shape_vs_oracle(model):
     walkers = [0, 1, 511, 512, 2047]
     ref = om.log_prob(spec, th, walkers=walkers)
     assert close(a[walkers], ref, 1e-12, 1e-9).all(), (a[walkers], ref)
+    sel = many_walkers(2048, seed=6)
+    refv = log_prob_vec(spec, np.ascontiguousarray(th[:, :, sel]))
+    ok = close(a[sel], refv, 1e-12, 1e-9)
+    assert ok.all(), (np.array(sel)[~ok], a[sel][~ok], refv[~ok])
+    u = lp.units(torch.from_numpy(th).cuda()).cpu().numpy()
+    assert close(u.sum(axis=0), a, 1e-12, 1e-9).all()
     lp.close()
 
 

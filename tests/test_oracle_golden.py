@@ -231,10 +231,14 @@ def test_g_tp_after_convolve_is_decayed(golden):
         assert close(g, ref, rtol=1e-12, atol=1e-300).all()
 
 
-@pytest.mark.parametrize("which", ["c2", "c3", "c4", "bmm_epm_piston", "bmm_exp_disp"])
+@pytest.mark.parametrize("which", ["c2", "c3", "c4", "bmm_epm_piston", "bmm_exp_disp", "c4_jac", "bmm_epm_piston_jac"])
 def test_vectorized_oracle_matches_per_walker_loop(which):
     """The vectorised CPU baseline (oracle/vectorized.py) is the same arithmetic as the
-    reference-faithful per-walker loop, up to the dot product's summation order."""
+    reference-faithful per-walker loop, up to the dot product's summation order (also with
+    the PyMC3 transform Jacobians: the transformed-space sampler's log-prob)."""
+    import dataclasses
+    jac = which.endswith("_jac")
+    which = which[:-4] if jac else which
     from noblegas_rtd_mcmc_amd import workloads as wl
     from oracle.vectorized import log_prob_vec
     if which == "c2":
@@ -252,6 +256,8 @@ def test_vectorized_oracle_matches_per_walker_loop(which):
         spec = wl.c4_spec(L=2, N=300, mod_type1="exponential", mod_type2="dispersion",
                           par_names=("tau1", "tau2", "f1", "D2", "J"))
         th = wl.sample_prior(spec, 24, np.random.default_rng(5))
+    if jac:
+        spec = dataclasses.replace(spec, jacobian=True)
     ref = omod.log_prob(spec, th)
     got = log_prob_vec(spec, th)
     assert close(got, ref, rtol=1e-12, atol=1e-9).all(), (got, ref)

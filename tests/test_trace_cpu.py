@@ -124,6 +124,70 @@ def test_our_trace_roundtrip(tmp_path):
     assert np.array_equal(back["observed_data"]["like"][1], idata["observed"])
 
 
+def test_inference_data_serves_reference_caller(tmp_path):
+    """conv_mcmc.sample_mcmc returns trace.InferenceData (what the reference returns:
+    az.from_pymc3(trace), run_age_mcmc_utils.py:407-429).  The reference's caller
+    (age_ens_runs_mcmc/run_age_mcmc.py:231-276) runs az.summary over it, copies it, takes the
+    summary's index as the variable list and reads every posterior draw as
+    np.asarray(dd['posterior'][v])[0, :][s]; that loop, restated here, must see the
+    sampler's chain-0 draws of every variable, and the object must round-trip through
+    to_netcdf."""
+    from noblegas_rtd_mcmc_amd import trace
+    idd, _ = _our_trace(tmp_path)
+    raw = {"samples": np.zeros(3), "accept_rate": 0.25}
+    mc_out = trace.InferenceData.from_dict(idd, raw=raw)
+    trace_summary = trace.summary(mc_out, round_to=6)                     # az.summary(mc_out, round_to=6)
+    assert list(trace_summary.columns[:2]) == ["mean", "sd"]
+    dd = mc_out.copy()
+    pp = {'tau1': False, 'tau2': False, 'f1': False, 'f2': False, 'eta1': False, 'eta2': False, 'J': False,
+          'D1': False, 'D2': False, 'thalf_cfc': False, 'lamsf6': False}
+    vrs = list(trace_summary.index)
+    assert {"tau1", "J", "thalf_cfc", "lamsf6", "nu"} <= set(vrs)
+    seen = {v: [] for v in vrs}
+    for s in range(np.asarray(dd['posterior']['tau1']).shape[1]):
+        for v in vrs:
+            pp[v] = np.asarray(dd['posterior'][v])[0, :][s]
+            seen[v].append(pp[v])
+    for v in vrs:
+        assert np.array_equal(seen[v], idd["posterior"][v][1][0]), v
+    assert np.array_equal(np.asarray(mc_out.posterior["tau1"]), idd["posterior"]["tau1"][1])
+    assert mc_out.posterior.var_dims["tau1"] == ("chain", "draw")
+    assert np.array_equal(mc_out["sample_stats"]["accepted"], idd["sample_stats"]["accepted"][1])
+    assert mc_out["accept_rate"] == 0.25 and set(mc_out.groups()) == {"posterior", "sample_stats", "observed_data"}
+    # the copy is independent of the original
+    dd["posterior"]["tau1"][0, 0] = -1.0
+    assert mc_out["posterior"]["tau1"][0, 0] != -1.0
+    back = trace.from_netcdf(trace.to_netcdf(mc_out, str(tmp_path / "again.netcdf")))
+    for k, (dims, arr) in idd["posterior"].items():
+        assert back["posterior"][k][0] == dims and np.array_equal(back["posterior"][k][1], arr), k
+
+
+def test_ce_prior_group_roundtrip(tmp_path):
+    """The CE trace carries the prior group az.from_pymc3(trace, prior=prior_checks) writes
+    (ng_interp/noble_gas_mcmc.py:276-283, :419; its plots read idata.prior[v], :544): every
+    posterior variable, Ae / F linear as the reference converts them before storing, one
+    chain; it round-trips through the netCDF-4 file without disturbing the posterior's coords."""
+    from noblegas_rtd_mcmc_amd import trace
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    spec, _ = wl.c1(W=4)
+    n = 500
+    th = wl.sample_prior(spec, n, np.random.default_rng(10))
+    g = trace.prior_group(spec, th)
+    assert {"Ae_beta", "m", "Ae", "F", "E", "b", "T", "nu"} <= set(g)
+    assert g["m"][0] == ("chain", "draw") and g["m"][1].shape == (1, n)
+    assert np.array_equal(g["m"][1][0], th[spec.roles.index("m"), 0])
+    D, W = 6, 2
+    s = np.stack([wl.sample_prior(spec, W, np.random.default_rng(i)) for i in range(D)])
+    res = {"samples": s, "accepted": np.ones((D, 1, W), np.uint8), "accept": np.ones((D, 1, W)),
+           "lamb": np.full((1, W), 0.5), "scaling": np.full((1, W), 1e-3), "tuning_steps": 5, "sampling_time": 1.0}
+    idd = trace.inference_data(res, spec, observed=spec.ce.obs)
+    mc = trace.InferenceData.from_dict(idd, prior=g)
+    assert "prior" in mc.groups() and mc.prior["m"].shape == (1, n)
+    back = trace.from_netcdf(trace.to_netcdf(mc, str(tmp_path / "ce.netcdf")))
+    assert np.array_equal(back["prior"]["m"][1], g["m"][1])
+    assert np.array_equal(back["coords"]["draw"], np.arange(D)) and np.array_equal(back["coords"]["chain"], np.arange(W))
+
+
 def test_writer_uncompressed_and_multiwell(tmp_path):
     """Contiguous (unfiltered) datasets and a third (well) dimension read back as written."""
     from noblegas_rtd_mcmc_amd import h5lite
