@@ -73,7 +73,13 @@ def parse():
     return ap.parse_args()
 
 
-def model_spec(args):
+# savenum digits -> the parameters they sample (run_age_mcmc.py:180-198): 1 log10 J (He4_ter
+# production), 2 thalf_cfc (CFC12 half-life), 3 lamsf6 (SF6 contamination); every published
+# 4-tracer run is savenum 123 (the shipped conv_traces/*.123.netcdf)
+SAVENUM_PARS = {"1": "J", "2": "thalf_cfc", "3": "lamsf6"}
+
+
+def model_spec(args, savenum=""):
     from noblegas_rtd_mcmc_amd import workloads
     pn = ["tau1"]
     m1, m2 = args.mod_type1, args.mod_type2
@@ -82,6 +88,7 @@ def model_spec(args):
     pn += [p + "1" for p in MODEL_PARS[m1]]
     if m2:
         pn += [p + "2" for p in MODEL_PARS[m2]]
+    pn += [SAVENUM_PARS[d] for d in str(savenum) if d in SAVENUM_PARS]
     return workloads.c4_spec(L=args.wells, N=args.ages, mod_type1=m1, mod_type2=m2, par_names=tuple(pn))
 
 
@@ -469,7 +476,12 @@ def sampler_line(args, spec, lp, theta, gpu):
     return out, us
 
 
-PUBLISHED_MODELS = (("exponential", "piston"), ("exp_pist_flow", None), ("exp_pist_flow", "piston"))
+# the RTD models of the reference's published runs (run_age_mcmc.py:61-70),
+# without (savenum 0) and with (123: J, thalf_cfc, lamsf6 sampled -- the published
+# configuration) the savenum parameters
+PUBLISHED_MODELS = (("exponential", None, ""), ("exponential", None, "123"), ("exponential", "piston", ""), ("exponential", "piston", "123"),
+                    ("exp_pist_flow", None, ""), ("exp_pist_flow", None, "123"), ("exp_pist_flow", "piston", ""),
+                    ("exp_pist_flow", "piston", "123"))
 
 
 def _time_plan(spec, W, gpu, steps, seed=34568):
@@ -511,23 +523,29 @@ def model_lines(args, gpu):
     steps = max(50, args.steps)
     W = args.walkers
     res = {}
-    for m1, m2 in PUBLISHED_MODELS:
+    base_ms = {("exponential", None): None}
+    for m1, m2, sv in PUBLISHED_MODELS:
         a = ap.Namespace(wells=args.wells, ages=args.ages, mod_type1=m1, mod_type2=m2)
-        spec = model_spec(a)
+        spec = model_spec(a, sv)
         build_ms, ms, finite, info = _time_plan(spec, W, gpu, steps)
-        mix = (1 if m2 == "piston" else 0) | (2 if m1 == "exp_pist_flow" else 0)
+        if not sv:
+            base_ms[(m1, m2)] = ms
+        mix = (1 if m2 == "piston" else 0) | (2 if m1 == "exp_pist_flow" else 0) | (32 if "2" in sv else 0)
         inst = "logp_fused_kernel<5, true, 2, %d>" % mix
         pmc, pmc_path = pmc_summary("logp_fused_kernel", inst)
         U = W * args.wells
         e = {"kernel_ms": ms, "evals_per_s": W / (ms * 1e-3), "plan_build_ms": build_ms,
              "value_amortized_20k": W * 20000 / (20000 * ms * 1e-3 + build_ms * 1e-3),
-             "finite_frac": finite, "kernel": inst, "surrogate": info.get("surrogate")}
+             "finite_frac": finite, "kernel": inst, "surrogate": info.get("surrogate"),
+             "sampled": ["tau1"] + [SAVENUM_PARS[d] for d in sv], "savenum": int(sv) if sv else 0}
+        if sv and base_ms.get((m1, m2)):
+            e["vs_savenum0_kernel"] = ms / base_ms[(m1, m2)]
         if pmc.get("fp64_flop_per_unit") and inst in (pmc_path or ""):
             fl = pmc["fp64_flop_per_unit"] * U
             e["roofline"] = {"bound": "fp64_valu", "achieved": fl / (ms * 1e-3) / 1e12, "peak": FP64_PEAK / 1e12,
                              "unit": "TFLOP/s", "frac": fl / (ms * 1e-3) / FP64_PEAK, "traffic": pmc.get("hbm_bytes_per_launch"),
                              "flop_source": "PMC fp64_flop_per_unit %.1f x %d units (%s)" % (pmc["fp64_flop_per_unit"], U, pmc_path)}
-        res[m1 + ("-" + m2 if m2 else "")] = e
+        res[m1 + ("-" + m2 if m2 else "") + ("." + sv if sv else "")] = e
     for name, (spec, _) in (("c2", workloads.c2(W=8)), ("c3", workloads.c3(W=8))):
         build_ms, ms, finite, info = _time_plan(spec, W, gpu, steps, seed=12345 if name == "c2" else 23456)
         res[name] = {"workload": {"c2": "CE log-prob, %d walkers x 3 wells (PLM1, PLM6, PLM7) x 5 gases" % W,

@@ -31,6 +31,9 @@ namespace ngrtd {
 hipError_t launch_fused_dz_instance(int mix, const RtdArgs& a, const UnitArgs& u, int WB, int64_t W, double* logp,
                                     const DemcAccept& da, size_t lds, size_t max_lds, hipStream_t st);
 bool fused_dz_instance_exists(int mix);
+// ngrtd_lw.hip: the log-prob instances with the sampled CFC12 half-life (MIX bit 5)
+hipError_t launch_fused_lw_instance(int C, bool full, int mix, const RtdArgs& a, const UnitArgs& u, int WB, int64_t W,
+                                    double* logp, const DemcAccept& da, size_t lds, size_t max_lds, hipStream_t st);
 }
 
 namespace {
@@ -169,11 +172,17 @@ struct TracerBuild {
     bool lamw;
 };
 
+// Channels of per-unit-decay tracers (lamw: the sampled CFC12 half-life) come first, so that
+// the single-launch kernel's LW instances find it at channel 0 (a compile-time index).
 static int build_table(ngrtd_ctx* ctx, const std::vector<TracerBuild>& trs, TableDev& tab) {
     const int64_t N = trs[0].s->n;
     std::vector<std::vector<double>> cols;
     int C = 0;
-    for (size_t t = 0; t < trs.size(); ++t) {
+    std::vector<size_t> order;
+    for (int pass = 0; pass < 2; ++pass)
+        for (size_t t = 0; t < trs.size(); ++t)
+            if (trs[t].lamw == (pass == 0)) order.push_back(t);
+    for (size_t t : order) {
         const TracerBuild& tb = trs[t];
         if (tb.s->n != N) return set_err(ctx, NGRTD_EINVAL, "tracers must share the series length");
         std::vector<double> d(N, 1.0);
@@ -641,7 +650,9 @@ static void launch_mfma(const RtdArgs& a, const UnitArgs& u, int32_t fuse, hipSt
 // packed per-well data (ce obs, 1/sd^2, sums of 0.5 log 1/sd^2, E_min; rtd obs, 1/sd^2,
 // sums; the Student-t normaliser table).
 static size_t fused_lds(const RtdArgs& a, const UnitArgs& u, int dz_p = 0) {
-    const size_t epm_tab = a.mod[0] == MOD_EPM ? (size_t)epm_lds_doubles(a.N, a.CP) : 0;   // EPM: the channel table
+    // EPM: the channel table, rows of cheb_cp(C) doubles in LDS (the kernel's layout; the global
+    // table's rows are a.CP = (C + 1) & ~1, shorter for C = 2, 4)
+    const size_t epm_tab = a.mod[0] == MOD_EPM ? (size_t)epm_lds_doubles(a.N, cheb_cp(a.C)) : 0;
     const size_t dz = (size_t)dz_p * kFusedUnits;                          // DZ step: the proposals
     return (size_t)(kFusedHdr + a.cheb_np * cheb_lds_stride(a.C) + epm_tab + u.wd_n + dz) *
            sizeof(double);
@@ -650,17 +661,43 @@ static size_t fused_lds(const RtdArgs& a, const UnitArgs& u, int dz_p = 0) {
 // Uniform prior and the RTD's tau is tau1, only the pieces over the prior's support
 // [tau1_lo, tau1_hi] -- a tau outside it makes the log-prob -inf whatever the channel sums
 // (the kernel's `skip` lanes), so no lane reads another piece.  Else the whole table.
+// The smallest tau_eff = 1 / (1 / tau + lam) of the sampled CFC12 half-life (LW) over tau >= tau_lo
+// and the thalf_cfc prior's support: t_half in [thalf_b, thalf_a + thalf_b], lam = ln2 / t_half
+// (0 when there is no such half-life or its range reaches 0: no bound).
+static double lw_tau_lo(const RtdArgs& a, double tau_lo) {
+    if (a.row_thalf < 0) return tau_lo;
+    const double tmin = std::min(a.thalf_b, a.thalf_a + a.thalf_b);
+    if (!(tmin > 0.0)) return 0.0;
+    return tau_lo * tmin / (tmin + kLn2Ref * tau_lo);
+}
 static void cheb_window(RtdArgs& a, const UnitArgs& u) {
     a.cheb_p0 = 0;
     a.cheb_np = a.cheb ? kChebPieces : 0;
     if (!a.cheb || !u.rtd_on || !(u.flags & NGRTD_WANT_PRIOR) || a.row_tau[0] != u.row_tau1) return;
     double x;
-    const int pa = cheb_piece(std::max(u.tau1_lo, kChebTauLo), x), pb = cheb_piece(u.tau1_hi, x);
+    // LW plans also read channel 0 at tau_eff <= tau: the window starts at the least tau_eff
+    // (a thalf_cfc outside its prior makes the log-prob -inf, like a tau outside tau1's)
+    const double lo = (a.row_thalf >= 0 && u.row_thalf >= 0) ? lw_tau_lo(a, u.tau1_lo) : u.tau1_lo;
+    if (!(lo > 0.0)) return;
+    const int pa = cheb_piece(std::max(lo, kChebTauLo), x), pb = cheb_piece(u.tau1_hi, x);
     if (pa < 0 || pb < pa) return;
     a.cheb_p0 = pa;
     a.cheb_np = pb - pa + 1;
 }
 constexpr size_t kFusedMaxLds = 157 * 1024;   // gfx950: 160 KiB per workgroup, less the static fexp/flog tables
+// A per-unit CFC12 half-life (row_thalf) runs in the single launch (the LW instances) when it
+// decays exactly one channel, channel 0 (build_table puts it first), with the instance
+// counts of lw_instance (C = 5 for the joint plans, C = 4 or 5 otherwise).
+static bool lw_instance(const UnitArgs& u, int C) {
+    const bool joint = u.ce_on && u.rtd_on && (u.flags & NGRTD_WANT_LIKE) && (u.flags & NGRTD_WANT_PRIOR);
+    return joint ? C == 5 : (C == 4 || C == 5);
+}
+static bool lw_ok(const RtdArgs& a, const UnitArgs& u) {
+    if (a.row_thalf < 0) return true;
+    int n = 0;
+    for (int c = 0; c < a.C; ++c) n += a.chan_lamw[c] ? 1 : 0;
+    return n == 1 && a.chan_lamw[0] && !a.chan_isB[0] && lw_instance(u, a.C);
+}
 static bool fused_path(const RtdArgs& a0, const UnitArgs& u) {
     static const bool disabled = std::getenv("NGRTD_NO_FUSED") != nullptr;
     RtdArgs a = a0;
@@ -673,7 +710,7 @@ static bool fused_path(const RtdArgs& a0, const UnitArgs& u) {
     a1.mod[0] = MOD_EXP;
     const bool mod2 = a.mod[1] == MOD_NONE || a.mod[1] == MOD_PISTON;
     const bool mods = mod2 && (a.mod[0] == MOD_EXP || (a.mod[0] == MOD_EPM && a.epm != nullptr));
-    return !disabled && mods && mfma_path(a1, a.row_thalf >= 0) && a.C <= 5 && u.L >= 1 &&
+    return !disabled && mods && mfma_path(a1, false) && lw_ok(a, u) && a.C <= 5 && u.L >= 1 &&
            u.L <= kFusedUnits && fused_lds(a, u) <= kFusedMaxLds;
 }
 // Waves per unit group (logp_fused_kernel ROLES): 2 = theta-only and RTD blocks in separate
@@ -737,10 +774,11 @@ static int dz_mix(const RtdArgs& a0, const UnitArgs& u, int P, bool transformed)
     if (!joint || jac != transformed || a.C != 5 || fused_roles() != 2 || P < 1 || P > kDzMaxP || !fused_path(a, u) ||
         fused_lds(a, u, transformed ? P : 0) > kFusedMaxLds)
         return -1;
-    const int mix = (a.mod[1] == MOD_PISTON ? 1 : 0) | (a.mod[0] == MOD_EPM ? 2 : 0);
-    if (!jac) return 8 | mix;
-    if (a.mod[1] == MOD_NONE) return 8 | 4 | mix;   // 12 (exponential), 14 (exp_pist_flow)
-    return -1;
+    const int mix = (a.mod[1] == MOD_PISTON ? 1 : 0) | (a.mod[0] == MOD_EPM ? 2 : 0) | (a.row_thalf >= 0 ? 32 : 0);
+    int r = -1;
+    if (!jac) r = 8 | mix;
+    else if (a.mod[1] == MOD_NONE) r = 8 | 4 | mix;   // 12 (exponential), 14 (exp_pist_flow) (+ 32: LW)
+    return (r >= 0 && fused_dz_instance_exists(r)) ? r : -1;
 }
 // Every theta row a single-launch step reads is one of ThetaPre's (the 6 CE rows, tau1,
 // nu_rtd: the joint exponential plan), all of them staged in the LDS proposal rows: no
@@ -779,6 +817,15 @@ static int launch_fused(ngrtd_ctx* ctx, const RtdArgs& a0, const UnitArgs& u, in
     RtdArgs a = a0;
     cheb_window(a, u);
     const DemcAccept da = dap ? *dap : DemcAccept{};
+    if (a.row_thalf >= 0) {   // the sampled CFC12 half-life (ngrtd_lw.hip, lw_ok)
+        const bool joint = u.ce_on && u.rtd_on && (u.flags & NGRTD_WANT_LIKE) && (u.flags & NGRTD_WANT_PRIOR);
+        const bool jac = (u.flags & NGRTD_WANT_JACOBIAN) != 0;
+        const bool single = a.mod[1] == MOD_NONE;
+        const bool full = joint && (!jac || single);
+        const int mix = 32 | (a.mod[1] == MOD_PISTON ? 1 : 0) | (a.mod[0] == MOD_EPM ? 2 : 0) | (full && jac ? 4 : 0);
+        HIP_TRY(ctx, launch_fused_lw_instance(a.C, full, mix, a, u, WB, W, logp, da, fused_lds(a, u), kFusedMaxLds, st));
+        return NGRTD_OK;
+    }
     switch (a.C) {
     case 1: launch_fused_c<1>(a, u, WB, W, logp, da, st); break;
     case 2: launch_fused_c<2>(a, u, WB, W, logp, da, st); break;
@@ -1392,7 +1439,9 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
         a.conc = p->conc.d();
         set_frag(a, p->table);
         a.cheb = nullptr;
-        if (a.mod[0] == MOD_EXP && (a.mod[1] == MOD_NONE || a.mod[1] == MOD_PISTON) && !any_lamw &&
+        // (a per-unit CFC12 half-life leaves its channel undecayed: the same surrogate serves it
+        // at tau_eff, lw_decay)
+        if (a.mod[0] == MOD_EXP && (a.mod[1] == MOD_NONE || a.mod[1] == MOD_PISTON) &&
             p->table.C <= 5 && p->dtp >= 0.0 &&
             !(d->flags & NGRTD_EXACT_RTD)) {
             NG_CHECK(cheb_prepare(ctx, p->table, (1.0 + p->dtp) - p->tp0));
@@ -1404,13 +1453,19 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
             const char* e = std::getenv("NGRTD_EPM_DIAG");     // timing diagnostics only
             a.epm_diag = e ? std::atoi(e) : 0;
         }
-        if (a.mod[0] == MOD_EPM && (a.mod[1] == MOD_NONE || a.mod[1] == MOD_PISTON) && !any_lamw &&
+        if (a.mod[0] == MOD_EPM && (a.mod[1] == MOD_NONE || a.mod[1] == MOD_PISTON) &&
             p->table.C <= 5 && p->dtp >= 0.0 && !(d->flags & NGRTD_EXACT_RTD) && ri[NGRTD_ROLE_ETA1] >= 0) {
             // block-tail surrogates over every tau' = tau / eta >= the priors' lower end (the
-            // table reaches 2^kEpmOct0); lanes below it or NaN sum their tails exactly
+            // table reaches 2^kEpmOct0); lanes below it or NaN sum their tails exactly.  A
+            // per-unit CFC12 half-life reads its channel at tau'_w = 1 / (eta / tau + lam) as well.
             static const bool disabled = std::getenv("NGRTD_NO_CHEB") != nullptr;
             double x;
-            const double lo = std::max(1.0 / (1 << -kEpmOct0), d->tau1_lo / d->eta1_hi);
+            double plo = d->tau1_lo / d->eta1_hi;
+            if (any_lamw) {
+                const double tmin = std::min(a.thalf_b, a.thalf_a + a.thalf_b);
+                plo = tmin > 0.0 ? std::min(plo, 1.0 / (d->eta1_hi / d->tau1_lo + kLn2Ref / tmin)) : 0.0;
+            }
+            const double lo = std::max(1.0 / (1 << -kEpmOct0), plo);
             const int pa = epm_piece(lo, x), pb = kEpmPieces - 1;
             if (!disabled && pa >= 0 && pb >= pa) {
                 NG_CHECK(epm_prepare(ctx, p->table, p->N, pa, pb + 1));

@@ -26,16 +26,22 @@ static hipError_t launch_dz_mix(const RtdArgs& a, const UnitArgs& u, int WB, int
     return hipGetLastError();
 }
 
-// The DZ instances: 8 | piston 1 | EPM 2 | Jacobian 4 | per-well chains 16.
+hipError_t launch_fused_dz_lw_instance(int mix, const RtdArgs& a, const UnitArgs& u, int WB, int64_t W, double* logp,
+                                       const DemcAccept& da, size_t lds, size_t max_lds, hipStream_t st);
+
+// The DZ instances: 8 | piston 1 | EPM 2 | Jacobian 4 | per-well chains 16 | the sampled
+// CFC12 half-life 32 (ngrtd_dz_lw.hip; the BMM ones exceed kDzMaxP rows at the c4 shape).
 bool fused_dz_instance_exists(int mix) {
     switch (mix & ~16) {
     case 8: case 9: case 10: case 11: case 12: case 14: return true;
+    case 40: case 42: case 44: case 46: return true;
     default: return false;
     }
 }
 // The DZ instance `mix` over W chains in blocks of WB (fused_dz_instance_exists(mix)).
 hipError_t launch_fused_dz_instance(int mix, const RtdArgs& a, const UnitArgs& u, int WB, int64_t W, double* logp,
                                     const DemcAccept& da, size_t lds, size_t max_lds, hipStream_t st) {
+    if (mix & 32) return launch_fused_dz_lw_instance(mix, a, u, WB, W, logp, da, lds, max_lds, st);
     switch (mix) {
     case 8: return launch_dz_mix<8>(a, u, WB, W, logp, da, lds, max_lds, st);
     case 9: return launch_dz_mix<9>(a, u, WB, W, logp, da, lds, max_lds, st);

@@ -866,15 +866,38 @@ __device__ __forceinline__ void unit_conc(const RtdArgs& a, int64_t u, const dou
 
 // Piston second component (BMM, convolution_integral_utils.py:178-181): the channel-table
 // row at the FIRST argmin |tp - tau2| -- a lookup, no age loop.
-template <int C>
-__device__ __forceinline__ void piston_num_tau(const RtdArgs& a, double tau2, double* num2) {
+// LW: channel 0 decays per unit (the sampled CFC12 half-life, decay constant lam): its row
+// value times exp(-lam tp_ix) (convolution_integral_utils.py:316, g * exp(-lamba tp)).
+template <int C, bool LW = false>
+__device__ __forceinline__ void piston_num_tau(const RtdArgs& a, double tau2, double* num2, double lam = 0.0) {
     const int ix = piston_index(tau2, a.tp0, a.dtp, a.N);
 #pragma unroll
     for (int c = 0; c < C; ++c) num2[c] = a.tab[(int64_t)ix * a.CP + c];
+    if (LW) num2[0] *= fexp(-lam * (ix == 0 ? a.tp0 : (double)ix + a.dtp));
 }
-template <int C>
-__device__ __forceinline__ void piston_num(const RtdArgs& a, int64_t u, double* num2) {
-    piston_num_tau<C>(a, a.theta[(int64_t)a.row_tau[1] * a.U + u], num2);
+template <int C, bool LW = false>
+__device__ __forceinline__ void piston_num(const RtdArgs& a, int64_t u, double* num2, double lam = 0.0) {
+    piston_num_tau<C, LW>(a, a.theta[(int64_t)a.row_tau[1] * a.U + u], num2, lam);
+}
+
+// The sampled CFC12 half-life (run_age_mcmc_utils.py:107-109, savenum with a 2) as the
+// single-launch kernel carries it (LW instances): the plan puts the CFC12 channel first and
+// leaves it undecayed, so that for a unit with decay constant lam = ln2 / t_half
+// (thalf_2_lambda, convolution_integral_utils.py:146-152) and exponential weights e^(-tp/tau)
+// the decayed numerator sum_k C_k e^(-tp_k / tau) e^(-lam tp_k) is
+//   e^(-lam tp_0) (C_0 + Z_0(tau_eff)),   1 / tau_eff = 1 / tau + lam,
+// with Z_0 the SAME channel function the surrogate fits (a function of one variable); the
+// normaliser stays a function of tau.  One reciprocal gives both lam and tau_eff:
+// tau_eff = tau t / (t + ln2 tau).
+struct LwDecay {
+    double lam, teff;
+};
+__device__ __forceinline__ LwDecay lw_decay(const RtdArgs& a, double tau, double thx) {
+    const double th = a.thalf_a * thx + a.thalf_b;                // t_half = 5 + 30 Beta (:334)
+    const double d[2] = {th, th + kLn2Ref * tau};
+    double r[2];
+    batch_recip<2>(d, r);
+    return LwDecay{kLn2Ref * r[0], (tau * th) * r[1]};
 }
 
 // The reference's exponential weights g = (1/tau) exp(-tp/tau) / sum(...) (:184, :270)
@@ -891,16 +914,21 @@ __device__ __forceinline__ bool exp_rtd_nan(const RtdArgs& a, double tau) {
 
 // Exact channel sums Y_c (matrix-core path) -> concentrations: the normaliser
 // 1 + s01 G with G = sum_{j<n} q^j = expm1(-beta n) / expm1(-beta) in closed form.
-template <int C>
+// LW: channel 0 decays per unit (lw_decay): yw = its exact sum Y_0 at tau_eff (bw = 1 / tau_eff)
+// and lam, numerator e^(-lam tp_0) (C_0 + s01(bw) yw).
+template <int C, bool LW = false>
 __device__ __forceinline__ void mfma_unit_conc(const RtdArgs& a, int64_t u, double bu, const double* yy,
-                                               double* conc, const double* num2 = nullptr) {
+                                               double* conc, const double* num2 = nullptr, double lam = 0.0,
+                                               double yw = 0.0, double bw = 0.0) {
     const int n = a.N - 1;
-    const double s01 = fexp(-bu * ((1.0 + a.dtp) - a.tp0));
+    const double d01 = (1.0 + a.dtp) - a.tp0;
+    const double s01 = fexp(-bu * d01);
     const double G = (n > 0) ? fexpm1(-bu * (double)n) / fexpm1(-bu) : 0.0;
     const double rden = 1.0 / (1.0 + s01 * G);     // one division for the K tracers (<= 1 ulp)
     double num[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) num[c] = a.tab0[c] + s01 * yy[c];
+    if (LW) num[0] = fexp(-lam * a.tp0) * (a.tab0[0] + fexp(-bw * d01) * yw);
     unit_conc<C>(a, u, num, rden, conc);
     const double tau = a.theta[(int64_t)a.row_tau[0] * a.U + u];
     if (exp_rtd_nan(a, tau))
@@ -1691,7 +1719,8 @@ __device__ __forceinline__ void walker_out(double* logp, const DemcAccept& d, co
 template <int C, bool FULL, bool SEQ, int MIX>
 __device__ __forceinline__ void fused_exact(const RtdArgs& a, const UnitArgs& ul, int WB, int64_t w0, int uw,
                                             bool mine, int64_t mu, int ml, double nub, double* conc,
-                                            double& like) {
+                                            double& like, LwDecay lw = LwDecay{0.0, 0.0}) {
+    constexpr bool LW = (MIX & 32) != 0;
     constexpr int NT = mfma_tiles(C);
     const int col = threadIdx.x & 15;
     const int L = ul.L;
@@ -1733,12 +1762,31 @@ __device__ __forceinline__ void fused_exact(const RtdArgs& a, const UnitArgs& ul
         mw.finish(a, y);
         mfma_pick_tile<C>(y, mw.beta, yy, bu);   // tile tq holds this lane's unit
     }
+    // LW: channel 0's exact sum at each unit's tau_eff (a second pass, one tile at a time:
+    // lanes 16 t .. 16 t + 15 hold tile t's units)
+    double yw = 0.0, bw = 0.0;
+    if (LW) {
+        const int tq = (threadIdx.x & 63) >> 4;
+#pragma unroll 1
+        for (int t = 0; t < NT; ++t) {
+            const double tv = __shfl(lw.teff, 16 * t + col, 64);
+            MfmaWave<C, 1> mw;
+            mw.init_tau(&tv);
+            mw.steps(a.frag, a.nsteps);
+            double y[1][C];
+            mw.finish(a, y);
+            if (t == tq) {
+                yw = y[0][0];
+                bw = mw.beta[0];
+            }
+        }
+    }
     if (mine) {
         ThetaPre tp;
         tp.nub = nub;
         double num2[C];
-        if (MIX & 1) piston_num<C>(a, mu, num2);
-        mfma_unit_conc<C>(a, mu, bu, yy, conc, (MIX & 1) ? num2 : nullptr);
+        if (MIX & 1) piston_num<C, LW>(a, mu, num2, lw.lam);
+        mfma_unit_conc<C, LW>(a, mu, bu, yy, conc, (MIX & 1) ? num2 : nullptr, lw.lam, yw, bw);
         like = unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL);
     }
 }
@@ -1825,9 +1873,15 @@ __device__ __forceinline__ void epm_tail_sums(const double* pt, double x, double
 //   den returned as dn / dd (dd = e^(-beta) - 1) for the caller's batched reciprocal.
 // Lanes whose tau' = 1 / beta the surrogate does not cover (or NaN) sum their tail exactly;
 // the loop is wave-uniform and runs only when some lane needs it.
-template <int C, int NPW = kEpmTailPre>
+// LW (the sampled CFC12 half-life, channel 0 undecayed in the table; see lw_decay): channel
+// 0's weights are e^(-sigma (k - m)), sigma = beta + lam, so its head runs its own weight
+// chain, its tail is the same block-tail function at tau'_w = 1 / sigma (a second piece), and
+// its numerator carries e^(-lam tp_m) (m >= 1) or e^(-lam tp_0) (f = 0).  thx: the unit's
+// thalf_cfc Beta value; *lam_out: its decay constant (the piston component needs it).
+template <int C, int NPW = kEpmTailPre, bool LW = false>
 __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, bool mvalid, double tau, double eta,
-                                         double* num, double& dn, double& dd) {
+                                         double* num, double& dn, double& dd, double thx = 0.0,
+                                         double* lam_out = nullptr) {
     constexpr int CP = cheb_cp(C), S = kEpmBlock;
     const int N = a.N;
     const double beta = eta / tau;
@@ -1842,6 +1896,20 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
     const double taup = tau * ie;
     int pc = (tail && a.epm) ? epm_piece(taup, ex) - a.epm_p0 : -1;
     pc = (unsigned)pc < (unsigned)a.epm_np ? pc : -1;
+    double lam = 0.0, qw = 0.0, taupw = 0.0, exw = 0.0;
+    int pcw = -1;
+    if (LW) {   // t_half -> lam and tau'_w = 1 / (eta / tau + lam) = tau t / (eta t + ln2 tau): one division
+        const double th = a.thalf_a * thx + a.thalf_b;
+        const double dl[2] = {th, eta * th + kLn2Ref * tau};
+        double rl[2];
+        batch_recip<2>(dl, rl);
+        lam = kLn2Ref * rl[0];
+        taupw = (tau * th) * rl[1];
+        qw = fexp(-(beta + lam));
+        pcw = (tail && a.epm) ? epm_piece(taupw, exw) - a.epm_p0 : -1;
+        pcw = (unsigned)pcw < (unsigned)a.epm_np ? pcw : -1;
+        if (lam_out) *lam_out = lam;
+    }
     const bool tail_on = tail && !(a.epm_diag & 2);
     const double* pt = a.epm + ((size_t)(tail_on ? blk - 1 : 0) * a.epm_np + (pc < 0 ? 0 : pc)) * (size_t)(kChebN * C);
     double2 tpre[epm_tail_pre_n(C, NPW) > 0 ? epm_tail_pre_n(C, NPW) : 1];
@@ -1858,21 +1926,23 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
     // waves holding such a lane and replaces only those lanes' sums, so every lane's result
     // is its own whatever its wave-mates are (the multi-step sampler's walker-major waves
     // and the log-prob kernel's well-major waves give the same bits).
-    double qB = -1.0;                                   // q^(B - m) from the head's weights (fast path)
+    double qB = -1.0, qBw = -1.0;                       // q^(B - m) from the head's weights (fast path)
     if (!(a.epm_diag & 1)) {
-        const bool qok = q <= 1.0;
+        const bool qok = q <= 1.0 && (!LW || qw <= 1.0);
         const double* hb = tabl + epm_row(B - S, CP);
-        double w = 0.0;
+        double w = 0.0, w2 = 0.0;
 #pragma unroll
         for (int i = 0; i < S; ++i) {
             const int k = B - S + i;
             w = k == m ? 1.0 : w * q;
+            if (LW) w2 = k == m ? 1.0 : w2 * qw;     // channel 0's own weights (LW)
             double rv[C];
             epm_row_load<C>(hb + i * CP, rv);
 #pragma unroll
-            for (int c = 0; c < C; ++c) y[c] = fma(rv[c], w, y[c]);
+            for (int c = 0; c < C; ++c) y[c] = fma(rv[c], (LW && c == 0) ? w2 : w, y[c]);
         }
         qB = qok ? w * q : -1.0;                        // w = q^(B - 1 - m) after the last row
+        if (LW) qBw = qok ? w2 * qw : -1.0;
         if (__any(!qok)) {
             const int kt = (B < N ? B : N) - 1;
             double yt[C];
@@ -1886,7 +1956,7 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
                 epm_row_load<C>(tabl + epm_row(on ? k : 0, CP), rv);
 #pragma unroll
                 for (int c = 0; c < C; ++c) {
-                    const double t = fma(yt[c], q, rv[c]);
+                    const double t = fma(yt[c], (LW && c == 0) ? qw : q, rv[c]);
                     yt[c] = on ? t : yt[c];
                 }
             }
@@ -1894,19 +1964,27 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
             for (int c = 0; c < C; ++c) y[c] = qok ? y[c] : yt[c];
         }
     }
-    const bool bad = mvalid && tail && pc < 0;
+    const bool bad = mvalid && tail && (pc < 0 || (LW && pcw < 0));
     double tl[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) tl[c] = 0.0;
     if (tail_on) epm_tail_sums<C, NPW>(pt, ex, tl, tpre);
+    if (LW && tail_on) {   // channel 0's tail at tau'_w: column 0 of its own piece (L2)
+        const double* pw = a.epm + ((size_t)(blk - 1) * a.epm_np + (pcw < 0 ? 0 : pcw)) * (size_t)(kChebN * C);
+        double v = pw[(kChebN - 1) * C];
+#pragma unroll
+        for (int k = kChebN - 2; k >= 0; --k) v = fma(v, exw, pw[k * C]);
+        tl[0] = v;
+    }
     if (__any(bad) && !(a.epm_diag & 4)) {              // exact tails of the uncovered lanes
         // tau' below the table (q < e^-16): the tail's terms fall below 1e-400 of its first
         // after 64 ages, so it is summed over [B, B + 64) only -- 64 iterations over each lane's own
         // LDS rows, whatever the spread of B across the wave; other uncovered tau' (NaN,
         // <= 0, beyond the table) over the whole series, the wave's union of those ranges.
-        // Both are the same top-down Horner as before per lane (same bits).
+        // Both are the same top-down Horner as before per lane (same bits).  LW: channel 0
+        // with its own q (qw); short only when both tau' and tau'_w are below the table.
         constexpr double kEpmTauLo = 1.0 / (double)(1 << -kEpmOct0);
-        const bool shortq = taup > 0.0 && taup < kEpmTauLo;
+        const bool shortq = taup > 0.0 && taup < kEpmTauLo && (!LW || (taupw > 0.0 && taupw < kEpmTauLo));
         const bool sb = bad && shortq, lb = bad && !shortq;
         double te[C];
 #pragma unroll
@@ -1920,7 +1998,7 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
                 epm_row_load<C>(tabl + epm_row(on ? k : 0, CP), rv);
 #pragma unroll
                 for (int c = 0; c < C; ++c) {
-                    const double t = fma(te[c], q, rv[c]);
+                    const double t = fma(te[c], (LW && c == 0) ? qw : q, rv[c]);
                     te[c] = on ? t : te[c];
                 }
             }
@@ -1940,7 +2018,7 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
                 epm_row_load<C>(tabl + epm_row(k, CP), rv);
 #pragma unroll
                 for (int c = 0; c < C; ++c) {
-                    const double t = fma(te[c], q, rv[c]);
+                    const double t = fma(te[c], (LW && c == 0) ? qw : q, rv[c]);
                     te[c] = on ? t : te[c];
                 }
             }
@@ -1950,21 +2028,25 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
     }
     if (tail) {
         if (qB < 0.0) qB = fexp(-beta * (double)(B - m));
+        if (LW && qBw < 0.0) qBw = fexp(-(beta + lam) * (double)(B - m));
 #pragma unroll
-        for (int c = 0; c < C; ++c) y[c] = fma(qB, tl[c], y[c]);
+        for (int c = 0; c < C; ++c) y[c] = fma((LW && c == 0) ? qBw : qB, tl[c], y[c]);
     }
     // the normaliser as a fraction den = dn / dd (the caller's one batched reciprocal
     // takes 1 / dn): G = (e^(-beta n) - 1) / (e^(-beta) - 1) over the n = N - m unmasked ages
     const int n = N - m;
     const double e1 = n > 0 ? fexpm1(-beta * (double)n) : 0.0, e2 = n > 0 ? fexpm1(-beta) : 1.0;
     if (f == 0) {
-        const double s01 = fexp(-beta * ((1.0 + a.dtp) - a.tp0));
+        const double d01 = (1.0 + a.dtp) - a.tp0;
+        const double s01 = fexp(-beta * d01);
 #pragma unroll
         for (int c = 0; c < C; ++c) num[c] = a.tab0[c] + s01 * y[c];
+        if (LW) num[0] = fexp(-lam * a.tp0) * (a.tab0[0] + fexp(-(beta + lam) * d01) * y[0]);
         dn = fma(s01, e1, e2);                          // (1 + s01 G) e2
     } else {
 #pragma unroll
         for (int c = 0; c < C; ++c) num[c] = y[c];
+        if (LW) num[0] = fexp(-lam * ((double)m + a.dtp)) * y[0];   // e^(-lam tp_m) Y_w
         dn = e1;                                        // G e2
     }
     dd = e2;
@@ -2043,6 +2125,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
                                                                               const DemcAccept dacc) {
     constexpr bool DZ = (MIX & 8) != 0;
     constexpr bool PW = DZ && (MIX & 16) != 0;   // per-well chains: one Metropolis decision per unit
+    constexpr bool LW = (MIX & 32) != 0;         // the sampled CFC12 half-life (channel 0, lw_decay)
     static_assert(!DZ || (FULL && ROLES == 2), "the DEMetropolisZ step runs in the FULL role-split kernel");
     static_assert(kFusedUnitsDz == kFusedUnits, "DZ staging stride");
     const RtdArgs& a = ak;
@@ -2107,13 +2190,14 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     // wait only for those) so that their HBM latency overlaps the prologue's barrier
     // (A/B against loading them after the barrier: 11.87 vs 11.95 us, tools/gpu_ab_libs.sh)
     ThetaPre tp0{};
-    double tau0 = 1.0, eta0 = 1.0, tau20 = 1.0;
+    double tau0 = 1.0, eta0 = 1.0, tau20 = 1.0, thx0 = 0.5;
     if (!DZ) {
         if (do_theta) theta_preload(ua, mu, tp0);
         if (do_rtd) {
             tau0 = mvalid ? a.theta[(int64_t)a.row_tau[0] * a.U + mu] : 1.0;
             if (EPM) eta0 = mvalid ? a.theta[(int64_t)a.row_eta[0] * a.U + mu] : 1.0;
             if (MIX & 1) tau20 = mvalid ? a.theta[(int64_t)a.row_tau[1] * a.U + mu] : 1.0;
+            if (LW) thx0 = mvalid ? a.theta[(int64_t)a.row_thalf * a.U + mu] : 0.5;
             tp0.nub = (FULL || ua.rtd_on) ? a.theta[(int64_t)ua.row_nu * a.U + mu] : 0.0;
         }
     }
@@ -2124,7 +2208,14 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         // whole blocks: the rows past N of the last block are zeros (epm_sums reads every row
         // of a unit's head block, weighting the ones before its first age by 0)
         const int n2 = (a.N + kEpmBlock - 1) / kEpmBlock * RB, nv = a.N * CP / 2;
-        for (int i = tid; i < n2; i += NTH) dst[(i / RB) * SB + i % RB] = i < nv ? src[i] : double2{0.0, 0.0};
+        if (a.CP == CP) {
+            for (int i = tid; i < n2; i += NTH) dst[(i / RB) * SB + i % RB] = i < nv ? src[i] : double2{0.0, 0.0};
+        } else {   // C = 2, 4: the global table's rows are (C + 1) & ~1 = C doubles, the LDS rows CP = C + 2
+            for (int i = tid; i < 2 * n2; i += NTH) {
+                const int k = i / CP, c = i % CP;
+                tabl[epm_row(k, CP) + c] = (k < a.N && c < C) ? a.tab[(int64_t)k * a.CP + c] : 0.0;
+            }
+        }
     }
 #pragma unroll
     for (int r = 0; r < kWdRegs; ++r) {
@@ -2175,7 +2266,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     double pf1[(kDzMaxP + kDzPfStep - 1) / kDzPfStep], pf2[(kDzMaxP + kDzPfStep - 1) / kDzPfStep];
     do {
         ThetaPre tp = tp0;                                // DZ: loaded per step below
-        double tau = tau0, eta = eta0, tau2 = tau20;
+        double tau = tau0, eta = eta0, tau2 = tau20, thx = thx0;
         // DZ: the argument structs through an opaque kernarg pointer per step, so that the
         // compiler re-reads their fields where they are used instead of hoisting every field
         // out of the step loop into registers (which spilled to scratch)
@@ -2270,6 +2361,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
                 tau = mvalid ? propl[a.row_tau[0] * kFusedUnits + mi] : 1.0;
                 if (EPM) eta = mvalid ? propl[a.row_eta[0] * kFusedUnits + mi] : 1.0;
                 if (MIX & 1) tau2 = mvalid ? propl[a.row_tau[1] * kFusedUnits + mi] : 1.0;
+                if (LW) thx = mvalid ? propl[a.row_thalf * kFusedUnits + mi] : 0.5;
                 tp.nub = propl[uk.row_nu * kFusedUnits + mi];
             }
         } else if (DZ) {                                      // the proposal's rows
@@ -2278,6 +2370,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
                 tau = mvalid ? a.theta[(int64_t)a.row_tau[0] * a.U + mu] : 1.0;
                 if (EPM) eta = mvalid ? a.theta[(int64_t)a.row_eta[0] * a.U + mu] : 1.0;
                 if (MIX & 1) tau2 = mvalid ? a.theta[(int64_t)a.row_tau[1] * a.U + mu] : 1.0;
+                if (LW) thx = mvalid ? a.theta[(int64_t)a.row_thalf * a.U + mu] : 0.5;
                 tp.nub = a.theta[(int64_t)uk.row_nu * a.U + mu];
             }
         }
@@ -2286,8 +2379,8 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         if (EPM && do_rtd) {
             double conc[kMaxTracer];
             {
-                double num[C], dn, dd;
-                epm_sums<C, DZ ? kEpmTailPreDz : kEpmTailPre>(a, tabl, mvalid, tau, eta, num, dn, dd);
+                double num[C], dn, dd, lam = 0.0;
+                epm_sums<C, DZ ? kEpmTailPreDz : kEpmTailPre, LW>(a, tabl, mvalid, tau, eta, num, dn, dd, thx, &lam);
                 const double dr[2] = {dn, tp.nub * (uk.rnu_max - uk.rnu_min) + uk.rnu_min};
                 double rr[2];
                 batch_recip<2>(dr, rr);
@@ -2295,6 +2388,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
                 if (MIX & 1) {                  // the piston row from the LDS channel table
                     const int ix = piston_index(tau2, a.tp0, a.dtp, a.N);
                     epm_row_load<C>(tabl + epm_row(ix, CP), num2);
+                    if (LW) num2[0] *= fexp(-lam * (ix == 0 ? a.tp0 : (double)ix + a.dtp));
                 }
                 unit_conc<C>(a, mu, num, dd * rr[0], conc, (MIX & 1) ? num2 : nullptr);
                 like = mvalid ? unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL, &rr[1]) : 0.0;
@@ -2308,6 +2402,16 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             double cx = 0.0;
             int cpc = a.cheb ? cheb_piece(tau, cx) - a.cheb_p0 : -1;
             cpc = (unsigned)cpc < (unsigned)a.cheb_np ? cpc : -1;   // outside the staged window
+            // LW: channel 0 from the surrogate at tau_eff (its own piece of the staged window)
+            LwDecay lw{0.0, 0.0};
+            double cxw = 0.0;
+            int cpw = 0;
+            if (LW) {
+                lw = lw_decay(a, tau, thx);
+                cpw = a.cheb ? cheb_piece(lw.teff, cxw) - a.cheb_p0 : -1;
+                cpw = (unsigned)cpw < (unsigned)a.cheb_np ? cpw : -1;
+            }
+            const bool unc = cpc < 0 || (LW && cpw < 0);
             // An uncovered tau (< 1/2, NaN) outside the support of the tau1 Uniform prior makes the
             // unit's log-prob -inf whatever the concentrations are -- unless they are NaN, which
             // the reference's weights produce exactly when (1/tau) exp(-tp/tau) overflows or
@@ -2315,29 +2419,39 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             // lane needs no channel sums, only that NaN predicate.  DE-MC proposals below the
             // prior bound are common; they would otherwise send whole waves to the exact path.
             bool skip = false, cnan = false;
-            if (cpc < 0 && a.cheb && (FULL || (uk.rtd_on && (uk.flags & NGRTD_WANT_PRIOR))) &&
-                a.row_tau[0] == uk.row_tau1 && !(tau >= uk.tau1_lo && tau <= uk.tau1_hi) &&
+            const bool prior_on = FULL || (uk.rtd_on && (uk.flags & NGRTD_WANT_PRIOR));
+            if (unc && a.cheb && prior_on && a.row_tau[0] == uk.row_tau1 && !(tau >= uk.tau1_lo && tau <= uk.tau1_hi) &&
                 !(uk.tau1_lo < kChebTauLo && tau >= uk.tau1_lo)) {
                 skip = true;
                 cnan = exp_rtd_nan(a, tau);
             }
-            const bool bad = cpc < 0 && !skip;
+            // LW: a thalf_cfc Beta value outside [0, 1] makes the log-prob -inf as well; NaN
+            // gives a NaN decay (and concentration), as the reference's
+            if (LW && unc && !skip && a.cheb && prior_on && a.row_thalf == uk.row_thalf && !(thx >= 0.0 && thx <= 1.0)) {
+                skip = true;
+                cnan = !(thx == thx) || exp_rtd_nan(a, tau);
+            }
+            const bool bad = unc && !skip;
             cpc = cpc < 0 ? 0 : cpc;
+            cpw = cpw < 0 ? 0 : cpw;
             double zz[C + 1];
             NGRTD_PROBE(4);
             cheb_sums<C + 1, ROLES == 2>(cheb + cpc * PST, CP, cx, zz);   // s01 Y_c (c < C), s01 G
+            double zw = 0.0;
+            if (LW) cheb_sums<1, ROLES == 2>(cheb + cpw * PST, CP, cxw, &zw);   // channel 0 at tau_eff
             NGRTD_PROBE(5);
             double conc[kMaxTracer];
             {
                 double num[C];
 #pragma unroll
                 for (int c = 0; c < C; ++c) num[c] = a.tab0[c] + zz[c];
+                if (LW) num[0] = fexp(-lw.lam * a.tp0) * (a.tab0[0] + zw);
                 // the normaliser's reciprocal and the Student-t 1/nu: one division
                 const double dr[2] = {1.0 + zz[C], tp.nub * (uk.rnu_max - uk.rnu_min) + uk.rnu_min};
                 double rr[2];
                 batch_recip<2>(dr, rr);
                 double num2[C];
-                if (MIX & 1) piston_num_tau<C>(a, tau2, num2);
+                if (MIX & 1) piston_num_tau<C, LW>(a, tau2, num2, lw.lam);
                 unit_conc<C>(a, mu, num, rr[0], conc, (MIX & 1) ? num2 : nullptr);
                 if (cnan)
                     for (int t = 0; t < a.K; ++t) conc[t] = __builtin_nan("");
@@ -2353,7 +2467,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
                     __threadfence_block();
                 }
                 // ROLES = 2: one tile per pass keeps the exact path inside the 128-VGPR budget
-                fused_exact<C, FULL, ROLES == 2, MIX>(a, ul, WB, w0, uw, mvalid && bad, mu, ml, tp.nub, conc, like);
+                fused_exact<C, FULL, ROLES == 2, MIX>(a, ul, WB, w0, uw, mvalid && bad, mu, ml, tp.nub, conc, like, lw);
             }
             if (!FULL && a.conc && mvalid)                        // forward(): model concentrations
                 for (int t = 0; t < a.K; ++t) a.conc[(int64_t)t * a.U + mu] = conc[t];

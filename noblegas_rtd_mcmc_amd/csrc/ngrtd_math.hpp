@@ -17,6 +17,8 @@ namespace ngrtd {
 
 constexpr double kNegInf = -__builtin_inf();
 constexpr double kPi = 3.141592653589793;
+// -1 * np.log(0.5): the numerator of thalf_2_lambda (convolution_integral_utils.py:146-152)
+constexpr double kLn2Ref = 0.6931471805599453;
 
 // Dry-air mole fractions, noble_gas_utils.py:38-73 (He, Ne, Ar, Kr, Xe)
 struct GasCoef {

@@ -17,7 +17,8 @@ def _same(a, b):
 
 @pytest.mark.parametrize("per_well", [True, False])
 @pytest.mark.parametrize("kind", ["joint", "ce_only", "joint_transformed", "bmm_transformed", "bmm", "epm",
-                                  "epm_piston", "epm_transformed", "joint_c4_transformed", "joint_l3"])
+                                  "epm_piston", "epm_transformed", "joint_c4_transformed", "joint_l3",
+                                  "joint_123", "epm_123_transformed", "bmm_123", "rtd_only_123_transformed"])
 def test_device_demcz_matches_torch_bitwise(kind, per_well):
     """Tuning (every 4 steps), stop_tuning's history drop and the draws: device chains ==
     torch chains, bit for bit.  joint / bmm / epm / epm_piston / joint_transformed /
@@ -26,7 +27,7 @@ def test_device_demcz_matches_torch_bitwise(kind, per_well):
     demc_accept_kernel; bmm_transformed: the proposal kernel + the log-prob kernel pair.
     *_transformed: PyMC3's logodds / interval / log space, the plan adds the Jacobian.
     joint_c4_transformed: the c4 shape (64 wells, 8 walkers per block), 520 chains: the last
-    block is partial.  joint_l3: 3 wells, so a block holds 170 walkers (510 of its 512 unit
+    block is partial.  *_123: savenum 123 (the per-unit CFC12 half-life in the single launch).  joint_l3: 3 wells, so a block holds 170 walkers (510 of its 512 unit
     slots) and the walker-major unit mapping of the multi-step launch leaves a ragged tail.
     per_well: every (walker, well) its own chain (the default; the per-unit decision inside
     the multi-step launch, or the per-unit proposal / log-prob / accept kernels) or one chain
@@ -54,6 +55,18 @@ def test_device_demcz_matches_torch_bitwise(kind, per_well):
         spec = wl.c4_spec(L=64, N=1200)
     if kind == "joint_l3":      # 3 wells: 170 walkers per block (510 units), not a power of two
         spec = wl.c4_spec(L=3, N=300)
+    if kind in ("joint_123", "epm_123_transformed", "bmm_123", "rtd_only_123_transformed"):
+        # savenum 123 (J, thalf_cfc, lamsf6 sampled): the single-launch LW instances
+        m1 = "exp_pist_flow" if kind.startswith("epm") else "exponential"
+        m2 = "piston" if kind.startswith("bmm") else None
+        pn = ("tau1",) + (("tau2", "f1") if m2 else ()) + (("eta1",) if m1 == "exp_pist_flow" else ()) + \
+            ("J", "thalf_cfc", "lamsf6")
+        spec = wl.c4_spec(L=4, N=1200, mod_type1=m1, mod_type2=m2, par_names=pn)
+        if kind.startswith("rtd_only"):
+            keep = [0, 1, 2, 4]
+            r = spec.rtd
+            spec = ModelSpec(n_wells=4, rtd=dataclasses.replace(r, tracers=[r.tracers[i] for i in keep],
+                                                                 obs=r.obs[:, keep], sd=r.sd[:, keep]))
     if kind.endswith("transformed"):
         spec = dataclasses.replace(spec, jacobian=True)
     W = 520 if kind == "joint_c4_transformed" else 200 if kind == "joint_l3" else 40

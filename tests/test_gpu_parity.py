@@ -215,6 +215,92 @@ def test_published_models_c4_shape_vs_oracle(model):
     lp.close()
 
 
+PN_123 = ("J", "thalf_cfc", "lamsf6")      # savenum 123 (run_age_mcmc.py:180-198)
+
+
+def _spec_123(model, L=64, jac=False, rtd_only=False, savenum_pars=PN_123):
+    import dataclasses
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    from noblegas_rtd_mcmc_amd.spec import ModelSpec
+    m1, _, m2 = model.partition("-")
+    pn = ["tau1"] + (["tau2", "f1"] if m2 else []) + (["eta1"] if m1 == "exp_pist_flow" else []) + list(savenum_pars)
+    spec = wl.c4_spec(L=L, N=1200, mod_type1=m1, mod_type2=m2 or None, par_names=tuple(pn))
+    if rtd_only:        # the reference's own RTD model: CFC12, SF6, H3, He4_ter, no CE block
+        keep = [0, 1, 2, 4]
+        r = spec.rtd
+        rtd = dataclasses.replace(r, tracers=[r.tracers[i] for i in keep], obs=r.obs[:, keep], sd=r.sd[:, keep])
+        spec = ModelSpec(n_wells=L, rtd=rtd)
+    return dataclasses.replace(spec, jacobian=jac)
+
+
+@pytest.mark.parametrize("model", ["exponential", "exp_pist_flow", "exponential-piston", "exp_pist_flow-piston"])
+@pytest.mark.parametrize("variant", ["joint", "joint_jac", "rtd_only", "rtd_only_savenum0"])
+def test_published_models_123_single_launch_vs_oracle(model, variant):
+    """The reference's published configuration, savenum 123 (J, thalf_cfc and lamsf6
+    sampled; every shipped conv_traces/*.123.netcdf): the per-walker CFC12 half-life runs in
+    the single-launch kernel (LW instances: the CFC12 channel's surrogate at
+    tau_eff = 1 / (1 / tau + lam), lw_decay) -- one launch, vs the vectorised oracle on 264
+    walkers across every block boundary, at the c4 shape (joint: 2048 x 64 x (5 gases + 5
+    tracers); joint_jac: with the transform Jacobians) and as the reference's own RTD-only
+    model (4 tracers, 64 wells; rtd_only_savenum0: without the savenum parameters -- its 4
+    channels once read a 6-double-row EPM table layout from the 4-double-row global table);
+    determinism and device == host; forward() (the posterior predictive) vs the per-walker
+    oracle."""
+    import torch
+    import oracle.models as om
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+    spec = _spec_123(model, jac=variant == "joint_jac", rtd_only=variant.startswith("rtd_only"),
+                     savenum_pars=() if variant.endswith("savenum0") else PN_123)
+    th = wl.sample_prior(spec, 2048, np.random.default_rng(34568))
+    lp = LogProb(spec, max_walkers=2048)
+    dev = torch.from_numpy(th).cuda()
+    lp.ctx.set_profiling(True)
+    lp.kernel_stats(reset=True)
+    a = lp(dev).cpu().numpy()
+    lp.ctx.set_profiling(False)
+    ks = lp.kernel_stats(reset=True)
+    assert ks["fused"][1] == 1 and ks["rtd"][1] == 0 and ks["unit"][1] == 0, ks   # one launch
+    assert np.array_equal(a, lp(dev).cpu().numpy()) and np.array_equal(a, lp(th, soa=True))
+    sel = many_walkers(2048, seed=7)
+    refv = log_prob_vec(spec, np.ascontiguousarray(th[:, :, sel]))
+    ok = close(a[sel], refv, 1e-12, 1e-9)
+    assert ok.all(), (np.array(sel)[~ok], a[sel][~ok], refv[~ok])
+    assert np.isfinite(a).mean() > 0.5
+    walkers = [0, 777, 2047]
+    ce, rt = lp.forward(th, soa=True)
+    ce_ref, rt_ref = om.forward(spec, th, walkers=walkers)
+    assert close(np.transpose(rt[:, :, walkers], (1, 0, 2)), rt_ref, 1e-12).all()
+    lp.close()
+
+
+@pytest.mark.parametrize("model", ["exponential", "exp_pist_flow", "exponential-piston", "exp_pist_flow-piston"])
+def test_published_models_123_edges(model):
+    """Savenum 123 in the single launch at its edges: thalf_cfc at its prior's ends (0, 1:
+    t_half 5 and 35 years), tau1 at 1 and 1000, the EPM eta at 1 and 5, and out-of-support
+    values of thalf_cfc (the log-prob is -inf, whatever the surrogate covers) vs the
+    per-walker oracle."""
+    import oracle.models as om
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+    spec = _spec_123(model, L=2)
+    W = 64
+    th = wl.sample_prior(spec, W, np.random.default_rng(3))
+    R = {r: i for i, r in enumerate(spec.roles)}
+    th[R["thalf_cfc_beta"], :, 0:8] = [[0.0, 1.0, 1e-12, 1 - 1e-12, 0.5, 0.0, 1.0, 0.25]] * 2
+    th[R["tau1"], :, 0:8] = [[1.0, 1.0, 1000.0, 1000.0, 1.0, 1000.0, 500.0, 1.0 + 1e-9]] * 2
+    if "eta1" in R:
+        th[R["eta1"], :, 0:8] = [[1.0, 5.0, 5.0, 1.0, 5.0, 1.0 + 1e-12, 5.0, 3.0]] * 2
+    th[R["thalf_cfc_beta"], :, 8:12] = [[-0.1, 1.2, -1.0 / 6.0, 7.0]] * 2     # outside the prior
+    lp = LogProb(spec, max_walkers=W)
+    a = lp(th, soa=True)
+    ref = om.log_prob(spec, th)
+    ok = close(a, ref, 1e-12, 1e-9) | (np.isneginf(ref) & ~np.isposinf(a) & ~(a > -np.inf))
+    assert ok.all(), (np.nonzero(~ok)[0], a[~ok], ref[~ok])
+    assert np.isfinite(a[[2, 3, 4, 7]]).all()      # (the Beta(2, 2) density is 0 at thalf_cfc 0 and 1)
+    lp.close()
+
+
 @pytest.mark.parametrize("model", ["exponential", "exp_pist_flow", "exponential-piston", "exp_pist_flow-piston"])
 def test_jacobian_plans_c4_shape_vs_oracle(model):
     """Plans with the PyMC3 transform Jacobians (the transformed-space sampler's log-prob;
