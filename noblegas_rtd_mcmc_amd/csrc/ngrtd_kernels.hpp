@@ -1828,6 +1828,16 @@ constexpr int kEpmTailPre = NGRTD_EPM_TAIL_PRE;
 #define NGRTD_EPM_TAIL_PRE_DZ 4
 #endif
 constexpr int kEpmTailPreDz = NGRTD_EPM_TAIL_PRE_DZ;
+// the LW instances (the sampled CFC12 half-life): channel 0's own tail column (kChebN doubles)
+// is loaded ahead too (kEpmLwPre), in place of some of the shared tail's chunks
+#ifndef NGRTD_EPM_TAIL_PRE_LW
+#define NGRTD_EPM_TAIL_PRE_LW 4
+#endif
+constexpr int kEpmTailPreLw = NGRTD_EPM_TAIL_PRE_LW;
+#ifndef NGRTD_EPM_LW_PRE
+#define NGRTD_EPM_LW_PRE 1
+#endif
+constexpr bool kEpmLwPre = NGRTD_EPM_LW_PRE != 0;
 __host__ __device__ constexpr int epm_tail_pre_n(int C, int want) { return want < kChebN * C / 2 ? want : kChebN * C / 2; }
 template <int C, int NPW>
 __device__ __forceinline__ void epm_tail_pre(const double* pt, bool on, double2* pre) {
@@ -1914,6 +1924,14 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
     const double* pt = a.epm + ((size_t)(tail_on ? blk - 1 : 0) * a.epm_np + (pc < 0 ? 0 : pc)) * (size_t)(kChebN * C);
     double2 tpre[epm_tail_pre_n(C, NPW) > 0 ? epm_tail_pre_n(C, NPW) : 1];
     epm_tail_pre<C, NPW>(pt, tail_on, tpre);
+    // LW: channel 0's tail coefficients at tau'_w (column 0 of its own piece, L2), loaded
+    // before the head loop as well (kEpmLwPre)
+    double twp[LW ? kChebN : 1];
+    if (LW && kEpmLwPre) {
+        const double* pw = a.epm + ((size_t)(tail_on ? blk - 1 : 0) * a.epm_np + (pcw < 0 ? 0 : pcw)) * (size_t)(kChebN * C);
+#pragma unroll
+        for (int k = 0; k < kChebN; ++k) twp[k] = tail_on ? pw[k * C] : 0.0;
+    }
     double y[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) y[c] = 0.0;
@@ -1971,9 +1989,9 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
     if (tail_on) epm_tail_sums<C, NPW>(pt, ex, tl, tpre);
     if (LW && tail_on) {   // channel 0's tail at tau'_w: column 0 of its own piece (L2)
         const double* pw = a.epm + ((size_t)(blk - 1) * a.epm_np + (pcw < 0 ? 0 : pcw)) * (size_t)(kChebN * C);
-        double v = pw[(kChebN - 1) * C];
+        double v = kEpmLwPre ? twp[kChebN - 1] : pw[(kChebN - 1) * C];
 #pragma unroll
-        for (int k = kChebN - 2; k >= 0; --k) v = fma(v, exw, pw[k * C]);
+        for (int k = kChebN - 2; k >= 0; --k) v = fma(v, exw, kEpmLwPre ? twp[k] : pw[k * C]);
         tl[0] = v;
     }
     if (__any(bad) && !(a.epm_diag & 4)) {              // exact tails of the uncovered lanes
@@ -2380,7 +2398,8 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             double conc[kMaxTracer];
             {
                 double num[C], dn, dd, lam = 0.0;
-                epm_sums<C, DZ ? kEpmTailPreDz : kEpmTailPre, LW>(a, tabl, mvalid, tau, eta, num, dn, dd, thx, &lam);
+                epm_sums<C, DZ ? kEpmTailPreDz : LW ? kEpmTailPreLw : kEpmTailPre, LW>(a, tabl, mvalid, tau, eta, num, dn,
+                                                                                     dd, thx, &lam);
                 const double dr[2] = {dn, tp.nub * (uk.rnu_max - uk.rnu_min) + uk.rnu_min};
                 double rr[2];
                 batch_recip<2>(dr, rr);
