@@ -23,6 +23,7 @@
 #include "ngrtd_kernels.hpp"
 #include "ngrtd_prep.hpp"
 #include "ngrtd_frac.hpp"
+#include "ngrtd_dzc.hpp"
 
 using namespace ngrtd;
 
@@ -31,6 +32,10 @@ namespace ngrtd {
 hipError_t launch_fused_dz_instance(int mix, const RtdArgs& a, const UnitArgs& u, int WB, int64_t W, double* logp,
                                     const DemcAccept& da, size_t lds, size_t max_lds, hipStream_t st);
 bool fused_dz_instance_exists(int mix);
+// ngrtd_dzc.hip: the lane-chain DEMetropolisZ instances (RTD-only / CE-only models, per-well chains)
+bool dz_chain_instance_exists(int C, int mix);
+hipError_t launch_dz_chain(int C, int mix, const RtdArgs& a, const UnitArgs& u, const DemcAccept& da, int64_t U,
+                           size_t lds, size_t max_lds, hipStream_t st);
 // ngrtd_lw.hip: the log-prob instances with the sampled CFC12 half-life (MIX bit 5)
 hipError_t launch_fused_lw_instance(int C, bool full, int mix, const RtdArgs& a, const UnitArgs& u, int WB, int64_t W,
                                     double* logp, const DemcAccept& da, size_t lds, size_t max_lds, hipStream_t st);
@@ -759,7 +764,10 @@ static void launch_fused_c(const RtdArgs& a, const UnitArgs& u, int WB, int64_t 
     if (joint && !jac) launch_fused_cf<C, true>(a, u, WB, W, logp, da, st);
     else if (joint && a.mod[1] == MOD_NONE && a.mod[0] == MOD_EXP) launch_fused_cfr<C, true, 2, 4>(a, u, WB, W, logp, da, st);
     else if (joint && a.mod[1] == MOD_NONE && a.mod[0] == MOD_EPM) launch_fused_cfr<C, true, 2, 6>(a, u, WB, W, logp, da, st);
-    else launch_fused_cf<C, false>(a, u, WB, W, logp, da, st);
+    else if (C == 5 && joint && a.mod[1] == MOD_PISTON) {   // the BMMs' transformed-space log-prob (c4: 5 channels)
+        if (a.mod[0] == MOD_EXP) launch_fused_cfr<C, true, 2, 5>(a, u, WB, W, logp, da, st);
+        else launch_fused_cfr<C, true, 2, 7>(a, u, WB, W, logp, da, st);
+    } else launch_fused_cf<C, false>(a, u, WB, W, logp, da, st);
 }
 // Single-launch DEMetropolisZ step (logp_fused_kernel MIX bit 3): the joint plan on a
 // FULL instance with C = 5 channels (the c3 / c4 / published-model workloads), the role-split
@@ -775,10 +783,34 @@ static int dz_mix(const RtdArgs& a0, const UnitArgs& u, int P, bool transformed)
         fused_lds(a, u, transformed ? P : 0) > kFusedMaxLds)
         return -1;
     const int mix = (a.mod[1] == MOD_PISTON ? 1 : 0) | (a.mod[0] == MOD_EPM ? 2 : 0) | (a.row_thalf >= 0 ? 32 : 0);
-    int r = -1;
-    if (!jac) r = 8 | mix;
-    else if (a.mod[1] == MOD_NONE) r = 8 | 4 | mix;   // 12 (exponential), 14 (exp_pist_flow) (+ 32: LW)
-    return (r >= 0 && fused_dz_instance_exists(r)) ? r : -1;
+    const int r = 8 | (jac ? 4 : 0) | mix;   // 12 (exponential), 13 / 15 (BMMs), 14 (exp_pist_flow) (+ 32: LW)
+    return fused_dz_instance_exists(r) ? r : -1;
+}
+// The lane-chain step (ngrtd_dzc.hpp dz_chain_kernel) for the plans the reference itself
+// samples: its RTD-only model (1 or 4 tracers, exponential / exp_pist_flow first component,
+// optional piston second, the sampled CFC12 half-life) and its CE-only model; per-well chains,
+// at most kDzcMaxP rows, the tables and the proposal rows fitting in LDS.  -1: none.
+static int dzc_mix(const RtdArgs& a0, const UnitArgs& u, int P, bool transformed, size_t* lds) {
+    const bool jac = (u.flags & NGRTD_WANT_JACOBIAN) != 0;
+    if (jac != transformed || P < 1 || P > kDzcMaxP) return -1;
+    RtdArgs a = a0;
+    int mix, C = 1;
+    if (u.ce_on && !u.rtd_on) {
+        mix = 64 | (jac ? 4 : 0);
+        a.cheb_np = 0;
+        a.N = 0;
+    } else if (u.rtd_on && !u.ce_on) {
+        cheb_window(a, u);
+        if (!fused_path(a, u)) return -1;
+        C = a.C;
+        mix = (a.mod[1] == MOD_PISTON ? 1 : 0) | (a.mod[0] == MOD_EPM ? 2 : 0) | (jac ? 4 : 0) |
+              (a.row_thalf >= 0 ? 32 : 0);
+    } else {
+        return -1;
+    }
+    if (!dz_chain_instance_exists(C, mix)) return -1;
+    *lds = dzc_lds_doubles(C, mix, (mix & 64) ? 0 : a.cheb_np, a.N, u.wd_n, P) * sizeof(double);
+    return *lds <= kFusedMaxLds ? mix : -1;
 }
 // Every theta row a single-launch step reads is one of ThetaPre's (the 6 CE rows, tau1,
 // nu_rtd: the joint exponential plan), all of them staged in the LDS proposal rows: no
@@ -1883,6 +1915,19 @@ int ngrtd_demcz_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64
         if (!(m_env && std::strcmp(m_env, "pair") == 0)) dzm = dz_mix(dr, du, p->desc.n_params, tr);
         if (dzm >= 0 && pw) dzm |= 16;   // per-well chains: one decision per unit
     }
+    // the lane-chain step (RTD-only / CE-only models, per-well chains), where no logp_fused_kernel
+    // instance steps the plan
+    int dzc = -1;
+    size_t dzc_lds = 0;
+    {
+        const char* m_env = std::getenv("NGRTD_DZ_MODE");
+        if (dzm < 0 && pw && !(m_env && std::strcmp(m_env, "pair") == 0)) {
+            du.theta = prop_x; du.U = (int64_t)p->desc.n_wells * W; du.W = W;
+            dr.theta = prop_x; dr.U = du.U; dr.conc = nullptr;
+            dzc = dzc_mix(dr, du, p->desc.n_params, tr, &dzc_lds);
+        }
+    }
+    const bool multi = dzm >= 0 || dzc >= 0;   // one launch per chunk of steps
     const dim3 gpw((unsigned)cdiv(U, 256));   // per-well proposal / accept kernels
     // single-launch instance: chunks of up to NGRTD_DZ_CHUNK (default 256) steps per launch,
     // each block running its own chains through the chunk (DemcAccept::Sched / dz_step)
@@ -1892,7 +1937,7 @@ int ngrtd_demcz_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64
     // like its history entries) for the whole call: transposed in here, back after the loop
     const int Lw = p->desc.n_wells;
     double* xw[2] = {nullptr, nullptr};
-    if (dzm >= 0) {
+    if (multi) {
         for (int i = 0; i < (tr ? 2 : 1); ++i) {
             HIP_TRY(ctx, p->demc_xw[i].ensure((size_t)E * sizeof(double)));
             xw[i] = p->demc_xw[i].d();
@@ -1910,7 +1955,7 @@ int ngrtd_demcz_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64
     double* cscal = z->scaling;
     int32_t* cnat = z->n_acc_tune;
     const dim3 g1((unsigned)cdiv(W, 32), (unsigned)cdiv(Lw, 32), 1u), g1b((unsigned)cdiv(Lw, 32), (unsigned)cdiv(W, 32), 1u);
-    if (dzm >= 0 && pw) {
+    if (multi && pw) {
         HIP_TRY(ctx, p->demc_pw.ensure((size_t)U * (3 * sizeof(double) + sizeof(int32_t))));
         cl = p->demc_pw.d(); clamb = cl + U; cscal = clamb + U;
         cnat = reinterpret_cast<int32_t*>(cscal + U);
@@ -1920,7 +1965,7 @@ int ngrtd_demcz_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64
         hipLaunchKernelGGL(dz_layout_i32_kernel, g1, dim3(256), 0, st, z->n_acc_tune, cnat, (int64_t)Lw, W);
         HIP_TRY(ctx, hipGetLastError());
     }
-    for (int64_t j = 0; dzm >= 0 && j < n_steps;) {
+    for (int64_t j = 0; multi && j < n_steps;) {
         const int64_t k = std::min(chunk, n_steps - j);
         DemcAccept da{cl, acc, cnt, xw[0], nullptr, p->desc.n_params, 0, cnat, clamb, cscal,
                       0, z->tune_target, z->tune_interval, accepted_log ? accepted_log + j * NC : nullptr,
@@ -1940,7 +1985,14 @@ int ngrtd_demcz_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64
         da.sch.tune_target = z->tune_target; da.sch.tune_interval = z->tune_interval;
         hipEvent_t ev = nullptr;
         NG_CHECK(timed_begin(p, ctx->profiling, st, &ev));
-        NG_CHECK(launch_fused_dz(ctx, dr, du, W, p->desc.n_wells, p->demc_lp.d(), st, da, dzm));
+        if (dzc >= 0) {
+            RtdArgs dwin = dr;
+            if (!(dzc & 64)) cheb_window(dwin, du);
+            da.state_lds = 0; da.prop_lds = 0; da.prop_skip = 0;
+            HIP_TRY(ctx, launch_dz_chain(dwin.C, dzc, dwin, du, da, du.U, dzc_lds, kFusedMaxLds, st));
+        } else {
+            NG_CHECK(launch_fused_dz(ctx, dr, du, W, p->desc.n_wells, p->demc_lp.d(), st, da, dzm));
+        }
         NG_CHECK(timed_end(p, ctx->profiling, st, 3, ev));
         // the host state after the chunk's last step (the kernel's own schedule)
         const DzStep last = dz_step(da.sch, k - 1);
@@ -1949,7 +2001,7 @@ int ngrtd_demcz_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64
         z->steps_done += k;
         j += k;
     }
-    if (dzm >= 0) {
+    if (multi) {
         const dim3 g((unsigned)cdiv(Lw, 32), (unsigned)cdiv(W, 32), (unsigned)p->desc.n_params);
         hipLaunchKernelGGL(dz_layout_kernel, g, dim3(256), 0, st, xw[0], theta, W, (int64_t)Lw);
         if (tr) hipLaunchKernelGGL(dz_layout_kernel, g, dim3(256), 0, st, xw[1], z->theta_u, W, (int64_t)Lw);
@@ -1961,7 +2013,7 @@ int ngrtd_demcz_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64
         }
         HIP_TRY(ctx, hipGetLastError());
     }
-    for (int64_t j = 0; dzm < 0 && j < n_steps; ++j) {
+    for (int64_t j = 0; !multi && j < n_steps; ++j) {
         const int64_t s = z->steps_done;
         const uint64_t key = demc_key(z->seed, (uint64_t)s);
         // the previous step's state becomes history entry s - 1 (the previous call appended

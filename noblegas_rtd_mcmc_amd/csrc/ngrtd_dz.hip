@@ -29,11 +29,12 @@ static hipError_t launch_dz_mix(const RtdArgs& a, const UnitArgs& u, int WB, int
 hipError_t launch_fused_dz_lw_instance(int mix, const RtdArgs& a, const UnitArgs& u, int WB, int64_t W, double* logp,
                                        const DemcAccept& da, size_t lds, size_t max_lds, hipStream_t st);
 
-// The DZ instances: 8 | piston 1 | EPM 2 | Jacobian 4 | per-well chains 16 | the sampled
+// The DZ instances: 8 | piston 1 | EPM 2 | Jacobian 4 (13 / 15: the transformed-space BMMs) |
+// per-well chains 16 | the sampled
 // CFC12 half-life 32 (ngrtd_dz_lw.hip; the BMM ones exceed kDzMaxP rows at the c4 shape).
 bool fused_dz_instance_exists(int mix) {
     switch (mix & ~16) {
-    case 8: case 9: case 10: case 11: case 12: case 14: return true;
+    case 8: case 9: case 10: case 11: case 12: case 13: case 14: case 15: return true;
     case 40: case 42: case 44: case 46: return true;
     default: return false;
     }
@@ -48,13 +49,17 @@ hipError_t launch_fused_dz_instance(int mix, const RtdArgs& a, const UnitArgs& u
     case 10: return launch_dz_mix<10>(a, u, WB, W, logp, da, lds, max_lds, st);
     case 11: return launch_dz_mix<11>(a, u, WB, W, logp, da, lds, max_lds, st);
     case 12: return launch_dz_mix<12>(a, u, WB, W, logp, da, lds, max_lds, st);
+    case 13: return launch_dz_mix<13>(a, u, WB, W, logp, da, lds, max_lds, st);
     case 14: return launch_dz_mix<14>(a, u, WB, W, logp, da, lds, max_lds, st);
+    case 15: return launch_dz_mix<15>(a, u, WB, W, logp, da, lds, max_lds, st);
     case 24: return launch_dz_mix<24>(a, u, WB, W, logp, da, lds, max_lds, st);
     case 25: return launch_dz_mix<25>(a, u, WB, W, logp, da, lds, max_lds, st);
     case 26: return launch_dz_mix<26>(a, u, WB, W, logp, da, lds, max_lds, st);
     case 27: return launch_dz_mix<27>(a, u, WB, W, logp, da, lds, max_lds, st);
     case 28: return launch_dz_mix<28>(a, u, WB, W, logp, da, lds, max_lds, st);
+    case 29: return launch_dz_mix<29>(a, u, WB, W, logp, da, lds, max_lds, st);
     case 30: return launch_dz_mix<30>(a, u, WB, W, logp, da, lds, max_lds, st);
+    case 31: return launch_dz_mix<31>(a, u, WB, W, logp, da, lds, max_lds, st);
     default: return hipErrorInvalidValue;
     }
 }

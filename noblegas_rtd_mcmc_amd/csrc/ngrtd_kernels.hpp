@@ -832,7 +832,7 @@ __host__ __device__ __forceinline__ void cheb_sums(const double* pc, int CP, dou
 // num2: the second BMM component's numerators when it is a piston (its normaliser is
 // g.sum() = 1, convolution_integral_utils.py:178-181, 270): cout = f1 cout1 + f2 cout2 with
 // f2 = 1 - f1 (the Deterministic of run_age_mcmc_utils.py:304).
-template <int C>
+template <int C, bool ST = false>
 __device__ __forceinline__ void unit_conc(const RtdArgs& a, int64_t u, const double* num, double rden,
                                           double* conc, const double* num2 = nullptr) {
     const double fmix = (a.row_f1 >= 0) ? a.theta[(int64_t)a.row_f1 * a.U + u] : 1.0;
@@ -841,7 +841,12 @@ __device__ __forceinline__ void unit_conc(const RtdArgs& a, int64_t u, const dou
         const double jv = a.theta[(int64_t)a.row_J * a.U + u];
         Jw = a.J_is_log10 ? exp10(jv) : jv;
     }
-    for (int t = 0; t < a.K; ++t) {
+    // ST (dz_chain_kernel, whose theta view is a modified local copy of a): t < C -- every tracer
+    // owns at least one channel, K <= C -- unrolled with compile-time tracer indices, so that
+    // the copy's arrays are indexed statically and the copy stays in registers (a runtime index
+    // put it in scratch).  The plain kernels keep the runtime loop (unrolled, their kernarg
+    // arrays went to ~250 spilled SGPRs).
+    auto tracer = [&](int t) {
         double sA = 0.0, sB = 0.0, sA2 = 0.0, sB2 = 0.0;
         bool hasB = false;
 #pragma unroll
@@ -861,6 +866,13 @@ __device__ __forceinline__ void unit_conc(const RtdArgs& a, int64_t u, const dou
         }
         if (a.tr_sf6[t] && a.row_lamsf6 >= 0) cout *= (1 + a.theta[(int64_t)a.row_lamsf6 * a.U + u]);
         conc[t] = cout;
+    };
+    if constexpr (ST) {
+#pragma unroll
+        for (int t = 0; t < C; ++t)
+            if (t < a.K) tracer(t);
+    } else {
+        for (int t = 0; t < a.K; ++t) tracer(t);
     }
 }
 
@@ -916,7 +928,7 @@ __device__ __forceinline__ bool exp_rtd_nan(const RtdArgs& a, double tau) {
 // 1 + s01 G with G = sum_{j<n} q^j = expm1(-beta n) / expm1(-beta) in closed form.
 // LW: channel 0 decays per unit (lw_decay): yw = its exact sum Y_0 at tau_eff (bw = 1 / tau_eff)
 // and lam, numerator e^(-lam tp_0) (C_0 + s01(bw) yw).
-template <int C, bool LW = false>
+template <int C, bool LW = false, bool ST = false>
 __device__ __forceinline__ void mfma_unit_conc(const RtdArgs& a, int64_t u, double bu, const double* yy,
                                                double* conc, const double* num2 = nullptr, double lam = 0.0,
                                                double yw = 0.0, double bw = 0.0) {
@@ -929,7 +941,7 @@ __device__ __forceinline__ void mfma_unit_conc(const RtdArgs& a, int64_t u, doub
 #pragma unroll
     for (int c = 0; c < C; ++c) num[c] = a.tab0[c] + s01 * yy[c];
     if (LW) num[0] = fexp(-lam * a.tp0) * (a.tab0[0] + fexp(-bw * d01) * yw);
-    unit_conc<C>(a, u, num, rden, conc);
+    unit_conc<C, ST>(a, u, num, rden, conc, num2);    // (num2: the piston component of a BMM)
     const double tau = a.theta[(int64_t)a.row_tau[0] * a.U + u];
     if (exp_rtd_nan(a, tau))
         for (int t = 0; t < a.K; ++t) conc[t] = __builtin_nan("");

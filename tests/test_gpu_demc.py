@@ -84,6 +84,74 @@ def test_device_demcz_matches_torch_bitwise(kind, per_well):
     lp.close()
 
 
+SHAPES = ["rtd4_exponential", "rtd4_exp_pist_flow", "rtd4_exponential-piston", "rtd4_exp_pist_flow-piston",
+          "rtd4_exponential_123", "rtd4_exp_pist_flow_123", "rtd4_exponential-piston_123",
+          "rtd4_exp_pist_flow-piston_123", "rtd1_exponential", "rtd1_exp_pist_flow", "ce_only", "joint_bmm",
+          "joint_epm_bmm"]
+
+
+def _shape_spec(shape, L=4):
+    """The reference's own model shapes: its RTD-only model over 4 tracers (CFC12, SF6, H3,
+    He4_ter; run_age_mcmc.py) or 1 (H3), savenum 0 or 123, its CE-only model (Ne, Ar, Kr, Xe;
+    noble_gas_mcmc.py), and the joint c4 BMMs."""
+    import dataclasses
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    from noblegas_rtd_mcmc_amd.spec import ModelSpec
+    if shape == "ce_only":
+        base = wl.c4_spec(L=L, N=300)
+        keep = [1, 2, 3, 4]
+        c = base.ce
+        return ModelSpec(n_wells=L, ce=dataclasses.replace(c, obs=c.obs[:, keep], sd=c.sd[:, keep],
+                                                           gases=tuple(c.gases[i] for i in keep)))
+    if shape.startswith("joint"):
+        m1 = "exp_pist_flow" if "epm" in shape else "exponential"
+        return wl.c4_spec(L=L, N=1200, mod_type1=m1, mod_type2="piston",
+                          par_names=("tau1", "tau2", "f1") + (("eta1",) if m1 == "exp_pist_flow" else ()))
+    kind, model = shape.split("_", 1)
+    sv = model.endswith("_123")
+    model = model[:-4] if sv else model
+    m1, _, m2 = model.partition("-")
+    pn = ("tau1",) + (("tau2", "f1") if m2 else ()) + (("eta1",) if m1 == "exp_pist_flow" else ()) + \
+        (("J", "thalf_cfc", "lamsf6") if sv else ())
+    base = wl.c4_spec(L=L, N=1200, mod_type1=m1, mod_type2=m2 or None, par_names=pn)
+    keep = [0, 1, 2, 4] if kind == "rtd4" else [2]
+    r = base.rtd
+    return ModelSpec(n_wells=L, rtd=dataclasses.replace(r, tracers=[r.tracers[i] for i in keep], obs=r.obs[:, keep],
+                                                        sd=r.sd[:, keep]))
+
+
+@pytest.mark.parametrize("jac", [False, True])
+@pytest.mark.parametrize("shape", SHAPES)
+def test_single_launch_step_reference_shapes(shape, jac):
+    """The reference's own sampled models run ONE launch per chunk of steps (the lane-chain
+    dz_chain_kernel for the RTD-only and CE-only models; logp_fused_kernel's BMM instances in
+    PyMC3's transformed space for the joint BMMs), per-well chains: device == torch
+    (sampler.DEMetropolisZ over ngrtd_logp_units) bit for bit through tuning, stop_tuning and
+    the draws, with walkers not a multiple of the block."""
+    import dataclasses
+    import torch
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+    from noblegas_rtd_mcmc_amd.sampler import DEMetropolisZ, DeviceDEMetropolisZ, Transform
+    spec = dataclasses.replace(_shape_spec(shape), jacobian=jac)
+    W = 301
+    x0 = torch.from_numpy(wl.sample_prior(spec, W, np.random.default_rng(17))).cuda()
+    lp = LogProb(spec, max_walkers=W)
+    kw = dict(tune_interval=4, seed=4242, per_well=True)
+    lp.ctx.set_profiling(True)
+    lp.kernel_stats(reset=True)
+    dev = DeviceDEMetropolisZ(lp, **kw).run(x0, tune=12, draws=8)
+    lp.ctx.set_profiling(False)
+    ks = lp.kernel_stats(reset=True)
+    assert ks["fused"][1] == 1, ks            # one launch for the 20 steps (a chunk of <= 256)
+    tf = Transform.from_spec(spec) if jac else None
+    ref = DEMetropolisZ(lambda t: lp.units(t), transform=tf, **kw).run(x0, tune=12, draws=8)
+    for k in ("x", "lp", "samples", "logp", "accepted", "accept", "lamb", "scaling"):
+        assert _same(dev[k], ref[k]), k
+    assert 0 < int(dev["accepted"].sum()) < dev["accepted"].numel()
+    lp.close()
+
+
 @pytest.mark.parametrize("per_well", [True, False])
 @pytest.mark.parametrize("jac", [False, True])
 def test_device_demcz_step_modes_bitwise(jac, per_well):
