@@ -437,7 +437,6 @@ def sampler_line(args, spec, lp, theta, gpu):
     import dataclasses
     import torch
     from noblegas_rtd_mcmc_amd.engine import LogProb
-    from noblegas_rtd_mcmc_amd.sampler import DeviceDEMetropolisZ
     n = max(1, args.sampler_steps)
     W = theta.shape[-1]
     out, us = {}, {}
@@ -449,31 +448,57 @@ def sampler_line(args, spec, lp, theta, gpu):
     L = spec.n_wells
     tune = max(0, args.sampler_tune)
     for name, plan, pw in (("transformed", lpj, True), ("natural", lp, True), ("transformed_joint", lpj, False)):
-        s = DeviceDEMetropolisZ(plan, tune_interval=100, seed=7, transformed=plan is lpj, per_well=pw)
-        # the timed window is the draw phase after `tune` tuning steps (stop_tuning included),
-        # the stationary regime of a reference-length run, not the first steps of fresh chains
-        x, l, z = s.start(theta, tune, tune + n + 1)
-        cnt = torch.zeros(1, dtype=torch.int64, device=theta.device)
-        plan.demcz(x, l, tune, z)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        plan.demcz(x, l, n, z, n_accepted=cnt)
-        torch.cuda.synchronize()
-        dt = (time.perf_counter() - t0) / n
-        us[name] = dt * 1e6
-        nch = W * (L if pw else 1)
-        out[name] = {"us_per_step": dt * 1e6, "chains": nch, "chain_steps_per_s": nch / dt,
-                     "walker_steps_per_s": W / dt, "steps": n, "after_tune_steps": tune,
-                     "accept_rate": int(cnt.item()) / float(n * nch),
-                     "chain": "one per (walker, well)" if pw else "one per walker over its %d wells" % L}
-        del x, l, z
+        out[name] = _dz_time(plan, theta, pw, plan is lpj, tune, n)
+        us[name] = out[name]["us_per_step"]
     out["transformed"]["plan_build_ms"] = build_ms
     lpj.close()
+    # the reference's own sampled models (one launch per chunk of steps: dz_chain_kernel), on
+    # the same walkers x wells in PyMC3's transformed space: its RTD-only model (4 tracers,
+    # savenum 123, exponential; 1 tracer, savenum 0) and its CE-only model (Ne, Ar, Kr, Xe)
+    if int(os.environ.get("WORLD_SIZE", "1")) == 1:
+        from noblegas_rtd_mcmc_amd import workloads
+        for name, sp in (("rtd_4tracer_123", workloads.rtd_only_spec(L, spec.rtd.n_ages)),
+                         ("rtd_4tracer_123_exp_pist_flow", workloads.rtd_only_spec(L, spec.rtd.n_ages,
+                                                                                   mod_type1="exp_pist_flow")),
+                         ("rtd_1tracer", workloads.rtd_only_spec(L, spec.rtd.n_ages, tracers=("H3",), savenum="")),
+                         ("ce_only", workloads.ce_only_spec(L))):
+            sp = dataclasses.replace(sp, jacobian=True)
+            th = torch.from_numpy(workloads.sample_prior(sp, W, np.random.default_rng(34568))).to(theta.device)
+            pl = LogProb(sp, max_walkers=W, device=gpu)
+            out[name] = _dz_time(pl, th, True, True, tune, n)
+            out[name]["model"] = {"rtd_4tracer_123": "RTD-only, CFC12 SF6 H3 He4_ter, exponential, J/thalf_cfc/lamsf6",
+                                  "rtd_4tracer_123_exp_pist_flow": "RTD-only, 4 tracers, exp_pist_flow, savenum 123",
+                                  "rtd_1tracer": "RTD-only, H3, exponential, savenum 0",
+                                  "ce_only": "CE-only, Ne Ar Kr Xe"}[name]
+            pl.close()
+            del th
     out["method"] = ("PyMC3 DEMetropolisZ, device-resident (ngrtd_demcz_run: one launch per <= 256 steps, "
                      "each block stepping its own chains); primary = per-well chains (one PyMC3 model per well, "
                      "as the reference runs them) in PyMC3's transformed space")
     out["us_per_step"] = out["transformed"]["us_per_step"]
     return out, us
+
+
+def _dz_time(plan, theta, pw, transformed, tune, n):
+    """Per-step time of ONE ngrtd_demcz_run call of n steps after `tune` tuning steps (the
+    timed window is the draw phase, stop_tuning included: the stationary regime of a
+    reference-length run, not the first steps of fresh chains), with its acceptance rate."""
+    import torch
+    from noblegas_rtd_mcmc_amd.sampler import DeviceDEMetropolisZ
+    W, L = theta.shape[-1], plan.spec.n_wells
+    s = DeviceDEMetropolisZ(plan, tune_interval=100, seed=7, transformed=transformed, per_well=pw)
+    x, l, z = s.start(theta, tune, tune + n + 1)
+    cnt = torch.zeros(1, dtype=torch.int64, device=theta.device)
+    plan.demcz(x, l, tune, z)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    plan.demcz(x, l, n, z, n_accepted=cnt)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / n
+    nch = W * (L if pw else 1)
+    return {"us_per_step": dt * 1e6, "chains": nch, "chain_steps_per_s": nch / dt, "walker_steps_per_s": W / dt,
+            "steps": n, "after_tune_steps": tune, "accept_rate": int(cnt.item()) / float(n * nch),
+            "chain": "one per (walker, well)" if pw else "one per walker over its %d wells" % L}
 
 
 # the RTD models of the reference's published runs (BASELINE.md rows 2-5, run_age_mcmc.py:61-70),

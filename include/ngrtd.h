@@ -388,6 +388,20 @@ int ngrtd_demcz_run(ngrtd_plan* plan, double* theta, double* logp, int64_t W, in
  * its sum over wells.  The per-well sampler's initial log-probs. */
 int ngrtd_logp_units(ngrtd_plan* plan, const double* theta, int64_t W, double* out, int32_t mem);
 
+/* The elementwise math of the device DEMetropolisZ step, for samplers that restate its
+ * arithmetic (sampler.DEMetropolisZ on torch ops) and must agree with it bit for bit.
+ * Device pointers, enqueued on the context stream.
+ * ngrtd_pymc3_backward: x = backward(u) of PyMC3 3.11's default transforms
+ * (pymc3/distributions/transforms.py; the Beta / Uniform / HalfNormal free variables of
+ * run_age_mcmc_utils.py:286-344 and noble_gas_mcmc.py:224-250): u, x [lead][P][inner], row p
+ * with transform kind[p] (enum ngrtd_transform) and interval bounds a[p], b[p] (P <=
+ * NGRTD_ROLE_COUNT); exp is the table-driven one the kernels use (<= 1 ulp).
+ * ngrtd_fm_log: out = log(in), the kernels' table-driven log (<= 1 ulp): the accept draw's
+ * log(u) of metrop_select (pymc3 step_methods/arraystep.py). */
+int ngrtd_pymc3_backward(ngrtd_ctx* ctx, const double* u, double* x, int64_t lead, int32_t P, int64_t inner,
+                         const int32_t* kind, const double* a, const double* b);
+int ngrtd_fm_log(ngrtd_ctx* ctx, const double* in, double* out, int64_t n);
+
 /* Host-only (no device needed): build the piecewise-Chebyshev surrogate the exponential
  * log-prob kernel uses for its channel sums and validate it against a long-double
  * evaluation of the same sums.  With s = 1/tau and s01 = exp(-(tp_1 - tp_0) s) (tp as in

@@ -109,6 +109,9 @@ PROTOTYPES = {
     "ngrtd_demcz_run": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_void_p,
                                   C.c_void_p, C.c_void_p, C.c_void_p]),
     "ngrtd_logp_units": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int32]),
+    "ngrtd_pymc3_backward": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int64, _i32p,
+                                       _dp, _dp]),
+    "ngrtd_fm_log": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]),
     "ngrtd_surrogate_check": (C.c_int, [_dp, C.c_int32, C.c_int64, C.c_double, _dp, _dp]),
     "ngrtd_c0_check": (C.c_int, [C.c_double, C.c_double, _dp, _i32p, _i32p, _dp]),
 }

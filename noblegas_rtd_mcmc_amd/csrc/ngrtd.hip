@@ -2055,6 +2055,35 @@ int ngrtd_demcz_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64
     return NGRTD_OK;
 }
 
+int ngrtd_pymc3_backward(ngrtd_ctx* ctx, const double* u, double* x, int64_t lead, int32_t P, int64_t inner,
+                         const int32_t* kind, const double* a, const double* b) {
+    if (!ctx) return NGRTD_ESTATE;
+    if (!u || !x || !kind || lead < 0 || inner < 0 || P < 1 || P > kRoleCount)
+        return set_err(ctx, NGRTD_EINVAL, "bad pymc3_backward arguments");
+    TrRows t{};
+    for (int p = 0; p < P; ++p) {
+        if (kind[p] < NGRTD_TR_NONE || kind[p] > NGRTD_TR_LOG) return set_err(ctx, NGRTD_EINVAL, "bad transform kind");
+        t.kind[p] = kind[p];
+        t.a[p] = a ? a[p] : 0.0;
+        t.b[p] = b ? b[p] : 0.0;
+    }
+    const int64_t n = lead * P * inner;
+    if (n == 0) return NGRTD_OK;
+    hipLaunchKernelGGL(pymc3_backward_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, S(ctx), u, x, n, P,
+                       inner, t);
+    HIP_TRY(ctx, hipGetLastError());
+    return NGRTD_OK;
+}
+
+int ngrtd_fm_log(ngrtd_ctx* ctx, const double* in, double* out, int64_t n) {
+    if (!ctx) return NGRTD_ESTATE;
+    if (!in || !out || n < 0) return set_err(ctx, NGRTD_EINVAL, "bad fm_log arguments");
+    if (n == 0) return NGRTD_OK;
+    hipLaunchKernelGGL(fm_log_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, S(ctx), in, out, n);
+    HIP_TRY(ctx, hipGetLastError());
+    return NGRTD_OK;
+}
+
 int ngrtd_surrogate_check(const double* cols, int32_t C, int64_t N, double dtp, double* coef, double* max_rel_err) {
     if (!cols || C < 1 || C > kMaxChan || N < 2 || !max_rel_err) return NGRTD_EINVAL;
     std::vector<std::vector<double>> cv((size_t)C);

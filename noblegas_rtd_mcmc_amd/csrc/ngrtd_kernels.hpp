@@ -1101,8 +1101,11 @@ __device__ __forceinline__ void count_accepts(unsigned long long* n, bool acc) {
 // (Flags rather than null tests: a null test of an LDS-derived generic pointer miscompiles.)
 // The accept draw's log: log(u) of the (key, rid) stream (a function of the step and the
 // chain only, so the multi-step launch takes it before the step's log-prob is known).
+// (flog: table-driven, <= 1 ulp; the torch restatement takes the same function through
+// ngrtd_fm_log, so the chains stay bitwise equal.  Every kernel that decides runs
+// fm_lds_init() and a barrier first.)
 __device__ __forceinline__ double demc_logu(uint64_t key, uint64_t rid) {
-    return log(rng_unit(rng_mix(rng_mix(key + 3) + rid)));
+    return flog(rng_unit(rng_mix(rng_mix(key + 3) + rid)));
 }
 template <class F64P, class I32P>
 __device__ __forceinline__ bool demc_decide_at_u(const DemcAccept& d, F64P lpa, F64P lamb, F64P scal, I32P nat,
@@ -1173,6 +1176,8 @@ __host__ __device__ __forceinline__ uint64_t dz_pw_elem(uint64_t cid, int p) {
 // walker's P*L proposal rows into the state (coalesced across the walkers of a wave)
 NGRTD_KLINK __global__ void __launch_bounds__(256) demc_accept_kernel(const DemcAccept d, const double* __restrict__ lp_prop,
                                                           int64_t W, int64_t R) {
+    fm_lds_init();                           // flog (demc_logu)
+    __syncthreads();
     const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= W) return;
     if (demc_decide(d, w, lp_prop[w])) {
@@ -1184,20 +1189,23 @@ NGRTD_KLINK __global__ void __launch_bounds__(256) demc_accept_kernel(const Demc
 
 // PyMC3 3.11 transforms (pymc3/distributions/transforms.py) backward(u): LogOdds
 // invlogit(u, 0) = 1 / (1 + exp(-u)); Interval s b + (1 - s) a with s = sigmoid(u); Log exp(u).
-// Plain OCML exp, so that sampler.Transform (torch on the same device) agrees bitwise.
+// exp is the table-driven fexp (<= 1 ulp, a third of OCML's instructions: the transformed
+// DEMetropolisZ step evaluates one per parameter row); sampler.Transform calls this same
+// function on the device (ngrtd_pymc3_backward), so the chains agree bitwise.  Kernels that
+// call it run fm_lds_init() and a barrier first (the host reads the constant table).
 __host__ __device__ __forceinline__ double pymc3_backward(int kind, double a, double b, double u) {
-    if (kind == NGRTD_TR_LOGODDS) return 1.0 / (1.0 + exp(-u));
+    if (kind == NGRTD_TR_LOGODDS) return 1.0 / (1.0 + fexp(-u));
     if (kind == NGRTD_TR_INTERVAL) {
-        const double s = 1.0 / (1.0 + exp(-u));
+        const double s = 1.0 / (1.0 + fexp(-u));
         return s * b + (1.0 - s) * a;
     }
-    if (kind == NGRTD_TR_LOG) return exp(u);
+    if (kind == NGRTD_TR_LOG) return fexp(u);
     return u;
 }
 // The same values with ONE exp call and selects (straight-line: what an unrolled loop
 // over the parameter rows wants); bitwise equal to pymc3_backward.
 __device__ __forceinline__ double pymc3_backward_sel(int kind, double a, double b, double u) {
-    const double ex = exp(kind == NGRTD_TR_LOG ? u : -u);
+    const double ex = fexp(kind == NGRTD_TR_LOG ? u : -u);
     const double s = 1.0 / (1.0 + ex);
     const double iv = s * b + (1.0 - s) * a;
     return kind == NGRTD_TR_LOGODDS ? s : kind == NGRTD_TR_INTERVAL ? iv : kind == NGRTD_TR_LOG ? ex : u;
@@ -1228,6 +1236,7 @@ __host__ __device__ __forceinline__ void demcz_partners(uint64_t key, uint64_t w
 constexpr int kZTileW = 16, kZTileR = 128, kZThreads = 256;
 constexpr int kZPer = kZTileW * kZTileR / kZThreads;   // tile elements per thread (8)
 NGRTD_KLINK __global__ void __launch_bounds__(kZThreads) demcz_propose_kernel(const DemczArgs d) {
+    fm_lds_init();                                    // fexp (pymc3_backward), behind the barrier below
     __shared__ double xs[kZTileW][kZTileR + 1];       // chain-major tiles (+1: no bank conflicts)
     __shared__ double ps[kZTileW][kZTileR + 1];
     __shared__ double px[kZTileW][kZTileR + 1];
@@ -1323,6 +1332,30 @@ NGRTD_KLINK __global__ void __launch_bounds__(kZThreads) demcz_propose_kernel(co
     }
 }
 
+// sampler.Transform.backward / the torch restatement's accept draws on the device: the same
+// pymc3_backward / flog the DEMetropolisZ kernels evaluate (ngrtd_pymc3_backward, ngrtd_fm_log)
+struct TrRows {
+    int32_t kind[kRoleCount];
+    double a[kRoleCount], b[kRoleCount];
+};
+NGRTD_KLINK __global__ void __launch_bounds__(256) pymc3_backward_kernel(const double* __restrict__ u,
+                                                                         double* __restrict__ x, int64_t n, int32_t P,
+                                                                         int64_t inner, const TrRows t) {
+    fm_lds_init();
+    __syncthreads();
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int p = (int)((i / inner) % P);
+    x[i] = pymc3_backward(t.kind[p], t.a[p], t.b[p], u[i]);
+}
+NGRTD_KLINK __global__ void __launch_bounds__(256) fm_log_kernel(const double* __restrict__ in, double* __restrict__ out,
+                                                                 int64_t n) {
+    fm_lds_init();
+    __syncthreads();
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) out[i] = flog(in[i]);
+}
+
 // out[p][b][a] = in[p][a][b] for p < P (a < A, b < B): the caller's [P][L][W] state into the
 // multi-step DEMetropolisZ launch's walker-major [P][W][L] and back (and, per-well chains,
 // the per-chain arrays [L][W] <-> [W][L]).  32 x 32 LDS tiles.
@@ -1401,6 +1434,8 @@ __device__ __forceinline__ double dz_value(const DemcAccept& d, bool de, double 
 // own stream (dz_cid), partner indices of the walker, the joint chains' history layout.  The
 // arithmetic of dz_stage's per-well branch (bitwise).
 NGRTD_KLINK __global__ void __launch_bounds__(256) demcz_propose_pw_kernel(const DemczArgs d) {
+    fm_lds_init();                           // fexp (pymc3_backward)
+    __syncthreads();
     const int64_t W = d.W, U = d.W * d.L;
     const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (c >= U) return;
@@ -1439,6 +1474,8 @@ NGRTD_KLINK __global__ void __launch_bounds__(256) demcz_propose_pw_kernel(const
 // thread per unit c = l W + w decides its own chain and copies its P proposal rows.
 NGRTD_KLINK __global__ void __launch_bounds__(256) demc_accept_pw_kernel(const DemcAccept d,
                                                                           const double* __restrict__ ulp, int64_t W) {
+    fm_lds_init();                           // flog (demc_logu)
+    __syncthreads();
     const int64_t U = W * d.L;
     const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (c >= U) return;

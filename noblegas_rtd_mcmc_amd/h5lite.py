@@ -690,13 +690,32 @@ def _dataspace_msg(dims, maxdims=False):
 
 
 _CHUNK_K = 32                                     # v1 B-tree K of chunked datasets (the default)
+# chunk byte bound: netCDF-4's default chunk size (NC_DEFAULT_CHUNK_SIZE, 4 MiB).  A variable
+# up to it is ONE chunk (the shipped traces' 3 x 10 000 draws are), a larger one is tiled.
+CHUNK_BYTES = 4 << 20
+
+
+def chunk_dims(shape, itemsize, limit=None):
+    """Chunk shape of a variable: the whole shape while it fits in ``limit`` bytes, else the
+    largest axis halved (rounded up) until it fits; zero-length axes get chunk extent 1
+    (HDF5 requires positive chunk dimensions; such a variable stores no chunk at all)."""
+    limit = CHUNK_BYTES if limit is None else limit
+    cd = [max(1, int(d)) for d in shape]
+    while int(np.prod(cd)) * itemsize > limit:
+        i = int(np.argmax(cd))
+        if cd[i] == 1:
+            break
+        cd[i] = (cd[i] + 1) // 2
+    return tuple(cd)
 
 
 class H5Writer:
     """Builds an HDF5 file: superblock v2, version-2 object headers (lookup3 checksums),
-    compact link and attribute storage, numeric datasets either contiguous or as ONE chunk
-    with the shuffle + deflate filters (a one-entry v1 B-tree chunk index), and one global
-    heap collection for variable-length attribute data.
+    compact link and attribute storage, numeric datasets either contiguous or chunked with
+    the shuffle + deflate filters (chunk_dims: one chunk up to 4 MiB, else tiled; a v1 B-tree
+    chunk index of as many levels as the chunk count needs, 2K = 64 entries per node), and
+    one global heap collection for variable-length attribute data.  ``save`` streams the file
+    (object headers, then every chunk compressed one at a time).
 
         w = H5Writer()
         g = w.group(w.root, "posterior")
@@ -791,14 +810,29 @@ class H5Writer:
             raise ValueError("link name too long")
         return struct.pack("<BBB", 1, 0x00, len(nb)) + nb + struct.pack("<Q", addr)
 
-    def _payload(self, h):
-        """The dataset's stored bytes (filtered when compressed)."""
+    def _chunk_list(self, h):
+        """Offsets (row-major order) of the dataset's chunks; none for a zero-size array."""
+        arr = self.objs[h]["arr"]
+        if arr.size == 0:
+            return []
+        cd = chunk_dims(arr.shape, arr.dtype.itemsize)
+        grid = [range(0, int(d), c) for d, c in zip(arr.shape, cd)]
+        return [tuple(o) for o in np.array(np.meshgrid(*grid, indexing="ij")).reshape(len(cd), -1).T]
+
+    def _chunk_payload(self, h, off):
+        """One chunk's stored bytes: the full chunk extent (edge chunks padded with the fill
+        value, as the library stores them), shuffled and deflated."""
         o = self.objs[h]
-        raw = o["arr"].tobytes()
-        if not self.compress:
-            return raw
-        es = o["arr"].dtype.itemsize
-        sh = np.frombuffer(raw, np.uint8).reshape(-1, es).T.tobytes()         # shuffle
+        arr = o["arr"]
+        cd = chunk_dims(arr.shape, arr.dtype.itemsize)
+        sl = tuple(slice(a, min(a + c, d)) for a, c, d in zip(off, cd, arr.shape))
+        blk = arr[sl]
+        if blk.shape != cd:
+            full = np.full(cd, o["fill"] if o["fill"] is not None else 0, dtype=arr.dtype)
+            full[tuple(slice(0, n) for n in blk.shape)] = blk
+            blk = full
+        es = arr.dtype.itemsize
+        sh = np.frombuffer(np.ascontiguousarray(blk).tobytes(), np.uint8).reshape(-1, es).T.tobytes()   # shuffle
         return zlib.compress(sh, self.level)
 
     def _messages(self, h, ctx):
@@ -825,7 +859,7 @@ class H5Writer:
                 es = arr.dtype.itemsize
                 msgs.append((0x0B, struct.pack("<BB", 2, 2) + struct.pack("<HHHI", 2, 1, 1, es)
                              + struct.pack("<HHHI", 1, 1, 1, self.level)))
-                dims = b"".join(struct.pack("<I", int(x)) for x in arr.shape) + struct.pack("<I", es)
+                dims = b"".join(struct.pack("<I", int(x)) for x in chunk_dims(arr.shape, es)) + struct.pack("<I", es)
                 msgs.append((0x08, struct.pack("<BBB", 3, 2, arr.ndim + 1) + struct.pack("<Q", ctx["btree"].get(h, UNDEF))
                              + dims))
             else:
@@ -834,26 +868,65 @@ class H5Writer:
             msgs.append((0x0C, self._attr_msg(name, v, nul, ctx)))
         return msgs
 
-    def _btree_node(self, h, chunk_addr, chunk_size):
-        """One-entry v1 B-tree (chunk index) of a one-chunk dataset, at its full capacity
-        (2K children, 2K + 1 keys) as the library reads it."""
-        arr = self.objs[h]["arr"]
-        rank = arr.ndim
-        ksz = 8 + 8 * (rank + 1)
-        k0 = struct.pack("<II", chunk_size, 0) + b"".join(struct.pack("<Q", 0) for _ in range(rank + 1))
-        # the right key: the next chunk's offsets (the library's scaled + 1, times the chunk dims)
-        k1 = struct.pack("<II", 0, 0) + b"".join(struct.pack("<Q", int(x)) for x in arr.shape) + \
-            struct.pack("<Q", arr.dtype.itemsize)
-        node = b"TREE" + struct.pack("<BBH", 1, 0, 1) + struct.pack("<QQ", UNDEF, UNDEF)
-        node += k0 + struct.pack("<Q", chunk_addr) + k1
-        full = 24 + 2 * _CHUNK_K * 8 + (2 * _CHUNK_K + 1) * ksz
-        return node + b"\0" * (full - len(node))
+    def _key(self, h, off, size):
+        """A chunk B-tree key: stored size, filter mask 0, the chunk's offsets and 0 for the
+        element dimension."""
+        return struct.pack("<II", size, 0) + b"".join(struct.pack("<Q", int(x)) for x in off) + struct.pack("<Q", 0)
 
-    def tobytes(self):
+    def _end_key(self, h, off):
+        """The key after chunk ``off`` (the node's right key): its offsets plus the chunk
+        dimensions, element dimension included (the library's scaled offsets + 1, times the
+        chunk dims; for a one-chunk dataset: its shape and the element size)."""
+        arr = self.objs[h]["arr"]
+        cd = chunk_dims(arr.shape, arr.dtype.itemsize) + (arr.dtype.itemsize,)
+        return struct.pack("<II", 0, 0) + b"".join(struct.pack("<Q", int(o) + int(c)) for o, c in zip(tuple(off) + (0,), cd))
+
+    def _node_size(self, h):
+        """A v1 B-tree node at full capacity (2K children, 2K + 1 keys), as the library reads it."""
+        ksz = 8 + 8 * (self.objs[h]["arr"].ndim + 1)
+        return 24 + 2 * _CHUNK_K * 8 + (2 * _CHUNK_K + 1) * ksz
+
+    @staticmethod
+    def _tree_shape(n):
+        """Node counts per level, leaves first, for n chunks (2K children per node)."""
+        levels = []
+        while True:
+            n = max(1, -(-n // (2 * _CHUNK_K)))
+            levels.append(n)
+            if n == 1:
+                return levels
+
+    def _btree_nodes(self, h, node_addr, chunks):
+        """The chunk index of a dataset: [(address, node bytes)].  chunks: [(offsets, address,
+        stored size)] in row-major order; node_addr: the addresses of its nodes, leaves first
+        (level by level, as _tree_shape counts them), the root last."""
+        full = self._node_size(h)
+        out = []
+        # level 0: chunk entries; entries of a level above: (first key, last end key, address)
+        ents = [(self._key(h, o, sz), self._end_key(h, o), a) for o, a, sz in chunks]
+        k = 0
+        for level, n in enumerate(self._tree_shape(len(chunks))):
+            groups = [ents[i * 2 * _CHUNK_K:(i + 1) * 2 * _CHUNK_K] for i in range(n)]
+            addrs = node_addr[k:k + n]
+            k += n
+            nxt = []
+            for i, g in enumerate(groups):
+                left = addrs[i - 1] if i > 0 else UNDEF
+                right = addrs[i + 1] if i + 1 < n else UNDEF
+                node = b"TREE" + struct.pack("<BBH", 1, level, len(g)) + struct.pack("<QQ", left, right)
+                for key, _, a in g:
+                    node += key + struct.pack("<Q", a)
+                node += g[-1][1]
+                out.append((addrs[i], node + b"\0" * (full - len(node))))
+                nxt.append((g[0][0], g[-1][1], addrs[i]))
+            ents = nxt
+        return out
+
+    def _layout(self):
+        """Pass 1: the sizes of every object header and of the global heap; returns their
+        address plan (datasets' storage is placed by ``save`` as it streams it)."""
         O = 8
         sb_size = 8 + 4 + 4 * O + 4
-        payload = {h: self._payload(h) for h in self.order if self.objs[h]["kind"] == "dataset"}
-        # pass 1: sizes (independent of the addresses written into them)
         ctx = {"addr": lambda x: 0, "gh_addr": 0, "gheap": [], "data": {}, "btree": {}}
         sizes = {h: len(self._ohdr(self._messages(h, ctx))) for h in self.order}
         gh_blobs = [len(x) for x in ctx["gheap"]]
@@ -864,45 +937,89 @@ class H5Writer:
         gh_addr = p
         gh_used = 16 + sum(16 + n + (-n % 8) for n in gh_blobs)
         gh_size = max(4096, gh_used + 16) if gh_blobs else 0
-        p += gh_size
-        btree, data = {}, {}
-        for h, pl in payload.items():
-            if self.compress:
-                btree[h] = p
-                p += len(self._btree_node(h, 0, 0))
-            p = (p + 7) // 8 * 8
-            data[h] = p
-            p += len(pl)
-        eof = p
-        # pass 2: the real addresses
-        ctx = {"addr": lambda x: addr[x], "gh_addr": gh_addr, "gheap": [], "data": data, "btree": btree}
-        out = bytearray(eof)
-        sb = _SIG + struct.pack("<BBBB", 2, O, O, 0) + struct.pack("<QQQQ", 0, UNDEF, eof, addr[self.root])
-        out[0:sb_size] = sb + struct.pack("<I", lookup3(sb))
-        for h in self.order:
-            blob = self._ohdr(self._messages(h, ctx))
-            if len(blob) != sizes[h]:
-                raise H5Error("object header size changed between passes")
-            out[addr[h]:addr[h] + len(blob)] = blob
-        if gh_size:
-            body = b"".join(struct.pack("<HHIQ", i + 1, 1, 0, len(x)) + x + b"\0" * (-len(x) % 8)
-                            for i, x in enumerate(ctx["gheap"]))
-            col = b"GCOL" + struct.pack("<B3xQ", 1, gh_size) + body
-            free = gh_size - len(col)
-            if free >= 16:
-                col += struct.pack("<HHIQ", 0, 0, 0, free)          # the free-space object
-            out[gh_addr:gh_addr + gh_size] = col + b"\0" * (gh_size - len(col))
-        for h, pl in payload.items():
-            if self.compress:
-                nb = self._btree_node(h, data[h], len(pl))
-                out[btree[h]:btree[h] + len(nb)] = nb
-            out[data[h]:data[h] + len(pl)] = pl
-        return bytes(out)
+        return {"sb_size": sb_size, "sizes": sizes, "addr": addr, "gh_addr": gh_addr, "gh_size": gh_size,
+                "end": p + gh_size}
 
-    def save(self, path):
-        with open(path, "wb") as f:
-            f.write(self.tobytes())
-        return path
+    def save(self, path_or_file):
+        """Write the file (a path or a seekable binary file object).  Datasets are streamed
+        after the metadata: a contiguous one as its bytes, a chunked one as its B-tree nodes
+        (their count follows from the chunk count) then each chunk, compressed and written
+        one at a time (only one chunk's payload is held); the superblock and object headers,
+        whose sizes pass 1 fixed, are written last, when every address is known."""
+        import io
+        lay = self._layout()
+        f = open(path_or_file, "wb") if isinstance(path_or_file, str) else path_or_file
+        try:
+            O = 8
+            addr = lay["addr"]
+            base = f.tell() if not isinstance(path_or_file, str) else 0
+            if base:
+                raise H5Error("H5Writer.save: the file object must be positioned at 0")
+
+            def put(a, blob):
+                f.seek(a)
+                f.write(blob)
+            p = lay["end"]
+            data, btree = {}, {}
+            for h in self.order:
+                if self.objs[h]["kind"] != "dataset":
+                    continue
+                arr = self.objs[h]["arr"]
+                if not self.compress:
+                    p = (p + 7) // 8 * 8
+                    data[h] = p
+                    put(p, np.ascontiguousarray(arr).tobytes())
+                    p += arr.nbytes
+                    continue
+                offs = self._chunk_list(h)
+                if not offs:              # nothing stored: the B-tree address stays undefined
+                    continue
+                nodes = []
+                for _ in range(sum(self._tree_shape(len(offs)))):
+                    nodes.append(p)
+                    p += self._node_size(h)
+                ch = []
+                for off in offs:
+                    pl = self._chunk_payload(h, off)
+                    p = (p + 7) // 8 * 8
+                    put(p, pl)
+                    ch.append((off, p, len(pl)))
+                    p += len(pl)
+                for na, node in self._btree_nodes(h, nodes, ch):
+                    put(na, node)
+                btree[h] = nodes[-1]      # the root
+            eof = p
+            ctx = {"addr": lambda x: addr[x], "gh_addr": lay["gh_addr"], "gheap": [], "data": data, "btree": btree}
+            sb = _SIG + struct.pack("<BBBB", 2, O, O, 0) + struct.pack("<QQQQ", 0, UNDEF, eof, addr[self.root])
+            put(0, sb + struct.pack("<I", lookup3(sb)))
+            for h in self.order:
+                blob = self._ohdr(self._messages(h, ctx))
+                if len(blob) != lay["sizes"][h]:
+                    raise H5Error("object header size changed between passes")
+                put(addr[h], blob)
+            gh_size = lay["gh_size"]
+            if gh_size:
+                body = b"".join(struct.pack("<HHIQ", i + 1, 1, 0, len(x)) + x + b"\0" * (-len(x) % 8)
+                                for i, x in enumerate(ctx["gheap"]))
+                col = b"GCOL" + struct.pack("<B3xQ", 1, gh_size) + body
+                free = gh_size - len(col)
+                if free >= 16:
+                    col += struct.pack("<HHIQ", 0, 0, 0, free)          # the free-space object
+                put(lay["gh_addr"], col + b"\0" * (gh_size - len(col)))
+            f.seek(0, io.SEEK_END)
+            if f.tell() < eof:            # (the end of file the superblock records)
+                f.seek(eof - 1)
+                f.write(b"\0")
+        finally:
+            if isinstance(path_or_file, str):
+                f.close()
+        return path_or_file
+
+    def tobytes(self):
+        import io
+        b = io.BytesIO()
+        self.save(b)
+        return b.getvalue()
 
 
 # ------------------------------------------------------------------ netCDF-4 on top

@@ -80,6 +80,29 @@ def unit_t(h):
     return (_lsr(h, 11).to(torch.float64) + 0.5) * (1.0 / 9007199254740992.0)
 
 
+def _dev_ctx(t):
+    """The libngrtd context of a CUDA tensor's device, enqueueing on torch's current stream;
+    None for a CPU tensor (CPU runs of this restatement use torch's own exp / log)."""
+    if not t.is_cuda:
+        return None
+    ctx = _lib.Context.get(t.device.index or 0)
+    ctx.set_stream(torch.cuda.current_stream(t.device).cuda_stream)
+    return ctx
+
+
+def fm_log(x):
+    """log(x) as the device DEMetropolisZ kernels take it for the accept draw (the table-driven
+    flog, <= 1 ulp: ngrtd_fm_log) on CUDA tensors, so that both samplers make the same
+    decisions bit for bit; torch.log on the CPU."""
+    ctx = _dev_ctx(x)
+    if ctx is None:
+        return torch.log(x)
+    x = x.contiguous()
+    out = torch.empty_like(x)
+    ctx.check(ctx.lib.ngrtd_fm_log(ctx.h, x.data_ptr(), out.data_ptr(), x.numel()), "ngrtd_fm_log")
+    return out
+
+
 def pymc3_tune(scale, acc_rate):
     """pymc3.step_methods.metropolis.tune (3.11): multiplicative update from the
     acceptance rate of the last tune interval (elementwise on tensors)."""
@@ -132,7 +155,24 @@ class Transform:
         return t.reshape(-1, len(self.kind), self.L, t.shape[-1])
 
     def backward(self, u):
-        """u [..., P, L, W] (any leading dims) -> natural x."""
+        """u [..., P, L, W] (any leading dims) -> natural x.  On CUDA tensors through
+        ngrtd_pymc3_backward -- the device DEMetropolisZ kernels' own function (its exp is the
+        table-driven fexp, <= 1 ulp), so that the two samplers' chains agree bit for bit;
+        torch's exp on the CPU."""
+        ctx = _dev_ctx(u)
+        if ctx is not None:
+            import ctypes as C
+            uc = u.contiguous()
+            out = torch.empty_like(uc)
+            P = len(self.kind)
+            inner = self.L * int(uc.shape[-1])
+            lead = uc.numel() // (P * inner) if inner else 0
+            kind = (C.c_int32 * P)(*self.kind)
+            a = (C.c_double * P)(*self.a)
+            b = (C.c_double * P)(*self.b)
+            ctx.check(ctx.lib.ngrtd_pymc3_backward(ctx.h, uc.data_ptr(), out.data_ptr(), lead, P, inner, kind, a, b),
+                      "ngrtd_pymc3_backward")
+            return out.reshape(u.shape)
         ur = self._rows(u)
         out = torch.empty_like(ur)
         for p, k in enumerate(self.kind):
@@ -281,7 +321,7 @@ class DEMetropolisZ:
             eps = (u2 if S is None else u2 * S) * scaling
             prop = (y + eps).reshape(x.shape)
             lp_prop = self.log_prob(tf.backward(prop) if tf is not None else prop)
-            logu = torch.log(unit_t(mix_t(w_idx + _s64(mix_int((key + 3) & _M64)))))
+            logu = fm_log(unit_t(mix_t(w_idx + _s64(mix_int((key + 3) & _M64)))))
             mr = lp_prop - lp
             acc = torch.isfinite(mr) & (logu < mr)
             x = torch.where(acc, prop, x)
@@ -356,7 +396,7 @@ class DEMetropolisZ:
             eps = (u2 if S is None else u2 * S) * scaling
             prop = y + eps
             lp_prop = self.log_prob(tf.backward(prop) if tf is not None else prop)
-            logu = torch.log(unit_t(mix_t(cid + _s64(mix_int((key + 3) & _M64)))))
+            logu = fm_log(unit_t(mix_t(cid + _s64(mix_int((key + 3) & _M64)))))
             mr = lp_prop - lp
             acc = torch.isfinite(mr) & (logu < mr)
             x = torch.where(acc, prop, x)

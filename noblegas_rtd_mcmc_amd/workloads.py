@@ -190,6 +190,32 @@ def c4_spec(L=64, N=1200, seed=34567, mod_type1="exponential", mod_type2=None, p
     return ModelSpec(n_wells=L, ce=ce, rtd=rtd)
 
 
+def rtd_only_spec(L=64, N=1200, tracers=("CFC12", "SF6", "H3", "He4_ter"), mod_type1="exponential", mod_type2=None,
+                  savenum="123", seed=34567):
+    """The reference's own RTD model (run_age_mcmc.py:122-231: RTD-only, the 4-tracer set or
+    one tracer; savenum digits 1 J, 2 thalf_cfc, 3 lamsf6 sampled) over L wells with c4's
+    synthetic per-well obs and series (the same seeded draws, restricted to these tracers)."""
+    import dataclasses
+    names = ("CFC12", "SF6", "H3", "He3", "He4_ter")
+    pn = ["tau1"] + (["tau2", "f1"] if mod_type2 else []) + (["eta1"] if mod_type1 == "exp_pist_flow" else [])
+    pn += [{"1": "J", "2": "thalf_cfc", "3": "lamsf6"}[d] for d in str(savenum) if d in "123"]
+    base = c4_spec(L=L, N=N, seed=seed, mod_type1=mod_type1, mod_type2=mod_type2, par_names=tuple(pn))
+    keep = [names.index(t) for t in tracers]
+    r = base.rtd
+    rtd = dataclasses.replace(r, tracers=[r.tracers[i] for i in keep], obs=r.obs[:, keep], sd=r.sd[:, keep])
+    return ModelSpec(n_wells=L, rtd=rtd)
+
+
+def ce_only_spec(L=64, gases=("Ne", "Ar", "Kr", "Xe"), seed=34567):
+    """The reference's own CE model (noble_gas_mcmc.py:216-267: Ne, Ar, Kr, Xe) over L wells
+    with c4's synthetic per-well obs."""
+    import dataclasses
+    base = c4_spec(L=L, N=60, seed=seed)
+    keep = [base.ce.gases.index(g) for g in gases]
+    c = base.ce
+    return ModelSpec(n_wells=L, ce=dataclasses.replace(c, obs=c.obs[:, keep], sd=c.sd[:, keep], gases=tuple(gases)))
+
+
 def c4(W=2048, L=64, N=1200):
     spec = c4_spec(L=L, N=N)
     return spec, sample_prior(spec, W, np.random.default_rng(34568))

@@ -203,3 +203,75 @@ def test_writer_uncompressed_and_multiwell(tmp_path):
         d2, a2, _ = back["posterior"]["vars"][k]
         assert d2 == dims and np.array_equal(a2, a)
     assert w is not None
+
+
+def _var_msgs(path, group, var):
+    from noblegas_rtd_mcmc_amd import h5lite
+    r = h5lite.H5Reader(path)
+    a = r.links(r.links(r.root)[group])[var]
+    return {t: bytes(d) for t, f, d in r.messages(a) if t != 0x0C}, r
+
+
+def test_writer_encodings_pinned_to_shipped_trace(tmp_path):
+    """The writer's low-level encodings against the bytes of a shipped trace
+    (tests/golden/traces/PLM1.H3.exponential.0.netcdf, netCDF 4.8.1 / HDF5): for a (chain,
+    draw) float64 variable of the same shape, the dataspace, datatype, fill-value, filter
+    pipeline (shuffle + deflate 4) and chunked-layout messages are byte-identical but for the
+    B-tree address, and the chunk B-tree node has the same header and keys (the first key's
+    stored size aside: a different compressed payload)."""
+    import struct
+    from noblegas_rtd_mcmc_amd import h5lite
+    ref, rr = _var_msgs(os.path.join(GOLD, "traces", "PLM1.H3.exponential.0.netcdf"), "posterior", "tau1")
+    groups = {"posterior": {"attrs": {}, "dims": {"chain": np.arange(3), "draw": np.arange(10000)},
+                            "vars": {"tau1": (("chain", "draw"), np.random.default_rng(0).normal(size=(3, 10000)), {})}}}
+    p = str(tmp_path / "t.nc")
+    h5lite.write_netcdf4(p, groups)
+    ours, r = _var_msgs(p, "posterior", "tau1")
+    for t in (0x01, 0x03, 0x05, 0x0B):
+        assert ours[t] == ref[t], hex(t)
+    lay_r, lay_o = ref[0x08], ours[0x08]
+    assert lay_o[:3] == lay_r[:3] and lay_o[11:] == lay_r[11:]          # version, class, rank; chunk dims
+    def node(rd, lay):
+        a = int.from_bytes(lay[3:11], "little")
+        b = rd.b
+        ksz = 8 + 8 * 3
+        head = bytes(b[a:a + 8])
+        k0 = bytes(b[a + 24:a + 24 + ksz])
+        k1 = bytes(b[a + 24 + ksz + 8:a + 24 + 2 * ksz + 8])
+        return head, k0, k1
+    hr, k0r, k1r = node(rr, lay_r)
+    ho, k0o, k1o = node(r, lay_o)
+    assert ho == hr and k0o[4:] == k0r[4:] and k1o == k1r
+    assert struct.unpack_from("<I", k0o)[0] > 0
+
+
+def test_writer_tiles_large_variables_and_empty_draws(tmp_path, monkeypatch):
+    """Variables above the chunk bound are tiled (chunk_dims) and indexed by a multi-level v1
+    B-tree (more than 2K = 64 chunks: the bound is lowered here to force 2 levels); a
+    zero-draw variable stores no chunk.  Both read back exactly; the stored chunk sizes stay
+    within the 32-bit fields whatever the variable size."""
+    from noblegas_rtd_mcmc_amd import h5lite
+    monkeypatch.setattr(h5lite, "CHUNK_BYTES", 2048)
+    rng = np.random.default_rng(1)
+    big = rng.normal(size=(5, 1999, 3))                   # 240 KB -> 2 KB chunks: 125 chunks
+    ints = np.arange(3 * 1001, dtype=np.int64).reshape(3, 1001)
+    groups = {"posterior": {"attrs": {"x": "y"}, "dims": {"chain": np.arange(5), "draw": np.arange(1999),
+                                                          "well": np.arange(3)},
+                            "vars": {"T": (("chain", "draw", "well"), big, {})}},
+              "sample_stats": {"attrs": {}, "dims": {"chain": np.arange(3), "draw": np.arange(1001),
+                                                     "none": np.arange(0)},
+                               "vars": {"n": (("chain", "draw"), ints, {}),
+                                        "empty": (("chain", "none"), np.zeros((3, 0)), {})}}}
+    p = str(tmp_path / "big.nc")
+    h5lite.write_netcdf4(p, groups)
+    back = h5lite.read_netcdf4(p)
+    assert np.array_equal(back["posterior"]["vars"]["T"][1], big)
+    assert np.array_equal(back["sample_stats"]["vars"]["n"][1], ints)
+    assert back["sample_stats"]["vars"]["empty"][1].shape == (3, 0)
+    assert h5lite.chunk_dims((5, 1999, 3), 8, 2048)[1] < 1999
+    assert h5lite.chunk_dims((2048, 50000, 6), 8) != (2048, 50000, 6)        # 4.9 GB: tiled at 4 MiB
+    r = h5lite.H5Reader(p)
+    a = r.links(r.links(r.root)["posterior"])["T"]
+    lay = [bytes(d) for t, f, d in r.messages(a) if t == 0x08][0]
+    bt = int.from_bytes(lay[3:11], "little")
+    assert r.b[bt + 5] == 1                                # the root is an internal node (2 levels)
