@@ -81,15 +81,9 @@ SAVENUM_PARS = {"1": "J", "2": "thalf_cfc", "3": "lamsf6"}
 
 def model_spec(args, savenum=""):
     from noblegas_rtd_mcmc_amd import workloads
-    pn = ["tau1"]
     m1, m2 = args.mod_type1, args.mod_type2
-    if m2:
-        pn += ["tau2", "f1"]
-    pn += [p + "1" for p in MODEL_PARS[m1]]
-    if m2:
-        pn += [p + "2" for p in MODEL_PARS[m2]]
-    pn += [SAVENUM_PARS[d] for d in str(savenum) if d in SAVENUM_PARS]
-    return workloads.c4_spec(L=args.wells, N=args.ages, mod_type1=m1, mod_type2=m2, par_names=tuple(pn))
+    return workloads.c4_spec(L=args.wells, N=args.ages, mod_type1=m1, mod_type2=m2,
+                             par_names=workloads.model_par_names(m1, m2, savenum))
 
 
 # ------------------------------------------------------------------ CPU baseline
@@ -507,6 +501,24 @@ def _dz_time(plan, theta, pw, transformed, tune, n):
 PUBLISHED_MODELS = (("exponential", None, ""), ("exponential", None, "123"), ("exponential", "piston", ""), ("exponential", "piston", "123"),
                     ("exp_pist_flow", None, ""), ("exp_pist_flow", None, "123"), ("exp_pist_flow", "piston", ""),
                     ("exp_pist_flow", "piston", "123"))
+# the other model pairs the reference's driver accepts (run_age_mcmc.py:61-70), on the generic
+# single-launch instances (MIX bit 6): piston / dispersion single components, BMMs with an
+# exponential / exp_pist_flow / dispersion second component, a piston first component
+OTHER_MODELS = (("piston", None, ""), ("piston", None, "123"), ("dispersion", None, ""), ("dispersion", None, "123"),
+                ("exponential", "exponential", ""), ("exponential", "exponential", "123"),
+                ("exp_pist_flow", "exponential", ""), ("exponential", "exp_pist_flow", ""),
+                ("exp_pist_flow", "exp_pist_flow", ""), ("exponential", "dispersion", ""), ("piston", "exponential", ""),
+                ("dispersion", "piston", ""))
+
+
+def fused_instance(m1, m2, sv, C=5):
+    """The logp_fused_kernel instance a joint c4-shape plan of this model runs (FULL, C = 5)."""
+    lw = 32 if "2" in sv else 0
+    if m1 in ("exponential", "exp_pist_flow") and m2 in (None, "piston"):
+        mix = (1 if m2 == "piston" else 0) | (2 if m1 == "exp_pist_flow" else 0) | lw
+    else:
+        mix = 64 | lw
+    return "logp_fused_kernel<%d, true, 2, %d>" % (C, mix)
 
 
 def _time_plan(spec, W, gpu, steps, seed=34568):
@@ -539,7 +551,8 @@ def _time_plan(spec, W, gpu, steps, seed=34568):
 
 def model_lines(args, gpu):
     """Side lines (N = 1, outside the headline's timed region): the RTD models the reference
-    published runs of (run_age_mcmc.py:61-70) on the c4 shape, and
+    published runs of (run_age_mcmc.py:61-70) on the c4 shape, the other
+    model pairs its driver accepts (OTHER_MODELS, the generic instances; "published": false), and
     the CE-only (c2) and RTD-only (c3) configurations of BASELINE.json.  Each: plan build,
     kernel time per launch, evals/s, PMC FP64 fraction (committed summary of the same kernel
     instance) and the rate amortised over a 20 000-step run."""
@@ -549,20 +562,22 @@ def model_lines(args, gpu):
     W = args.walkers
     res = {}
     base_ms = {("exponential", None): None}
-    for m1, m2, sv in PUBLISHED_MODELS:
+    for m1, m2, sv in PUBLISHED_MODELS + OTHER_MODELS:
         a = ap.Namespace(wells=args.wells, ages=args.ages, mod_type1=m1, mod_type2=m2)
         spec = model_spec(a, sv)
-        build_ms, ms, finite, info = _time_plan(spec, W, gpu, steps)
+        # (dispersion sums every age exactly: fewer launches keep the line short)
+        n = max(20, steps // 10) if "dispersion" in (m1, m2) else steps
+        build_ms, ms, finite, info = _time_plan(spec, W, gpu, n)
         if not sv:
             base_ms[(m1, m2)] = ms
-        mix = (1 if m2 == "piston" else 0) | (2 if m1 == "exp_pist_flow" else 0) | (32 if "2" in sv else 0)
-        inst = "logp_fused_kernel<5, true, 2, %d>" % mix
+        inst = fused_instance(m1, m2, sv)
         pmc, pmc_path = pmc_summary("logp_fused_kernel", inst)
         U = W * args.wells
         e = {"kernel_ms": ms, "evals_per_s": W / (ms * 1e-3), "plan_build_ms": build_ms,
              "value_amortized_20k": W * 20000 / (20000 * ms * 1e-3 + build_ms * 1e-3),
              "finite_frac": finite, "kernel": inst, "surrogate": info.get("surrogate"),
-             "sampled": ["tau1"] + [SAVENUM_PARS[d] for d in sv], "savenum": int(sv) if sv else 0}
+             "sampled": list(spec.rtd.par_names), "savenum": int(sv) if sv else 0,
+             "published": (m1, m2, sv) in PUBLISHED_MODELS}
         if sv and base_ms.get((m1, m2)):
             e["vs_savenum0_kernel"] = ms / base_ms[(m1, m2)]
         if pmc.get("fp64_flop_per_unit") and inst in (pmc_path or ""):

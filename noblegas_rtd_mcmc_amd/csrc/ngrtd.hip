@@ -36,6 +36,10 @@ bool fused_dz_instance_exists(int mix);
 bool dz_chain_instance_exists(int C, int mix);
 hipError_t launch_dz_chain(int C, int mix, const RtdArgs& a, const UnitArgs& u, const DemcAccept& da, int64_t U,
                            size_t lds, size_t max_lds, hipStream_t st);
+// ngrtd_gen.hip: the generic-component log-prob instances (MIX bit 6, gen_component)
+bool gen_instance_exists(int C, bool full, int mix);
+hipError_t launch_fused_gen_instance(int C, bool full, int mix, const RtdArgs& a, const UnitArgs& u, int WB, int64_t W,
+                                     double* logp, const DemcAccept& da, size_t lds, size_t max_lds, hipStream_t st);
 // ngrtd_lw.hip: the log-prob instances with the sampled CFC12 half-life (MIX bit 5)
 hipError_t launch_fused_lw_instance(int C, bool full, int mix, const RtdArgs& a, const UnitArgs& u, int WB, int64_t W,
                                     double* logp, const DemcAccept& da, size_t lds, size_t max_lds, hipStream_t st);
@@ -70,6 +74,7 @@ struct TableDev {
     bool cheb_ok = false;
     double cheb_err = -1.0; // max relative error measured by the validation (-1: not built)
     DevBuf epm;             // exp_pist_flow block-tail surrogates (epm_prepare)
+    DevBuf disp;            // dispersion components: 1 / tp_k, tp_k^(-3/2) (RtdArgs::disp_aux)
     bool epm_ok = false;
     double epm_err = -1.0;
     int epm_nb = 0, epm_p0 = 0, epm_np = 0;
@@ -657,7 +662,7 @@ static void launch_mfma(const RtdArgs& a, const UnitArgs& u, int32_t fuse, hipSt
 static size_t fused_lds(const RtdArgs& a, const UnitArgs& u, int dz_p = 0) {
     // EPM: the channel table, rows of cheb_cp(C) doubles in LDS (the kernel's layout; the global
     // table's rows are a.CP = (C + 1) & ~1, shorter for C = 2, 4)
-    const size_t epm_tab = a.mod[0] == MOD_EPM ? (size_t)epm_lds_doubles(a.N, cheb_cp(a.C)) : 0;
+    const size_t epm_tab = (a.mod[0] == MOD_EPM || a.mod[1] == MOD_EPM) ? (size_t)epm_lds_doubles(a.N, cheb_cp(a.C)) : 0;
     const size_t dz = (size_t)dz_p * kFusedUnits;                          // DZ step: the proposals
     return (size_t)(kFusedHdr + a.cheb_np * cheb_lds_stride(a.C) + epm_tab + u.wd_n + dz) *
            sizeof(double);
@@ -718,6 +723,61 @@ static bool fused_path(const RtdArgs& a0, const UnitArgs& u) {
     return !disabled && mods && mfma_path(a1, false) && lw_ok(a, u) && a.C <= 5 && u.L >= 1 &&
            u.L <= kFusedUnits && fused_lds(a, u) <= kFusedMaxLds;
 }
+// The generic instances (MIX bit 6, ngrtd_gen.hip) for the model pairs fused_path does not
+// take: the staged surrogate window covers the Uniform priors' supports of every exponential
+// component's tau (tau1, tau2; down to the least tau_eff with the sampled half-life), or the
+// whole table when a component's tau has no prior in the plan.
+static bool gen_mods(const RtdArgs& a) {
+    auto ok = [](int m) { return m == MOD_PISTON || m == MOD_EXP || m == MOD_EPM || m == MOD_DISP; };
+    return ok(a.mod[0]) && (a.mod[1] == MOD_NONE || ok(a.mod[1]));
+}
+static void gen_cheb_window(RtdArgs& a, const UnitArgs& u) {
+    a.cheb_p0 = 0;
+    a.cheb_np = a.cheb ? kChebPieces : 0;
+    if (!a.cheb) return;
+    int pa = kChebPieces, pb = -1;
+    for (int c = 0; c < 2; ++c) {
+        if (a.mod[c] != MOD_EXP) continue;
+        const bool t1 = a.row_tau[c] == u.row_tau1, t2 = a.row_tau[c] == u.row_tau2 && u.row_tau2 >= 0;
+        if (!u.rtd_on || !(u.flags & NGRTD_WANT_PRIOR) || !(t1 || t2)) return;   // no bound: every piece
+        double lo = t1 ? u.tau1_lo : u.tau2_lo;
+        const double hi = t1 ? u.tau1_hi : u.tau2_hi;
+        if (a.row_thalf >= 0 && u.row_thalf >= 0) lo = lw_tau_lo(a, lo);
+        double x;
+        if (!(lo > 0.0)) return;
+        const int qa = cheb_piece(std::max(lo, kChebTauLo), x), qb = cheb_piece(hi, x);
+        if (qa < 0 || qb < qa) return;
+        pa = std::min(pa, qa);
+        pb = std::max(pb, qb);
+    }
+    if (pb < pa) {   // no exponential component: nothing staged
+        a.cheb_np = 0;
+        return;
+    }
+    a.cheb_p0 = pa;
+    a.cheb_np = pb - pa + 1;
+}
+static bool gen_full(const UnitArgs& u) {
+    return u.ce_on && u.rtd_on && (u.flags & NGRTD_WANT_LIKE) && (u.flags & NGRTD_WANT_PRIOR);
+}
+static int gen_mix(const RtdArgs& a, const UnitArgs& u) {
+    return 64 | (a.row_thalf >= 0 ? 32 : 0) | (gen_full(u) && (u.flags & NGRTD_WANT_JACOBIAN) ? 4 : 0);
+}
+static bool gen_path(const RtdArgs& a0, const UnitArgs& u) {
+    static const bool disabled = std::getenv("NGRTD_NO_GEN") != nullptr;
+    if (disabled || !gen_mods(a0) || fused_path(a0, u)) return false;
+    RtdArgs a = a0;
+    gen_cheb_window(a, u);
+    const bool exp_c = a.mod[0] == MOD_EXP || a.mod[1] == MOD_EXP;
+    const bool epm_c = a.mod[0] == MOD_EPM || a.mod[1] == MOD_EPM;
+    const bool disp_c = a.mod[0] == MOD_DISP || a.mod[1] == MOD_DISP;
+    if ((exp_c && !a.cheb) || (epm_c && !a.epm) || (disp_c && !a.disp_aux)) return false;
+    return a.C >= 1 && a.C <= 5 && lw_ok(a, u) && u.L >= 1 && u.L <= kFusedUnits &&
+           fused_lds(a, u) <= kFusedMaxLds && gen_instance_exists(a.C, gen_full(u), gen_mix(a, u));
+}
+// one launch for the plan's log-prob / forward outputs: a specialised or a generic instance
+static bool single_path(const RtdArgs& a, const UnitArgs& u) { return fused_path(a, u) || gen_path(a, u); }
+
 // Waves per unit group (logp_fused_kernel ROLES): 2 = theta-only and RTD blocks in separate
 // waves (default), 1 = one wave runs the whole unit.  NGRTD_FUSED_ROLES overrides (A/B runs).
 static int fused_roles() {
@@ -847,8 +907,14 @@ static int launch_fused(ngrtd_ctx* ctx, const RtdArgs& a0, const UnitArgs& u, in
                         hipStream_t st, const DemcAccept* dap = nullptr) {
     const int WB = kFusedUnits / L;
     RtdArgs a = a0;
-    cheb_window(a, u);
     const DemcAccept da = dap ? *dap : DemcAccept{};
+    if (!fused_path(a0, u)) {   // the generic instances (gen_path)
+        gen_cheb_window(a, u);
+        HIP_TRY(ctx, launch_fused_gen_instance(a.C, gen_full(u), gen_mix(a, u), a, u, WB, W, logp, da, fused_lds(a, u),
+                                               kFusedMaxLds, st));
+        return NGRTD_OK;
+    }
+    cheb_window(a, u);
     if (a.row_thalf >= 0) {   // the sampled CFC12 half-life (ngrtd_lw.hip, lw_ok)
         const bool joint = u.ce_on && u.rtd_on && (u.flags & NGRTD_WANT_LIKE) && (u.flags & NGRTD_WANT_PRIOR);
         const bool jac = (u.flags & NGRTD_WANT_JACOBIAN) != 0;
@@ -1473,8 +1539,8 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
         a.cheb = nullptr;
         // (a per-unit CFC12 half-life leaves its channel undecayed: the same surrogate serves it
         // at tau_eff, lw_decay)
-        if (a.mod[0] == MOD_EXP && (a.mod[1] == MOD_NONE || a.mod[1] == MOD_PISTON) &&
-            p->table.C <= 5 && p->dtp >= 0.0 &&
+        // (generic instances: any exponential component, gen_path)
+        if ((a.mod[0] == MOD_EXP || a.mod[1] == MOD_EXP) && p->table.C <= 5 && p->dtp >= 0.0 &&
             !(d->flags & NGRTD_EXACT_RTD)) {
             NG_CHECK(cheb_prepare(ctx, p->table, (1.0 + p->dtp) - p->tp0));
             if (p->table.cheb_ok) a.cheb = p->table.cheb.d();
@@ -1485,18 +1551,24 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
             const char* e = std::getenv("NGRTD_EPM_DIAG");     // timing diagnostics only
             a.epm_diag = e ? std::atoi(e) : 0;
         }
-        if (a.mod[0] == MOD_EPM && (a.mod[1] == MOD_NONE || a.mod[1] == MOD_PISTON) &&
-            p->table.C <= 5 && p->dtp >= 0.0 && !(d->flags & NGRTD_EXACT_RTD) && ri[NGRTD_ROLE_ETA1] >= 0) {
+        const bool epm1 = a.mod[0] == MOD_EPM && ri[NGRTD_ROLE_ETA1] >= 0;
+        const bool epm2 = a.mod[1] == MOD_EPM && ri[NGRTD_ROLE_ETA2] >= 0;
+        if ((epm1 || epm2) && p->table.C <= 5 && p->dtp >= 0.0 && !(d->flags & NGRTD_EXACT_RTD)) {
             // block-tail surrogates over every tau' = tau / eta >= the priors' lower end (the
             // table reaches 2^kEpmOct0); lanes below it or NaN sum their tails exactly.  A
             // per-unit CFC12 half-life reads its channel at tau'_w = 1 / (eta / tau + lam) as well.
+            // (generic instances: either component exp_pist_flow, the window over both)
             static const bool disabled = std::getenv("NGRTD_NO_CHEB") != nullptr;
             double x;
-            double plo = d->tau1_lo / d->eta1_hi;
-            if (any_lamw) {
-                const double tmin = std::min(a.thalf_b, a.thalf_a + a.thalf_b);
-                plo = tmin > 0.0 ? std::min(plo, 1.0 / (d->eta1_hi / d->tau1_lo + kLn2Ref / tmin)) : 0.0;
-            }
+            double plo = HUGE_VAL;
+            const double tmin = std::min(a.thalf_b, a.thalf_a + a.thalf_b);
+            auto low = [&](double tau_lo, double eta_hi) {
+                double v = tau_lo / eta_hi;
+                if (any_lamw) v = tmin > 0.0 ? std::min(v, 1.0 / (eta_hi / tau_lo + kLn2Ref / tmin)) : 0.0;
+                plo = std::min(plo, v);
+            };
+            if (epm1) low(d->tau1_lo, d->eta1_hi);
+            if (epm2) low(d->tau2_lo, d->eta2_hi);
             const double lo = std::max(1.0 / (1 << -kEpmOct0), plo);
             const int pa = epm_piece(lo, x), pb = kEpmPieces - 1;
             if (!disabled && pa >= 0 && pb >= pa) {
@@ -1506,6 +1578,17 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
                     a.epm_nb = p->table.epm_nb; a.epm_p0 = p->table.epm_p0; a.epm_np = p->table.epm_np;
                 }
             }
+        }
+        a.disp_aux = nullptr;
+        if (a.mod[0] == MOD_DISP || a.mod[1] == MOD_DISP) {   // gen_exact's per-age factors
+            std::vector<double> aux(2 * (size_t)p->N);
+            for (int k = 0; k < p->N; ++k) {
+                const double tp = k == 0 ? p->tp0 : (double)k + p->dtp;
+                aux[k] = 1.0 / tp;
+                aux[p->N + k] = std::pow(tp, -1.5);
+            }
+            NG_CHECK(upload(ctx, p->table.disp, aux.data(), aux.size()));
+            a.disp_aux = p->table.disp.d();
         }
         u.rtd_on = 1; u.K = K;
         u.rtd_obs = p->rtd_obs.d(); u.rtd_sd = p->rtd_sd.d(); u.conc = p->conc.d();
@@ -1663,7 +1746,7 @@ static int plan_run(ngrtd_plan* p, const double* theta, int64_t W, double* logp,
     if (p->desc.rtd_enabled && ((logp && !ce_out && !rtd_out) || (!logp && (ce_out || rtd_out)))) {
         RtdArgs a = p->rtd;
         a.theta = theta; a.U = U; a.conc = logp ? nullptr : rtd_out;
-        if (fused_path(a, u)) {
+        if (single_path(a, u)) {
             NG_CHECK(timed_begin(p, prof, st, &ev));
             NG_CHECK(launch_fused(ctx, a, u, W, p->desc.n_wells, logp, st, dap));
             NG_CHECK(timed_end(p, prof, st, 3, ev));
@@ -1788,7 +1871,7 @@ static int plan_run_units(ngrtd_plan* p, const double* theta, int64_t W, double*
     if (p->desc.rtd_enabled) {
         RtdArgs a = p->rtd;
         a.theta = theta; a.U = U; a.conc = nullptr;
-        if (fused_path(a, u)) {
+        if (single_path(a, u)) {
             u.unit_out = out;
             return launch_fused(ctx, a, u, W, L, out, st);
         }

@@ -48,6 +48,9 @@ struct RtdArgs {
     int32_t epm_nb, epm_p0, epm_np;
     int32_t epm_diag;       // timing diagnostics only (NGRTD_EPM_DIAG, tools/epm_probe.py): bit 0 skips
                             // the head, bit 1 the tail surrogate, bit 2 the exact tails (wrong results)
+    // dispersion components of the generic single-launch instances (gen_exact): per age k,
+    // 1 / tp_k at [k] and tp_k^(-3/2) at [N + k]; null when the plan has no dispersion component
+    const double* disp_aux;
 };
 
 // exp_pist_flow (convolution_integral_utils.py:186-190) on the yearly grid: the unmasked

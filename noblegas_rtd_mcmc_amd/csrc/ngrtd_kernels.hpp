@@ -829,12 +829,12 @@ __host__ __device__ __forceinline__ void cheb_sums(const double* pc, int CP, dou
 // Numerators num_c = A_{c,0} + s01 Y_c and the reciprocal normaliser 1 / (1 + s01 G) ->
 // tracer concentrations of unit u (rtd_conc_kernel's combination step): per tracer
 // (A + J B) / den, the BMM mix and the SF6 factor (run_age_mcmc_utils.py:154-161).
-// num2: the second BMM component's numerators when it is a piston (its normaliser is
-// g.sum() = 1, convolution_integral_utils.py:178-181, 270): cout = f1 cout1 + f2 cout2 with
+// num2: the second BMM component's numerators, rden2 its reciprocal normaliser (a piston's
+// is g.sum() = 1, convolution_integral_utils.py:178-181, 270): cout = f1 cout1 + f2 cout2 with
 // f2 = 1 - f1 (the Deterministic of run_age_mcmc_utils.py:304).
 template <int C, bool ST = false>
 __device__ __forceinline__ void unit_conc(const RtdArgs& a, int64_t u, const double* num, double rden,
-                                          double* conc, const double* num2 = nullptr) {
+                                          double* conc, const double* num2 = nullptr, double rden2 = 1.0) {
     const double fmix = (a.row_f1 >= 0) ? a.theta[(int64_t)a.row_f1 * a.U + u] : 1.0;
     double Jw = 0.0;
     if (a.row_J >= 0) {
@@ -859,7 +859,7 @@ __device__ __forceinline__ void unit_conc(const RtdArgs& a, int64_t u, const dou
         const double cc = hasB ? (sA + J * sB) * rden : sA * rden;
         double cout;
         if (num2) {
-            const double cc2 = hasB ? (sA2 + J * sB2) : sA2;
+            const double cc2 = (hasB ? (sA2 + J * sB2) : sA2) * rden2;
             cout = fmix * cc + (1 - fmix) * cc2;
         } else {
             cout = fmix * cc + 0.0 * 0.0;   // f1*cout1 + f2*cout2, run_age_mcmc_utils.py:154
@@ -916,12 +916,13 @@ __device__ __forceinline__ LwDecay lw_decay(const RtdArgs& a, double tau, double
 // are NaN for every age when exp overflows for some age (inf / inf), when every weight
 // underflows to 0 (0 / 0), and for tau = 0 or NaN; otherwise finite.  -tp/tau is monotone
 // in tp, so its extremes are at tp_0 and tp_{N-1}.
+// tau = +-inf: 1/tau = 0 makes every weight 0 (0 / 0 as well).
 __device__ __forceinline__ bool exp_rtd_nan(const RtdArgs& a, double tau) {
     const double tpN = (a.N > 1) ? (double)(a.N - 1) + a.dtp : a.tp0;
     const double x0 = (-a.tp0) / tau, xN = (-tpN) / tau;
     const double xmax = x0 > xN ? x0 : xN;
-    return !(tau == tau) || tau == 0.0 || !(xmax == xmax) || xmax > 709.782712893384 ||
-           xmax < -745.1332191019412;
+    return !(tau == tau) || tau == 0.0 || !(fabs(tau) <= 1.7976931348623157e308) || !(xmax == xmax) ||
+           xmax > 709.782712893384 || xmax < -745.1332191019412;
 }
 
 // Exact channel sums Y_c (matrix-core path) -> concentrations: the normaliser
@@ -2119,6 +2120,145 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
     dd = e2;
 }
 
+// ------------------------------------------------------ generic components (MIX bit 6)
+// The single-launch kernel's generic instances serve every model pair of run_age_mcmc.py:61-70
+// that has no specialised instance: first component piston / exponential / exp_pist_flow /
+// dispersion, second none or any of the four (convolution_integral_utils.py:178-196 per
+// component, the mix of run_age_mcmc_utils.py:96-154).  Per component and lane:
+//   piston         the channel-table row at the first argmin |tp - tau| (a lookup);
+//   exponential    the surrogate (cheb_sums) when tau (and tau_eff, LW) lie in the staged
+//                  window, else gen_exact -- or, with the priors on and tau outside its Uniform
+//                  prior's support, no sums at all (the log-prob is -inf) but exp_rtd_nan;
+//   exp_pist_flow  epm_sums (head Horner + block-tail surrogate, exact tails where uncovered);
+//   dispersion     gen_exact.
+//
+// Exact channel sums of one component over all N ages, for the lanes with `on` (the age loop is
+// wave-uniform: all lanes read the same table row), with the reference's weights
+//   exponential    w = (1/tau) e^(-tp/tau)                                         (:184)
+//   exp_pist_flow  w = (eta/tau) e^(-eta tp/tau + eta - 1) where tp >= tau (1 - 1/eta), else 0
+//   dispersion     w = (1/tau) / sqrt(4 pi D x) (1/x) e^(-(1-x)^2 / (4 D x)),  x = tp/tau
+//                    = sqrt(tau / (4 pi D)) tp^(-3/2) e^(-(1-x)^2 (tau/tp) / (4 D))
+//                  with 1/tp_k and tp_k^(-3/2) from a.disp_aux (no division, sqrt or power per age)
+// num_c = sum_k A_{c,k} w_k (the per-unit decayed channel, LW: w_k e^(-lam tp_k)), den = sum_k w_k,
+// so conc = num / den is the normalised g (:270) dotted with the series (:336-340).  Zero, inf and
+// NaN weights give the reference's NaN / inf concentrations (0 / 0, inf / inf).
+template <int C, bool LW>
+__device__ __forceinline__ void gen_exact(const RtdArgs& a, int mod, bool on, double tau, double eta, double D,
+                                          double lam, double* num, double& den) {
+    double s[C + 1];
+#pragma unroll
+    for (int c = 0; c <= C; ++c) s[c] = 0.0;
+    if (__any(on)) {
+        const double rt = 1.0 / tau;
+        double k1, k2 = 0.0, thr = 0.0;
+        if (mod == MOD_EXP) {
+            k1 = rt;
+        } else if (mod == MOD_EPM) {
+            k1 = eta / tau;
+            k2 = eta - 1;
+            thr = tau * (1 - (1 / eta));
+        } else {
+            k1 = sqrt(tau / (4. * kPi * D));
+            k2 = 1.0 / (4. * D);
+        }
+        const int N = a.N;
+        for (int k = 0; k < N; ++k) {
+            const double tp = (k == 0) ? a.tp0 : ((double)k + a.dtp);
+            double w;
+            if (mod == MOD_EXP) {
+                w = k1 * fexp(-tp * k1);
+            } else if (mod == MOD_EPM) {
+                w = (tp >= thr) ? k1 * fexp(fma(-k1, tp, k2)) : 0.0;
+            } else {
+                const double d = 1.0 - tp * rt;
+                w = (k1 * a.disp_aux[N + k]) * fexp(-((d * d) * (tau * a.disp_aux[k])) * k2);
+            }
+            const double wd = LW ? w * fexp(-lam * tp) : w;
+            const double* row = a.tab + (int64_t)k * a.CP;
+#pragma unroll
+            for (int c = 0; c < C; ++c) s[c] = fma(row[c], (LW && a.chan_lamw[c]) ? wd : w, s[c]);
+            s[C] += w;
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) num[c] = s[c];
+    den = s[C];
+}
+
+// One component (comp 0: tau1 / eta1 / D1, comp 1: tau2 / eta2 / D2) of a unit: its numerators
+// num[c] and reciprocal normaliser rden (conc = (A + J B) rden, unit_conc), and *nanc when the
+// concentrations are NaN without being summed (the skip lanes above).  tau: the component's tau
+// (loaded by the caller); thx: the unit's thalf_cfc Beta value (LW).
+template <int C, bool ROLES2, bool LW>
+__device__ __forceinline__ void gen_component(const RtdArgs& a, const UnitArgs& uk, const double* cheb,
+                                              const double* tabl, int comp, bool mvalid, int64_t mu, bool prior_on,
+                                              double tau, double thx, double* num, double& rden, bool& nanc) {
+    constexpr int CP = cheb_cp(C), PST = kChebN * CP + 2;   // = cheb_lds_stride(C)
+    const int mod = a.mod[comp];
+    const double eta = (mod == MOD_EPM && mvalid) ? a.theta[(int64_t)a.row_eta[comp] * a.U + mu] : 1.0;
+    const double D = (mod == MOD_DISP && mvalid) ? a.theta[(int64_t)a.row_D[comp] * a.U + mu] : 1.0;
+    LwDecay lw{0.0, 0.0};
+    if (LW) lw = lw_decay(a, tau, thx);
+    nanc = false;
+    bool ex = false;                                      // this lane's sums by gen_exact
+    if (mod == MOD_PISTON) {
+        const int ix = piston_index(tau, a.tp0, a.dtp, a.N);
+#pragma unroll
+        for (int c = 0; c < C; ++c) num[c] = a.tab[(int64_t)ix * a.CP + c];
+        if (LW) num[0] *= fexp(-lw.lam * (ix == 0 ? a.tp0 : (double)ix + a.dtp));
+        rden = 1.0;
+    } else if (mod == MOD_EXP) {
+        double cx = 0.0, cxw = 0.0;
+        int pc = a.cheb ? cheb_piece(tau, cx) - a.cheb_p0 : -1;
+        pc = (unsigned)pc < (unsigned)a.cheb_np ? pc : -1;
+        int pcw = 0;
+        if (LW) {
+            pcw = a.cheb ? cheb_piece(lw.teff, cxw) - a.cheb_p0 : -1;
+            pcw = (unsigned)pcw < (unsigned)a.cheb_np ? pcw : -1;
+        }
+        const bool unc = pc < 0 || (LW && pcw < 0);
+        // the log-prob is -inf whatever the sums when tau is outside its Uniform prior (or,
+        // LW, thalf_cfc outside [0, 1]); the concentrations matter only through their NaN-ness
+        bool skip = false;
+        if (unc && prior_on) {
+            const int rt = a.row_tau[comp];
+            const bool t1 = rt == uk.row_tau1, t2 = rt == uk.row_tau2;
+            const double lo = t1 ? uk.tau1_lo : uk.tau2_lo, hi = t1 ? uk.tau1_hi : uk.tau2_hi;
+            if ((t1 || t2) && !(tau >= lo && tau <= hi)) {
+                skip = true;
+                nanc = exp_rtd_nan(a, tau);
+            } else if (LW && a.row_thalf == uk.row_thalf && !(thx >= 0.0 && thx <= 1.0)) {
+                skip = true;
+                nanc = !(thx == thx) || exp_rtd_nan(a, tau);
+            }
+        }
+        ex = mvalid && unc && !skip;
+        double zz[C + 1];
+        cheb_sums<C + 1, ROLES2>(cheb + (pc < 0 ? 0 : pc) * PST, CP, cx, zz);   // s01 Y_c (c < C), s01 G
+        double zw = 0.0;
+        if (LW) cheb_sums<1, ROLES2>(cheb + (pcw < 0 ? 0 : pcw) * PST, CP, cxw, &zw);
+#pragma unroll
+        for (int c = 0; c < C; ++c) num[c] = a.tab0[c] + zz[c];
+        if (LW) num[0] = fexp(-lw.lam * a.tp0) * (a.tab0[0] + zw);
+        rden = 1.0 / (1.0 + zz[C]);
+    } else if (mod == MOD_EPM) {
+        double dn, dd, lam;
+        epm_sums<C, kEpmTailPreDz, LW>(a, tabl, mvalid, tau, eta, num, dn, dd, thx, &lam);
+        rden = dd / dn;
+    } else {
+        ex = mvalid;
+    }
+    if (__any(ex)) {
+        double en[C], den;
+        gen_exact<C, LW>(a, mod, ex, tau, eta, D, lw.lam, en, den);
+        if (ex) {
+#pragma unroll
+            for (int c = 0; c < C; ++c) num[c] = en[c];
+            rden = 1.0 / den;
+        }
+    }
+}
+
 // A kernel argument read through a pointer the compiler cannot see through (an empty asm
 // redefines the kernarg segment pointer): loads of its fields stay where they are used --
 // a multi-step loop would otherwise hoist every field into registers for the whole loop.
@@ -2243,8 +2383,12 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     // per-well observation data -> LDS (read per lane by the likelihood blocks): all loads
     // issued before any store, so the prologue pays one memory latency
     constexpr bool EPM = (MIX & 2) != 0;
+    constexpr bool GEN = (MIX & 64) != 0;        // generic components (gen_component)
+    static_assert(!GEN || (MIX & (1 | 2 | 8 | 16)) == 0, "generic instances: plain log-prob, runtime models");
+    // the channel table staged in LDS: exp_pist_flow components (epm_sums)
+    const bool EPMS = EPM || (GEN && (a.mod[0] == MOD_EPM || a.mod[1] == MOD_EPM));
     double* tabl = cheb + a.cheb_np * PST;                // EPM: the channel table (epm_row)
-    double* wd = tabl + (EPM ? epm_lds_doubles(a.N, CP) : 0);
+    double* wd = tabl + (EPMS ? epm_lds_doubles(a.N, CP) : 0);
     constexpr int kWdRegs = (4 * 64 * kFusedWaves + NTH - 1) / NTH;
     double wv[kWdRegs];
 #pragma unroll
@@ -2268,7 +2412,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             tp0.nub = (FULL || ua.rtd_on) ? a.theta[(int64_t)ua.row_nu * a.U + mu] : 0.0;
         }
     }
-    if (EPM) {   // channel table -> LDS (rows of CP doubles, CP even: 16-B copies)
+    if (EPMS) {   // channel table -> LDS (rows of CP doubles, CP even: 16-B copies)
         const double2* src = reinterpret_cast<const double2*>(a.tab);
         double2* dst = reinterpret_cast<double2*>(tabl);
         constexpr int RB = kEpmBlock * CP / 2, SB = epm_blk_stride(CP) / 2;   // double2 per block / padded
@@ -2365,7 +2509,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         // zero partial sums land on no walker's slots
         const int pi = (DZ && mwl >= WB) ? mi : ml * WB + mwl;
         double* tabl = cheb + a.cheb_np * PST;
-        double* wd = tabl + (EPM ? epm_lds_doubles(a.N, CP) : 0);
+        double* wd = tabl + (EPMS ? epm_lds_doubles(a.N, CP) : 0);
         double* thl = wd + uk.wd_n;
         double* propl = thl + (((MIX & 4) && DZ) ? dk.P * kFusedUnits : 0);   // DZ: [P][512] proposals
         DzLds dl;                                         // DZ: the chains' LDS state (or none)
@@ -2443,7 +2587,26 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         }
         double th = 0.0, like = 0.0;
         if (do_theta) th = mvalid ? unit_logp_theta(ul, mu, ml, &tp, FULL, (MIX & 4) != 0) : 0.0;
-        if (EPM && do_rtd) {
+        if (GEN && do_rtd) {
+            // generic components: the first from tau (prologue), the second (BMM) from tau2
+            const bool prior_on = FULL || (uk.rtd_on && (uk.flags & NGRTD_WANT_PRIOR));
+            double conc[kMaxTracer];
+            double n1[C], r1, n2[C], r2 = 1.0;
+            bool nan1, nan2 = false;
+            gen_component<C, ROLES == 2, LW>(a, uk, cheb, tabl, 0, mvalid, mu, prior_on, tau, thx, n1, r1, nan1);
+            const bool two = a.mod[1] != MOD_NONE;
+            if (two) {
+                const double t2 = mvalid ? a.theta[(int64_t)a.row_tau[1] * a.U + mu] : 1.0;
+                gen_component<C, ROLES == 2, LW>(a, uk, cheb, tabl, 1, mvalid, mu, prior_on, t2, thx, n2, r2, nan2);
+            }
+            unit_conc<C>(a, mu, n1, r1, conc, two ? n2 : nullptr, r2);
+            if (nan1 || nan2)
+                for (int t = 0; t < a.K; ++t) conc[t] = __builtin_nan("");
+            const double rnu = 1.0 / (tp.nub * (uk.rnu_max - uk.rnu_min) + uk.rnu_min);
+            like = mvalid ? unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL, &rnu) : 0.0;
+            if (!FULL && a.conc && mvalid)                        // forward(): model concentrations
+                for (int t = 0; t < a.K; ++t) a.conc[(int64_t)t * a.U + mu] = conc[t];
+        } else if (EPM && do_rtd) {
             double conc[kMaxTracer];
             {
                 double num[C], dn, dd, lam = 0.0;
@@ -2463,7 +2626,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             }
             if (!FULL && a.conc && mvalid)                        // forward(): model concentrations
                 for (int t = 0; t < a.K; ++t) a.conc[(int64_t)t * a.U + mu] = conc[t];
-        } else if (do_rtd) {
+        } else if (!GEN && do_rtd) {
             // The surrogate channel sums, the concentrations and the RTD likelihood.  Lanes
             // whose tau the surrogate does not cover evaluate piece 0 here and are redone
             // exactly below.

@@ -190,6 +190,22 @@ def c4_spec(L=64, N=1200, seed=34567, mod_type1="exponential", mod_type2=None, p
     return ModelSpec(n_wells=L, ce=ce, rtd=rtd)
 
 
+# the parameters each RTD model adds (run_age_mcmc.py:140-178: eta for exp_pist_flow, D for
+# dispersion; tau2 and f1 for a BMM) and the savenum digits (1 J, 2 thalf_cfc, 3 lamsf6)
+RTD_MODEL_PARS = {"exponential": (), "piston": (), "exp_pist_flow": ("eta",), "dispersion": ("D",)}
+
+
+def model_par_names(mod_type1="exponential", mod_type2=None, savenum=""):
+    """par_names of a model in the reference's order: tau1, [tau2, f1], the first component's
+    eta1 / D1, the second's eta2 / D2, then the savenum parameters."""
+    pn = ["tau1"] + (["tau2", "f1"] if mod_type2 else [])
+    pn += [q + "1" for q in RTD_MODEL_PARS[mod_type1]]
+    if mod_type2:
+        pn += [q + "2" for q in RTD_MODEL_PARS[mod_type2]]
+    pn += [{"1": "J", "2": "thalf_cfc", "3": "lamsf6"}[d] for d in str(savenum or "") if d in "123"]
+    return tuple(pn)
+
+
 def rtd_only_spec(L=64, N=1200, tracers=("CFC12", "SF6", "H3", "He4_ter"), mod_type1="exponential", mod_type2=None,
                   savenum="123", seed=34567):
     """The reference's own RTD model (run_age_mcmc.py:122-231: RTD-only, the 4-tracer set or
@@ -197,9 +213,8 @@ def rtd_only_spec(L=64, N=1200, tracers=("CFC12", "SF6", "H3", "He4_ter"), mod_t
     synthetic per-well obs and series (the same seeded draws, restricted to these tracers)."""
     import dataclasses
     names = ("CFC12", "SF6", "H3", "He3", "He4_ter")
-    pn = ["tau1"] + (["tau2", "f1"] if mod_type2 else []) + (["eta1"] if mod_type1 == "exp_pist_flow" else [])
-    pn += [{"1": "J", "2": "thalf_cfc", "3": "lamsf6"}[d] for d in str(savenum) if d in "123"]
-    base = c4_spec(L=L, N=N, seed=seed, mod_type1=mod_type1, mod_type2=mod_type2, par_names=tuple(pn))
+    pn = model_par_names(mod_type1, mod_type2, savenum)
+    base = c4_spec(L=L, N=N, seed=seed, mod_type1=mod_type1, mod_type2=mod_type2, par_names=pn)
     keep = [names.index(t) for t in tracers]
     r = base.rtd
     rtd = dataclasses.replace(r, tracers=[r.tracers[i] for i in keep], obs=r.obs[:, keep], sd=r.sd[:, keep])

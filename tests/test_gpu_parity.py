@@ -274,6 +274,105 @@ def test_published_models_123_single_launch_vs_oracle(model, variant):
     lp.close()
 
 
+# model pairs of run_age_mcmc.py:61-70 without a specialised instance: the generic instances
+GEN_MODELS = ["piston", "dispersion", "exponential-exponential", "exponential-exp_pist_flow",
+              "exp_pist_flow-exponential", "exp_pist_flow-exp_pist_flow", "exponential-dispersion", "piston-exponential",
+              "dispersion-piston", "piston-piston"]
+
+
+def _gen_spec(model, variant, L=64):
+    import dataclasses
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    m1, _, m2 = model.partition("-")
+    sv = "123" if variant.endswith("123") else ""
+    if variant.startswith("rtd_only"):
+        return wl.rtd_only_spec(L=L, N=1200, mod_type1=m1, mod_type2=m2 or None, savenum=sv)
+    spec = wl.c4_spec(L=L, N=1200, mod_type1=m1, mod_type2=m2 or None, par_names=wl.model_par_names(m1, m2 or None, sv))
+    return dataclasses.replace(spec, jacobian=variant.startswith("joint_jac"))
+
+
+@pytest.mark.parametrize("model", GEN_MODELS)
+@pytest.mark.parametrize("variant", ["joint", "joint_123", "rtd_only_123"])
+def test_generic_models_single_launch_vs_oracle(model, variant):
+    """Every other model pair the reference's driver accepts (run_age_mcmc.py:61-70: piston or
+    dispersion single components, BMMs with an exponential / exp_pist_flow / dispersion second
+    component, piston first components) in ONE launch of the generic instances (gen_component:
+    piston lookups, surrogate sums at tau1 and tau2, epm_sums for either component, exact
+    per-age sums for dispersion) at the c4 shape (joint: 2048 x 64 x (5 gases + 5 tracers); _123:
+    J, thalf_cfc, lamsf6 sampled; rtd_only_123: the reference's own 4-tracer RTD model) vs the
+    vectorised oracle on 264 walkers, determinism, device == host, forward() vs the per-walker
+    oracle."""
+    import torch
+    import oracle.models as om
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+    spec = _gen_spec(model, variant)
+    th = wl.sample_prior(spec, 2048, np.random.default_rng(34568))
+    lp = LogProb(spec, max_walkers=2048)
+    dev = torch.from_numpy(th).cuda()
+    lp.ctx.set_profiling(True)
+    lp.kernel_stats(reset=True)
+    a = lp(dev).cpu().numpy()
+    lp.ctx.set_profiling(False)
+    ks = lp.kernel_stats(reset=True)
+    assert ks["fused"][1] == 1 and ks["rtd"][1] == 0 and ks["unit"][1] == 0, ks   # one launch
+    assert np.array_equal(a, lp(dev).cpu().numpy()) and np.array_equal(a, lp(th, soa=True))
+    sel = many_walkers(2048, seed=11)
+    refv = log_prob_vec(spec, np.ascontiguousarray(th[:, :, sel]))
+    ok = close(a[sel], refv, 1e-12, 1e-9)
+    assert ok.all(), (np.array(sel)[~ok], a[sel][~ok], refv[~ok])
+    if "exp_pist_flow" not in model.partition("-")[2]:     # (a second EPM's mask can exclude every age: NaN)
+        assert np.isfinite(a).mean() > 0.5
+    walkers = [0, 777, 2047]
+    ce, rt = lp.forward(th, soa=True)
+    ce_ref, rt_ref = om.forward(spec, th, walkers=walkers)
+    assert close(np.transpose(rt[:, :, walkers], (1, 0, 2)), rt_ref, 1e-12).all()
+    lp.close()
+
+
+@pytest.mark.parametrize("model", ["piston", "dispersion-piston", "exponential-exponential", "exp_pist_flow-exponential"])
+def test_generic_models_jacobian_and_edges(model):
+    """The generic instances with the transform Jacobians (the transformed-space sampler's
+    log-prob, FULL + Jacobian instance) on 264 walkers, and at their edges on 2 wells: tau1,
+    tau2 at and beyond their priors' ends (the skip lanes: -inf, or NaN where the weights are),
+    tau2 below the surrogate (exact sums), the EPM eta at 1 and 5, D at its ends and 0 (NaN),
+    f1 at 0 and 1 -- vs the per-walker oracle."""
+    import torch
+    import oracle.models as om
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+    spec = _gen_spec(model, "joint_jac")
+    th = wl.sample_prior(spec, 2048, np.random.default_rng(5))
+    lp = LogProb(spec, max_walkers=2048)
+    a = lp(torch.from_numpy(th).cuda()).cpu().numpy()
+    sel = many_walkers(2048, seed=13)
+    refv = log_prob_vec(spec, np.ascontiguousarray(th[:, :, sel]))
+    ok = close(a[sel], refv, 1e-12, 1e-9)
+    assert ok.all(), (np.array(sel)[~ok], a[sel][~ok], refv[~ok])
+    lp.close()
+    spec = _gen_spec(model, "joint", L=2)
+    W = 64
+    th = wl.sample_prior(spec, W, np.random.default_rng(3))
+    R = {r: i for i, r in enumerate(spec.roles)}
+    edits = {"tau1": [1.0, 1000.0, 0.3, 1500.0, 0.0, -2.0], "tau2": [50.0, 15000.0, 0.2, 20000.0, 3.0],
+             "eta1": [1.0, 5.0], "eta2": [1.0, 5.0], "D1": [0.01, 2.0, 0.0, 3.0], "D2": [0.01, 2.0, 0.0],
+             "f1": [0.01, 0.99, 0.0, 1.0]}
+    w = 0
+    for role, vals in edits.items():
+        if role not in R:
+            continue
+        for v in vals:
+            th[R[role], :, w] = v
+            w += 1
+    assert w <= W
+    lp = LogProb(spec, max_walkers=W)
+    got = lp(th, soa=True)
+    ref = om.log_prob(spec, th, walkers=range(W))
+    ok = close(got, ref, 1e-12, 1e-9)
+    assert ok.all(), (np.nonzero(~ok)[0], got[~ok], ref[~ok])
+    lp.close()
+
+
 @pytest.mark.parametrize("model", ["exponential", "exp_pist_flow", "exponential-piston", "exp_pist_flow-piston"])
 def test_published_models_123_edges(model):
     """Savenum 123 in the single launch at its edges: thalf_cfc at its prior's ends (0, 1:
