@@ -903,9 +903,25 @@ static int launch_fused_dz(ngrtd_ctx* ctx, const RtdArgs& a0, const UnitArgs& u,
     HIP_TRY(ctx, launch_fused_dz_instance(mix, a, u, WB, W, logp, d, lds, kFusedMaxLds, st));
     return NGRTD_OK;
 }
+// Walkers per block of a log-prob launch: kFusedUnits / L fills all 8 unit waves of every
+// block, but a small ensemble then leaves most CUs idle (a c5 shard, 256 walkers x 64 wells:
+// 32 blocks on 256 CUs; c3, 2048 walkers x 1 well: 4).  Fewer walkers per block (halving)
+// until the grid covers the CUs; the blocks' unit waves past WB L units skip their body.
+// NGRTD_FUSED_WB=max keeps kFusedUnits / L (A/B runs).
+constexpr int kCUs = 256;
+static int fused_wb(int64_t W, int L) {
+    static const bool fixed = [] {
+        const char* e = std::getenv("NGRTD_FUSED_WB");
+        return e && std::strcmp(e, "max") == 0;
+    }();
+    int wb = kFusedUnits / L;
+    if (fixed) return wb;
+    while (wb > 1 && cdiv(W, wb) < kCUs) wb /= 2;
+    return wb;
+}
 static int launch_fused(ngrtd_ctx* ctx, const RtdArgs& a0, const UnitArgs& u, int64_t W, int L, double* logp,
                         hipStream_t st, const DemcAccept* dap = nullptr) {
-    const int WB = kFusedUnits / L;
+    const int WB = fused_wb(W, L);
     RtdArgs a = a0;
     const DemcAccept da = dap ? *dap : DemcAccept{};
     if (!fused_path(a0, u)) {   // the generic instances (gen_path)

@@ -155,6 +155,41 @@ NGRTD_FM double flog(double x) {
     return res;
 }
 
+// flog for arguments the caller knows to be positive, normal and finite (a product of
+// factors >= 1, a product of Beta factors >= 1e-280): the same arithmetic as flog on them --
+// the same bits -- without the subnormal scaling and the special-value selects (~17 VALU
+// instructions fewer); any other argument gives an unspecified value.
+NGRTD_FM double flog_pn(double x) {
+    const double LN2_HI = 6.93147180369123816490e-01;
+    const double LN2_LO = 1.90821492927058770002e-10;
+    const unsigned hi = fm_hi(x);
+    const int i64 = (int)(((hi >> 13) & 127) + 1) >> 1;
+    const bool wrap = i64 == 64;
+    const int i = wrap ? 0 : i64;
+    const int e = (int)((hi >> 20) & 0x7FF) - 1023 + (wrap ? 1 : 0);
+    const double m = fm_with_hi(x, (hi & 0x000FFFFFu) | (wrap ? 0x3FE00000u : 0x3FF00000u));
+    const double ci = fm_with_hi(0.0, 0x3FF00000u | ((unsigned)i << 14));
+    const double f = m - ci;
+    const double r = f * NGRTD_FMT[2 * kFmExpN + 3 * i];
+    double q = -0.125;
+    q = fma_k(q, r, 1.0 / 7.0);
+    q = fma_k(q, r, -1.0 / 6.0);
+    q = fma_k(q, r, 0.2);
+    q = fma_k(q, r, -0.25);
+    q = fma_k(q, r, 1.0 / 3.0);
+    q = fma_k(q, r, -0.5);
+    const double l1p = fma(r * r, q, r);
+    const double ed = (double)e;
+    const double t1 = fma(ed, LN2_HI, NGRTD_FMT[2 * kFmExpN + 3 * i + 1]);
+    const double t2 = fma(ed, LN2_LO, NGRTD_FMT[2 * kFmExpN + 3 * i + 2]) + l1p;
+    return t1 + t2;
+}
+// ... and for 0 as well (log(0) = -inf): 1 - x for x in [0, 1] is 0 or >= 2^-53
+NGRTD_FM double flog_z(double x) {
+    const double r = flog_pn(x);
+    return x == 0.0 ? -__builtin_inf() : r;
+}
+
 // expm1(x) = 2^k (e^r - 1) + (2^k - 1), x = k ln2 + r, |r| <= ln2/2: e^r - 1 by its Taylor
 // series to r^14/14! (truncation < 2e-19 relative), then ONE fma with the exact 2^k - 1
 // (|k| <= 57 below), so there is no cancellation for small |x| and <= 2 ulp everywhere

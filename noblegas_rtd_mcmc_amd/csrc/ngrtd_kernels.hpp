@@ -505,12 +505,13 @@ __device__ __forceinline__ double beta_block(const UnitArgs& a, int64_t u, const
             inb &= (x >= 0 && x <= 1);
             pint *= ipow_small(x, a.bt_ia[i]) * ipow_small(1 - x, a.bt_ib[i]);
             if (a.bt_fa[i] != 0.0) lsum += a.bt_fa[i] * flog(x);
-            if (a.bt_fb[i] != 0.0) lsum += a.bt_fb[i] * flog(1 - x);
+            // (1 - x for x in [0, 1]: 0 or >= 2^-53; x outside makes the sum -inf anyway)
+            if (a.bt_fb[i] != 0.0) lsum += a.bt_fb[i] * flog_z(1 - x);
         }
     }
     double lint;
     if (pint >= 1e-280) {
-        lint = flog(pint);
+        lint = flog_pn(pint);   // (a normal number: <= 1 in bounds; out of bounds the sum is -inf)
     } else {
         lint = 0.0;
 #pragma unroll
@@ -2587,7 +2588,10 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         }
         double th = 0.0, like = 0.0;
         if (do_theta) th = mvalid ? unit_logp_theta(ul, mu, ml, &tp, FULL, (MIX & 4) != 0) : 0.0;
-        if (GEN && do_rtd) {
+        // RTD waves without a unit (blocks of fewer walkers than kFusedUnits / L: fused_wb) skip
+        // their body (wave-uniform)
+        const bool rtd_w = do_rtd && (DZ || __any(mvalid));
+        if (GEN && rtd_w) {
             // generic components: the first from tau (prologue), the second (BMM) from tau2
             const bool prior_on = FULL || (uk.rtd_on && (uk.flags & NGRTD_WANT_PRIOR));
             double conc[kMaxTracer];
@@ -2606,7 +2610,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             like = mvalid ? unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL, &rnu) : 0.0;
             if (!FULL && a.conc && mvalid)                        // forward(): model concentrations
                 for (int t = 0; t < a.K; ++t) a.conc[(int64_t)t * a.U + mu] = conc[t];
-        } else if (EPM && do_rtd) {
+        } else if (EPM && rtd_w) {
             double conc[kMaxTracer];
             {
                 double num[C], dn, dd, lam = 0.0;
@@ -2626,7 +2630,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             }
             if (!FULL && a.conc && mvalid)                        // forward(): model concentrations
                 for (int t = 0; t < a.K; ++t) a.conc[(int64_t)t * a.U + mu] = conc[t];
-        } else if (!GEN && do_rtd) {
+        } else if (!GEN && rtd_w) {
             // The surrogate channel sums, the concentrations and the RTD likelihood.  Lanes
             // whose tau the surrogate does not cover evaluate piece 0 here and are redone
             // exactly below.
@@ -2743,13 +2747,17 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
                 const unsigned long long m = __ballot(a != 0);
                 if (lane == 0) wcnt[uw] = __popcll(m);
             }
-        } else if (WB <= 64 && (WB & (WB - 1)) == 0) {
+        } else if (const int WBc = kFusedUnits / L; WBc <= 64 && (WBc & (WBc - 1)) == 0) {
+            // the addition order is the one of WBc = kFusedUnits / L walkers per block whatever
+            // WB (<= WBc, a power of two: fused_wb halves WBc), so a walker's log-prob does not
+            // depend on the ensemble size (a c5 shard's walkers give the single-GPU run's bits)
             if (wave == 0) {
-                const int G = 64 / WB;                        // well groups (power of two)
+                const int G = 64 / WBc;                       // well groups (power of two)
                 const int wl = lane % WB, g = lane / WB;
                 double tot = 0.0;
-                for (int l = g; l < L; l += G) tot += part[l * WB + wl];
-                for (int off = WB; off < 64; off <<= 1) tot += __shfl_xor(tot, off);
+                if (g < G)
+                    for (int l = g; l < L; l += G) tot += part[l * WB + wl];
+                for (int off = WB; off < WB * G; off <<= 1) tot += __shfl_xor(tot, off);
                 if (g == 0 && w0 + wl < W) walker_out<DZ>(logp, dk, sj, log_off, w0 + wl, tot, dec + wl, dl, wl);
             }
         } else if (tid < WB && w0 + tid < W) {

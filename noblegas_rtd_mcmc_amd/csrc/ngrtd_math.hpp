@@ -358,7 +358,9 @@ NGRTD_HD double st_block_inu(int n, const double* obs, const double* mu, const d
     }
     double Lg;
     if (!big) {
-        Lg = flog(prod);
+        // prod >= 1 (finite) whenever the block is in bounds (nu > 0, lam > 0); else the result
+        // is -inf whatever Lg is
+        Lg = flog_pn(prod);
     } else {
         // inf/NaN z or z >= 1e38: one log per factor (log(1 + z) = log1p(z) + O(2^-53))
         Lg = 0.0;

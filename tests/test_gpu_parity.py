@@ -373,6 +373,32 @@ def test_generic_models_jacobian_and_edges(model):
     lp.close()
 
 
+@pytest.mark.parametrize("case", ["c4", "c4_123_epm", "c3", "c4_dispersion"])
+def test_logp_independent_of_ensemble_size(case):
+    """A walker's log-prob does not depend on how many walkers share the launch: the single
+    launch takes fewer walkers per block for small ensembles (fused_wb: a c5 shard of 256
+    walkers covers the CUs with 256 blocks of one walker) but adds its wells in the order of
+    the full blocks -- so the shards of a strong-scaled run give the one-GPU run's bits."""
+    import torch
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+    if case == "c3":
+        spec, _ = wl.c3(W=8)
+    elif case == "c4":
+        spec = wl.c4_spec(L=64, N=1200)
+    elif case == "c4_123_epm":
+        spec = _spec_123("exp_pist_flow")
+    else:
+        spec = wl.c4_spec(L=64, N=1200, mod_type1="dispersion", par_names=wl.model_par_names("dispersion"))
+    th = wl.sample_prior(spec, 2048, np.random.default_rng(21))
+    lp = LogProb(spec, max_walkers=2048)
+    full = lp(torch.from_numpy(th).cuda()).cpu().numpy()
+    for lo, n in ((0, 256), (1536, 256), (5, 1), (100, 37), (0, 1024)):
+        sub = lp(torch.from_numpy(np.ascontiguousarray(th[:, :, lo:lo + n])).cuda()).cpu().numpy()
+        assert np.array_equal(sub, full[lo:lo + n], equal_nan=True), (case, lo, n)
+    lp.close()
+
+
 @pytest.mark.parametrize("model", ["exponential", "exp_pist_flow", "exponential-piston", "exp_pist_flow-piston"])
 def test_published_models_123_edges(model):
     """Savenum 123 in the single launch at its edges: thalf_cfc at its prior's ends (0, 1:
