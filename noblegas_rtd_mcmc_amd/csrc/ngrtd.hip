@@ -899,6 +899,12 @@ static int launch_fused_dz(ngrtd_ctx* ctx, const RtdArgs& a0, const UnitArgs& u,
     if (d.state_lds) lds += sb;   // after the proposal rows (logp_fused_kernel's carve-up)
     // no global proposal rows when nothing reads them (NGRTD_DZ_PROP_WRITE=1 writes them, A/B)
     d.prop_skip = (d.prop_lds && dz_theta_all_lds(a, u, da.P) && !std::getenv("NGRTD_DZ_PROP_WRITE")) ? 1 : 0;
+    // per-well chains: pairwise waits instead of the step's block barriers (pair_sync);
+    // NGRTD_DZ_PAIRSYNC=0/1 chooses (A/B runs; the chains are the same bit for bit)
+    {
+        const char* e = std::getenv("NGRTD_DZ_PAIRSYNC");
+        d.pair_sync = (da.per_well && e && std::atoi(e) == 1) ? 1 : 0;
+    }
     if (!fused_dz_instance_exists(mix)) return set_err(ctx, NGRTD_EINVAL, "no single-launch DEMetropolisZ instance %d", mix);
     HIP_TRY(ctx, launch_fused_dz_instance(mix, a, u, WB, W, logp, d, lds, kFusedMaxLds, st));
     return NGRTD_OK;

@@ -160,6 +160,9 @@ NGRTD_FM double flog(double x) {
 // the same bits -- without the subnormal scaling and the special-value selects (~17 VALU
 // instructions fewer); any other argument gives an unspecified value.
 NGRTD_FM double flog_pn(double x) {
+#ifdef NGRTD_NO_FLOG_PN   // (A/B builds: the general flog)
+    return flog(x);
+#endif
     const double LN2_HI = 6.93147180369123816490e-01;
     const double LN2_LO = 1.90821492927058770002e-10;
     const unsigned hi = fm_hi(x);

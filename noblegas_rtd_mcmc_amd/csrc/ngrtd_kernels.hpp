@@ -1998,11 +1998,15 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
     double qB = -1.0, qBw = -1.0;                       // q^(B - m) from the head's weights (fast path)
     if (!(a.epm_diag & 1)) {
         const bool qok = q <= 1.0 && (!LW || qw <= 1.0);
-        const double* hb = tabl + epm_row(B - S, CP);
+        // m >= N (every age masked: tau (1 - 1/eta) beyond the series, the reference's g is 0 / 0):
+        // m's block is past the staged table, so read the last staged block, where k < m for every
+        // row and every weight stays 0 (then y = 0, G = 0: NaN concentrations, as the reference's)
+        const int hb0 = B - S < (N - 1) / S * S ? B - S : (N - 1) / S * S;
+        const double* hb = tabl + epm_row(hb0, CP);
         double w = 0.0, w2 = 0.0;
 #pragma unroll
         for (int i = 0; i < S; ++i) {
-            const int k = B - S + i;
+            const int k = hb0 + i;
             w = k == m ? 1.0 : w * q;
             if (LW) w2 = k == m ? 1.0 : w2 * qw;     // channel 0's own weights (LW)
             double rv[C];
@@ -2303,6 +2307,25 @@ constexpr int kFusedPrefetch = 6;   // double2 per thread (512 threads): covers 
 // §LDS: a b128 lane group conflicts on equal slots).
 __host__ __device__ constexpr int cheb_lds_stride(int C) { return kChebN * cheb_cp(C) + 2; }
 
+// Per-well chains (DemcAccept::pair_sync): every exchange inside a multi-step launch's step is
+// between the two waves of one unit group -- theta wave uw and RTD wave uw + kFusedWaves share
+// the units 64 uw .. 64 uw + 63 (staged rows of both parities, the RTD likelihood, the
+// decision, the commit) -- so the step's block barriers become pairwise waits on per-wave LDS
+// phase counters: the 8 pairs of a block need not meet (one pair's staging loads can overlap
+// another's log-prob).  Release / acquire fences at workgroup scope order the LDS and global
+// writes around the wait, as the barrier did.  The wait is bounded (~0.5 s): a pair can never
+// hang the GPU, whatever happens to its partner.
+__device__ __forceinline__ void pair_sync(int* pf, int wave, int phase) {
+    const int partner = wave < kFusedWaves ? wave + kFusedWaves : wave - kFusedWaves;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if ((threadIdx.x & 63) == 0) __hip_atomic_store(pf + wave, phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    for (int n = 0; n < (1 << 23); ++n) {
+        if (__hip_atomic_load(pf + partner, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= phase) break;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 // ROLES = 1: one wave per 64 units runs the whole unit (2 waves/SIMD at c4, 228 VGPRs).
 // ROLES = 2: the block has 2 x 8 waves; waves 0-7 run the theta-only block (priors, CE model,
 // CE likelihood) and waves 8-15 the RTD block (surrogate channel sums, concentrations, RTD
@@ -2351,6 +2374,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     double* part2 = lds + kFusedUnits;                    // [512] RTD likelihood (ROLES = 2)
     int* dec = reinterpret_cast<int*>(lds + 2 * kFusedUnits);   // [512] DE-MC decisions per walker
     int* wcnt = reinterpret_cast<int*>(lds + 2 * kFusedUnits + kFusedUnits / 2);   // [16] per-wave accept counts
+    int* pflag = wcnt + 16;                               // [16] pair_sync phase counters ([8]: PS accept total)
     double* cheb = lds + kFusedHdr;                       // [kChebPieces][kChebN][CP]
     if (!DZ) NGRTD_PROBE(0);   // (a stamp here broke the DZ instances' instruction selection)
     const int tid = threadIdx.x;
@@ -2449,6 +2473,11 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     // DZ, LDS state (dacc.state_lds): the block's chains -> LDS, once per launch (each lane the
     // rows of its unit it stages: theta waves the even rows, RTD waves the odd ones)
     bool moved = false;                                   // ... a row of this lane's unit changed
+    const bool PS = PW && dacc.pair_sync != 0;            // pairwise step synchronisation (pair_sync)
+    if (PS && tid < 16) {
+        pflag[tid] = 0;
+        wcnt[tid] = 0;
+    }
     if (DZ && dacc.state_lds) {
         double* st = thl + ((MIX & 4) ? dacc.P * kFusedUnits : 0) + (dacc.prop_lds ? dacc.P * kFusedUnits : 0);
         const int dwl = mi / L, dml = mi % L;
@@ -2469,6 +2498,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         }
         __syncthreads();
     }
+    if (PS && !dacc.state_lds) __syncthreads();           // (the tables: the steps' waits are pairwise)
     // DZ: dacc.n_steps steps of the block's own chains, the tables staged once above
     // (a do-while: without DZ there is no back edge at all -- a one-trip for loop changed the
     // register allocation of the plain log-prob instances)
@@ -2560,7 +2590,8 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
                                                   PW ? mi : mwl);
         }
         NGRTD_PROBE(9);
-        __syncthreads();
+        if (PS) pair_sync(pflag, wave, 3 * js + 1);
+        else __syncthreads();
         NGRTD_PROBE(1);
         if (DZ && dk.prop_lds) {                              // the proposal's rows, from LDS
             if (do_theta) {
@@ -2719,7 +2750,8 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             part[pi] = th + like;
         } else {
             if (do_rtd) part2[pi] = like;
-            __syncthreads();
+            if (PS) pair_sync(pflag, wave, 3 * js + 2);
+            else __syncthreads();
             if (do_theta) part[pi] = th + part2[pi];          // th + like, as ROLES = 1
         }
         if (!DZ && uk.unit_out) {   // ngrtd_logp_units: each unit's log-prob, no per-walker sum
@@ -2745,7 +2777,10 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             }
             if (do_theta && dk.n_acc) {        // the wave's accept count -> LDS (summed after the barrier)
                 const unsigned long long m = __ballot(a != 0);
-                if (lane == 0) wcnt[uw] = __popcll(m);
+                if (lane == 0) {
+                    if (PS) atomicAdd(&wcnt[8], (int)__popcll(m));   // (the launch's total, added at its end)
+                    else wcnt[uw] = __popcll(m);
+                }
             }
         } else if (const int WBc = kFusedUnits / L; WBc <= 64 && (WBc & (WBc - 1)) == 0) {
             // the addition order is the one of WBc = kFusedUnits / L walkers per block whatever
@@ -2767,9 +2802,10 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         }
         if (DZ) {
             NGRTD_PROBE(10);
-            __syncthreads();
+            if (PS) pair_sync(pflag, wave, 3 * js + 3);
+            else __syncthreads();
             NGRTD_PROBE(11);
-            if (PW && dk.n_acc && tid == 0) {  // one accept-count atomic per block and step
+            if (!PS && PW && dk.n_acc && tid == 0) {  // one accept-count atomic per block and step
                 int n = 0;
 #pragma unroll
                 for (int i = 0; i < kFusedWaves; ++i) n += wcnt[i];
@@ -2790,6 +2826,10 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             }
         }
     } while (DZ && ++js < nst);   // steps
+    if (PS) {                     // the launch's accept count: one atomic per block
+        __syncthreads();
+        if (tid == 0 && dacc.n_acc && wcnt[8]) atomicAdd(dacc.n_acc, (unsigned long long)wcnt[8]);
+    }
     if (DZ && dacc.state_lds) {   // the LDS state back: the rows of the units that moved, every chain's scalars
         __syncthreads();
         const double* st = thl + ((MIX & 4) ? dacc.P * kFusedUnits : 0) + (dacc.prop_lds ? dacc.P * kFusedUnits : 0);

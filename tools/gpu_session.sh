@@ -8,6 +8,7 @@
 #   bench20              the driver's command: bench.py --gpus 1 --steps 20 --warmup 5
 #   stats[=ARGS]         rocprofv3 --kernel-trace --stats of bench.py ARGS -> $OUT/stats*/
 #   probe=SCRIPT[:ARGS]  python tools/SCRIPT ARGS         -> $OUT/probe*.json
+#   sh=COMMAND           bash -c COMMAND (a GPU command of its own, e.g. an env-var A/B) -> $OUT/sh*.log
 # Outputs under gpurun_out/TAG/; steps.log records each step and its exit status.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -42,6 +43,9 @@ for st in "$@"; do
       scr=${arg%%:*}; pa=""; [ "$scr" != "$arg" ] && pa=${arg#*:}
       timeout -k 10 400 python tools/$scr $pa > $OUT/probe$n.json 2> $OUT/probe$n.err; rc=$?
       head -c 1500 $OUT/probe$n.json; echo ;;
+    sh)
+      timeout -k 10 900 bash -c "$arg" > $OUT/sh$n.log 2>&1; rc=$?
+      tail -5 $OUT/sh$n.log ;;
     *) log "unknown step $name"; exit 2 ;;
   esac
   log "rc=$rc"
