@@ -814,13 +814,33 @@ static void launch_fused_cf(const RtdArgs& a, const UnitArgs& u, int WB, int64_t
         else launch_fused_cfr<C, FULL, 1, 0>(a, u, WB, W, logp, da, st);
     }
 }
+// The plan's Beta slots are the reference's priors (kRefBeta[set - 1], exactly as add_beta split
+// them): 1 bare, 2 with the Jacobians, 0 other.  NGRTD_NO_REFB=1 ignores it (A/B runs).
+static int ref_beta_set(const UnitArgs& u) {
+    if (std::getenv("NGRTD_NO_REFB")) return 0;
+    const int s = (u.flags & NGRTD_WANT_JACOBIAN) ? 1 : 0;
+    const BetaExp& e = kRefBeta[s];
+    if (u.bt_n != e.n) return 0;
+    for (int i = 0; i < e.n; ++i)
+        if (u.bt_ia[i] != e.ia[i] || u.bt_ib[i] != e.ib[i] || u.bt_fa[i] != e.fa[i] || u.bt_fb[i] != e.fb[i]) return 0;
+    return s + 1;
+}
 // FULL instances: CE + RTD blocks, priors and likelihoods on (the joint model), without or
-// -- single-component RTD -- with the transform Jacobians (the transformed-space sampler)
+// -- single-component RTD -- with the transform Jacobians (the transformed-space sampler);
+// the exponential c4-shape ones (C = 5) also with the reference's Beta priors compiled in (MIX
+// bit 7, ref_beta_set)
 template <int C>
 static void launch_fused_c(const RtdArgs& a, const UnitArgs& u, int WB, int64_t W, double* logp,
                            const DemcAccept& da, hipStream_t st) {
     const bool joint = u.ce_on && u.rtd_on && (u.flags & NGRTD_WANT_LIKE) && (u.flags & NGRTD_WANT_PRIOR);
     const bool jac = (u.flags & NGRTD_WANT_JACOBIAN) != 0;
+    if constexpr (C == 5) {
+        if (joint && a.mod[0] == MOD_EXP && a.mod[1] == MOD_NONE && fused_roles() == 2 && ref_beta_set(u)) {
+            if (jac) launch_fused_cfr<C, true, 2, 128 | 4>(a, u, WB, W, logp, da, st);
+            else launch_fused_cfr<C, true, 2, 128>(a, u, WB, W, logp, da, st);
+            return;
+        }
+    }
     if (joint && !jac) launch_fused_cf<C, true>(a, u, WB, W, logp, da, st);
     else if (joint && a.mod[1] == MOD_NONE && a.mod[0] == MOD_EXP) launch_fused_cfr<C, true, 2, 4>(a, u, WB, W, logp, da, st);
     else if (joint && a.mod[1] == MOD_NONE && a.mod[0] == MOD_EPM) launch_fused_cfr<C, true, 2, 6>(a, u, WB, W, logp, da, st);

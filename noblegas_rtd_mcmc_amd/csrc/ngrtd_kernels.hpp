@@ -492,21 +492,46 @@ __device__ __forceinline__ double beta_x(const UnitArgs& a, int64_t u, int i, co
     return a.theta[(int64_t)a.bt_row[i] * a.U + u];
 }
 
+// The reference's own Beta priors as compile-time exponent sets (REFB, logp_fused_kernel MIX
+// bit 7): CE Ae (2, 2), F (2, 2), E (2, 4), b (2, 2.5), nu (2, 0.1) (noble_gas_mcmc.py:224-226,
+// 237, 249) and the RTD nu (2, 0.1) (run_age_mcmc_utils.py:333-335), in the host's slot order
+// (ngrtd.hip add_beta, whose split into integer parts and non-integer coefficients the
+// expressions below restate): set 0 bare, set 1 with the logodds Jacobians (every exponent
+// + 1).  With the exponents known the integer powers need no selects and the non-integer
+// terms no uniform branches; the arithmetic -- and so every bit -- is the runtime loop's.
+struct BetaExp {
+    int n;
+    int ia[kMaxBeta], ib[kMaxBeta];
+    double fa[kMaxBeta], fb[kMaxBeta];
+};
+constexpr BetaExp kRefBeta[2] = {
+    {6, {1, 1, 1, 1, 1, 1, 0}, {1, 1, 3, 0, 0, 0, 0}, {0, 0, 0, 0, 0, 0, 0},
+     {0, 0, 0, 2.5 - 1, 0.1 - 1, 0.1 - 1, 0}},
+    {6, {2, 2, 2, 2, 2, 2, 0}, {2, 2, 4, 0, 0, 0, 0}, {0, 0, 0, 0, 0, 0, 0},
+     {0, 0, 0, (2.5 - 1) + 1.0, (0.1 - 1) + 1.0, (0.1 - 1) + 1.0, 0}}};
+
+template <int REFB = 0>
 __device__ __forceinline__ double beta_block(const UnitArgs& a, int64_t u, const ThetaPre* pre = nullptr,
                                              bool full = false) {
+    constexpr BetaExp E = REFB ? kRefBeta[REFB - 1] : BetaExp{};
+    const int n = REFB ? E.n : a.bt_n;
+    auto IA = [&](int i) { return REFB ? E.ia[i] : a.bt_ia[i]; };
+    auto IB = [&](int i) { return REFB ? E.ib[i] : a.bt_ib[i]; };
+    auto FA = [&](int i) { return REFB ? E.fa[i] : a.bt_fa[i]; };
+    auto FB = [&](int i) { return REFB ? E.fb[i] : a.bt_fb[i]; };
     double pint = 1.0, lsum = 0.0;
     bool inb = true;
     double xs[kMaxBeta];
 #pragma unroll
     for (int i = 0; i < kMaxBeta; ++i) {
-        if (i < a.bt_n) {
+        if (i < n) {
             const double x = beta_x(a, u, i, pre, full);
             xs[i] = x;
             inb &= (x >= 0 && x <= 1);
-            pint *= ipow_small(x, a.bt_ia[i]) * ipow_small(1 - x, a.bt_ib[i]);
-            if (a.bt_fa[i] != 0.0) lsum += a.bt_fa[i] * flog(x);
+            pint *= ipow_small(x, IA(i)) * ipow_small(1 - x, IB(i));
+            if (FA(i) != 0.0) lsum += FA(i) * flog(x);
             // (1 - x for x in [0, 1]: 0 or >= 2^-53; x outside makes the sum -inf anyway)
-            if (a.bt_fb[i] != 0.0) lsum += a.bt_fb[i] * flog_z(1 - x);
+            if (FB(i) != 0.0) lsum += FB(i) * flog_z(1 - x);
         }
     }
     double lint;
@@ -516,9 +541,9 @@ __device__ __forceinline__ double beta_block(const UnitArgs& a, int64_t u, const
         lint = 0.0;
 #pragma unroll
         for (int i = 0; i < kMaxBeta; ++i) {
-            if (i < a.bt_n) {
-                if (a.bt_ia[i]) lint += (double)a.bt_ia[i] * flog(xs[i]);
-                if (a.bt_ib[i]) lint += (double)a.bt_ib[i] * flog(1 - xs[i]);
+            if (i < n) {
+                if (IA(i)) lint += (double)IA(i) * flog(xs[i]);
+                if (IB(i)) lint += (double)IB(i) * flog(1 - xs[i]);
             }
         }
     }
@@ -527,6 +552,8 @@ __device__ __forceinline__ double beta_block(const UnitArgs& a, int64_t u, const
 
 // full_jac: compile-time promise (with full) that the plan also carries the PyMC3
 // transform Jacobians -- the transformed-space sampler's log-prob (sampler.py)
+// REFB: the plan's Beta slots are the reference's (kRefBeta[REFB - 1]; FULL instances only)
+template <int REFB = 0>
 __device__ __forceinline__ double unit_logp_theta(const UnitArgs& a, int64_t u, int l,
                                                   const ThetaPre* pre = nullptr, bool full = false,
                                                   bool full_jac = false) {
@@ -534,7 +561,7 @@ __device__ __forceinline__ double unit_logp_theta(const UnitArgs& a, int64_t u, 
     const bool want_prior = full || (a.flags & NGRTD_WANT_PRIOR);
     const bool jac = full ? full_jac : (a.flags & NGRTD_WANT_JACOBIAN) != 0;
     double lp = 0.0;
-    if (want_prior) lp += beta_block(a, u, pre, full);
+    if (want_prior) lp += beta_block<REFB>(a, u, pre, full);
     if (full || a.ce_on) {
         double p[6];
 #pragma unroll
@@ -2357,6 +2384,10 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     constexpr bool DZ = (MIX & 8) != 0;
     constexpr bool PW = DZ && (MIX & 16) != 0;   // per-well chains: one Metropolis decision per unit
     constexpr bool LW = (MIX & 32) != 0;         // the sampled CFC12 half-life (channel 0, lw_decay)
+    // MIX bit 7: the reference's Beta priors as compile-time exponents (kRefBeta; with the
+    // Jacobians the second set)
+    constexpr int REFB = (MIX & 128) ? ((MIX & 4) ? 2 : 1) : 0;
+    static_assert(!REFB || FULL, "compile-time Beta exponents: FULL instances");
     static_assert(!DZ || (FULL && ROLES == 2), "the DEMetropolisZ step runs in the FULL role-split kernel");
     static_assert(kFusedUnitsDz == kFusedUnits, "DZ staging stride");
     const RtdArgs& a = ak;
@@ -2618,7 +2649,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             }
         }
         double th = 0.0, like = 0.0;
-        if (do_theta) th = mvalid ? unit_logp_theta(ul, mu, ml, &tp, FULL, (MIX & 4) != 0) : 0.0;
+        if (do_theta) th = mvalid ? unit_logp_theta<REFB>(ul, mu, ml, &tp, FULL, (MIX & 4) != 0) : 0.0;
         // RTD waves without a unit (blocks of fewer walkers than kFusedUnits / L: fused_wb) skip
         // their body (wave-uniform)
         const bool rtd_w = do_rtd && (DZ || __any(mvalid));
