@@ -698,15 +698,28 @@ constexpr size_t kFusedMaxLds = 157 * 1024;   // gfx950: 160 KiB per workgroup, 
 // A per-unit CFC12 half-life (row_thalf) runs in the single launch (the LW instances) when it
 // decays exactly one channel, channel 0 (build_table puts it first), with the instance
 // counts of lw_instance (C = 5 for the joint plans, C = 4 or 5 otherwise).
-static bool lw_instance(const UnitArgs& u, int C) {
+// The FULL instances' plan: the joint model (CE and RTD blocks, priors and likelihoods) with
+// the reference's Beta priors, which they compile in (kRefBeta: the set of the plan's Jacobian
+// flag and sampled half-life, compared exactly with add_beta's split).  Other joint plans run
+// the runtime-flag instances.  NGRTD_NO_REFB=1 treats every plan as other (A/B runs).
+static bool full_plan(const RtdArgs& a, const UnitArgs& u) {
     const bool joint = u.ce_on && u.rtd_on && (u.flags & NGRTD_WANT_LIKE) && (u.flags & NGRTD_WANT_PRIOR);
-    return joint ? C == 5 : (C == 4 || C == 5);
+    if (!joint || std::getenv("NGRTD_NO_REFB")) return false;
+    const BetaExp& e = kRefBeta[((u.flags & NGRTD_WANT_JACOBIAN) ? 1 : 0) + (a.row_thalf >= 0 ? 2 : 0)];
+    if (u.bt_n != e.n) return false;
+    for (int i = 0; i < e.n; ++i)
+        if (u.bt_ia[i] != e.ia[i] || u.bt_ib[i] != e.ib[i] || u.bt_fa[i] != e.fa[i] || u.bt_fb[i] != e.fb[i])
+            return false;
+    return true;
+}
+static bool lw_instance(const RtdArgs& a, const UnitArgs& u, int C) {
+    return full_plan(a, u) ? C == 5 : (C == 4 || C == 5);
 }
 static bool lw_ok(const RtdArgs& a, const UnitArgs& u) {
     if (a.row_thalf < 0) return true;
     int n = 0;
     for (int c = 0; c < a.C; ++c) n += a.chan_lamw[c] ? 1 : 0;
-    return n == 1 && a.chan_lamw[0] && !a.chan_isB[0] && lw_instance(u, a.C);
+    return n == 1 && a.chan_lamw[0] && !a.chan_isB[0] && lw_instance(a, u, a.C);
 }
 static bool fused_path(const RtdArgs& a0, const UnitArgs& u) {
     static const bool disabled = std::getenv("NGRTD_NO_FUSED") != nullptr;
@@ -757,11 +770,8 @@ static void gen_cheb_window(RtdArgs& a, const UnitArgs& u) {
     a.cheb_p0 = pa;
     a.cheb_np = pb - pa + 1;
 }
-static bool gen_full(const UnitArgs& u) {
-    return u.ce_on && u.rtd_on && (u.flags & NGRTD_WANT_LIKE) && (u.flags & NGRTD_WANT_PRIOR);
-}
 static int gen_mix(const RtdArgs& a, const UnitArgs& u) {
-    return 64 | (a.row_thalf >= 0 ? 32 : 0) | (gen_full(u) && (u.flags & NGRTD_WANT_JACOBIAN) ? 4 : 0);
+    return 64 | (a.row_thalf >= 0 ? 32 : 0) | (full_plan(a, u) && (u.flags & NGRTD_WANT_JACOBIAN) ? 4 : 0);
 }
 static bool gen_path(const RtdArgs& a0, const UnitArgs& u) {
     static const bool disabled = std::getenv("NGRTD_NO_GEN") != nullptr;
@@ -773,7 +783,7 @@ static bool gen_path(const RtdArgs& a0, const UnitArgs& u) {
     const bool disp_c = a.mod[0] == MOD_DISP || a.mod[1] == MOD_DISP;
     if ((exp_c && !a.cheb) || (epm_c && !a.epm) || (disp_c && !a.disp_aux)) return false;
     return a.C >= 1 && a.C <= 5 && lw_ok(a, u) && u.L >= 1 && u.L <= kFusedUnits &&
-           fused_lds(a, u) <= kFusedMaxLds && gen_instance_exists(a.C, gen_full(u), gen_mix(a, u));
+           fused_lds(a, u) <= kFusedMaxLds && gen_instance_exists(a.C, full_plan(a, u), gen_mix(a, u));
 }
 // one launch for the plan's log-prob / forward outputs: a specialised or a generic instance
 static bool single_path(const RtdArgs& a, const UnitArgs& u) { return fused_path(a, u) || gen_path(a, u); }
@@ -814,33 +824,13 @@ static void launch_fused_cf(const RtdArgs& a, const UnitArgs& u, int WB, int64_t
         else launch_fused_cfr<C, FULL, 1, 0>(a, u, WB, W, logp, da, st);
     }
 }
-// The plan's Beta slots are the reference's priors (kRefBeta[set - 1], exactly as add_beta split
-// them): 1 bare, 2 with the Jacobians, 0 other.  NGRTD_NO_REFB=1 ignores it (A/B runs).
-static int ref_beta_set(const UnitArgs& u) {
-    if (std::getenv("NGRTD_NO_REFB")) return 0;
-    const int s = (u.flags & NGRTD_WANT_JACOBIAN) ? 1 : 0;
-    const BetaExp& e = kRefBeta[s];
-    if (u.bt_n != e.n) return 0;
-    for (int i = 0; i < e.n; ++i)
-        if (u.bt_ia[i] != e.ia[i] || u.bt_ib[i] != e.ib[i] || u.bt_fa[i] != e.fa[i] || u.bt_fb[i] != e.fb[i]) return 0;
-    return s + 1;
-}
 // FULL instances: CE + RTD blocks, priors and likelihoods on (the joint model), without or
-// -- single-component RTD -- with the transform Jacobians (the transformed-space sampler);
-// the exponential c4-shape ones (C = 5) also with the reference's Beta priors compiled in (MIX
-// bit 7, ref_beta_set)
+// -- single-component RTD -- with the transform Jacobians (the transformed-space sampler)
 template <int C>
 static void launch_fused_c(const RtdArgs& a, const UnitArgs& u, int WB, int64_t W, double* logp,
                            const DemcAccept& da, hipStream_t st) {
-    const bool joint = u.ce_on && u.rtd_on && (u.flags & NGRTD_WANT_LIKE) && (u.flags & NGRTD_WANT_PRIOR);
+    const bool joint = full_plan(a, u);
     const bool jac = (u.flags & NGRTD_WANT_JACOBIAN) != 0;
-    if constexpr (C == 5) {
-        if (joint && a.mod[0] == MOD_EXP && a.mod[1] == MOD_NONE && fused_roles() == 2 && ref_beta_set(u)) {
-            if (jac) launch_fused_cfr<C, true, 2, 128 | 4>(a, u, WB, W, logp, da, st);
-            else launch_fused_cfr<C, true, 2, 128>(a, u, WB, W, logp, da, st);
-            return;
-        }
-    }
     if (joint && !jac) launch_fused_cf<C, true>(a, u, WB, W, logp, da, st);
     else if (joint && a.mod[1] == MOD_NONE && a.mod[0] == MOD_EXP) launch_fused_cfr<C, true, 2, 4>(a, u, WB, W, logp, da, st);
     else if (joint && a.mod[1] == MOD_NONE && a.mod[0] == MOD_EPM) launch_fused_cfr<C, true, 2, 6>(a, u, WB, W, logp, da, st);
@@ -856,7 +846,7 @@ static void launch_fused_c(const RtdArgs& a, const UnitArgs& u, int WB, int64_t 
 static int dz_mix(const RtdArgs& a0, const UnitArgs& u, int P, bool transformed) {
     RtdArgs a = a0;
     cheb_window(a, u);
-    const bool joint = u.ce_on && u.rtd_on && (u.flags & NGRTD_WANT_LIKE) && (u.flags & NGRTD_WANT_PRIOR);
+    const bool joint = full_plan(a, u);
     const bool jac = (u.flags & NGRTD_WANT_JACOBIAN) != 0;
     // transformed chains <=> the Jacobian instance (its proposals go through backward())
     if (!joint || jac != transformed || a.C != 5 || fused_roles() != 2 || P < 1 || P > kDzMaxP || !fused_path(a, u) ||
@@ -919,12 +909,6 @@ static int launch_fused_dz(ngrtd_ctx* ctx, const RtdArgs& a0, const UnitArgs& u,
     if (d.state_lds) lds += sb;   // after the proposal rows (logp_fused_kernel's carve-up)
     // no global proposal rows when nothing reads them (NGRTD_DZ_PROP_WRITE=1 writes them, A/B)
     d.prop_skip = (d.prop_lds && dz_theta_all_lds(a, u, da.P) && !std::getenv("NGRTD_DZ_PROP_WRITE")) ? 1 : 0;
-    // per-well chains: pairwise waits instead of the step's block barriers (pair_sync);
-    // NGRTD_DZ_PAIRSYNC=0/1 chooses (A/B runs; the chains are the same bit for bit)
-    {
-        const char* e = std::getenv("NGRTD_DZ_PAIRSYNC");
-        d.pair_sync = (da.per_well && e && std::atoi(e) == 1) ? 1 : 0;
-    }
     if (!fused_dz_instance_exists(mix)) return set_err(ctx, NGRTD_EINVAL, "no single-launch DEMetropolisZ instance %d", mix);
     HIP_TRY(ctx, launch_fused_dz_instance(mix, a, u, WB, W, logp, d, lds, kFusedMaxLds, st));
     return NGRTD_OK;
@@ -952,13 +936,13 @@ static int launch_fused(ngrtd_ctx* ctx, const RtdArgs& a0, const UnitArgs& u, in
     const DemcAccept da = dap ? *dap : DemcAccept{};
     if (!fused_path(a0, u)) {   // the generic instances (gen_path)
         gen_cheb_window(a, u);
-        HIP_TRY(ctx, launch_fused_gen_instance(a.C, gen_full(u), gen_mix(a, u), a, u, WB, W, logp, da, fused_lds(a, u),
+        HIP_TRY(ctx, launch_fused_gen_instance(a.C, full_plan(a, u), gen_mix(a, u), a, u, WB, W, logp, da, fused_lds(a, u),
                                                kFusedMaxLds, st));
         return NGRTD_OK;
     }
     cheb_window(a, u);
     if (a.row_thalf >= 0) {   // the sampled CFC12 half-life (ngrtd_lw.hip, lw_ok)
-        const bool joint = u.ce_on && u.rtd_on && (u.flags & NGRTD_WANT_LIKE) && (u.flags & NGRTD_WANT_PRIOR);
+        const bool joint = full_plan(a, u);
         const bool jac = (u.flags & NGRTD_WANT_JACOBIAN) != 0;
         const bool single = a.mod[1] == MOD_NONE;
         const bool full = joint && (!jac || single);

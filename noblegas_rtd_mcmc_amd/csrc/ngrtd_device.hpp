@@ -240,10 +240,6 @@ struct DemcAccept {
     int32_t per_well;
     int64_t well0;
     double* ar_log;         // [chains] this step's PyMC3 `accept` stat exp(mr) (null: not logged)
-    // 1 (per-well chains, multi-step launch): the step's block barriers become pairwise waits
-    // of the two waves of each unit group (logp_fused_kernel pair_sync); the acceptance count
-    // is summed in LDS and added once per launch
-    int32_t pair_sync;
 };
 
 // One DEMetropolisZ step's schedule (ngrtd_demcz_run's host loop, restated so that a

@@ -97,7 +97,8 @@ __device__ __forceinline__ double dzc_rtd_like(const RtdArgs& a, const UnitArgs&
     double like = 0.0;
     if (EPM) {
         double num[C], dn, dd, lam = 0.0;
-        epm_sums<C, kEpmTailPreDz, LW>(a, tabl, valid, tau, eta, num, dn, dd, thx, &lam);
+        bool wnan;
+        epm_sums<C, kEpmTailPreDz, LW>(a, tabl, valid, tau, eta, num, dn, dd, thx, &lam, &wnan);
         const double dr[2] = {dn, nub * (ul.rnu_max - ul.rnu_min) + ul.rnu_min};
         double rr[2];
         batch_recip<2>(dr, rr);
@@ -108,6 +109,9 @@ __device__ __forceinline__ double dzc_rtd_like(const RtdArgs& a, const UnitArgs&
             if (LW) num2[0] *= fexp(-lam * (ix == 0 ? a.tp0 : (double)ix + a.dtp));
         }
         unit_conc<C, true>(a, slot, num, dd * rr[0], conc, (MIX & 1) ? num2 : nullptr);
+        if (wnan)
+            for (int t = 0; t < C; ++t)
+                if (t < a.K) conc[t] = __builtin_nan("");
         like = valid ? unit_like_rtd<C>(ul, slot, ml, conc, &tp, false, &rr[1]) : 0.0;
         return like;
     }

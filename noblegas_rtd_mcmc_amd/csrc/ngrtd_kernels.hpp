@@ -492,22 +492,28 @@ __device__ __forceinline__ double beta_x(const UnitArgs& a, int64_t u, int i, co
     return a.theta[(int64_t)a.bt_row[i] * a.U + u];
 }
 
-// The reference's own Beta priors as compile-time exponent sets (REFB, logp_fused_kernel MIX
-// bit 7): CE Ae (2, 2), F (2, 2), E (2, 4), b (2, 2.5), nu (2, 0.1) (noble_gas_mcmc.py:224-226,
-// 237, 249) and the RTD nu (2, 0.1) (run_age_mcmc_utils.py:333-335), in the host's slot order
-// (ngrtd.hip add_beta, whose split into integer parts and non-integer coefficients the
-// expressions below restate): set 0 bare, set 1 with the logodds Jacobians (every exponent
-// + 1).  With the exponents known the integer powers need no selects and the non-integer
-// terms no uniform branches; the arithmetic -- and so every bit -- is the runtime loop's.
+// The reference's own Beta priors as compile-time exponent sets (REFB: every FULL instance of
+// logp_fused_kernel, the joint plan with the reference's priors): CE Ae (2, 2), F (2, 2), E (2, 4),
+// b (2, 2.5), nu (2, 0.1) (noble_gas_mcmc.py:224-226, 237, 249), the RTD nu (2, 0.1) and, with
+// the sampled CFC12 half-life, thalf_cfc (2, 2) (run_age_mcmc_utils.py:333-335), in the host's
+// slot order (ngrtd.hip add_beta, whose split into integer parts and non-integer coefficients
+// the expressions below restate): sets 0 / 1 bare / with the logodds Jacobians (every exponent
+// + 1), 2 / 3 the same with thalf_cfc.  With the exponents known the integer powers need no
+// selects and the non-integer terms no uniform branches; the arithmetic -- and so every bit --
+// is the runtime loop's (A/B: 11.95 -> 11.37 us per c4 launch, profiles/r04i_refb_ab.txt).
 struct BetaExp {
     int n;
     int ia[kMaxBeta], ib[kMaxBeta];
     double fa[kMaxBeta], fb[kMaxBeta];
 };
-constexpr BetaExp kRefBeta[2] = {
+constexpr BetaExp kRefBeta[4] = {
     {6, {1, 1, 1, 1, 1, 1, 0}, {1, 1, 3, 0, 0, 0, 0}, {0, 0, 0, 0, 0, 0, 0},
      {0, 0, 0, 2.5 - 1, 0.1 - 1, 0.1 - 1, 0}},
     {6, {2, 2, 2, 2, 2, 2, 0}, {2, 2, 4, 0, 0, 0, 0}, {0, 0, 0, 0, 0, 0, 0},
+     {0, 0, 0, (2.5 - 1) + 1.0, (0.1 - 1) + 1.0, (0.1 - 1) + 1.0, 0}},
+    {7, {1, 1, 1, 1, 1, 1, 1}, {1, 1, 3, 0, 0, 0, 1}, {0, 0, 0, 0, 0, 0, 0},
+     {0, 0, 0, 2.5 - 1, 0.1 - 1, 0.1 - 1, 0}},
+    {7, {2, 2, 2, 2, 2, 2, 2}, {2, 2, 4, 0, 0, 0, 2}, {0, 0, 0, 0, 0, 0, 0},
      {0, 0, 0, (2.5 - 1) + 1.0, (0.1 - 1) + 1.0, (0.1 - 1) + 1.0, 0}}};
 
 template <int REFB = 0>
@@ -1966,15 +1972,37 @@ __device__ __forceinline__ void epm_tail_sums(const double* pt, double x, double
 // chain, its tail is the same block-tail function at tau'_w = 1 / sigma (a second piece), and
 // its numerator carries e^(-lam tp_m) (m >= 1) or e^(-lam tp_0) (f = 0).  thx: the unit's
 // thalf_cfc Beta value; *lam_out: its decay constant (the piston component needs it).
+// *nan_out: the reference's normalised weights are NaN as a whole for this unit (epm_sums below).
 template <int C, int NPW = kEpmTailPre, bool LW = false>
 __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, bool mvalid, double tau, double eta,
                                          double* num, double& dn, double& dd, double thx = 0.0,
-                                         double* lam_out = nullptr) {
+                                         double* lam_out = nullptr, bool* nan_out = nullptr) {
     constexpr int CP = cheb_cp(C), S = kEpmBlock;
     const int N = a.N;
     const double beta = eta / tau;
     const double ie = 1 / eta;                          // the mask's 1/eta (:189), also tau' = tau / eta
     const int f = epm_first(tau * (1 - ie), a.tp0, a.dtp, N);
+    // The reference's weights (eta/tau) e^(-eta tp/tau + eta - 1) over the unmasked ages give NaN
+    // concentrations as a whole (0 / 0 or inf / inf after g /= g.sum(), :270) when every age is
+    // masked, and when the weights are 0, inf or NaN at both ends of the unmasked range (they are
+    // monotone in tp): tau or eta 0, inf or NaN, or the largest weight under- / overflowing.
+    // The sums below work relative to the first unmasked weight and stay finite there, so the
+    // predicate is evaluated exactly -- in waves holding a lane near those cases only.
+    if (nan_out) {
+        const double tpf = f == 0 ? a.tp0 : (double)f + a.dtp;
+        const double xf = -(eta * tpf / tau) + eta - 1;
+        const bool susp = f >= N || !(beta > 0.0 && beta <= 1.7976931348623157e308) || !(xf > -700.0);
+        bool wn = false;
+        if (__any(susp) && susp) {
+            const double tpl = N > 1 ? (double)(N - 1) + a.dtp : a.tp0;
+            const double xl = -(eta * tpl / tau) + eta - 1;
+            const double ce = eta / tau;
+            const double w0 = ce * fexp(xf), w1 = ce * fexp(xl);
+            wn = f >= N || !(fabs(w0) <= 1.7976931348623157e308) || !(fabs(w1) <= 1.7976931348623157e308) ||
+                 (w0 == 0.0 && w1 == 0.0);
+        }
+        *nan_out = wn;
+    }
     const int m = f > 1 ? f : 1;
     const int blk = m / S + 1, B = blk * S;
     const double q = fexp(-beta);
@@ -2275,7 +2303,7 @@ __device__ __forceinline__ void gen_component(const RtdArgs& a, const UnitArgs& 
         rden = 1.0 / (1.0 + zz[C]);
     } else if (mod == MOD_EPM) {
         double dn, dd, lam;
-        epm_sums<C, kEpmTailPreDz, LW>(a, tabl, mvalid, tau, eta, num, dn, dd, thx, &lam);
+        epm_sums<C, kEpmTailPreDz, LW>(a, tabl, mvalid, tau, eta, num, dn, dd, thx, &lam, &nanc);
         rden = dd / dn;
     } else {
         ex = mvalid;
@@ -2334,25 +2362,6 @@ constexpr int kFusedPrefetch = 6;   // double2 per thread (512 threads): covers 
 // §LDS: a b128 lane group conflicts on equal slots).
 __host__ __device__ constexpr int cheb_lds_stride(int C) { return kChebN * cheb_cp(C) + 2; }
 
-// Per-well chains (DemcAccept::pair_sync): every exchange inside a multi-step launch's step is
-// between the two waves of one unit group -- theta wave uw and RTD wave uw + kFusedWaves share
-// the units 64 uw .. 64 uw + 63 (staged rows of both parities, the RTD likelihood, the
-// decision, the commit) -- so the step's block barriers become pairwise waits on per-wave LDS
-// phase counters: the 8 pairs of a block need not meet (one pair's staging loads can overlap
-// another's log-prob).  Release / acquire fences at workgroup scope order the LDS and global
-// writes around the wait, as the barrier did.  The wait is bounded (~0.5 s): a pair can never
-// hang the GPU, whatever happens to its partner.
-__device__ __forceinline__ void pair_sync(int* pf, int wave, int phase) {
-    const int partner = wave < kFusedWaves ? wave + kFusedWaves : wave - kFusedWaves;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if ((threadIdx.x & 63) == 0) __hip_atomic_store(pf + wave, phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    for (int n = 0; n < (1 << 23); ++n) {
-        if (__hip_atomic_load(pf + partner, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= phase) break;
-        __builtin_amdgcn_s_sleep(1);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-
 // ROLES = 1: one wave per 64 units runs the whole unit (2 waves/SIMD at c4, 228 VGPRs).
 // ROLES = 2: the block has 2 x 8 waves; waves 0-7 run the theta-only block (priors, CE model,
 // CE likelihood) and waves 8-15 the RTD block (surrogate channel sums, concentrations, RTD
@@ -2384,10 +2393,10 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     constexpr bool DZ = (MIX & 8) != 0;
     constexpr bool PW = DZ && (MIX & 16) != 0;   // per-well chains: one Metropolis decision per unit
     constexpr bool LW = (MIX & 32) != 0;         // the sampled CFC12 half-life (channel 0, lw_decay)
-    // MIX bit 7: the reference's Beta priors as compile-time exponents (kRefBeta; with the
-    // Jacobians the second set)
-    constexpr int REFB = (MIX & 128) ? ((MIX & 4) ? 2 : 1) : 0;
-    static_assert(!REFB || FULL, "compile-time Beta exponents: FULL instances");
+    // FULL: the reference's Beta priors as compile-time exponents (kRefBeta: bare / with the
+    // Jacobians, without / with thalf_cfc) -- not in the DEMetropolisZ steps, where the folded
+    // code spilled 17-37 VGPRs inside the step loop; their runtime loop gives the same bits
+    constexpr int REFB = (FULL && !DZ) ? 1 + ((MIX & 4) ? 1 : 0) + (LW ? 2 : 0) : 0;
     static_assert(!DZ || (FULL && ROLES == 2), "the DEMetropolisZ step runs in the FULL role-split kernel");
     static_assert(kFusedUnitsDz == kFusedUnits, "DZ staging stride");
     const RtdArgs& a = ak;
@@ -2405,7 +2414,6 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     double* part2 = lds + kFusedUnits;                    // [512] RTD likelihood (ROLES = 2)
     int* dec = reinterpret_cast<int*>(lds + 2 * kFusedUnits);   // [512] DE-MC decisions per walker
     int* wcnt = reinterpret_cast<int*>(lds + 2 * kFusedUnits + kFusedUnits / 2);   // [16] per-wave accept counts
-    int* pflag = wcnt + 16;                               // [16] pair_sync phase counters ([8]: PS accept total)
     double* cheb = lds + kFusedHdr;                       // [kChebPieces][kChebN][CP]
     if (!DZ) NGRTD_PROBE(0);   // (a stamp here broke the DZ instances' instruction selection)
     const int tid = threadIdx.x;
@@ -2504,11 +2512,6 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     // DZ, LDS state (dacc.state_lds): the block's chains -> LDS, once per launch (each lane the
     // rows of its unit it stages: theta waves the even rows, RTD waves the odd ones)
     bool moved = false;                                   // ... a row of this lane's unit changed
-    const bool PS = PW && dacc.pair_sync != 0;            // pairwise step synchronisation (pair_sync)
-    if (PS && tid < 16) {
-        pflag[tid] = 0;
-        wcnt[tid] = 0;
-    }
     if (DZ && dacc.state_lds) {
         double* st = thl + ((MIX & 4) ? dacc.P * kFusedUnits : 0) + (dacc.prop_lds ? dacc.P * kFusedUnits : 0);
         const int dwl = mi / L, dml = mi % L;
@@ -2529,7 +2532,6 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         }
         __syncthreads();
     }
-    if (PS && !dacc.state_lds) __syncthreads();           // (the tables: the steps' waits are pairwise)
     // DZ: dacc.n_steps steps of the block's own chains, the tables staged once above
     // (a do-while: without DZ there is no back edge at all -- a one-trip for loop changed the
     // register allocation of the plain log-prob instances)
@@ -2621,8 +2623,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
                                                   PW ? mi : mwl);
         }
         NGRTD_PROBE(9);
-        if (PS) pair_sync(pflag, wave, 3 * js + 1);
-        else __syncthreads();
+        __syncthreads();
         NGRTD_PROBE(1);
         if (DZ && dk.prop_lds) {                              // the proposal's rows, from LDS
             if (do_theta) {
@@ -2676,8 +2677,9 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             double conc[kMaxTracer];
             {
                 double num[C], dn, dd, lam = 0.0;
+                bool wnan;
                 epm_sums<C, DZ ? kEpmTailPreDz : LW ? kEpmTailPreLw : kEpmTailPre, LW>(a, tabl, mvalid, tau, eta, num, dn,
-                                                                                     dd, thx, &lam);
+                                                                                     dd, thx, &lam, &wnan);
                 const double dr[2] = {dn, tp.nub * (uk.rnu_max - uk.rnu_min) + uk.rnu_min};
                 double rr[2];
                 batch_recip<2>(dr, rr);
@@ -2688,6 +2690,8 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
                     if (LW) num2[0] *= fexp(-lam * (ix == 0 ? a.tp0 : (double)ix + a.dtp));
                 }
                 unit_conc<C>(a, mu, num, dd * rr[0], conc, (MIX & 1) ? num2 : nullptr);
+                if (wnan)
+                    for (int t = 0; t < a.K; ++t) conc[t] = __builtin_nan("");
                 like = mvalid ? unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL, &rr[1]) : 0.0;
             }
             if (!FULL && a.conc && mvalid)                        // forward(): model concentrations
@@ -2781,8 +2785,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             part[pi] = th + like;
         } else {
             if (do_rtd) part2[pi] = like;
-            if (PS) pair_sync(pflag, wave, 3 * js + 2);
-            else __syncthreads();
+            __syncthreads();
             if (do_theta) part[pi] = th + part2[pi];          // th + like, as ROLES = 1
         }
         if (!DZ && uk.unit_out) {   // ngrtd_logp_units: each unit's log-prob, no per-walker sum
@@ -2808,10 +2811,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             }
             if (do_theta && dk.n_acc) {        // the wave's accept count -> LDS (summed after the barrier)
                 const unsigned long long m = __ballot(a != 0);
-                if (lane == 0) {
-                    if (PS) atomicAdd(&wcnt[8], (int)__popcll(m));   // (the launch's total, added at its end)
-                    else wcnt[uw] = __popcll(m);
-                }
+                if (lane == 0) wcnt[uw] = __popcll(m);
             }
         } else if (const int WBc = kFusedUnits / L; WBc <= 64 && (WBc & (WBc - 1)) == 0) {
             // the addition order is the one of WBc = kFusedUnits / L walkers per block whatever
@@ -2833,10 +2833,9 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         }
         if (DZ) {
             NGRTD_PROBE(10);
-            if (PS) pair_sync(pflag, wave, 3 * js + 3);
-            else __syncthreads();
+            __syncthreads();
             NGRTD_PROBE(11);
-            if (!PS && PW && dk.n_acc && tid == 0) {  // one accept-count atomic per block and step
+            if (PW && dk.n_acc && tid == 0) {  // one accept-count atomic per block and step
                 int n = 0;
 #pragma unroll
                 for (int i = 0; i < kFusedWaves; ++i) n += wcnt[i];
@@ -2857,10 +2856,6 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             }
         }
     } while (DZ && ++js < nst);   // steps
-    if (PS) {                     // the launch's accept count: one atomic per block
-        __syncthreads();
-        if (tid == 0 && dacc.n_acc && wcnt[8]) atomicAdd(dacc.n_acc, (unsigned long long)wcnt[8]);
-    }
     if (DZ && dacc.state_lds) {   // the LDS state back: the rows of the units that moved, every chain's scalars
         __syncthreads();
         const double* st = thl + ((MIX & 4) ? dacc.P * kFusedUnits : 0) + (dacc.prop_lds ? dacc.P * kFusedUnits : 0);

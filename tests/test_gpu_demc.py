@@ -160,8 +160,7 @@ def test_device_demcz_step_modes_bitwise(jac, per_well):
     steps per launch, each block running its chains through them), one step per launch
     (NGRTD_DZ_CHUNK=1), chunks of 3 (launch boundaries between the tune steps and across
     stop_tuning's history drop at step 8) and the proposal kernel + log-prob kernel pair
-    (NGRTD_DZ_MODE=pair), and per-well chains with pairwise waits instead of the step's
-    block barriers (NGRTD_DZ_PAIRSYNC=1)."""
+    (NGRTD_DZ_MODE=pair)."""
     import dataclasses
     import os
     import torch
@@ -175,18 +174,16 @@ def test_device_demcz_step_modes_bitwise(jac, per_well):
     x0 = torch.from_numpy(wl.sample_prior(spec, W, np.random.default_rng(15))).cuda()
     lp = LogProb(spec, max_walkers=W)
     res = {}
-    modes = {"fused": ("fused", "256", "0"), "pair": ("pair", "256", "0"), "chunk1": ("fused", "1", "0"),
-             "chunk3": ("fused", "3", "0"), "pairsync": ("fused", "256", "1"), "pairsync3": ("fused", "3", "1")}
+    modes = {"fused": ("fused", "256"), "pair": ("pair", "256"), "chunk1": ("fused", "1"), "chunk3": ("fused", "3")}
     try:
-        for mode, (m, ch, ps) in modes.items():
+        for mode, (m, ch) in modes.items():
             os.environ["NGRTD_DZ_MODE"] = m
             os.environ["NGRTD_DZ_CHUNK"] = ch
-            os.environ["NGRTD_DZ_PAIRSYNC"] = ps
             res[mode] = DeviceDEMetropolisZ(lp, tune_interval=4, seed=99, per_well=per_well).run(x0, tune=8, draws=6)
     finally:
-        for k in ("NGRTD_DZ_MODE", "NGRTD_DZ_CHUNK", "NGRTD_DZ_PAIRSYNC"):
+        for k in ("NGRTD_DZ_MODE", "NGRTD_DZ_CHUNK"):
             os.environ.pop(k, None)
-    for mode in ("pair", "chunk1", "chunk3", "pairsync", "pairsync3"):
+    for mode in ("pair", "chunk1", "chunk3"):
         for k in ("x", "lp", "samples", "logp", "accepted", "accept", "lamb", "scaling"):
             assert _same(res[mode][k], res["fused"][k]), (mode, k)
     if jac:
