@@ -25,9 +25,11 @@
 namespace ngrtd {
 
 constexpr int kDzcMaxP = 8;        // parameter rows of a lane-chain step
-// threads per block: the EPM instances hold the whole channel table in LDS (57 KB at N = 1200)
-// and take 1024-lane blocks (one per CU, 4 waves per SIMD); the others 512 (two per CU)
-__host__ __device__ constexpr int dzc_threads(int mix) { return (mix & 2) ? 1024 : 512; }
+// threads per block: 512, so that the c4 shape's 2048 x 64 chains fill all 256 CUs with one
+// block each (2 waves per SIMD; 1024-lane EPM blocks left half the CUs idle: 32.0 us per step,
+// profiles/r04i_bench.json) -- and each lane may hold up to 256 VGPRs (the chain's state, the
+// next step's partner rows and the log-prob body without spills; 128 spilled up to 46)
+__host__ __device__ constexpr int dzc_threads(int) { return 512; }
 // LDS doubles: the surrogate window, the EPM table, the per-well data, the proposal rows
 __host__ __device__ constexpr size_t dzc_lds_doubles(int C, int mix, int cheb_np, int N, int wd_n, int P) {
     return (size_t)cheb_np * cheb_lds_stride(C) + ((mix & 2) ? (size_t)epm_lds_doubles(N, cheb_cp(C)) : 0) +
@@ -178,7 +180,7 @@ constexpr size_t kDzcArgD = ka_align(kDzcArgU + sizeof(UnitArgs), alignof(DemcAc
 // dacc.x / dacc.xu the natural / transformed rows ([P][W][L], walker-major), the per-chain
 // lp / lamb / scaling / tuning counters [W][L]; logs [n_steps][L][W].
 template <int C, int MIX>
-__global__ void __launch_bounds__(dzc_threads(MIX), 4)
+__global__ void __launch_bounds__(dzc_threads(MIX), 2)
     dz_chain_kernel(const RtdArgs ak, const UnitArgs ua, const DemcAccept dacc) {
     constexpr int NT = dzc_threads(MIX);
     constexpr bool EPM = (MIX & 2) != 0, TR = (MIX & 4) != 0, LW = (MIX & 32) != 0, CEO = (MIX & 64) != 0;
@@ -229,24 +231,35 @@ __global__ void __launch_bounds__(dzc_threads(MIX), 4)
     int32_t nat = dacc.n_acc_tune ? dacc.n_acc_tune[gv] : 0;
     unsigned long long nacc = 0;
     const int nst = dacc.n_steps;
-    for (int js = 0; js < nst; ++js) {
-        const RtdArgs& a = kernarg_opaque<RtdArgs>(0);
-        const UnitArgs& uk = kernarg_opaque<UnitArgs>(kDzcArgU);
-        const DemcAccept& d = kernarg_opaque<DemcAccept>(kDzcArgD);
-        const DzStep sj = dz_step(d.sch, js);
-        // partners (keyed by the walker, each well reading its own history rows)
-        int64_t e1, e2;
-        dz_partners(d, sj, w, e1, e2);
-        const bool de = e1 >= 0;
+    // Step j's partner entries (keyed by the walker, each well reading its own history rows) and
+    // their rows, loaded one step ahead: step j + 1's loads are issued right after step j's
+    // proposal, so they land during its log-prob.  Every entry they read was appended by this
+    // lane earlier in program order, except step j + 1's own append (the state after step j's
+    // decision), which the c1 / c2 substitution below takes from the registers.
+    int64_t e1 = -1, e2 = -1;
+    double a1[kDzcMaxP], a2[kDzcMaxP];
+    auto partner_rows = [&](const DemcAccept& d, int j) {
+        const bool on = j < nst;
+        const DzStep sp = dz_step(d.sch, on ? j : 0);
+        dz_partners(d, sp, w, e1, e2);
+        const bool de = on && e1 >= 0;
         const int64_t R = (int64_t)P * L;
         const double* z1 = d.hist + ((size_t)(de ? e1 : 0) * W + w) * R + l;
         const double* z2 = d.hist + ((size_t)(de ? e2 : 0) * W + w) * R + l;
-        double a1[kDzcMaxP], a2[kDzcMaxP];
 #pragma unroll
         for (int p = 0; p < kDzcMaxP; ++p) {
             a1[p] = (de && p < P) ? z1[(int64_t)p * L] : 0.0;
             a2[p] = (de && p < P) ? z2[(int64_t)p * L] : 0.0;
         }
+    };
+    partner_rows(dacc, 0);
+    for (int js = 0; js < nst; ++js) {
+        const RtdArgs& a = kernarg_opaque<RtdArgs>(0);
+        const UnitArgs& uk = kernarg_opaque<UnitArgs>(kDzcArgU);
+        const DemcAccept& d = kernarg_opaque<DemcAccept>(kDzcArgD);
+        const DzStep sj = dz_step(d.sch, js);
+        const bool de = e1 >= 0;
+        const int64_t R = (int64_t)P * L;
         // the state becomes history entry sj.at (chains' space)
         if (valid && sj.at >= 0) {
             double* hrow = d.hist + ((size_t)sj.at * W + w) * R + l;
@@ -268,6 +281,7 @@ __global__ void __launch_bounds__(dzc_threads(MIX), 4)
                 v[p] = 0.0;
             }
         }
+        partner_rows(d, js + 1);                          // the next step's partners (in flight from here)
         // the proposal's log-prob: the log-prob kernels' functions over the LDS rows
         RtdArgs ar = a;
         ar.theta = props;
