@@ -540,18 +540,24 @@ __device__ __forceinline__ double beta_block(const UnitArgs& a, int64_t u, const
             if (FB(i) != 0.0) lsum += FB(i) * flog_z(1 - x);
         }
     }
-    double lint;
-    if (pint >= 1e-280) {
-        lint = flog_pn(pint);   // (a normal number: <= 1 in bounds; out of bounds the sum is -inf)
-    } else {
-        lint = 0.0;
+    // (a normal number: <= 1 in bounds; out of bounds the sum is -inf).  The term-by-term
+    // fallback sits behind a wave-uniform branch: as a per-lane branch the compiler evaluated
+    // its logs in every lane (9 full logs per unit with the compile-time exponents).  A lane
+    // out of bounds needs no fallback (its sum is -inf): in the natural-space sampler a
+    // proposal past a Beta variable's [0, 1] made the product negative and sent the wave
+    // through it.
+    double lint = flog_pn(pint);
+    const bool small = inb && !(pint >= 1e-280);
+    if (__builtin_expect(__any(small), 0)) {
+        double lt = 0.0;
 #pragma unroll
         for (int i = 0; i < kMaxBeta; ++i) {
             if (i < n) {
-                if (IA(i)) lint += (double)IA(i) * flog(xs[i]);
-                if (IB(i)) lint += (double)IB(i) * flog(1 - xs[i]);
+                if (IA(i)) lt += (double)IA(i) * flog(xs[i]);
+                if (IB(i)) lt += (double)IB(i) * flog(1 - xs[i]);
             }
         }
+        lint = small ? lt : lint;
     }
     return inb ? (lint + lsum) - a.bt_betaln : kNegInf;
 }
@@ -1990,10 +1996,11 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
     // predicate is evaluated exactly -- in waves holding a lane near those cases only.
     if (nan_out) {
         const double tpf = f == 0 ? a.tp0 : (double)f + a.dtp;
-        const double xf = -(eta * tpf / tau) + eta - 1;
-        const bool susp = f >= N || !(beta > 0.0 && beta <= 1.7976931348623157e308) || !(xf > -700.0);
+        // (the screen without a division; the check itself in the reference's operation order)
+        const bool susp = f >= N || !(beta > 0.0 && beta <= 1.7976931348623157e308) || !(fma(-beta, tpf, eta - 1) > -700.0);
         bool wn = false;
         if (__any(susp) && susp) {
+            const double xf = -(eta * tpf / tau) + eta - 1;
             const double tpl = N > 1 ? (double)(N - 1) + a.dtp : a.tp0;
             const double xl = -(eta * tpl / tau) + eta - 1;
             const double ce = eta / tau;

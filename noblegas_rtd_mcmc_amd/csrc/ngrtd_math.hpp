@@ -339,10 +339,13 @@ NGRTD_HD double st_block_inu(int n, const double* obs, const double* mu, const d
     double c0;
     double cx;
     const int cp = c0t.t ? c0_piece(nu, c0t.e0, c0t.np, cx) : -1;
-    if (cp >= 0)
-        c0 = c0_poly(c0t.t + cp * kC0N, cx);
-    else
-        c0 = st_c0_exact(nu, inu);
+    c0 = c0t.t ? c0_poly(c0t.t + (cp >= 0 ? cp : 0) * kC0N, cx) : 0.0;
+#if defined(__HIP_DEVICE_COMPILE__)
+    // the exact normaliser behind a wave-uniform branch (nu outside the table: a proposal past
+    // its prior's support), so that waves without such a lane never evaluate it
+    if (__any(cp < 0))
+#endif
+        if (cp < 0) c0 = st_c0_exact(nu, inu);
     // unrolled over NMAX constant slots (slots j >= n masked; their loads clamp to n - 1)
     double prod = 1.0;
     bool big = false, ok = nu > 0;
