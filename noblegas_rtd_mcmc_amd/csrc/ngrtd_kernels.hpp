@@ -604,12 +604,12 @@ __device__ __forceinline__ double unit_logp_theta(const UnitArgs& a, int64_t u, 
         const double tau1 = pre ? pre->tau1 : a.theta[(int64_t)a.row_tau1 * a.U + u];
         if (want_prior) {
             lp += uniform_logp(tau1, a.tau1_lo, a.tau1_hi, a.tau1_nlw);
-            if (jac) lp += jac_interval(tau1, a.tau1_lo, a.tau1_hi);
+            if (jac) lp += jac_interval(tau1, a.tau1_lo, a.tau1_hi, a.tau1_nlw);
 #define NGRTD_UNIF(row, lo, hi, nlw)                                                   \
     if (a.row >= 0) {                                                                  \
         const double x = a.theta[(int64_t)a.row * a.U + u];                            \
         lp += uniform_logp(x, a.lo, a.hi, a.nlw);                                      \
-        if (jac) lp += jac_interval(x, a.lo, a.hi);                                    \
+        if (jac) lp += jac_interval(x, a.lo, a.hi, a.nlw);                             \
     }
             NGRTD_UNIF(row_tau2, tau2_lo, tau2_hi, tau2_nlw)
             NGRTD_UNIF(row_f1, f1_lo, f1_hi, f1_nlw)
@@ -622,7 +622,7 @@ __device__ __forceinline__ double unit_logp_theta(const UnitArgs& a, int64_t u, 
             if (a.row_lamsf6 >= 0) {
                 const double x = a.theta[(int64_t)a.row_lamsf6 * a.U + u];
                 lp += halfnormal_logp(x, a.ls_tau, a.ls_half_log);
-                if (jac) lp += log(x);
+                if (jac) lp += flog(x);
             }
         }
     }
@@ -879,7 +879,7 @@ __device__ __forceinline__ void unit_conc(const RtdArgs& a, int64_t u, const dou
     double Jw = 0.0;
     if (a.row_J >= 0) {
         const double jv = a.theta[(int64_t)a.row_J * a.U + u];
-        Jw = a.J_is_log10 ? exp10(jv) : jv;
+        Jw = a.J_is_log10 ? fexp10(jv) : jv;   // (<= 0.51 ulp: the J of 4He accumulation, 10**J)
     }
     // ST (dz_chain_kernel, whose theta view is a modified local copy of a): t < C -- every tracer
     // owns at least one channel, K <= C -- unrolled with compile-time tracer indices, so that
@@ -2393,6 +2393,12 @@ __host__ __device__ constexpr int cheb_lds_stride(int C) { return kChebN * cheb_
 // into the state (and, transformed, recompute and write the chains'-space value).  Per
 // step: 3 reads + 2 writes of the state's size in HBM, against 6 reads + 3 writes (+ the
 // accepted copies) for the proposal kernel + log-prob kernel pair.
+// the reference's Beta priors compiled into the DEMetropolisZ instances too (A/B builds:
+// 4-16 VGPRs spill in their step loop)
+#ifndef NGRTD_DZ_REFB
+#define NGRTD_DZ_REFB 0
+#endif
+constexpr bool kDzRefB = NGRTD_DZ_REFB != 0;
 template <int C, bool FULL, int ROLES, int MIX>
 __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(const RtdArgs ak, const UnitArgs ua,
                                                                               int32_t WB, double* __restrict__ logp,
@@ -2401,9 +2407,9 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     constexpr bool PW = DZ && (MIX & 16) != 0;   // per-well chains: one Metropolis decision per unit
     constexpr bool LW = (MIX & 32) != 0;         // the sampled CFC12 half-life (channel 0, lw_decay)
     // FULL: the reference's Beta priors as compile-time exponents (kRefBeta: bare / with the
-    // Jacobians, without / with thalf_cfc) -- not in the DEMetropolisZ steps, where the folded
-    // code spilled 17-37 VGPRs inside the step loop; their runtime loop gives the same bits
-    constexpr int REFB = (FULL && !DZ) ? 1 + ((MIX & 4) ? 1 : 0) + (LW ? 2 : 0) : 0;
+    // Jacobians, without / with thalf_cfc) -- not in the DEMetropolisZ steps (kDzRefB), where the
+    // folded code spilled VGPRs inside the step loop; their runtime loop gives the same bits
+    constexpr int REFB = (FULL && (!DZ || kDzRefB)) ? 1 + ((MIX & 4) ? 1 : 0) + (LW ? 2 : 0) : 0;
     static_assert(!DZ || (FULL && ROLES == 2), "the DEMetropolisZ step runs in the FULL role-split kernel");
     static_assert(kFusedUnitsDz == kFusedUnits, "DZ staging stride");
     const RtdArgs& a = ak;

@@ -400,6 +400,9 @@ NGRTD_HD double halfnormal_logp(double x, double tau, double half_log_tau_2_pi) 
 }
 // PyMC3 default transforms' log|Jacobian| (logodds / interval / log)
 NGRTD_HD double jac_logodds(double x) { return log(x) + log1p(-x); }
-NGRTD_HD double jac_interval(double x, double a, double b) { return log(x - a) + log(b - x) - log(b - a); }
+// The Interval transform's log-Jacobian log(x - a) + log(b - x) - log(b - a) as ONE table log of
+// the product (<= ((b - a) / 2)^2, no overflow; x = a or b gives -inf as the sum does) plus
+// nlw = -log(b - a) from the plan (three OCML logs before: ~1.1 us per c4 launch).
+NGRTD_HD double jac_interval(double x, double a, double b, double nlw) { return flog((x - a) * (b - x)) + nlw; }
 
 }  // namespace ngrtd
