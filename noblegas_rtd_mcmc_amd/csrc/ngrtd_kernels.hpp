@@ -2393,10 +2393,11 @@ __host__ __device__ constexpr int cheb_lds_stride(int C) { return kChebN * cheb_
 // into the state (and, transformed, recompute and write the chains'-space value).  Per
 // step: 3 reads + 2 writes of the state's size in HBM, against 6 reads + 3 writes (+ the
 // accepted copies) for the proposal kernel + log-prob kernel pair.
-// the reference's Beta priors compiled into the DEMetropolisZ instances too (A/B builds:
-// 4-16 VGPRs spill in their step loop)
+// the reference's Beta priors compiled into the DEMetropolisZ instances too: 4-16 VGPRs spill
+// in their step loop, yet the c4 per-well step runs 20.7 -> 18.7 us transformed and 18.7 ->
+// 16.7 us natural (profiles/r04m_dz_refb_ab.jsonl; NGRTD_DZ_REFB=0 builds the runtime loop)
 #ifndef NGRTD_DZ_REFB
-#define NGRTD_DZ_REFB 0
+#define NGRTD_DZ_REFB 1
 #endif
 constexpr bool kDzRefB = NGRTD_DZ_REFB != 0;
 template <int C, bool FULL, int ROLES, int MIX>
@@ -2407,8 +2408,8 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     constexpr bool PW = DZ && (MIX & 16) != 0;   // per-well chains: one Metropolis decision per unit
     constexpr bool LW = (MIX & 32) != 0;         // the sampled CFC12 half-life (channel 0, lw_decay)
     // FULL: the reference's Beta priors as compile-time exponents (kRefBeta: bare / with the
-    // Jacobians, without / with thalf_cfc) -- not in the DEMetropolisZ steps (kDzRefB), where the
-    // folded code spilled VGPRs inside the step loop; their runtime loop gives the same bits
+    // Jacobians, without / with thalf_cfc), in the DEMetropolisZ steps too (kDzRefB); the
+    // runtime loop gives the same bits
     constexpr int REFB = (FULL && (!DZ || kDzRefB)) ? 1 + ((MIX & 4) ? 1 : 0) + (LW ? 2 : 0) : 0;
     static_assert(!DZ || (FULL && ROLES == 2), "the DEMetropolisZ step runs in the FULL role-split kernel");
     static_assert(kFusedUnitsDz == kFusedUnits, "DZ staging stride");
