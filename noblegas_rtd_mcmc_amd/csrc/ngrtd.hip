@@ -1560,6 +1560,9 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
             a.chan_lamw[c] = p->table.chan_lamw[c];
         }
         for (int t = 0; t < K; ++t) { a.tr_sf6[t] = d->tracers[t].is_sf6; a.tr_J[t] = d->tracers[t].J; }
+        a.conc_ident = p->table.C == K ? 1 : 0;
+        for (int c = 0; c < p->table.C; ++c)
+            if (a.chan_tracer[c] != c) a.conc_ident = 0;
         a.conc = p->conc.d();
         set_frag(a, p->table);
         a.cheb = nullptr;

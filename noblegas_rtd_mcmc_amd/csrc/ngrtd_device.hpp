@@ -51,6 +51,8 @@ struct RtdArgs {
     // dispersion components of the generic single-launch instances (gen_exact): per age k,
     // 1 / tp_k at [k] and tp_k^(-3/2) at [N + k]; null when the plan has no dispersion component
     const double* disp_aux;
+    // 1: K = C and tracer t owns exactly channel t (unit_conc's direct path)
+    int32_t conc_ident;
 };
 
 // exp_pist_flow (convolution_integral_utils.py:186-190) on the yearly grid: the unmasked

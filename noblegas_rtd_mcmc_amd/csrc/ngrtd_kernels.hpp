@@ -912,6 +912,29 @@ __device__ __forceinline__ void unit_conc(const RtdArgs& a, int64_t u, const dou
         for (int t = 0; t < C; ++t)
             if (t < a.K) tracer(t);
     } else {
+        if (a.conc_ident) {
+            // tracer t owns exactly channel t (the plan's table order; K = C): no channel search,
+            // the same expressions as tracer(t) with one channel (the SF6 factor as a select:
+            // x * 1.0 is x, so the bits are the branch's)
+            const double sf = (a.row_lamsf6 >= 0) ? 1 + a.theta[(int64_t)a.row_lamsf6 * a.U + u] : 1.0;
+#pragma unroll
+            for (int t = 0; t < C; ++t) {
+                const bool isB = a.chan_isB[t] != 0;
+                const double J = (a.row_J >= 0) ? Jw : a.tr_J[t];
+                const double sA = isB ? 0.0 : num[t], sB = isB ? num[t] : 0.0;
+                const double cc = isB ? (sA + J * sB) * rden : sA * rden;
+                double cout;
+                if (num2) {
+                    const double sA2 = isB ? 0.0 : num2[t], sB2 = isB ? num2[t] : 0.0;
+                    const double cc2 = (isB ? (sA2 + J * sB2) : sA2) * rden2;
+                    cout = fmix * cc + (1 - fmix) * cc2;
+                } else {
+                    cout = fmix * cc + 0.0 * 0.0;
+                }
+                conc[t] = cout * (a.tr_sf6[t] ? sf : 1.0);
+            }
+            return;
+        }
         for (int t = 0; t < a.K; ++t) tracer(t);
     }
 }
@@ -1145,8 +1168,9 @@ __device__ __forceinline__ void count_accepts(unsigned long long* n, bool acc) {
 // (flog: table-driven, <= 1 ulp; the torch restatement takes the same function through
 // ngrtd_fm_log, so the chains stay bitwise equal.  Every kernel that decides runs
 // fm_lds_init() and a barrier first.)
+// (rng_unit lies in [2^-54, 1 - 2^-54]: flog_pn gives flog's bits there)
 __device__ __forceinline__ double demc_logu(uint64_t key, uint64_t rid) {
-    return flog(rng_unit(rng_mix(rng_mix(key + 3) + rid)));
+    return flog_pn(rng_unit(rng_mix(rng_mix(key + 3) + rid)));
 }
 template <class F64P, class I32P>
 __device__ __forceinline__ bool demc_decide_at_u(const DemcAccept& d, F64P lpa, F64P lamb, F64P scal, I32P nat,
