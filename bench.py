@@ -580,7 +580,13 @@ def model_lines(args, gpu):
              "published": (m1, m2, sv) in PUBLISHED_MODELS}
         if sv and base_ms.get((m1, m2)):
             e["vs_savenum0_kernel"] = ms / base_ms[(m1, m2)]
-        if pmc.get("fp64_flop_per_unit") and inst in (pmc_path or ""):
+        if inst.endswith(", 64>") or inst.endswith(", 96>"):
+            # the generic instance runs several models (piston, dispersion, BMM pairs): a PMC
+            # summary keyed by kernel instance cannot say which model it counted, so no FLOP rate
+            e["roofline"] = None
+            e["roofline_note"] = "generic instance shared by %d model pairs; PMC counts are per instance, not per model" % (
+                sum(1 for mm in OTHER_MODELS if fused_instance(*mm) == inst))
+        elif pmc.get("fp64_flop_per_unit") and inst in (pmc_path or ""):
             fl = pmc["fp64_flop_per_unit"] * U
             e["roofline"] = {"bound": "fp64_valu", "achieved": fl / (ms * 1e-3) / 1e12, "peak": FP64_PEAK / 1e12,
                              "unit": "TFLOP/s", "frac": fl / (ms * 1e-3) / FP64_PEAK, "traffic": pmc.get("hbm_bytes_per_launch"),
