@@ -662,7 +662,10 @@ static void launch_mfma(const RtdArgs& a, const UnitArgs& u, int32_t fuse, hipSt
 static size_t fused_lds(const RtdArgs& a, const UnitArgs& u, int dz_p = 0) {
     // EPM: the channel table, rows of cheb_cp(C) doubles in LDS (the kernel's layout; the global
     // table's rows are a.CP = (C + 1) & ~1, shorter for C = 2, 4)
-    const size_t epm_tab = (a.mod[0] == MOD_EPM || a.mod[1] == MOD_EPM) ? (size_t)epm_lds_doubles(a.N, cheb_cp(a.C)) : 0;
+    // generic instances with a dispersion component: the same table, and disp_aux [2N]
+    const bool disp = a.disp_aux && (a.mod[0] == MOD_DISP || a.mod[1] == MOD_DISP);
+    const size_t epm_tab = (a.mod[0] == MOD_EPM || a.mod[1] == MOD_EPM || disp)
+                               ? (size_t)epm_lds_doubles(a.N, cheb_cp(a.C)) + (disp ? 2 * (size_t)a.N : 0) : 0;
     const size_t dz = (size_t)dz_p * kFusedUnits;                          // DZ step: the proposals
     return (size_t)(kFusedHdr + a.cheb_np * cheb_lds_stride(a.C) + epm_tab + u.wd_n + dz) *
            sizeof(double);

@@ -2233,12 +2233,63 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
 // num_c = sum_k A_{c,k} w_k (the per-unit decayed channel, LW: w_k e^(-lam tp_k)), den = sum_k w_k,
 // so conc = num / den is the normalised g (:270) dotted with the series (:336-340).  Zero, inf and
 // NaN weights give the reference's NaN / inf concentrations (0 / 0, inf / inf).
+//
+// Dispersion plans stage the channel table (epm_row layout) and disp_aux in LDS (tl, dl non-null):
+// the dispersion loop then reads its per-age operands from LDS, unrolled by 4 so that four ages'
+// reads are in flight at once (the global loads of the generic loop waited once per age: ~530 us
+// per c4 launch).  Same expressions in the same order: the same bits as the generic loop.
+#ifndef NGRTD_GEN_DISP_UNROLL
+#define NGRTD_GEN_DISP_UNROLL 4
+#endif
+constexpr int kGenDispUnroll = NGRTD_GEN_DISP_UNROLL;
 template <int C, bool LW>
 __device__ __forceinline__ void gen_exact(const RtdArgs& a, int mod, bool on, double tau, double eta, double D,
-                                          double lam, double* num, double& den) {
+                                          double lam, double* num, double& den, const double* tl = nullptr,
+                                          const double* dl = nullptr) {
     double s[C + 1];
 #pragma unroll
     for (int c = 0; c <= C; ++c) s[c] = 0.0;
+    if (mod == MOD_DISP && tl && dl) {
+        if (__any(on)) {
+            constexpr int CP = cheb_cp(C);
+            const double rt = 1.0 / tau;
+            const double k1 = sqrt(tau / (4. * kPi * D));
+            const double k2 = 1.0 / (4. * D);
+            const int N = a.N;
+            // one age: its weight (the generic loop's expressions) into the sums, in age order
+            auto age = [&](int k, double ia, double ip, const double* row) {
+                const double tp = (k == 0) ? a.tp0 : ((double)k + a.dtp);
+                const double d = 1.0 - tp * rt;
+                const double w = (k1 * ip) * fexp(-((d * d) * (tau * ia)) * k2);
+                const double wd = LW ? w * fexp(-lam * tp) : w;
+#pragma unroll
+                for (int c = 0; c < C; ++c) s[c] = fma(row[c], (LW && a.chan_lamw[c]) ? wd : w, s[c]);
+                s[C] += w;
+            };
+            constexpr int UA = kGenDispUnroll;
+            int k = 0;
+            for (; k + UA <= N; k += UA) {                 // UA ages' LDS operands first, then their sums
+                double ia[UA], ip[UA], row[UA][C];
+#pragma unroll
+                for (int j = 0; j < UA; ++j) {
+                    ia[j] = dl[k + j];
+                    ip[j] = dl[N + k + j];
+                    epm_row_load<C>(tl + epm_row(k + j, CP), row[j]);
+                }
+#pragma unroll
+                for (int j = 0; j < UA; ++j) age(k + j, ia[j], ip[j], row[j]);
+            }
+            for (; k < N; ++k) {
+                double row[C];
+                epm_row_load<C>(tl + epm_row(k, CP), row);
+                age(k, dl[k], dl[N + k], row);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < C; ++c) num[c] = s[c];
+        den = s[C];
+        return;
+    }
     if (__any(on)) {
         const double rt = 1.0 / tau;
         double k1, k2 = 0.0, thr = 0.0;
@@ -2283,7 +2334,8 @@ __device__ __forceinline__ void gen_exact(const RtdArgs& a, int mod, bool on, do
 template <int C, bool ROLES2, bool LW>
 __device__ __forceinline__ void gen_component(const RtdArgs& a, const UnitArgs& uk, const double* cheb,
                                               const double* tabl, int comp, bool mvalid, int64_t mu, bool prior_on,
-                                              double tau, double thx, double* num, double& rden, bool& nanc) {
+                                              double tau, double thx, double* num, double& rden, bool& nanc,
+                                              const double* daux = nullptr) {
     constexpr int CP = cheb_cp(C), PST = kChebN * CP + 2;   // = cheb_lds_stride(C)
     const int mod = a.mod[comp];
     const double eta = (mod == MOD_EPM && mvalid) ? a.theta[(int64_t)a.row_eta[comp] * a.U + mu] : 1.0;
@@ -2341,7 +2393,7 @@ __device__ __forceinline__ void gen_component(const RtdArgs& a, const UnitArgs& 
     }
     if (__any(ex)) {
         double en[C], den;
-        gen_exact<C, LW>(a, mod, ex, tau, eta, D, lw.lam, en, den);
+        gen_exact<C, LW>(a, mod, ex, tau, eta, D, lw.lam, en, den, daux ? tabl : nullptr, daux);
         if (ex) {
 #pragma unroll
             for (int c = 0; c < C; ++c) num[c] = en[c];
@@ -2488,9 +2540,12 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     constexpr bool GEN = (MIX & 64) != 0;        // generic components (gen_component)
     static_assert(!GEN || (MIX & (1 | 2 | 8 | 16)) == 0, "generic instances: plain log-prob, runtime models");
     // the channel table staged in LDS: exp_pist_flow components (epm_sums)
-    const bool EPMS = EPM || (GEN && (a.mod[0] == MOD_EPM || a.mod[1] == MOD_EPM));
+    // ... and dispersion components (gen_exact's LDS loop), with their per-age disp_aux
+    const bool DISPS = GEN && a.disp_aux && (a.mod[0] == MOD_DISP || a.mod[1] == MOD_DISP);
+    const bool EPMS = EPM || (GEN && (a.mod[0] == MOD_EPM || a.mod[1] == MOD_EPM)) || DISPS;
     double* tabl = cheb + a.cheb_np * PST;                // EPM: the channel table (epm_row)
-    double* wd = tabl + (EPMS ? epm_lds_doubles(a.N, CP) : 0);
+    double* daux = tabl + (EPMS ? epm_lds_doubles(a.N, CP) : 0);   // DISPS: disp_aux [2N]
+    double* wd = daux + (DISPS ? 2 * a.N : 0);
     constexpr int kWdRegs = (4 * 64 * kFusedWaves + NTH - 1) / NTH;
     double wv[kWdRegs];
 #pragma unroll
@@ -2530,6 +2585,8 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             }
         }
     }
+    if (DISPS)
+        for (int i = tid; i < 2 * a.N; i += NTH) daux[i] = a.disp_aux[i];
 #pragma unroll
     for (int r = 0; r < kWdRegs; ++r) {
         const int i = tid + r * NTH;
@@ -2611,7 +2668,8 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         // zero partial sums land on no walker's slots
         const int pi = (DZ && mwl >= WB) ? mi : ml * WB + mwl;
         double* tabl = cheb + a.cheb_np * PST;
-        double* wd = tabl + (EPMS ? epm_lds_doubles(a.N, CP) : 0);
+        double* daux = tabl + (EPMS ? epm_lds_doubles(a.N, CP) : 0);
+        double* wd = daux + (DISPS ? 2 * a.N : 0);
         double* thl = wd + uk.wd_n;
         double* propl = thl + (((MIX & 4) && DZ) ? dk.P * kFusedUnits : 0);   // DZ: [P][512] proposals
         DzLds dl;                                         // DZ: the chains' LDS state (or none)
@@ -2698,11 +2756,12 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             double conc[kMaxTracer];
             double n1[C], r1, n2[C], r2 = 1.0;
             bool nan1, nan2 = false;
-            gen_component<C, ROLES == 2, LW>(a, uk, cheb, tabl, 0, mvalid, mu, prior_on, tau, thx, n1, r1, nan1);
+            const double* dxl = DISPS ? daux : nullptr;
+            gen_component<C, ROLES == 2, LW>(a, uk, cheb, tabl, 0, mvalid, mu, prior_on, tau, thx, n1, r1, nan1, dxl);
             const bool two = a.mod[1] != MOD_NONE;
             if (two) {
                 const double t2 = mvalid ? a.theta[(int64_t)a.row_tau[1] * a.U + mu] : 1.0;
-                gen_component<C, ROLES == 2, LW>(a, uk, cheb, tabl, 1, mvalid, mu, prior_on, t2, thx, n2, r2, nan2);
+                gen_component<C, ROLES == 2, LW>(a, uk, cheb, tabl, 1, mvalid, mu, prior_on, t2, thx, n2, r2, nan2, dxl);
             }
             unit_conc<C>(a, mu, n1, r1, conc, two ? n2 : nullptr, r2);
             if (nan1 || nan2)
