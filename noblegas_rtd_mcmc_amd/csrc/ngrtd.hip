@@ -667,7 +667,9 @@ static size_t fused_lds(const RtdArgs& a, const UnitArgs& u, int dz_p = 0) {
     const size_t epm_tab = (a.mod[0] == MOD_EPM || a.mod[1] == MOD_EPM || disp)
                                ? (size_t)epm_lds_doubles(a.N, cheb_cp(a.C)) + (disp ? 2 * (size_t)a.N : 0) : 0;
     const size_t dz = (size_t)dz_p * kFusedUnits;                          // DZ step: the proposals
-    return (size_t)(kFusedHdr + a.cheb_np * cheb_lds_stride(a.C) + epm_tab + u.wd_n + dz) *
+    // generic instances, dispersion split over the unit's two waves: the theta waves' partial sums
+    const size_t xch = (disp && a.disp_split > 0) ? (size_t)(a.C + 1) * kFusedUnits : 0;
+    return (size_t)(kFusedHdr + a.cheb_np * cheb_lds_stride(a.C) + epm_tab + u.wd_n + dz + xch) *
            sizeof(double);
 }
 // Surrogate pieces the fused kernel stages: when the unit's log-prob carries the tau1
@@ -773,6 +775,16 @@ static void gen_cheb_window(RtdArgs& a, const UnitArgs& u) {
     a.cheb_p0 = pa;
     a.cheb_np = pb - pa + 1;
 }
+// The dispersion component's age split between the unit's theta and RTD waves (the kernel's GEN
+// branch): half the ages each, when the theta waves' partial sums fit the LDS budget (else the
+// RTD wave sums all ages).  NGRTD_NO_DISP_SPLIT=1 disables it (A/B runs).
+static void gen_disp_split(RtdArgs& a, const UnitArgs& u) {
+    static const bool off = std::getenv("NGRTD_NO_DISP_SPLIT") != nullptr;
+    a.disp_split = 0;
+    if (off || !a.disp_aux || !(a.mod[0] == MOD_DISP || a.mod[1] == MOD_DISP) || a.N < 2) return;
+    a.disp_split = a.N / 2;
+    if (fused_lds(a, u) > kFusedMaxLds) a.disp_split = 0;
+}
 static int gen_mix(const RtdArgs& a, const UnitArgs& u) {
     return 64 | (a.row_thalf >= 0 ? 32 : 0) | (full_plan(a, u) && (u.flags & NGRTD_WANT_JACOBIAN) ? 4 : 0);
 }
@@ -781,6 +793,7 @@ static bool gen_path(const RtdArgs& a0, const UnitArgs& u) {
     if (disabled || !gen_mods(a0) || fused_path(a0, u)) return false;
     RtdArgs a = a0;
     gen_cheb_window(a, u);
+    gen_disp_split(a, u);
     const bool exp_c = a.mod[0] == MOD_EXP || a.mod[1] == MOD_EXP;
     const bool epm_c = a.mod[0] == MOD_EPM || a.mod[1] == MOD_EPM;
     const bool disp_c = a.mod[0] == MOD_DISP || a.mod[1] == MOD_DISP;
@@ -939,6 +952,7 @@ static int launch_fused(ngrtd_ctx* ctx, const RtdArgs& a0, const UnitArgs& u, in
     const DemcAccept da = dap ? *dap : DemcAccept{};
     if (!fused_path(a0, u)) {   // the generic instances (gen_path)
         gen_cheb_window(a, u);
+        gen_disp_split(a, u);
         HIP_TRY(ctx, launch_fused_gen_instance(a.C, full_plan(a, u), gen_mix(a, u), a, u, WB, W, logp, da, fused_lds(a, u),
                                                kFusedMaxLds, st));
         return NGRTD_OK;

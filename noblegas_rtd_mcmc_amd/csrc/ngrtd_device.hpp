@@ -53,6 +53,9 @@ struct RtdArgs {
     const double* disp_aux;
     // 1: K = C and tracer t owns exactly channel t (unit_conc's direct path)
     int32_t conc_ident;
+    // generic instances with a dispersion component (ngrtd.hip gen_disp_split): its ages
+    // [0, disp_split) are summed by the unit's theta wave, [disp_split, N) by its RTD wave; 0: not split
+    int32_t disp_split;
 };
 
 // exp_pist_flow (convolution_integral_utils.py:186-190) on the yearly grid: the unmasked

@@ -2245,7 +2245,7 @@ constexpr int kGenDispUnroll = NGRTD_GEN_DISP_UNROLL;
 template <int C, bool LW>
 __device__ __forceinline__ void gen_exact(const RtdArgs& a, int mod, bool on, double tau, double eta, double D,
                                           double lam, double* num, double& den, const double* tl = nullptr,
-                                          const double* dl = nullptr) {
+                                          const double* dl = nullptr, int age0 = 0, int age1 = -1) {
     double s[C + 1];
 #pragma unroll
     for (int c = 0; c <= C; ++c) s[c] = 0.0;
@@ -2267,8 +2267,9 @@ __device__ __forceinline__ void gen_exact(const RtdArgs& a, int mod, bool on, do
                 s[C] += w;
             };
             constexpr int UA = kGenDispUnroll;
-            int k = 0;
-            for (; k + UA <= N; k += UA) {                 // UA ages' LDS operands first, then their sums
+            const int ke = age1 < 0 ? N : age1;             // ages [age0, ke)
+            int k = age0;
+            for (; k + UA <= ke; k += UA) {                 // UA ages' LDS operands first, then their sums
                 double ia[UA], ip[UA], row[UA][C];
 #pragma unroll
                 for (int j = 0; j < UA; ++j) {
@@ -2279,7 +2280,7 @@ __device__ __forceinline__ void gen_exact(const RtdArgs& a, int mod, bool on, do
 #pragma unroll
                 for (int j = 0; j < UA; ++j) age(k + j, ia[j], ip[j], row[j]);
             }
-            for (; k < N; ++k) {
+            for (; k < ke; ++k) {
                 double row[C];
                 epm_row_load<C>(tl + epm_row(k, CP), row);
                 age(k, dl[k], dl[N + k], row);
@@ -2335,7 +2336,7 @@ template <int C, bool ROLES2, bool LW>
 __device__ __forceinline__ void gen_component(const RtdArgs& a, const UnitArgs& uk, const double* cheb,
                                               const double* tabl, int comp, bool mvalid, int64_t mu, bool prior_on,
                                               double tau, double thx, double* num, double& rden, bool& nanc,
-                                              const double* daux = nullptr) {
+                                              const double* daux = nullptr, int split = 0) {
     constexpr int CP = cheb_cp(C), PST = kChebN * CP + 2;   // = cheb_lds_stride(C)
     const int mod = a.mod[comp];
     const double eta = (mod == MOD_EPM && mvalid) ? a.theta[(int64_t)a.row_eta[comp] * a.U + mu] : 1.0;
@@ -2393,11 +2394,13 @@ __device__ __forceinline__ void gen_component(const RtdArgs& a, const UnitArgs& 
     }
     if (__any(ex)) {
         double en[C], den;
-        gen_exact<C, LW>(a, mod, ex, tau, eta, D, lw.lam, en, den, daux ? tabl : nullptr, daux);
+        // split (dispersion, staged tables): this wave's ages [split, N); rden holds the raw
+        // normaliser sum until the caller adds the theta wave's [0, split)
+        gen_exact<C, LW>(a, mod, ex, tau, eta, D, lw.lam, en, den, daux ? tabl : nullptr, daux, split);
         if (ex) {
 #pragma unroll
             for (int c = 0; c < C; ++c) num[c] = en[c];
-            rden = 1.0 / den;
+            rden = split ? den : 1.0 / den;
         }
     }
 }
@@ -2750,19 +2753,59 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         // RTD waves without a unit (blocks of fewer walkers than kFusedUnits / L: fused_wb) skip
         // their body (wave-uniform)
         const bool rtd_w = do_rtd && (DZ || __any(mvalid));
-        if (GEN && rtd_w) {
-            // generic components: the first from tau (prologue), the second (BMM) from tau2
-            const bool prior_on = FULL || (uk.rtd_on && (uk.flags & NGRTD_WANT_PRIOR));
-            double conc[kMaxTracer];
-            double n1[C], r1, n2[C], r2 = 1.0;
-            bool nan1, nan2 = false;
-            const double* dxl = DISPS ? daux : nullptr;
-            gen_component<C, ROLES == 2, LW>(a, uk, cheb, tabl, 0, mvalid, mu, prior_on, tau, thx, n1, r1, nan1, dxl);
-            const bool two = a.mod[1] != MOD_NONE;
-            if (two) {
-                const double t2 = mvalid ? a.theta[(int64_t)a.row_tau[1] * a.U + mu] : 1.0;
-                gen_component<C, ROLES == 2, LW>(a, uk, cheb, tabl, 1, mvalid, mu, prior_on, t2, thx, n2, r2, nan2, dxl);
+        if (GEN) {
+            // generic components: the first from tau (prologue), the second (BMM) from tau2.
+            // A dispersion component's exact age sum is split over the unit's two waves
+            // (a.disp_split, ROLES = 2): the theta wave, done with its CE block early, sums ages
+            // [0, split) into LDS, the RTD wave [split, N), and the RTD wave adds the two after a
+            // barrier (block-uniform: every wave reaches it)
+            const int dsp = (DISPS && ROLES == 2) ? a.disp_split : 0;
+            const int dcomp = a.mod[0] == MOD_DISP ? 0 : 1;
+            double* xch = wd + uk.wd_n;                       // [C + 1][kFusedUnits]
+            if (dsp && do_theta) {
+                double pn[C], pd;
+                const double tc = mvalid ? a.theta[(int64_t)a.row_tau[dcomp] * a.U + mu] : 1.0;
+                const double Dc = mvalid ? a.theta[(int64_t)a.row_D[dcomp] * a.U + mu] : 1.0;
+                double lam = 0.0;
+                if (LW) lam = lw_decay(a, tc, mvalid ? a.theta[(int64_t)a.row_thalf * a.U + mu] : 0.5).lam;
+                gen_exact<C, LW>(a, MOD_DISP, mvalid, tc, 1.0, Dc, lam, pn, pd, tabl, daux, 0, dsp);
+#pragma unroll
+                for (int c = 0; c < C; ++c) xch[c * kFusedUnits + mi] = pn[c];
+                xch[C * kFusedUnits + mi] = pd;
             }
+            const bool prior_on = FULL || (uk.rtd_on && (uk.flags & NGRTD_WANT_PRIOR));
+            double n1[C], r1 = 1.0, n2[C], r2 = 1.0;
+#pragma unroll
+            for (int c = 0; c < C; ++c) n1[c] = n2[c] = 0.0;
+            bool nan1 = false, nan2 = false;
+            const bool two = a.mod[1] != MOD_NONE;
+            const double* dxl = DISPS ? daux : nullptr;
+            if (rtd_w) {
+                gen_component<C, ROLES == 2, LW>(a, uk, cheb, tabl, 0, mvalid, mu, prior_on, tau, thx, n1, r1, nan1, dxl,
+                                                 dcomp == 0 ? dsp : 0);
+                if (two) {
+                    const double t2 = mvalid ? a.theta[(int64_t)a.row_tau[1] * a.U + mu] : 1.0;
+                    gen_component<C, ROLES == 2, LW>(a, uk, cheb, tabl, 1, mvalid, mu, prior_on, t2, thx, n2, r2, nan2,
+                                                     dxl, dcomp == 1 ? dsp : 0);
+                }
+            }
+            if (dsp) {
+                __syncthreads();
+                if (rtd_w) {   // the split component: theta's ages [0, split) + this wave's [split, N)
+                    const double pd = xch[C * kFusedUnits + mi];
+                    if (dcomp == 0) {
+#pragma unroll
+                        for (int c = 0; c < C; ++c) n1[c] = xch[c * kFusedUnits + mi] + n1[c];
+                        r1 = 1.0 / (pd + r1);
+                    } else {
+#pragma unroll
+                        for (int c = 0; c < C; ++c) n2[c] = xch[c * kFusedUnits + mi] + n2[c];
+                        r2 = 1.0 / (pd + r2);
+                    }
+                }
+            }
+          if (rtd_w) {
+            double conc[kMaxTracer];
             unit_conc<C>(a, mu, n1, r1, conc, two ? n2 : nullptr, r2);
             if (nan1 || nan2)
                 for (int t = 0; t < a.K; ++t) conc[t] = __builtin_nan("");
@@ -2770,6 +2813,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             like = mvalid ? unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL, &rnu) : 0.0;
             if (!FULL && a.conc && mvalid)                        // forward(): model concentrations
                 for (int t = 0; t < a.K; ++t) a.conc[(int64_t)t * a.U + mu] = conc[t];
+          }
         } else if (EPM && rtd_w) {
             double conc[kMaxTracer];
             {
