@@ -517,7 +517,7 @@ def fused_instance(m1, m2, sv, C=5):
     if m1 in ("exponential", "exp_pist_flow") and m2 in (None, "piston"):
         mix = (1 if m2 == "piston" else 0) | (2 if m1 == "exp_pist_flow" else 0) | lw
     else:
-        mix = 64 | lw
+        mix = 64 | lw | (128 if "dispersion" in (m1, m2) else 0)   # generic; +128: the dispersion instances
     return "logp_fused_kernel<%d, true, 2, %d>" % (C, mix)
 
 
@@ -580,7 +580,7 @@ def model_lines(args, gpu):
              "published": (m1, m2, sv) in PUBLISHED_MODELS}
         if sv and base_ms.get((m1, m2)):
             e["vs_savenum0_kernel"] = ms / base_ms[(m1, m2)]
-        if inst.endswith(", 64>") or inst.endswith(", 96>"):
+        if int(inst.rsplit(", ", 1)[1].rstrip(">")) & 64:
             # the generic instance runs several models (piston, dispersion, BMM pairs): a PMC
             # summary keyed by kernel instance cannot say which model it counted, so no FLOP rate
             e["roofline"] = None

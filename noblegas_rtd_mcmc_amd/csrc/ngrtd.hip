@@ -786,7 +786,8 @@ static void gen_disp_split(RtdArgs& a, const UnitArgs& u) {
     if (fused_lds(a, u) > kFusedMaxLds) a.disp_split = 0;
 }
 static int gen_mix(const RtdArgs& a, const UnitArgs& u) {
-    return 64 | (a.row_thalf >= 0 ? 32 : 0) | (full_plan(a, u) && (u.flags & NGRTD_WANT_JACOBIAN) ? 4 : 0);
+    const bool disp = a.disp_aux && (a.mod[0] == MOD_DISP || a.mod[1] == MOD_DISP);   // the dispersion instances
+    return 64 | (disp ? 128 : 0) | (a.row_thalf >= 0 ? 32 : 0) | (full_plan(a, u) && (u.flags & NGRTD_WANT_JACOBIAN) ? 4 : 0);
 }
 static bool gen_path(const RtdArgs& a0, const UnitArgs& u) {
     static const bool disabled = std::getenv("NGRTD_NO_GEN") != nullptr;

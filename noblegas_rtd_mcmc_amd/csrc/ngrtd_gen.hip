@@ -27,15 +27,21 @@ static hipError_t launch_gen(const RtdArgs& a, const UnitArgs& u, int WB, int64_
 // The instances: FULL (the joint plan) at C = 5 with / without the Jacobians and the sampled
 // CFC12 half-life (64, 68, 96, 100); the other plans (RTD-only, forward()) at C = 1..5 (64)
 // and, with the half-life, C = 4, 5 (96) -- the channel counts of the reference's tracer sets.
+// Each also with MIX bit 7 (+128): plans with a dispersion component (ngrtd_gen_disp.hip).
 bool gen_instance_exists(int C, bool full, int mix) {
+    mix &= ~128;
     if (full) return C == 5 && (mix == 64 || mix == 68 || mix == 96 || mix == 100);
     if (mix == 64) return C >= 1 && C <= 5;
     return mix == 96 && (C == 4 || C == 5);
 }
+hipError_t launch_fused_gen_disp_instance(int C, bool full, int mix, const RtdArgs& a, const UnitArgs& u, int WB,
+                                          int64_t W, double* logp, const DemcAccept& da, size_t lds, size_t max_lds,
+                                          hipStream_t st);
 
 hipError_t launch_fused_gen_instance(int C, bool full, int mix, const RtdArgs& a, const UnitArgs& u, int WB, int64_t W,
                                      double* logp, const DemcAccept& da, size_t lds, size_t max_lds, hipStream_t st) {
     if (!gen_instance_exists(C, full, mix)) return hipErrorInvalidValue;
+    if (mix & 128) return launch_fused_gen_disp_instance(C, full, mix, a, u, WB, W, logp, da, lds, max_lds, st);
     if (full) {
         switch (mix) {
         case 64: return launch_gen<5, true, 64>(a, u, WB, W, logp, da, lds, max_lds, st);

@@ -2242,14 +2242,14 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
 #define NGRTD_GEN_DISP_UNROLL 4
 #endif
 constexpr int kGenDispUnroll = NGRTD_GEN_DISP_UNROLL;
-template <int C, bool LW>
+template <int C, bool LW, bool DSP = false>
 __device__ __forceinline__ void gen_exact(const RtdArgs& a, int mod, bool on, double tau, double eta, double D,
                                           double lam, double* num, double& den, const double* tl = nullptr,
                                           const double* dl = nullptr, int age0 = 0, int age1 = -1) {
     double s[C + 1];
 #pragma unroll
     for (int c = 0; c <= C; ++c) s[c] = 0.0;
-    if (mod == MOD_DISP && tl && dl) {
+    if (DSP && mod == MOD_DISP && tl && dl) {
         if (__any(on)) {
             constexpr int CP = cheb_cp(C);
             const double rt = 1.0 / tau;
@@ -2332,7 +2332,7 @@ __device__ __forceinline__ void gen_exact(const RtdArgs& a, int mod, bool on, do
 // num[c] and reciprocal normaliser rden (conc = (A + J B) rden, unit_conc), and *nanc when the
 // concentrations are NaN without being summed (the skip lanes above).  tau: the component's tau
 // (loaded by the caller); thx: the unit's thalf_cfc Beta value (LW).
-template <int C, bool ROLES2, bool LW>
+template <int C, bool ROLES2, bool LW, bool DSP = false>
 __device__ __forceinline__ void gen_component(const RtdArgs& a, const UnitArgs& uk, const double* cheb,
                                               const double* tabl, int comp, bool mvalid, int64_t mu, bool prior_on,
                                               double tau, double thx, double* num, double& rden, bool& nanc,
@@ -2396,11 +2396,15 @@ __device__ __forceinline__ void gen_component(const RtdArgs& a, const UnitArgs& 
         double en[C], den;
         // split (dispersion, staged tables): this wave's ages [split, N); rden holds the raw
         // normaliser sum until the caller adds the theta wave's [0, split)
-        gen_exact<C, LW>(a, mod, ex, tau, eta, D, lw.lam, en, den, daux ? tabl : nullptr, daux, split);
+        if (DSP) {
+            gen_exact<C, LW, true>(a, mod, ex, tau, eta, D, lw.lam, en, den, daux ? tabl : nullptr, daux, split);
+        } else {
+            gen_exact<C, LW>(a, mod, ex, tau, eta, D, lw.lam, en, den);
+        }
         if (ex) {
 #pragma unroll
             for (int c = 0; c < C; ++c) num[c] = en[c];
-            rden = split ? den : 1.0 / den;
+            rden = (DSP && split) ? den : 1.0 / den;
         }
     }
 }
@@ -2543,8 +2547,11 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     constexpr bool GEN = (MIX & 64) != 0;        // generic components (gen_component)
     static_assert(!GEN || (MIX & (1 | 2 | 8 | 16)) == 0, "generic instances: plain log-prob, runtime models");
     // the channel table staged in LDS: exp_pist_flow components (epm_sums)
-    // ... and dispersion components (gen_exact's LDS loop), with their per-age disp_aux
-    const bool DISPS = GEN && a.disp_aux && (a.mod[0] == MOD_DISP || a.mod[1] == MOD_DISP);
+    // ... and dispersion components (gen_exact's LDS loop), with their per-age disp_aux: the
+    // generic instances with MIX bit 7 (a plan with a dispersion component; the others keep
+    // the code without it)
+    constexpr bool DSPI = GEN && (MIX & 128) != 0;
+    const bool DISPS = DSPI && a.disp_aux && (a.mod[0] == MOD_DISP || a.mod[1] == MOD_DISP);
     const bool EPMS = EPM || (GEN && (a.mod[0] == MOD_EPM || a.mod[1] == MOD_EPM)) || DISPS;
     double* tabl = cheb + a.cheb_np * PST;                // EPM: the channel table (epm_row)
     double* daux = tabl + (EPMS ? epm_lds_doubles(a.N, CP) : 0);   // DISPS: disp_aux [2N]
@@ -2753,7 +2760,26 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         // RTD waves without a unit (blocks of fewer walkers than kFusedUnits / L: fused_wb) skip
         // their body (wave-uniform)
         const bool rtd_w = do_rtd && (DZ || __any(mvalid));
-        if (GEN) {
+        if (GEN && !DSPI && rtd_w) {
+            // generic components: the first from tau (prologue), the second (BMM) from tau2
+            const bool prior_on = FULL || (uk.rtd_on && (uk.flags & NGRTD_WANT_PRIOR));
+            double conc[kMaxTracer];
+            double n1[C], r1, n2[C], r2 = 1.0;
+            bool nan1, nan2 = false;
+            gen_component<C, ROLES == 2, LW>(a, uk, cheb, tabl, 0, mvalid, mu, prior_on, tau, thx, n1, r1, nan1);
+            const bool two = a.mod[1] != MOD_NONE;
+            if (two) {
+                const double t2 = mvalid ? a.theta[(int64_t)a.row_tau[1] * a.U + mu] : 1.0;
+                gen_component<C, ROLES == 2, LW>(a, uk, cheb, tabl, 1, mvalid, mu, prior_on, t2, thx, n2, r2, nan2);
+            }
+            unit_conc<C>(a, mu, n1, r1, conc, two ? n2 : nullptr, r2);
+            if (nan1 || nan2)
+                for (int t = 0; t < a.K; ++t) conc[t] = __builtin_nan("");
+            const double rnu = 1.0 / (tp.nub * (uk.rnu_max - uk.rnu_min) + uk.rnu_min);
+            like = mvalid ? unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL, &rnu) : 0.0;
+            if (!FULL && a.conc && mvalid)                        // forward(): model concentrations
+                for (int t = 0; t < a.K; ++t) a.conc[(int64_t)t * a.U + mu] = conc[t];
+        } else if (DSPI) {
             // generic components: the first from tau (prologue), the second (BMM) from tau2.
             // A dispersion component's exact age sum is split over the unit's two waves
             // (a.disp_split, ROLES = 2): the theta wave, done with its CE block early, sums ages
@@ -2768,7 +2794,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
                 const double Dc = mvalid ? a.theta[(int64_t)a.row_D[dcomp] * a.U + mu] : 1.0;
                 double lam = 0.0;
                 if (LW) lam = lw_decay(a, tc, mvalid ? a.theta[(int64_t)a.row_thalf * a.U + mu] : 0.5).lam;
-                gen_exact<C, LW>(a, MOD_DISP, mvalid, tc, 1.0, Dc, lam, pn, pd, tabl, daux, 0, dsp);
+                gen_exact<C, LW, true>(a, MOD_DISP, mvalid, tc, 1.0, Dc, lam, pn, pd, tabl, daux, 0, dsp);
 #pragma unroll
                 for (int c = 0; c < C; ++c) xch[c * kFusedUnits + mi] = pn[c];
                 xch[C * kFusedUnits + mi] = pd;
@@ -2781,11 +2807,11 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             const bool two = a.mod[1] != MOD_NONE;
             const double* dxl = DISPS ? daux : nullptr;
             if (rtd_w) {
-                gen_component<C, ROLES == 2, LW>(a, uk, cheb, tabl, 0, mvalid, mu, prior_on, tau, thx, n1, r1, nan1, dxl,
+                gen_component<C, ROLES == 2, LW, true>(a, uk, cheb, tabl, 0, mvalid, mu, prior_on, tau, thx, n1, r1, nan1, dxl,
                                                  dcomp == 0 ? dsp : 0);
                 if (two) {
                     const double t2 = mvalid ? a.theta[(int64_t)a.row_tau[1] * a.U + mu] : 1.0;
-                    gen_component<C, ROLES == 2, LW>(a, uk, cheb, tabl, 1, mvalid, mu, prior_on, t2, thx, n2, r2, nan2,
+                    gen_component<C, ROLES == 2, LW, true>(a, uk, cheb, tabl, 1, mvalid, mu, prior_on, t2, thx, n2, r2, nan2,
                                                      dxl, dcomp == 1 ? dsp : 0);
                 }
             }
