@@ -584,7 +584,7 @@ def model_lines(args, gpu):
             # the generic instance runs several models (piston, dispersion, BMM pairs): a PMC
             # summary keyed by kernel instance cannot say which model it counted, so no FLOP rate
             e["roofline"] = None
-            e["roofline_note"] = "generic instance shared by %d model pairs; PMC counts are per instance, not per model" % (
+            e["roofline_note"] = "generic instance shared by %d model pair(s); PMC counts are per instance, not per model" % (
                 sum(1 for mm in OTHER_MODELS if fused_instance(*mm) == inst))
         elif pmc.get("fp64_flop_per_unit") and inst in (pmc_path or ""):
             fl = pmc["fp64_flop_per_unit"] * U
