@@ -1466,8 +1466,16 @@ constexpr bool kDzPrefetch = NGRTD_DZ_PREFETCH != 0;   // partner rows one step 
 #ifndef NGRTD_DZ_PF_STEP
 #define NGRTD_DZ_PF_STEP 2
 #endif
-// 2: each role prefetches and stages its parity's rows; 1: the theta lanes all of them
+// 2: each role prefetches and stages its parity's rows; 1: the theta lanes all of them.
+// Per-well chains stage from the theta lanes only (their RTD waves carry the longer log-prob
+// body, so the step's critical path loses the RTD waves' staging: A/B 17.5-18.2 -> 16.9-17.1 us
+// transformed, 15.7-15.8 -> 15.2-15.3 us natural, profiles/r04y_dz_pfstep_ab.txt); joint
+// chains keep the split (1 was 0.15 us slower there).
+#ifndef NGRTD_DZ_PF_STEP_PW
+#define NGRTD_DZ_PF_STEP_PW 1
+#endif
 constexpr int kDzPfStep = NGRTD_DZ_PF_STEP;
+constexpr int kDzPfStepPw = NGRTD_DZ_PF_STEP_PW;
 constexpr int kFusedUnitsDz = 512;   // = kFusedUnits (units per logp_fused_kernel block)
 
 // One element of a DEMetropolisZ proposal, the arithmetic of demcz_propose_kernel (bitwise):
@@ -2643,7 +2651,8 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     const int nst = DZ ? dacc.n_steps : 1;
     int js = 0;
     // DZ: the next step's partner rows, issued at the end of this step's log-prob body
-    double pf1[(kDzMaxP + kDzPfStep - 1) / kDzPfStep], pf2[(kDzMaxP + kDzPfStep - 1) / kDzPfStep];
+    constexpr int PFS = PW ? kDzPfStepPw : kDzPfStep;    // rows per role of the staging (above)
+    double pf1[(kDzMaxP + PFS - 1) / PFS], pf2[(kDzMaxP + PFS - 1) / PFS];
     do {
         ThetaPre tp = tp0;                                // DZ: loaded per step below
         double tau = tau0, eta = eta0, tau2 = tau20, thx = thx0;
@@ -2717,10 +2726,10 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             // each role stages its rows of the unit from partner rows loaded one step ahead
             // (the first step of the launch loads its own here)
             if (js == 0)
-                dz_partner_rows<kDzMaxP, kDzPfStep>(dk, sj, w0 + mwl, ml, L, W, mvalid && (kDzPfStep == 2 || do_theta),
+                dz_partner_rows<kDzMaxP, PFS>(dk, sj, w0 + mwl, ml, L, W, mvalid && (PFS == 2 || do_theta),
                                                     do_theta ? 0 : 1, pf1, pf2);
-            if (kDzPfStep == 2 || do_theta)
-                dz_stage_all<kDzMaxP, kDzPfStep, (MIX & 4) != 0, PW>(dk, sj, uk.U, mu, mi, w0 + mwl, ml, L, W, mvalid,
+            if (PFS == 2 || do_theta)
+                dz_stage_all<kDzMaxP, PFS, (MIX & 4) != 0, PW>(dk, sj, uk.U, mu, mi, w0 + mwl, ml, L, W, mvalid,
                                                                      thl, dk.prop_lds ? propl : nullptr, dl,
                                                                      PW ? mi : mwl, do_theta ? 0 : 1, pf1, pf2);
         } else if (DZ) {
@@ -2943,8 +2952,8 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         NGRTD_PROBE(3);
         if (DZ && kDzPrefetch)   // the next step's partner rows, theta lanes (loads only; zeros elsewhere and
                                  // after the last step: unconditional, so no earlier value stays live)
-            dz_partner_rows<kDzMaxP, kDzPfStep>(dk, dz_step(dk.sch, js + 1), w0 + mwl, ml, L, W,
-                                                mvalid && (kDzPfStep == 2 || do_theta) && js + 1 < nst,
+            dz_partner_rows<kDzMaxP, PFS>(dk, dz_step(dk.sch, js + 1), w0 + mwl, ml, L, W,
+                                          mvalid && (PFS == 2 || do_theta) && js + 1 < nst,
                                                 do_theta ? 0 : 1, pf1, pf2);
         if (DZ) NGRTD_PROBE(13);
         if (!logp && !dk.lp) return;                        // forward() launch: no log-prob
