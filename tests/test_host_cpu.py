@@ -225,3 +225,21 @@ def test_trace_layout_roundtrip(tmp_path):
         for k, (dims, arr) in idata[g].items():
             assert back[g][k][0] == dims and np.array_equal(back[g][k][1], arr, equal_nan=arr.dtype.kind == "f"), (g, k)
     assert np.array_equal(back["coords"]["chain"], np.arange(W))
+
+
+def test_bench_model_lines_name_the_instance_each_plan_runs():
+    """bench.py's `models` lines cite the logp_fused_kernel instance of each c4 plan (MIX bits:
+    1 piston second, 2 exp_pist_flow first, 32 sampled CFC12 half-life, 64 generic, 128 the
+    generic instances of plans with a dispersion component -- ngrtd.hip gen_mix) and attach a
+    PMC FLOP rate only to instances that run one model."""
+    import bench
+    inst = {(m1, m2, sv): bench.fused_instance(m1, m2, sv) for m1, m2, sv in bench.PUBLISHED_MODELS + bench.OTHER_MODELS}
+    assert inst[("exponential", None, "")] == "logp_fused_kernel<5, true, 2, 0>"
+    assert inst[("exp_pist_flow", "piston", "123")] == "logp_fused_kernel<5, true, 2, 35>"
+    assert inst[("piston", None, "")] == "logp_fused_kernel<5, true, 2, 64>"
+    assert inst[("dispersion", None, "")] == "logp_fused_kernel<5, true, 2, 192>"
+    assert inst[("dispersion", None, "123")] == "logp_fused_kernel<5, true, 2, 224>"
+    assert inst[("exponential", "dispersion", "")] == "logp_fused_kernel<5, true, 2, 192>"
+    # the specialised instances are one per published model and savenum
+    spec_inst = [v for (m1, m2, sv), v in inst.items() if not int(v.rsplit(", ", 1)[1].rstrip(">")) & 64]
+    assert len(spec_inst) == len(set(spec_inst)) == len(bench.PUBLISHED_MODELS)
