@@ -2484,6 +2484,11 @@ __host__ __device__ constexpr int cheb_lds_stride(int C) { return kChebN * cheb_
 // into the state (and, transformed, recompute and write the chains'-space value).  Per
 // step: 3 reads + 2 writes of the state's size in HBM, against 6 reads + 3 writes (+ the
 // accepted copies) for the proposal kernel + log-prob kernel pair.
+// MIX bit 4 (with bit 3): per-well chains (one Metropolis decision per unit).
+// MIX bit 5: the sampled CFC12 half-life (channel 0's own decay, lw_decay).
+// MIX bit 6: the generic components (gen_component: every other model pair, runtime models).
+// MIX bit 7 (with bit 6): the plan has a dispersion component (its tables staged in LDS, its
+// age sum split over the unit's two waves; csrc/ngrtd_gen_disp.hip).
 // the reference's Beta priors compiled into the DEMetropolisZ instances too: 4-16 VGPRs spill
 // in their step loop, yet the c4 per-well step runs 20.7 -> 18.7 us transformed and 18.7 ->
 // 16.7 us natural (profiles/r04m_dz_refb_ab.jsonl; NGRTD_DZ_REFB=0 builds the runtime loop)
