@@ -70,6 +70,9 @@ def parse():
                          "all-gather through host memory: the multi-rank rehearsal on a one-GPU box)")
     ap.add_argument("--one-device", action="store_true",
                     help="every rank uses cuda:0 (rehearsal of the N > 1 path on a one-GPU box; needs --backend gloo)")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="gather every step through LogpStepLoop's two-deep async pipeline even at N = 1 (RCCL at "
+                         "world size 1: the device-tensor branch of the N > 1 step on a one-GPU box)")
     return ap.parse_args()
 
 
@@ -175,7 +178,12 @@ def main():
     gpu = 0 if args.one_device else local
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
-    if world > 1:
+    if world > 1 or args.pipeline:
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29531")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -195,7 +203,7 @@ def main():
     lp = LogProb(spec, max_walkers=Wb, device=gpu)       # plan: tables, surrogate fit + validation, c0 table
     torch.cuda.synchronize()
     plan_build_ms = (time.perf_counter() - t0) * 1e3
-    loop = LogpStepLoop(None, W_total, dev)
+    loop = LogpStepLoop(None, W_total, dev, pipeline=True if args.pipeline else None)
     fasts = {o.data_ptr(): lp.bind(theta, o) for o in loop.outs}   # one bound launch per block buffer
     fast_n = lp.bind_n(theta, loop.out)
     loop.evaluate = lambda out: fasts[out.data_ptr()]()
@@ -246,7 +254,7 @@ def main():
         loop.step()
     torch.cuda.synchronize()
     # the ensemble vector of an untimed step: the timed steps must reproduce it bit for bit
-    ref_ens = loop.step().clone() if world > 1 else loop.out.clone()
+    ref_ens = loop.step().clone() if loop.collective else loop.out.clone()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -259,7 +267,7 @@ def main():
     #  * otherwise the kernels of every k-th step get their own event pairs (read back
     #    after the region, no host syncs inside it).
     lp.kernel_stats(reset=True)
-    per_step_events = world > 1 or not single_kernel
+    per_step_events = loop.collective or not single_kernel
     t0 = time.perf_counter()
     if per_step_events:
         def hook(i, before):
@@ -280,7 +288,7 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX) if args.backend == "nccl" else _host_max(t)
         dt = float(t.item())
-    last = loop.gathered if world > 1 else loop.out
+    last = loop.gathered if loop.collective else loop.out
     if not torch.equal(last.nan_to_num(), ref_ens.nan_to_num()) or \
             not torch.equal(torch.isnan(last), torch.isnan(ref_ens)):
         raise SystemExit("bench: the timed steps' log-probs differ from an untimed evaluation")
@@ -293,11 +301,12 @@ def main():
         line["ensemble_finite_frac"] = finite_frac
         if samp is not None:
             line["sampler"] = samp
-        if world > 1:
+        if loop.collective:
             line["config"]["backend"] = args.backend + (" (host-staged all-gather)" if args.backend == "gloo" else "")
             line["config"]["one_device"] = bool(args.one_device)
+            line["config"]["pipeline"] = bool(args.pipeline or world > 1)
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -399,7 +399,8 @@ static int cheb_prepare(ngrtd_ctx* ctx, TableDev& tab, double d01) {
 // turned into monomial form (long double) and every piece is validated at 26 points through
 // epm_piece + cheb_sums, the kernel's own code, at the plan tolerance kChebTol.  Threads split
 // the pieces.  Used only if every table validates (else the plan keeps the multi-kernel path).
-static int epm_prepare(ngrtd_ctx* ctx, TableDev& tab, int N, int p_lo, int p_hi) {
+// nb_cap > 0: only blocks 1..nb_cap (the blocks a windowed table's units reach, epm_window).
+static int epm_prepare(ngrtd_ctx* ctx, TableDev& tab, int N, int p_lo, int p_hi, int nb_cap = 0) {
     tab.epm_ok = false;
     const int C = tab.C, S = kEpmBlock, n = kChebN;
     if (C < 1 || C > 5 || tab.cols_host.empty() || N <= S + 1 || p_lo < 0 || p_hi > kEpmPieces || p_hi <= p_lo)
@@ -407,7 +408,7 @@ static int epm_prepare(ngrtd_ctx* ctx, TableDev& tab, int N, int p_lo, int p_hi)
     for (int c = 0; c < C; ++c)
         for (double v : tab.cols_host[c])
             if (!(v >= 0.0) || !std::isfinite(v)) return NGRTD_OK;   // the relative bound needs A >= 0
-    const int nb = (N - 1) / S;                    // b S < N for b = 1..nb
+    const int nb = nb_cap > 0 ? std::min((N - 1) / S, nb_cap) : (N - 1) / S;   // b S < N for b = 1..nb
     const int np = p_hi - p_lo;
     // the C channel columns only (the kernel sums the normaliser's tail in closed form), rows
     // packed: a piece is kChebN * C contiguous doubles, read with 16-B loads (kChebN even)
@@ -428,7 +429,7 @@ static int epm_prepare(ngrtd_ctx* ctx, TableDev& tab, int N, int p_lo, int p_hi)
             long double r = 0.0L;
             for (int k = N - 1; k >= S; --k) {
                 r = r * q + (long double)tab.cols_host[c][k];
-                if (k % S == 0) out[(size_t)(k / S - 1) * C + c] = r;
+                if (k % S == 0 && k / S <= nb) out[(size_t)(k / S - 1) * C + c] = r;   // (nb_cap: blocks 1..nb)
             }
         }
     };
@@ -659,13 +660,14 @@ static void launch_mfma(const RtdArgs& a, const UnitArgs& u, int32_t fuse, hipSt
 // read from global memory: they are needed only by waves with an uncovered tau) and the
 // packed per-well data (ce obs, 1/sd^2, sums of 0.5 log 1/sd^2, E_min; rtd obs, 1/sd^2,
 // sums; the Student-t normaliser table).
+constexpr size_t kFusedMaxLds = 157 * 1024;   // gfx950: 160 KiB per workgroup, less the static fexp/flog tables
 static size_t fused_lds(const RtdArgs& a, const UnitArgs& u, int dz_p = 0) {
     // EPM: the channel table, rows of cheb_cp(C) doubles in LDS (the kernel's layout; the global
     // table's rows are a.CP = (C + 1) & ~1, shorter for C = 2, 4)
     // generic instances with a dispersion component: the same table, and disp_aux [2N]
     const bool disp = a.disp_aux && (a.mod[0] == MOD_DISP || a.mod[1] == MOD_DISP);
     const size_t epm_tab = (a.mod[0] == MOD_EPM || a.mod[1] == MOD_EPM || disp)
-                               ? (size_t)epm_lds_doubles(a.N, cheb_cp(a.C)) + (disp ? 2 * (size_t)a.N : 0) : 0;
+                               ? (size_t)epm_lds_doubles(a.epm_nw, cheb_cp(a.C)) + (disp ? 2 * (size_t)a.N : 0) : 0;
     const size_t dz = (size_t)dz_p * kFusedUnits;                          // DZ step: the proposals
     // generic instances, dispersion split over the unit's two waves: the theta waves' partial sums
     const size_t xch = (disp && a.disp_split > 0) ? (size_t)(a.C + 1) * kFusedUnits : 0;
@@ -685,7 +687,51 @@ static double lw_tau_lo(const RtdArgs& a, double tau_lo) {
     if (!(tmin > 0.0)) return 0.0;
     return tau_lo * tmin / (tmin + kLn2Ref * tau_lo);
 }
+// The exp_pist_flow channel-table rows a single-launch EPM plan stages in LDS (RtdArgs::epm_nw;
+// the kernel's side: epm_sums).  The whole table fits LDS up to N ~ 1600 (C = 5); the
+// reference's own runs convolve N = 25 256 ages (run_age_mcmc.py:46,209), 1.24 MB.  But a unit
+// reads only its head block [B - 16, B) of the table, B = (m / 16 + 1) 16 past its first unmasked
+// age m (the tail comes from the block-tail surrogate), and m is bounded over the priors'
+// support: tp_m >= tau (1 - 1/eta) is first met at m <= ceil(tau1_hi (1 - 1/eta1_hi) - dtp).  So a
+// plan whose exp_pist_flow component is tau1 / eta1 under their Uniform priors stages rows
+// [0, (m_max / 16 + 1) 16 + 80) (the +64 rows serve the exact short tails, which no unit of the
+// support needs: the block-tail table covers its tau'); units outside the support box have
+// log-prob -inf by their priors and epm_sums gives them finite zero sums (or NaN where the
+// reference's weights are NaN).  NGRTD_EPM_WINDOW: 1 (default) only when the whole table does not
+// fit, 2 whenever the window is smaller (A/B runs), 0 never.
+static int epm_window_rows(double tau_hi, double eta_hi, double dtp, int N) {
+    if (!(tau_hi >= 0.0 && eta_hi >= 1.0) || !std::isfinite(tau_hi) || !std::isfinite(eta_hi)) return -1;
+    const double mm = std::ceil(tau_hi * (1 - 1 / eta_hi) - dtp) + 1.0;
+    if (!(mm >= 0.0 && mm < (double)N)) return -1;
+    return ((int)mm / kEpmBlock + 1) * kEpmBlock + 64 + kEpmBlock;
+}
+static void epm_window(RtdArgs& a, const UnitArgs& u) {
+    static const int mode = [] {
+        const char* e = std::getenv("NGRTD_EPM_WINDOW");
+        return e ? std::atoi(e) : 1;
+    }();
+    a.epm_nw = (int)cdiv(a.N, kEpmBlock) * kEpmBlock;
+    a.ew_on = 0;
+    if (mode == 0 || a.mod[0] != MOD_EPM || !(a.mod[1] == MOD_NONE || a.mod[1] == MOD_PISTON) || !a.epm) return;
+    if (!u.rtd_on || !(u.flags & NGRTD_WANT_PRIOR) || u.row_eta1 < 0 || a.row_tau[0] != u.row_tau1 ||
+        a.row_eta[0] != u.row_eta1 || (a.row_thalf >= 0 && a.row_thalf != u.row_thalf))
+        return;
+    if (!(u.tau1_lo <= u.tau1_hi && u.eta1_lo <= u.eta1_hi && u.eta1_lo > 0.0)) return;
+    const int rows = epm_window_rows(u.tau1_hi, u.eta1_hi, a.dtp, a.N);
+    if (rows < 0 || rows >= a.epm_nw || rows / kEpmBlock > a.epm_nb) return;
+    if (mode == 1 && fused_lds(a, u, 0) <= kFusedMaxLds) return;
+    a.epm_nw = rows;
+    a.ew_on = 1;
+    a.ew_tau_lo = u.tau1_lo; a.ew_tau_hi = u.tau1_hi;
+    a.ew_eta_lo = u.eta1_lo; a.ew_eta_hi = u.eta1_hi;
+}
+static void cheb_window_tau(RtdArgs& a, const UnitArgs& u);
+// the staged windows of a single-launch plan: the surrogate pieces and the EPM table rows
 static void cheb_window(RtdArgs& a, const UnitArgs& u) {
+    cheb_window_tau(a, u);
+    epm_window(a, u);
+}
+static void cheb_window_tau(RtdArgs& a, const UnitArgs& u) {
     a.cheb_p0 = 0;
     a.cheb_np = a.cheb ? kChebPieces : 0;
     if (!a.cheb || !u.rtd_on || !(u.flags & NGRTD_WANT_PRIOR) || a.row_tau[0] != u.row_tau1) return;
@@ -699,7 +745,6 @@ static void cheb_window(RtdArgs& a, const UnitArgs& u) {
     a.cheb_p0 = pa;
     a.cheb_np = pb - pa + 1;
 }
-constexpr size_t kFusedMaxLds = 157 * 1024;   // gfx950: 160 KiB per workgroup, less the static fexp/flog tables
 // A per-unit CFC12 half-life (row_thalf) runs in the single launch (the LW instances) when it
 // decays exactly one channel, channel 0 (build_table puts it first), with the instance
 // counts of lw_instance (C = 5 for the joint plans, C = 4 or 5 otherwise).
@@ -896,7 +941,7 @@ static int dzc_mix(const RtdArgs& a0, const UnitArgs& u, int P, bool transformed
         return -1;
     }
     if (!dz_chain_instance_exists(C, mix)) return -1;
-    *lds = dzc_lds_doubles(C, mix, (mix & 64) ? 0 : a.cheb_np, a.N, u.wd_n, P) * sizeof(double);
+    *lds = dzc_lds_doubles(C, mix, (mix & 64) ? 0 : a.cheb_np, a.epm_nw, u.wd_n, P) * sizeof(double);
     return *lds <= kFusedMaxLds ? mix : -1;
 }
 // Every theta row a single-launch step reads is one of ThetaPre's (the 6 CE rows, tau1,
@@ -1594,6 +1639,9 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
         }
         a.epm = nullptr;
         a.epm_nb = a.epm_p0 = a.epm_np = 0;
+        a.epm_nw = (int)cdiv(p->N, kEpmBlock) * kEpmBlock;   // the whole table (epm_window narrows it per launch)
+        a.ew_on = 0;
+        a.ew_tau_lo = a.ew_tau_hi = a.ew_eta_lo = a.ew_eta_hi = 0.0;
         {
             const char* e = std::getenv("NGRTD_EPM_DIAG");     // timing diagnostics only
             a.epm_diag = e ? std::atoi(e) : 0;
@@ -1618,8 +1666,16 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
             if (epm2) low(d->tau2_lo, d->eta2_hi);
             const double lo = std::max(1.0 / (1 << -kEpmOct0), plo);
             const int pa = epm_piece(lo, x), pb = kEpmPieces - 1;
-            if (!disabled && pa >= 0 && pb >= pa) {
-                NG_CHECK(epm_prepare(ctx, p->table, p->N, pa, pb + 1));
+            // a table too long for LDS serves windowed launches only (epm_window): the blocks the
+            // window's units reach, or nothing when the priors bound no window
+            int nb_cap = 0;
+            if ((size_t)epm_lds_doubles(p->N, cheb_cp(p->table.C)) * sizeof(double) > kFusedMaxLds) {
+                const int rows = (epm1 && !epm2 && (d->flags & NGRTD_WANT_PRIOR))
+                                     ? epm_window_rows(d->tau1_hi, d->eta1_hi, p->dtp, p->N) : -1;
+                nb_cap = rows > 0 ? rows / kEpmBlock : -1;
+            }
+            if (!disabled && pa >= 0 && pb >= pa && nb_cap >= 0) {
+                NG_CHECK(epm_prepare(ctx, p->table, p->N, pa, pb + 1, nb_cap));
                 if (p->table.epm_ok) {
                     a.epm = p->table.epm.d();
                     a.epm_nb = p->table.epm_nb; a.epm_p0 = p->table.epm_p0; a.epm_np = p->table.epm_np;

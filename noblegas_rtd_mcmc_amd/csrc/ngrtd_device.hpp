@@ -46,6 +46,14 @@ struct RtdArgs {
     // laid out [b - 1][piece - epm_p0][kChebN][C] (rows packed); null when the plan has none
     const double* epm;
     int32_t epm_nb, epm_p0, epm_np;
+    // rows [0, epm_nw) of the channel table staged in LDS for the exp_pist_flow sums (a multiple
+    // of kEpmBlock).  The whole table, padded, unless the plan's priors bound every in-support
+    // unit's first unmasked age (ngrtd.hip epm_window: ew_on = 1; the reference's series length
+    // N = 25 256 does not fit LDS): then only the rows those units read, and units outside the
+    // support box [ew_tau_lo, ew_tau_hi] x [ew_eta_lo, ew_eta_hi] (x thalf_cfc's Beta [0, 1])
+    // -- whose log-prob is -inf by their priors -- read no table row past it (epm_sums)
+    int32_t epm_nw, ew_on;
+    double ew_tau_lo, ew_tau_hi, ew_eta_lo, ew_eta_hi;
     int32_t epm_diag;       // timing diagnostics only (NGRTD_EPM_DIAG, tools/epm_probe.py): bit 0 skips
                             // the head, bit 1 the tail surrogate, bit 2 the exact tails (wrong results)
     // dispersion components of the generic single-launch instances (gen_exact): per age k,

@@ -17,8 +17,11 @@
 //
 // The log-prob functions read theta rows through a pointer: the lane writes its proposal's
 // natural values to its own LDS slot of a [P][NT] block (a.theta / ua.theta point there,
-// U = NT, unit index = slot), and reads them back in the same lane (program order, no
-// barrier).
+// U = NT, unit index = slot) and reads them back in the same lane (program order).  The one
+// exception is the exact matrix-core fallback (dzc_exact): its MFMA tiles read the tau rows
+// of all 64 lanes of the wave.  A wave's LDS accesses complete in issue order, so those rows
+// are the ones the lanes just wrote; a wave barrier before the fallback keeps the compiler
+// from moving its loads above the other lanes' stores.
 #pragma once
 #include "ngrtd_kernels.hpp"
 
@@ -31,8 +34,9 @@ constexpr int kDzcMaxP = 8;        // parameter rows of a lane-chain step
 // next step's partner rows and the log-prob body without spills; 128 spilled up to 46)
 __host__ __device__ constexpr int dzc_threads(int) { return 512; }
 // LDS doubles: the surrogate window, the EPM table, the per-well data, the proposal rows
-__host__ __device__ constexpr size_t dzc_lds_doubles(int C, int mix, int cheb_np, int N, int wd_n, int P) {
-    return (size_t)cheb_np * cheb_lds_stride(C) + ((mix & 2) ? (size_t)epm_lds_doubles(N, cheb_cp(C)) : 0) +
+// (epm_nw: the EPM table rows staged, RtdArgs::epm_nw)
+__host__ __device__ constexpr size_t dzc_lds_doubles(int C, int mix, int cheb_np, int epm_nw, int wd_n, int P) {
+    return (size_t)cheb_np * cheb_lds_stride(C) + ((mix & 2) ? (size_t)epm_lds_doubles(epm_nw, cheb_cp(C)) : 0) +
            (size_t)((wd_n + 1) & ~1) + (size_t)P * dzc_threads(mix);
 }
 
@@ -107,7 +111,7 @@ __device__ __forceinline__ double dzc_rtd_like(const RtdArgs& a, const UnitArgs&
         double num2[C];
         if (MIX & 1) {
             const int ix = piston_index(tau2, a.tp0, a.dtp, a.N);
-            epm_row_load<C>(tabl + epm_row(ix, CP), num2);
+            epm_piston_row<C>(a, tabl, ix, num2);
             if (LW) num2[0] *= fexp(-lam * (ix == 0 ? a.tp0 : (double)ix + a.dtp));
         }
         unit_conc<C, true>(a, slot, num, dd * rr[0], conc, (MIX & 1) ? num2 : nullptr);
@@ -162,7 +166,10 @@ __device__ __forceinline__ double dzc_rtd_like(const RtdArgs& a, const UnitArgs&
             for (int t = 0; t < a.K; ++t) conc[t] = __builtin_nan("");
         like = valid ? unit_like_rtd<C>(ul, slot, ml, conc, &tp, false, &rr[1]) : 0.0;
     }
-    if (__any(bad)) dzc_exact<C, MIX>(a, ul, slot0, valid && bad, slot, ml, nub, conc, like, lw);
+    if (__any(bad)) {
+        __builtin_amdgcn_wave_barrier();                  // the wave's proposal rows (see the header)
+        dzc_exact<C, MIX>(a, ul, slot0, valid && bad, slot, ml, nub, conc, like, lw);
+    }
     return like;
 }
 
@@ -193,7 +200,7 @@ __global__ void __launch_bounds__(dzc_threads(MIX), 2)
     // ---- prologue: tables -> LDS, once per launch
     double* cheb = lds;
     double* tabl = cheb + (CEO ? 0 : a0.cheb_np * PST);
-    double* wd = tabl + ((!CEO && EPM) ? epm_lds_doubles(a0.N, CP) : 0);
+    double* wd = tabl + ((!CEO && EPM) ? epm_lds_doubles(a0.epm_nw, CP) : 0);
     double* props = wd + ((ua.wd_n + 1) & ~1);            // [P][NT] the lanes' proposals (natural)
     if constexpr (!CEO) {
         if (a0.cheb) {
@@ -204,7 +211,7 @@ __global__ void __launch_bounds__(dzc_threads(MIX), 2)
         }
     }
     if constexpr (!CEO && EPM) {
-        const int nrow = (a0.N + kEpmBlock - 1) / kEpmBlock * kEpmBlock;
+        const int nrow = a0.epm_nw;                      // (a windowed table: its rows only)
         for (int i = tid; i < nrow * CP; i += NT) {
             const int k = i / CP, c = i % CP;
             tabl[epm_row(k, CP) + c] = (k < a0.N && c < C) ? a0.tab[(int64_t)k * a0.CP + c] : 0.0;

@@ -2045,6 +2045,12 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
     const int m = f > 1 ? f : 1;
     const int blk = m / S + 1, B = blk * S;
     const double q = fexp(-beta);
+    // the staged rows [0, Nst); a windowed table (a.ew_on, ngrtd.hip epm_window) holds the rows of
+    // every unit inside the priors' support box, and the units outside it (log-prob -inf by their
+    // priors; NaN where nan_out says so) read no row past it: no exact tails, zero sums
+    const int Nst = a.epm_nw < N ? a.epm_nw : N;
+    const bool outw = a.ew_on && !(tau >= a.ew_tau_lo && tau <= a.ew_tau_hi && eta >= a.ew_eta_lo &&
+                                   eta <= a.ew_eta_hi && (!LW || (thx >= 0.0 && thx <= 1.0)));
     // the block tail's surrogate piece first: its top chunks are loaded before the head loop
     const bool tail = B < N;
     double ex = 0.0;
@@ -2066,14 +2072,15 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
         if (lam_out) *lam_out = lam;
     }
     const bool tail_on = tail && !(a.epm_diag & 2);
-    const double* pt = a.epm + ((size_t)(tail_on ? blk - 1 : 0) * a.epm_np + (pc < 0 ? 0 : pc)) * (size_t)(kChebN * C);
+    const int bt = (tail_on ? (blk < a.epm_nb ? blk : a.epm_nb) : 1) - 1;   // (a windowed table's blocks: clamped)
+    const double* pt = a.epm + ((size_t)bt * a.epm_np + (pc < 0 ? 0 : pc)) * (size_t)(kChebN * C);
     double2 tpre[epm_tail_pre_n(C, NPW) > 0 ? epm_tail_pre_n(C, NPW) : 1];
     epm_tail_pre<C, NPW>(pt, tail_on, tpre);
     // LW: channel 0's tail coefficients at tau'_w (column 0 of its own piece, L2), loaded
     // before the head loop as well (kEpmLwPre)
     double twp[LW ? kChebN : 1];
     if (LW && kEpmLwPre) {
-        const double* pw = a.epm + ((size_t)(tail_on ? blk - 1 : 0) * a.epm_np + (pcw < 0 ? 0 : pcw)) * (size_t)(kChebN * C);
+        const double* pw = a.epm + ((size_t)bt * a.epm_np + (pcw < 0 ? 0 : pcw)) * (size_t)(kChebN * C);
 #pragma unroll
         for (int k = 0; k < kChebN; ++k) twp[k] = tail_on ? pw[k * C] : 0.0;
     }
@@ -2095,7 +2102,7 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
         // m >= N (every age masked: tau (1 - 1/eta) beyond the series, the reference's g is 0 / 0):
         // m's block is past the staged table, so read the last staged block, where k < m for every
         // row and every weight stays 0 (then y = 0, G = 0: NaN concentrations, as the reference's)
-        const int hb0 = B - S < (N - 1) / S * S ? B - S : (N - 1) / S * S;
+        const int hb0 = B - S < (Nst - 1) / S * S ? B - S : (Nst - 1) / S * S;
         const double* hb = tabl + epm_row(hb0, CP);
         double w = 0.0, w2 = 0.0;
 #pragma unroll
@@ -2111,14 +2118,14 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
         qB = qok ? w * q : -1.0;                        // w = q^(B - 1 - m) after the last row
         if (LW) qBw = qok ? w2 * qw : -1.0;
         if (__any(!qok)) {
-            const int kt = (B < N ? B : N) - 1;
+            const int kt = (B < Nst ? B : Nst) - 1;
             double yt[C];
 #pragma unroll
             for (int c = 0; c < C; ++c) yt[c] = 0.0;
 #pragma unroll 4
             for (int i = 0; i < S; ++i) {
                 const int k = kt - i;
-                const bool on = !qok && k >= m;
+                const bool on = !qok && k >= m && !outw;
                 double rv[C];
                 epm_row_load<C>(tabl + epm_row(on ? k : 0, CP), rv);
 #pragma unroll
@@ -2131,13 +2138,13 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
             for (int c = 0; c < C; ++c) y[c] = qok ? y[c] : yt[c];
         }
     }
-    const bool bad = mvalid && tail && (pc < 0 || (LW && pcw < 0));
+    const bool bad = mvalid && tail && !outw && (pc < 0 || (LW && pcw < 0));
     double tl[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) tl[c] = 0.0;
     if (tail_on) epm_tail_sums<C, NPW>(pt, ex, tl, tpre);
     if (LW && tail_on) {   // channel 0's tail at tau'_w: column 0 of its own piece (L2)
-        const double* pw = a.epm + ((size_t)(blk - 1) * a.epm_np + (pcw < 0 ? 0 : pcw)) * (size_t)(kChebN * C);
+        const double* pw = a.epm + ((size_t)bt * a.epm_np + (pcw < 0 ? 0 : pcw)) * (size_t)(kChebN * C);
         double v = kEpmLwPre ? twp[kChebN - 1] : pw[(kChebN - 1) * C];
 #pragma unroll
         for (int k = kChebN - 2; k >= 0; --k) v = fma(v, exw, kEpmLwPre ? twp[k] : pw[k * C]);
@@ -2160,7 +2167,7 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
 #pragma unroll 8
             for (int j = 63; j >= 0; --j) {
                 const int k = B + j;
-                const bool on = sb && k <= N - 1;
+                const bool on = sb && k <= Nst - 1;
                 double rv[C];
                 epm_row_load<C>(tabl + epm_row(on ? k : 0, CP), rv);
 #pragma unroll
@@ -2171,7 +2178,7 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
             }
         }
         if (__any(lb)) {
-            int bmin = lb ? B : N, kmax = lb ? N - 1 : -1;
+            int bmin = lb ? B : N, kmax = lb ? Nst - 1 : -1;
 #pragma unroll
             for (int off = 32; off >= 1; off >>= 1) {
                 const int o = __shfl_xor(bmin, off, 64), o2 = __shfl_xor(kmax, off, 64);
@@ -2217,6 +2224,26 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
         dn = e1;                                        // G e2
     }
     dd = e2;
+    if (outw) {                                         // outside the window: finite zeros (see above)
+#pragma unroll
+        for (int c = 0; c < C; ++c) num[c] = 0.0;
+        dn = 1.0;
+        dd = 1.0;
+    }
+}
+
+// The piston component's channel-table row ix of an exp_pist_flow plan (BMM exp_pist_flow-piston):
+// from the LDS table when staged there, else (a windowed table, ix past its rows) from the global
+// table -- the same values.
+template <int C>
+__device__ __forceinline__ void epm_piston_row(const RtdArgs& a, const double* tabl, int ix, double* v) {
+    constexpr int CP = cheb_cp(C);
+    if (ix < a.epm_nw) {
+        epm_row_load<C>(tabl + epm_row(ix, CP), v);
+    } else {
+#pragma unroll
+        for (int c = 0; c < C; ++c) v[c] = a.tab[(int64_t)ix * a.CP + c];
+    }
 }
 
 // ------------------------------------------------------ generic components (MIX bit 6)
@@ -2567,7 +2594,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     const bool DISPS = DSPI && a.disp_aux && (a.mod[0] == MOD_DISP || a.mod[1] == MOD_DISP);
     const bool EPMS = EPM || (GEN && (a.mod[0] == MOD_EPM || a.mod[1] == MOD_EPM)) || DISPS;
     double* tabl = cheb + a.cheb_np * PST;                // EPM: the channel table (epm_row)
-    double* daux = tabl + (EPMS ? epm_lds_doubles(a.N, CP) : 0);   // DISPS: disp_aux [2N]
+    double* daux = tabl + (EPMS ? epm_lds_doubles(a.epm_nw, CP) : 0);   // DISPS: disp_aux [2N]
     double* wd = daux + (DISPS ? 2 * a.N : 0);
     constexpr int kWdRegs = (4 * 64 * kFusedWaves + NTH - 1) / NTH;
     double wv[kWdRegs];
@@ -2597,14 +2624,16 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         double2* dst = reinterpret_cast<double2*>(tabl);
         constexpr int RB = kEpmBlock * CP / 2, SB = epm_blk_stride(CP) / 2;   // double2 per block / padded
         // whole blocks: the rows past N of the last block are zeros (epm_sums reads every row
-        // of a unit's head block, weighting the ones before its first age by 0)
-        const int n2 = (a.N + kEpmBlock - 1) / kEpmBlock * RB, nv = a.N * CP / 2;
+        // of a unit's head block, weighting the ones before its first age by 0); the rows
+        // [0, epm_nw) of a windowed table
+        const int nr = a.N < a.epm_nw ? a.N : a.epm_nw;
+        const int n2 = a.epm_nw / kEpmBlock * RB, nv = nr * CP / 2;
         if (a.CP == CP) {
             for (int i = tid; i < n2; i += NTH) dst[(i / RB) * SB + i % RB] = i < nv ? src[i] : double2{0.0, 0.0};
         } else {   // C = 2, 4: the global table's rows are (C + 1) & ~1 = C doubles, the LDS rows CP = C + 2
             for (int i = tid; i < 2 * n2; i += NTH) {
                 const int k = i / CP, c = i % CP;
-                tabl[epm_row(k, CP) + c] = (k < a.N && c < C) ? a.tab[(int64_t)k * a.CP + c] : 0.0;
+                tabl[epm_row(k, CP) + c] = (k < nr && c < C) ? a.tab[(int64_t)k * a.CP + c] : 0.0;
             }
         }
     }
@@ -2692,7 +2721,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         // zero partial sums land on no walker's slots
         const int pi = (DZ && mwl >= WB) ? mi : ml * WB + mwl;
         double* tabl = cheb + a.cheb_np * PST;
-        double* daux = tabl + (EPMS ? epm_lds_doubles(a.N, CP) : 0);
+        double* daux = tabl + (EPMS ? epm_lds_doubles(a.epm_nw, CP) : 0);
         double* wd = daux + (DISPS ? 2 * a.N : 0);
         double* thl = wd + uk.wd_n;
         double* propl = thl + (((MIX & 4) && DZ) ? dk.P * kFusedUnits : 0);   // DZ: [P][512] proposals
@@ -2865,9 +2894,9 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
                 double rr[2];
                 batch_recip<2>(dr, rr);
                 double num2[C];
-                if (MIX & 1) {                  // the piston row from the LDS channel table
+                if (MIX & 1) {                  // the piston row from the channel table (LDS)
                     const int ix = piston_index(tau2, a.tp0, a.dtp, a.N);
-                    epm_row_load<C>(tabl + epm_row(ix, CP), num2);
+                    epm_piston_row<C>(a, tabl, ix, num2);
                     if (LW) num2[0] *= fexp(-lam * (ix == 0 ? a.tp0 : (double)ix + a.dtp));
                 }
                 unit_conc<C>(a, mu, num, dd * rr[0], conc, (MIX & 1) ? num2 : nullptr);

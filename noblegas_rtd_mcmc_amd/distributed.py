@@ -53,9 +53,15 @@ class LogpStepLoop:
 
     The same function runs under torchrun (RCCL) and in the world-size-2 gloo tests
     (tests/test_distributed_cpu.py), so the bench's multi-GPU step has no untested branch.
+
+    ``pipeline``: None (default) gathers -- and pipelines the gathers of device-side
+    collectives -- only when world > 1; True gathers every step through the two-deep
+    pipeline at ANY world size (a process group must be initialised), so the async branch
+    runs on one GPU with RCCL at world size 1 (tests/test_gpu_distributed.py); False never
+    pipelines.
     """
 
-    def __init__(self, evaluate, W_total, device, dtype=torch.float64, group=None, evaluate_n=None):
+    def __init__(self, evaluate, W_total, device, dtype=torch.float64, group=None, evaluate_n=None, pipeline=None):
         self.evaluate = evaluate
         self.evaluate_n = evaluate_n      # optional: evaluate_n(out, k) = k evaluations in one call
         self.group = group
@@ -64,16 +70,21 @@ class LogpStepLoop:
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.lo, self.hi = shard_walkers(self.W_total, self.rank, self.world)
         self.per = (self.W_total + self.world - 1) // self.world
-        nb = 2 if self.world > 1 else 1
+        if pipeline and not dist.is_initialized():
+            raise ValueError("LogpStepLoop(pipeline=True) needs an initialised process group")
+        self.pipeline = pipeline
+        # gather every step: several ranks, or a forced pipeline (world 1 included)
+        self.collective = self.world > 1 or bool(pipeline)
+        nb = 2 if self.collective else 1
         self.bufs = [torch.full((self.per,), float("nan"), dtype=dtype, device=device) for _ in range(nb)]
         self.outs = [b[: self.hi - self.lo] for b in self.bufs]
         self.gathers = ([torch.empty(self.per * self.world, dtype=dtype, device=device) for _ in range(nb)]
-                        if self.world > 1 else self.bufs)
+                        if self.collective else self.bufs)
         self.buf, self.out, self.gathered = self.bufs[0], self.outs[0], self.gathers[0]
 
     def step(self):
         self.evaluate(self.outs[0])
-        if self.world > 1:
+        if self.collective:
             all_gather_into(self.gathers[0], self.bufs[0], group=self.group)
         self.gathered = self.gathers[0]
         return self.gathered
@@ -88,17 +99,17 @@ class LogpStepLoop:
         Otherwise (host-staged gloo rehearsals) k sequential ``step()``s.  ``hook(i, before)``
         runs around step i's evaluation (bench.py's event sampling)."""
         k = int(k)
-        if self.world == 1 and self.evaluate_n is not None and hook is None:
+        if not self.collective and self.evaluate_n is not None and hook is None:
             self.evaluate_n(self.out, k)
             return self.gathered
-        if self.world == 1 or host_staged(self.group, self.bufs[0]):
+        if not self.collective or self.pipeline is False or host_staged(self.group, self.bufs[0]):
             for i in range(k):
                 if hook:
                     hook(i, True)
                 self.evaluate(self.outs[0])
                 if hook:
                     hook(i, False)
-                if self.world > 1:
+                if self.collective:
                     all_gather_into(self.gathers[0], self.bufs[0], group=self.group)
             self.gathered = self.gathers[0]
             return self.gathered
@@ -121,7 +132,7 @@ class LogpStepLoop:
         return self.gathered
 
     def ensemble(self):
-        if self.world == 1:
+        if not self.collective:
             return self.out
         return torch.cat([self.gathered[r * self.per: r * self.per + (lambda s: s[1] - s[0])(
             shard_walkers(self.W_total, r, self.world))] for r in range(self.world)])

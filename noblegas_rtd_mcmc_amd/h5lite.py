@@ -902,7 +902,10 @@ class H5Writer:
         (level by level, as _tree_shape counts them), the root last."""
         full = self._node_size(h)
         out = []
-        # level 0: chunk entries; entries of a level above: (first key, last end key, address)
+        # level 0: chunk entries; entries of a level above: (first key, right key, address).
+        # A node's right key (the bound after its last child) is its right sibling's first key,
+        # as the library's node splits share that key; the last node of a level ends with the
+        # end key of the dataset's last chunk.
         ents = [(self._key(h, o, sz), self._end_key(h, o), a) for o, a, sz in chunks]
         k = 0
         for level, n in enumerate(self._tree_shape(len(chunks))):
@@ -913,12 +916,13 @@ class H5Writer:
             for i, g in enumerate(groups):
                 left = addrs[i - 1] if i > 0 else UNDEF
                 right = addrs[i + 1] if i + 1 < n else UNDEF
+                rkey = groups[i + 1][0][0] if i + 1 < n else g[-1][1]
                 node = b"TREE" + struct.pack("<BBH", 1, level, len(g)) + struct.pack("<QQ", left, right)
                 for key, _, a in g:
                     node += key + struct.pack("<Q", a)
-                node += g[-1][1]
+                node += rkey
                 out.append((addrs[i], node + b"\0" * (full - len(node))))
-                nxt.append((g[0][0], g[-1][1], addrs[i]))
+                nxt.append((g[0][0], rkey, addrs[i]))
             ents = nxt
         return out
 

@@ -97,6 +97,8 @@ def fm_log(x):
     ctx = _dev_ctx(x)
     if ctx is None:
         return torch.log(x)
+    if x.dtype != torch.float64:
+        raise TypeError("fm_log: the device log takes float64 tensors, got %s" % (x.dtype,))
     x = x.contiguous()
     out = torch.empty_like(x)
     ctx.check(ctx.lib.ngrtd_fm_log(ctx.h, x.data_ptr(), out.data_ptr(), x.numel()), "ngrtd_fm_log")
@@ -162,6 +164,8 @@ class Transform:
         ctx = _dev_ctx(u)
         if ctx is not None:
             import ctypes as C
+            if u.dtype != torch.float64:
+                raise TypeError("Transform.backward: the device transform takes float64 tensors, got %s" % (u.dtype,))
             uc = u.contiguous()
             out = torch.empty_like(uc)
             P = len(self.kind)

@@ -141,7 +141,8 @@ class Dataset(dict):
     """One InferenceData group, the access patterns the reference's scripts use on an
     xarray Dataset: ``ds[name]`` and ``ds.name`` give the variable as a numpy array
     (``np.asarray(ds[name])`` is [chain, draw(, well)], as run_age_mcmc.py:251-276 indexes
-    it), ``ds.dims[name]`` its dimension names, ``ds.attrs`` the group attributes."""
+    it), ``ds.var_dims[name]`` its dimension names, ``ds.dims`` the group's {dimension: size}
+    (xarray's ``Dataset.dims``), ``ds.attrs`` the group attributes."""
 
     def __init__(self, variables=None, attrs=None):
         super().__init__()
@@ -154,6 +155,15 @@ class Dataset(dict):
     @property
     def data_vars(self):
         return list(self.keys())
+
+    @property
+    def dims(self):
+        """{dimension name: size} over the group's variables, as xarray's Dataset.dims."""
+        out = {}
+        for name, dims in self.var_dims.items():
+            for d, n in zip(dims, np.shape(self[name])):
+                out.setdefault(d, int(n))
+        return out
 
     def __getattr__(self, name):
         try:
@@ -227,20 +237,36 @@ class InferenceData(dict):
         return d
 
 
+def hdi(a, hdi_prob=0.94):
+    """The highest-density interval ArviZ 0.11's ``az.hdi`` returns for one unimodal sample:
+    sort the values, take every window of floor(hdi_prob * n) + 1 consecutive order
+    statistics and keep the narrowest (the first one on ties)."""
+    a = np.sort(np.asarray(a, dtype=np.float64).ravel())
+    n = a.size
+    inc = int(np.floor(hdi_prob * n))
+    n_int = n - inc
+    if n_int <= 0:
+        raise ValueError("too few draws for an HDI of %g" % hdi_prob)
+    width = a[inc:] - a[:n_int]
+    i = int(np.argmin(width))
+    return a[i], a[i + inc]
+
+
 def summary(idata, round_to=None, hdi_prob=0.94):
     """The columns of ``az.summary`` the reference's scripts read (run_age_mcmc.py:232 prints
     it and takes ``list(trace_summary.index)`` as the variable list of the posterior
-    predictive loop): one row per posterior variable, mean, sd and the equal-tailed
-    interval of ``hdi_prob`` over all chains and draws (ArviZ's HDI is the narrowest such
-    interval; here the central one -- ArviZ is not installed)."""
+    predictive loop): one row per posterior variable, mean, sd (ddof = 1) and the
+    highest-density interval of ``hdi_prob`` over all chains and draws (``hdi``: the
+    narrowest window, as ArviZ computes it; columns hdi_3% / hdi_97% at the default 0.94)."""
     import pandas as pd
     post = idata["posterior"]
     rows = {}
     lo_q, hi_q = (1 - hdi_prob) / 2, 1 - (1 - hdi_prob) / 2
     for name in post:
         a = np.asarray(post[name], dtype=np.float64).ravel()
-        rows[name] = {"mean": a.mean(), "sd": a.std(ddof=0),
-                      "hdi_%g%%" % (100 * lo_q): np.quantile(a, lo_q), "hdi_%g%%" % (100 * hi_q): np.quantile(a, hi_q)}
+        lo, hi = hdi(a, hdi_prob)
+        rows[name] = {"mean": a.mean(), "sd": a.std(ddof=1) if a.size > 1 else 0.0,
+                      "hdi_%g%%" % (100 * lo_q): lo, "hdi_%g%%" % (100 * hi_q): hi}
     df = pd.DataFrame.from_dict(rows, orient="index")
     return df.round(round_to) if round_to is not None else df
 

@@ -1,0 +1,67 @@
+"""One rank of RCCL at world size 1 on a one-GPU box (tests/test_gpu_distributed.py): the
+device-tensor branch of distributed.LogpStepLoop.run -- two steps in flight, each step's
+all_gather_into_tensor issued async_op on RCCL's stream while the next step's log-prob
+kernel runs, step i + 2 waiting (stream dependency) before it reuses block buffer i % 2 --
+which the gloo rehearsals (host-staged, sequential) never reach.
+
+Started as a child process (never an exec of a process that touched the GPU).  Every step
+evaluates a DIFFERENT walker ensemble, and the hook before step i's evaluation snapshots the
+gathered vector of step i - 2 on the compute stream (after the wait on that step's gather,
+before anything can overwrite it), so a buffer-reuse race would show as a snapshot that
+differs from the direct evaluation of its own step.  Writes <outdir>/pipeline.npz."""
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main():
+    outdir, W, L, K = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
+    import torch
+    import torch.distributed as dist
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        from noblegas_rtd_mcmc_amd import workloads as wl
+        from noblegas_rtd_mcmc_amd.distributed import LogpStepLoop
+        from noblegas_rtd_mcmc_amd.engine import LogProb
+        spec = wl.c4_spec(L=L, N=1200)
+        thetas = [torch.from_numpy(wl.sample_prior(spec, W, np.random.default_rng(100 + i))).to(dev) for i in range(K)]
+        lp = LogProb(spec, max_walkers=W, device=0)
+        direct = torch.stack([lp(t).clone() for t in thetas])
+        loop = LogpStepLoop(None, W, dev, pipeline=True)
+        assert loop.collective and len(loop.bufs) == 2
+        binds = {(i, o.data_ptr()): lp.bind(thetas[i], o) for i in range(K) for o in loop.outs}
+        step = {"i": 0}
+
+        def evaluate(out):
+            binds[(step["i"], out.data_ptr())]()
+        loop.evaluate = evaluate
+        snaps = torch.full((K, W), float("nan"), dtype=torch.float64, device=dev)
+
+        def hook(i, before):
+            if before:
+                step["i"] = i
+                if i >= 2:
+                    snaps[i - 2].copy_(loop.gathers[i & 1][:W])
+        last = loop.run(K, hook=hook).clone()
+        snaps[K - 2].copy_(loop.gathers[(K - 2) & 1][:W])
+        snaps[K - 1].copy_(last[:W])
+        ens = loop.ensemble().clone()
+        # the sequential branch over the same process group (one step: evaluate, then gather)
+        step["i"] = K - 1
+        seq = loop.step().clone()
+        torch.cuda.synchronize()
+        np.savez(os.path.join(outdir, "pipeline.npz"), direct=direct.cpu().numpy(), snaps=snaps.cpu().numpy(),
+                 ens=ens.cpu().numpy(), seq=seq.cpu().numpy(), backend=dist.get_backend())
+        lp.close()
+    finally:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

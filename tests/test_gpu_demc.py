@@ -90,10 +90,11 @@ SHAPES = ["rtd4_exponential", "rtd4_exp_pist_flow", "rtd4_exponential-piston", "
           "joint_epm_bmm"]
 
 
-def _shape_spec(shape, L=4):
+def _shape_spec(shape, L=4, N=1200):
     """The reference's own model shapes: its RTD-only model over 4 tracers (CFC12, SF6, H3,
     He4_ter; run_age_mcmc.py) or 1 (H3), savenum 0 or 123, its CE-only model (Ne, Ar, Kr, Xe;
-    noble_gas_mcmc.py), and the joint c4 BMMs."""
+    noble_gas_mcmc.py), and the joint c4 BMMs; N ages of the input series (the reference's
+    runs: 25 256)."""
     import dataclasses
     from noblegas_rtd_mcmc_amd import workloads as wl
     from noblegas_rtd_mcmc_amd.spec import ModelSpec
@@ -105,7 +106,7 @@ def _shape_spec(shape, L=4):
                                                            gases=tuple(c.gases[i] for i in keep)))
     if shape.startswith("joint"):
         m1 = "exp_pist_flow" if "epm" in shape else "exponential"
-        return wl.c4_spec(L=L, N=1200, mod_type1=m1, mod_type2="piston",
+        return wl.c4_spec(L=L, N=N, mod_type1=m1, mod_type2="piston",
                           par_names=("tau1", "tau2", "f1") + (("eta1",) if m1 == "exp_pist_flow" else ()))
     kind, model = shape.split("_", 1)
     sv = model.endswith("_123")
@@ -113,7 +114,7 @@ def _shape_spec(shape, L=4):
     m1, _, m2 = model.partition("-")
     pn = ("tau1",) + (("tau2", "f1") if m2 else ()) + (("eta1",) if m1 == "exp_pist_flow" else ()) + \
         (("J", "thalf_cfc", "lamsf6") if sv else ())
-    base = wl.c4_spec(L=L, N=1200, mod_type1=m1, mod_type2=m2 or None, par_names=pn)
+    base = wl.c4_spec(L=L, N=N, mod_type1=m1, mod_type2=m2 or None, par_names=pn)
     keep = [0, 1, 2, 4] if kind == "rtd4" else [2]
     r = base.rtd
     return ModelSpec(n_wells=L, rtd=dataclasses.replace(r, tracers=[r.tracers[i] for i in keep], obs=r.obs[:, keep],
@@ -149,6 +150,73 @@ def test_single_launch_step_reference_shapes(shape, jac):
     for k in ("x", "lp", "samples", "logp", "accepted", "accept", "lamb", "scaling"):
         assert _same(dev[k], ref[k]), k
     assert 0 < int(dev["accepted"].sum()) < dev["accepted"].numel()
+    lp.close()
+
+
+@pytest.mark.parametrize("jac", [True, False])
+@pytest.mark.parametrize("shape", ["rtd4_exp_pist_flow_123", "rtd4_exp_pist_flow-piston_123", "rtd4_exp_pist_flow",
+                                   "rtd1_exp_pist_flow", "joint_epm_bmm"])
+def test_single_launch_step_full_series(shape, jac):
+    """The reference's own exp_pist_flow runs at their series length N = 25 256 step in ONE
+    launch (the lane-chain step for the RTD-only model, logp_fused_kernel's step for the joint
+    BMM) on the windowed channel table (ngrtd.hip epm_window), 3 wells x 67 walkers: device ==
+    torch (sampler.DEMetropolisZ over ngrtd_logp_units, itself the windowed single launch) bit
+    for bit through tuning, stop_tuning and the draws."""
+    import dataclasses
+    import torch
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+    from noblegas_rtd_mcmc_amd.sampler import DEMetropolisZ, DeviceDEMetropolisZ, Transform
+    spec = dataclasses.replace(_shape_spec(shape, L=3, N=25256), jacobian=jac)
+    W = 67
+    x0 = torch.from_numpy(wl.sample_prior(spec, W, np.random.default_rng(29))).cuda()
+    lp = LogProb(spec, max_walkers=W)
+    kw = dict(tune_interval=4, seed=25256, per_well=True)
+    lp.ctx.set_profiling(True)
+    lp.kernel_stats(reset=True)
+    dev = DeviceDEMetropolisZ(lp, **kw).run(x0, tune=12, draws=8)
+    lp.ctx.set_profiling(False)
+    ks = lp.kernel_stats(reset=True)
+    assert ks["fused"][1] == 1 and ks["rtd"][1] == 0 and ks["unit"][1] == 0, ks
+    tf = Transform.from_spec(spec) if jac else None
+    ref = DEMetropolisZ(lambda t: lp.units(t), transform=tf, **kw).run(x0, tune=12, draws=8)
+    for k in ("x", "lp", "samples", "logp", "accepted", "accept", "lamb", "scaling"):
+        assert _same(dev[k], ref[k]), k
+    assert 0 < int(dev["accepted"].sum()) < dev["accepted"].numel()
+    lp.close()
+
+
+@pytest.mark.parametrize("jac", [False, True])
+@pytest.mark.parametrize("shape", ["rtd4_exponential", "rtd4_exponential_123", "rtd1_exponential"])
+def test_lane_chain_step_exact_fallback(shape, jac):
+    """The lane-chain step's exact matrix-core fallback (dzc_exact: its tiles read the tau rows
+    of every lane of the wave from LDS): a tau1 prior U(0.05, 3) puts many proposals inside
+    the prior but below the surrogate's reach (tau < 1/2), so waves take the fallback every
+    step.  Device chains == torch chains bit for bit, one launch, and states below 1/2 are
+    visited (their proposals went through the fallback)."""
+    import dataclasses
+    import torch
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+    from noblegas_rtd_mcmc_amd.sampler import DEMetropolisZ, DeviceDEMetropolisZ, Transform
+    base = _shape_spec(shape)
+    spec = dataclasses.replace(base, rtd=dataclasses.replace(base.rtd, tau1=(0.05, 3.0)), jacobian=jac)
+    W = 301
+    x0 = torch.from_numpy(wl.sample_prior(spec, W, np.random.default_rng(23))).cuda()
+    lp = LogProb(spec, max_walkers=W)
+    kw = dict(tune_interval=4, seed=5151, per_well=True)
+    lp.ctx.set_profiling(True)
+    lp.kernel_stats(reset=True)
+    dev = DeviceDEMetropolisZ(lp, **kw).run(x0, tune=12, draws=8)
+    lp.ctx.set_profiling(False)
+    ks = lp.kernel_stats(reset=True)
+    assert ks["fused"][1] == 1, ks
+    tf = Transform.from_spec(spec) if jac else None
+    ref = DEMetropolisZ(lambda t: lp.units(t), transform=tf, **kw).run(x0, tune=12, draws=8)
+    for k in ("x", "lp", "samples", "logp", "accepted", "accept", "lamb", "scaling"):
+        assert _same(dev[k], ref[k]), k
+    tau = dev["samples"][:, spec.roles.index("tau1")]
+    assert int((tau < 0.5).sum()) > 0 and int((tau >= 0.5).sum()) > 0
     lp.close()
 
 
@@ -414,3 +482,66 @@ def test_c1_torch_sampler_path():
     m = CEModel(field_data()["obs"], ["PLM1"], max_walkers=64)
     res = m.sample(nwalkers=32, tune=40, draws=20, seed=3, tune_interval=20, sampler="torch")
     assert res["samples"].shape[0] == 20 and 0.0 < res["accept_rate"] < 1.0
+
+
+def _ulp_dist(a, b):
+    """|a - b| in units of the last place of b (float64 tensors, finite entries)."""
+    import torch
+    sp = torch.nextafter(b.abs(), torch.full_like(b, float("inf"))) - b.abs()
+    return ((a - b).abs() / sp)
+
+
+def test_fm_log_matches_torch_log():
+    """ngrtd_fm_log (the accept draw's table-driven log, sampler.fm_log on CUDA tensors)
+    against torch.log on the CPU: <= 1 ulp on random, tiny, huge, near-1 and subnormal
+    inputs, and the IEEE specials (0 -> -inf, inf -> inf, x < 0 and NaN -> NaN) exactly;
+    a non-float64 tensor is refused."""
+    import torch
+    from noblegas_rtd_mcmc_amd.sampler import fm_log
+    rng = np.random.default_rng(11)
+    x = np.concatenate([rng.uniform(0, 1, 4096), 10 ** rng.uniform(-300, 300, 4096), 1 + rng.uniform(-1e-3, 1e-3, 1024),
+                        [1.0, 2.0, 0.5, np.nextafter(1.0, 2.0), np.nextafter(1.0, 0.0), 5e-324, 2.2e-308, 1.7e308,
+                         1.1102230246251565e-16]])
+    got = fm_log(torch.from_numpy(x).cuda()).cpu()
+    ref = torch.log(torch.from_numpy(x))
+    ok = ref != 0
+    assert float(_ulp_dist(got[ok], ref[ok]).max()) <= 1.0
+    assert float(got[~ok].abs().max()) == 0.0
+    sp = torch.tensor([0.0, -0.0, float("inf"), -1.0, float("nan")], dtype=torch.float64)
+    gs = fm_log(sp.cuda()).cpu()
+    assert gs[0] == -float("inf") and gs[1] == -float("inf") and gs[2] == float("inf")
+    assert torch.isnan(gs[3]) and torch.isnan(gs[4])
+    with pytest.raises(TypeError):
+        fm_log(torch.ones(4, dtype=torch.float32, device="cuda"))
+
+
+def test_pymc3_backward_matches_torch_backward():
+    """ngrtd_pymc3_backward (the device step's backward transform, Transform.backward on CUDA
+    tensors) against the same transform in torch on the CPU (torch.exp): logodds, interval
+    and log rows within 2 / 4 / 1 ulp over random u and the edges (0, +-1, +-inf, NaN, |u| up to 800,
+    where exp over- and underflows); identity rows bitwise; a non-float64 tensor is refused."""
+    import torch
+    from noblegas_rtd_mcmc_amd.sampler import Transform
+    tf = Transform([Transform.LOGODDS, Transform.INTERVAL, Transform.LOG, Transform.NONE, Transform.INTERVAL],
+                   [0.0, 1.0, 0.0, 0.0, 50.0], [0.0, 1000.0, 0.0, 0.0, 15000.0], L=3)
+    rng = np.random.default_rng(12)
+    W = 4000
+    u = rng.normal(0, 4, (5, 3, W))
+    u[:, :, :8] = np.array([0.0, 1.0, -1.0, 40.0, -40.0, 700.0, -745.5, 800.0])[None, None, :]
+    u[:, :, 8:24] = 10 ** rng.uniform(-300, 2.9, 16) * rng.choice([-1, 1], 16)
+    u[:, 0, 24:27] = [np.inf, -np.inf, np.nan]
+    ut = torch.from_numpy(u)
+    got = tf.backward(ut.cuda()).cpu()
+    ref = tf.backward(ut)
+    both_nan = torch.isnan(got) & torch.isnan(ref)
+    assert bool((both_nan | ~torch.isnan(ref)).all()) and bool((both_nan | ~torch.isnan(got)).all())
+    fin = torch.isfinite(ref) & (ref != 0)
+    # exp <= 1 ulp; logodds 1 / (1 + e) adds an add and a division; interval s b + (1 - s) a two more
+    for row, bound in ((0, 2.0), (1, 4.0), (2, 1.0), (4, 4.0)):
+        f = fin[row]
+        assert float(_ulp_dist(got[row][f], ref[row][f]).max()) <= bound, row
+    same_special = ~fin & ~both_nan
+    assert torch.equal(got[same_special], ref[same_special])
+    assert _same(got[3], ut[3])
+    with pytest.raises(TypeError):
+        tf.backward(ut.float().cuda())

@@ -90,3 +90,22 @@ def test_bench_ranks_one_gpu(nproc):
     assert d["n_gpus"] == nproc and d["value"] > 0 and d["config"]["walkers_per_gpu"] == 2048 // nproc
     assert d["config"]["one_device"] is True and d["ensemble_finite_frac"] > 0.5
     assert "error" not in d["sampler"] and d["sampler"]["transformed"]["us_per_step"] > 0
+
+
+def test_rccl_pipeline_world_one(tmp_path):
+    """LogpStepLoop's RCCL branch on device tensors, at world size 1 on the one GPU
+    (LogpStepLoop(pipeline=True)): 12 steps over 12 different ensembles with two steps in
+    flight; every step's gathered vector equals the direct log-prob of its own ensemble bit
+    for bit (snapshots taken behind the wait on each gather), as does the sequential step()."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()), RANK="0", WORLD_SIZE="1",
+               LOCAL_RANK="0")
+    subprocess.run([sys.executable, os.path.join(REPO, "tests", "dist_gpu_pipeline.py"), str(tmp_path), "1000", "8",
+                    "12"], check=True, timeout=300, env=env, cwd=REPO)
+    z = np.load(tmp_path / "pipeline.npz")
+    assert str(z["backend"]) == "nccl"
+    direct, snaps = z["direct"], z["snaps"]
+    assert np.isfinite(direct).mean() > 0.5 and not np.array_equal(direct[0], direct[1], equal_nan=True)
+    for i in range(direct.shape[0]):
+        assert np.array_equal(snaps[i], direct[i], equal_nan=True), i
+    assert np.array_equal(z["ens"], direct[-1], equal_nan=True)
+    assert np.array_equal(z["seq"], direct[-1], equal_nan=True)

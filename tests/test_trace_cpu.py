@@ -275,3 +275,105 @@ def test_writer_tiles_large_variables_and_empty_draws(tmp_path, monkeypatch):
     lay = [bytes(d) for t, f, d in r.messages(a) if t == 0x08][0]
     bt = int.from_bytes(lay[3:11], "little")
     assert r.b[bt + 5] == 1                                # the root is an internal node (2 levels)
+
+
+def test_multilevel_chunk_btree_layout(tmp_path, monkeypatch):
+    """The v1 B-tree of a tiled variable, decoded node by node against the format's rules
+    (HDF5 spec, "Version 1 B-trees"): every node is a TREE of type 1 with its level, holds
+    1..2K entries, its left / right sibling addresses link the nodes of one level in order
+    (undefined at the ends); keys are monotone in chunk order; a node's right key (after its
+    last child) equals its right sibling's first key (the last node of a level: the dataset's
+    end key); a parent's key i is child i's first key and its key i + 1 child i's right key;
+    the leaves' chunk addresses cover every chunk once."""
+    import struct
+    from noblegas_rtd_mcmc_amd import h5lite
+    monkeypatch.setattr(h5lite, "CHUNK_BYTES", 2048)
+    rng = np.random.default_rng(2)
+    big = rng.normal(size=(3, 9001, 2))      # 432 KB in 2 KB chunks: more than 2K = 64 leaves, two levels
+    p = str(tmp_path / "tree.nc")
+    groups = {"posterior": {"attrs": {}, "dims": {"chain": np.arange(3), "draw": np.arange(9001), "well": np.arange(2)},
+                            "vars": {"T": (("chain", "draw", "well"), big, {})}}}
+    h5lite.write_netcdf4(p, groups)
+    assert np.array_equal(h5lite.read_netcdf4(p)["posterior"]["vars"]["T"][1], big)
+    r = h5lite.H5Reader(p)
+    a = r.links(r.links(r.root)["posterior"])["T"]
+    lay = [bytes(d) for t, f, d in r.messages(a) if t == 0x08][0]
+    root = int.from_bytes(lay[3:11], "little")
+    b = r.b
+    rank = 4                                               # 3 dims + the element dimension
+    ksz = 8 + 8 * rank
+    K2 = 2 * h5lite._CHUNK_K
+    UNDEF = h5lite.UNDEF
+
+    def node(addr):
+        assert b[addr:addr + 4] == b"TREE" and b[addr + 4] == 1
+        level, n = b[addr + 5], struct.unpack_from("<H", b, addr + 6)[0]
+        left, right = struct.unpack_from("<QQ", b, addr + 8)
+        q = addr + 24
+        keys, kids = [], []
+        for _ in range(n):
+            keys.append(bytes(b[q:q + ksz]))
+            kids.append(struct.unpack_from("<Q", b, q + ksz)[0])
+            q += ksz + 8
+        keys.append(bytes(b[q:q + ksz]))
+        return level, n, left, right, keys, kids
+
+    def offs(key):
+        return struct.unpack_from("<%dQ" % rank, key, 8)
+
+    levels = {}
+    def walk(addr, depth_level):
+        lv, n, left, right, keys, kids = node(addr)
+        assert lv == depth_level and 1 <= n <= K2
+        levels.setdefault(lv, []).append((addr, left, right, keys))
+        for i, kid in enumerate(kids):
+            if lv:
+                klv, kn, _, _, kkeys, _ = node(kid)
+                assert kkeys[0] == keys[i] and kkeys[-1] == keys[i + 1], (lv, i)
+                walk(kid, lv - 1)
+        return kids
+    top = node(root)[0]
+    assert top >= 1                                        # the bound above forces 2 levels
+    walk(root, top)
+    chunks = []
+    for lv, nodes in levels.items():
+        for j, (addr, left, right, keys) in enumerate(nodes):
+            assert left == (nodes[j - 1][0] if j else UNDEF) and right == (nodes[j + 1][0] if j + 1 < len(nodes) else UNDEF)
+            if j + 1 < len(nodes):
+                assert keys[-1] == nodes[j + 1][3][0], (lv, j)
+            ks = [offs(k) for k in keys]
+            assert all(x < y for x, y in zip(ks, ks[1:])), (lv, j)
+            if lv == 0:
+                chunks += ks[:-1]
+    cd = h5lite.chunk_dims(big.shape, 8)
+    want = [tuple(int(v) for v in o) + (0,) for o in np.array(np.meshgrid(
+        *[range(0, d, c) for d, c in zip(big.shape, cd)], indexing="ij")).reshape(3, -1).T]
+    assert chunks == want
+    last = offs(levels[0][-1][3][-1])
+    assert last == tuple(int(o) + int(c) for o, c in zip(want[-1][:3], cd)) + (8,)
+
+
+def test_summary_hdi_is_narrowest_interval():
+    """trace.hdi is ArviZ's HDI (the narrowest window of floor(p n) + 1 order statistics): it
+    equals a brute-force search on small samples, for a skewed posterior (Exp(1)) it is
+    [~0, ~ln(1/0.06)] where the equal-tailed interval is [0.031, 2.81], and summary() carries
+    it under ArviZ's column names; Dataset.dims is {dimension: size} as xarray's."""
+    from noblegas_rtd_mcmc_amd import trace
+    rng = np.random.default_rng(4)
+    for n in (2, 3, 17, 100):
+        a = rng.lognormal(0, 1.5, n)
+        s = np.sort(a)
+        k = int(np.floor(0.94 * n))
+        best = min(range(n - k), key=lambda i: (s[i + k] - s[i], i))
+        assert trace.hdi(a) == (s[best], s[best + k])
+    x = rng.exponential(1.0, 400000)
+    lo, hi = trace.hdi(x)
+    assert lo < 1e-3 and abs(hi - np.log(1 / 0.06)) < 0.02
+    idd = {"posterior": {"tau": (("chain", "draw"), x.reshape(4, -1))},
+           "sample_stats": {"accepted": (("chain", "draw"), np.ones((4, 100000), np.uint8))}}
+    mc = trace.InferenceData.from_dict(idd)
+    df = trace.summary(mc)
+    assert list(df.columns) == ["mean", "sd", "hdi_3%", "hdi_97%"]
+    assert df.loc["tau", "hdi_3%"] == lo and df.loc["tau", "hdi_97%"] == hi
+    assert df.loc["tau", "sd"] == x.std(ddof=1)
+    assert mc.posterior.dims == {"chain": 4, "draw": 100000}
