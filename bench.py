@@ -70,6 +70,8 @@ def parse():
                          "all-gather through host memory: the multi-rank rehearsal on a one-GPU box)")
     ap.add_argument("--one-device", action="store_true",
                     help="every rank uses cuda:0 (rehearsal of the N > 1 path on a one-GPU box; needs --backend gloo)")
+    ap.add_argument("--no-reference-runs", action="store_true",
+                    help="skip the reference's own sampling runs, timed end to end (N = 1)")
     ap.add_argument("--pipeline", action="store_true",
                     help="gather every step through LogpStepLoop's two-deep async pipeline even at N = 1 (RCCL at "
                          "world size 1: the device-tensor branch of the N > 1 step on a one-GPU box)")
@@ -230,6 +232,11 @@ def main():
             side["models"] = model_lines(args, gpu)
         except Exception as e:        # noqa: BLE001
             side["models"] = {"error": repr(e)}
+    if world == 1 and not args.no_reference_runs:
+        try:
+            side["reference_runs"] = reference_runs(gpu)
+        except Exception as e:        # noqa: BLE001
+            side["reference_runs"] = {"error": repr(e)}
     # device DEMetropolisZ on every rank (its own chains: no collective), max over ranks
     samp = None
     if not args.no_sampler:
@@ -520,6 +527,23 @@ OTHER_MODELS = (("piston", None, ""), ("piston", None, "123"), ("dispersion", No
                 ("dispersion", "piston", ""))
 
 
+N_FULL = 25256            # the reference's series length: the whole C_in_dict (run_age_mcmc.py:46,209)
+TAU2_HI_EPM2 = 1000.0     # tau2 range of a second exp_pist_flow component's lines at N = 1200
+MODEL_PMC_SUMMARIES = ("r05_model_pmc.json",)   # tools/gpu_model_pmc.sh + tools/model_pmc_summary.py, newest first
+
+
+def model_pmc_summary(key):
+    """The per-model PMC entry ("model[.savenum]@N") of the committed summary, or ({}, None)."""
+    for name in MODEL_PMC_SUMMARIES:
+        path = os.environ.get("NGRTD_MODEL_PMC_SUMMARY") or os.path.join(REPO, "profiles", name)
+        if os.path.exists(path):
+            with open(path) as f:
+                summ = json.load(f)
+            if key in summ:
+                return summ[key], os.path.relpath(path, REPO)
+    return {}, None
+
+
 def fused_instance(m1, m2, sv, C=5):
     """The logp_fused_kernel instance a joint c4-shape plan of this model runs (FULL, C = 5)."""
     lw = 32 if "2" in sv else 0
@@ -530,13 +554,18 @@ def fused_instance(m1, m2, sv, C=5):
     return "logp_fused_kernel<%d, true, 2, %d>" % (C, mix)
 
 
-def _time_plan(spec, W, gpu, steps, seed=34568):
+def _time_plan(spec, W, gpu, steps, seed=34568, tau2_hi=None):
     """Plan build time and the per-launch time of the plan's log-prob (HIP events on the
-    launch stream around `steps` back-to-back launches) on a seeded prior ensemble."""
+    launch stream around `steps` back-to-back launches) on a seeded prior ensemble (tau2 from
+    U(50, tau2_hi) instead of its prior when given, as tools/model_pmc.py)."""
     import torch
     from noblegas_rtd_mcmc_amd import workloads
     from noblegas_rtd_mcmc_amd.engine import LogProb
-    th = torch.from_numpy(workloads.sample_prior(spec, W, np.random.default_rng(seed))).cuda(gpu)
+    th = workloads.sample_prior(spec, W, np.random.default_rng(seed))
+    if tau2_hi is not None:
+        R = {r: i for i, r in enumerate(spec.roles)}
+        th[R["tau2"]] = np.random.default_rng(8).uniform(50.0, tau2_hi, th[R["tau2"]].shape)
+    th = torch.from_numpy(th).cuda(gpu)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     lp = LogProb(spec, max_walkers=W, device=gpu)
@@ -571,36 +600,66 @@ def model_lines(args, gpu):
     W = args.walkers
     res = {}
     base_ms = {("exponential", None): None}
-    for m1, m2, sv in PUBLISHED_MODELS + OTHER_MODELS:
-        a = ap.Namespace(wells=args.wells, ages=args.ages, mod_type1=m1, mod_type2=m2)
+    lines = [(m1, m2, sv, args.ages) for m1, m2, sv in PUBLISHED_MODELS + OTHER_MODELS]
+    # the published configuration at the reference's own series length (run_age_mcmc.py:46,209)
+    lines += [(m1, m2, sv, N_FULL) for m1, m2, sv in PUBLISHED_MODELS if sv and args.ages != N_FULL]
+    for m1, m2, sv, N in lines:
+        a = ap.Namespace(wells=args.wells, ages=N, mod_type1=m1, mod_type2=m2)
         spec = model_spec(a, sv)
         # (dispersion sums every age exactly: fewer launches keep the line short)
         n = max(20, steps // 10) if "dispersion" in (m1, m2) else steps
-        build_ms, ms, finite, info = _time_plan(spec, W, gpu, n)
-        if not sv:
+        # a second exp_pist_flow component masks every age of a short series once tau2 (1 - 1/eta2)
+        # passes N (the reference's g is then 0 / 0: NaN): tau2 from U(50, 1000) inside its prior
+        t2 = TAU2_HI_EPM2 if (m2 == "exp_pist_flow" and N < 15000) else None
+        build_ms, ms, finite, info = _time_plan(spec, W, gpu, n, tau2_hi=t2)
+        if not sv and N == args.ages:
             base_ms[(m1, m2)] = ms
         inst = fused_instance(m1, m2, sv)
-        pmc, pmc_path = pmc_summary("logp_fused_kernel", inst)
+        key = m1 + ("-" + m2 if m2 else "") + ("." + sv if sv else "")
         U = W * args.wells
         e = {"kernel_ms": ms, "evals_per_s": W / (ms * 1e-3), "plan_build_ms": build_ms,
              "value_amortized_20k": W * 20000 / (20000 * ms * 1e-3 + build_ms * 1e-3),
-             "finite_frac": finite, "kernel": inst, "surrogate": info.get("surrogate"),
+             "finite_frac": finite, "kernel": inst, "surrogate": info.get("surrogate"), "ages": N,
              "sampled": list(spec.rtd.par_names), "savenum": int(sv) if sv else 0,
              "published": (m1, m2, sv) in PUBLISHED_MODELS}
-        if sv and base_ms.get((m1, m2)):
+        if t2 is not None:
+            e["tau2_sample"] = ("U(50, %g) inside tau2's U(50, 15000) prior: at N = %d a second exp_pist_flow "
+                                "component with tau2 (1 - 1/eta2) > N masks every age (NaN, as the reference)" % (t2, N))
+        if sv and base_ms.get((m1, m2)) and N == args.ages:
             e["vs_savenum0_kernel"] = ms / base_ms[(m1, m2)]
-        if int(inst.rsplit(", ", 1)[1].rstrip(">")) & 64:
+        if sv and N != args.ages and ("%s.%s" % (m1 + ("-" + m2 if m2 else ""), sv)) in res:
+            e["vs_N%d_kernel" % args.ages] = ms / res["%s.%s" % (m1 + ("-" + m2 if m2 else ""), sv)]["kernel_ms"]
+        # the model's own PMC summary (tools/gpu_model_pmc.sh: one plan per profiled process)
+        mp, mp_path = model_pmc_summary("%s@N%d" % (key, N))
+        pmc, pmc_path = (mp, mp_path) if mp else pmc_summary("logp_fused_kernel", inst)
+        if mp and mp.get("fp64_flop_per_unit"):
+            fl = mp["fp64_flop_per_unit"] * U
+            e["roofline"] = {"bound": "fp64_valu", "achieved": fl / (ms * 1e-3) / 1e12, "peak": FP64_PEAK / 1e12,
+                             "unit": "TFLOP/s", "frac": fl / (ms * 1e-3) / FP64_PEAK,
+                             "traffic": mp.get("hbm_bytes_per_launch"),
+                             "lds_bank_conflict_cycles": mp.get("SQ_LDS_BANK_CONFLICT"),
+                             "flop_source": "PMC fp64_flop_per_unit %.1f x %d units (%s, this model's launches only)" % (
+                                 mp["fp64_flop_per_unit"], U, mp_path)}
+        elif int(inst.rsplit(", ", 1)[1].rstrip(">")) & 64:
             # the generic instance runs several models (piston, dispersion, BMM pairs): a PMC
             # summary keyed by kernel instance cannot say which model it counted, so no FLOP rate
             e["roofline"] = None
             e["roofline_note"] = "generic instance shared by %d model pair(s); PMC counts are per instance, not per model" % (
                 sum(1 for mm in OTHER_MODELS if fused_instance(*mm) == inst))
-        elif pmc.get("fp64_flop_per_unit") and inst in (pmc_path or ""):
+        elif pmc.get("fp64_flop_per_unit") and inst in (pmc_path or "") and N == args.ages:
             fl = pmc["fp64_flop_per_unit"] * U
             e["roofline"] = {"bound": "fp64_valu", "achieved": fl / (ms * 1e-3) / 1e12, "peak": FP64_PEAK / 1e12,
                              "unit": "TFLOP/s", "frac": fl / (ms * 1e-3) / FP64_PEAK, "traffic": pmc.get("hbm_bytes_per_launch"),
                              "flop_source": "PMC fp64_flop_per_unit %.1f x %d units (%s)" % (pmc["fp64_flop_per_unit"], U, pmc_path)}
-        res[m1 + ("-" + m2 if m2 else "") + ("." + sv if sv else "")] = e
+        else:
+            e["roofline"] = None
+        if not finite >= 0.5:
+            # a rate over a workload whose log-probs are mostly NaN / -inf says nothing: no rate
+            e["valid"] = False
+            e["invalid_reason"] = "finite_frac %.3f < 0.5" % finite
+            for k in ("evals_per_s", "value_amortized_20k", "roofline"):
+                e[k] = None
+        res[key + ("@N%d" % N if N != args.ages else "")] = e
     for name, (spec, _) in (("c2", workloads.c2(W=8)), ("c3", workloads.c3(W=8))):
         build_ms, ms, finite, info = _time_plan(spec, W, gpu, steps, seed=12345 if name == "c2" else 23456)
         res[name] = {"workload": {"c2": "CE log-prob, %d walkers x 3 wells (PLM1, PLM6, PLM7) x 5 gases" % W,
@@ -609,6 +668,116 @@ def model_lines(args, gpu):
                      "kernel_ms": ms, "evals_per_s": W / (ms * 1e-3), "plan_build_ms": build_ms,
                      "value_amortized_20k": W * 20000 / (20000 * ms * 1e-3 + build_ms * 1e-3), "finite_frac": finite}
     return res
+
+
+# The reference's published runs (age_ens_runs_mcmc/conv_traces/*.netcdf):
+# (tracers, mod_type1, mod_type2, savenum digits) per well
+REFERENCE_RUNS = ((("CFC12",), "exponential", None, ()), (("SF6",), "exponential", None, ()),
+                  (("H3",), "exponential", None, ()), (("He4_ter",), "exponential", None, ()),
+                  (("CFC12", "SF6", "H3", "He4_ter"), "exponential", None, (1, 2, 3)),
+                  (("CFC12", "SF6", "H3", "He4_ter"), "exp_pist_flow", None, (1, 2, 3)),
+                  (("CFC12", "SF6", "H3", "He4_ter"), "exponential", "piston", (1, 2, 3)),
+                  (("CFC12", "SF6", "H3", "He4_ter"), "exp_pist_flow", "piston", (1, 2, 3)))
+
+
+def _run_name(well, tracers, m1, m2, sv):
+    return "%s.%s.%s.%s.netcdf" % (well, ".".join(tracers), m1 + ("-" + m2 if m2 else ""),
+                                   "".join(str(d) for d in sv) or "0")
+
+
+def reference_runs(gpu, wells=("PLM1",)):
+    """The reference's own runs, end to end: ``conv_mcmc(...).sample_mcmc()`` (the drop-in,
+    run_age_mcmc.py:229-231 -> run_age_mcmc_utils.py:407-429) with the reference's arguments --
+    1 well, the full series (N = 25 256), DEMetropolisZ in PyMC3's transformed space, 3 chains,
+    tune 10 000, draws 10 000, tune_interval 1000, seed 123423 -- for every published model of
+    PLM1 (the four single-tracer exponential runs at savenum 0 and the four 4-tracer models at
+    savenum 123).  Wall seconds per run include the plan build (tables, surrogates), the
+    sampling and the netCDF-4 trace write, beside the shipped trace's own sampling_time (PyMC3,
+    3 processes, hardware unrecorded) and acceptance rate.  ens_dict.pk is not shipped: the
+    observation mean is the trace's observed_data and sigma the fit of
+    tests/golden/make_pymc3_accept.py (the ensemble a two-point [mu - s, mu + s]).  Then the same
+    runs for the three published wells batched into ONE call (a 3-well plan, per-well chains:
+    3 chains per well)."""
+    import dataclasses
+    import tempfile
+    import torch
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    from noblegas_rtd_mcmc_amd.run_age_mcmc_utils import conv_mcmc
+    from noblegas_rtd_mcmc_amd.sampler import sample_model
+    from noblegas_rtd_mcmc_amd.spec import ModelSpec
+    fit = {e["name"]: e for e in json.load(open(os.path.join(REPO, "tests", "golden", "pymc3_accept_fit.json"))).values()}
+    attrs = json.load(open(os.path.join(REPO, "tests", "golden", "trace_attrs.json")))
+    C_in = wl.c_in_dict()
+    tmp = tempfile.mkdtemp(prefix="ngrtd_runs_")
+    runs, cfg = [], dict(chains=3, tune=10000, draws=10000, seed=123423, tune_interval=1000)
+
+    def kwargs(well, tr, m1, m2, sv):
+        e = fit[_run_name(well, tr, m1, m2, sv)]
+        perr = wl.OBS_PERR_ALT if (m2 == "piston" and m1 == "exponential") else None
+        return e, wl.reference_run_kwargs(well, tr, m1, m2 or False, sv or (0,), e["mu"], e["sd"], perr=perr,
+                                         tau1=e["tau1"], C_in=C_in)
+    for well in wells:
+        for tr, m1, m2, sv in REFERENCE_RUNS:
+            name = _run_name(well, tr, m1, m2, sv)
+            if name not in fit:
+                continue
+            e, (okw, ckw, pkw) = kwargs(well, tr, m1, m2, sv)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            mc = conv_mcmc(well, list(tr), okw, ckw, pkw, tmp, "".join(str(d) for d in sv) or "0", max_walkers=3,
+                           device=gpu)
+            t1 = time.perf_counter()
+            mc.build_mcmc_model_joint_sT()
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            out = mc.sample_mcmc(**cfg)
+            torch.cuda.synchronize()
+            t3 = time.perf_counter()
+            ref_t = attrs.get(name, {}).get("sampling_time")
+            ref_acc = e["n_acc"] / (3.0 * 9999.0)
+            runs.append({"run": name[:-len(".netcdf")], "wall_s": t3 - t0, "plan_build_s": t2 - t1,
+                         "sample_s": float(out["sampling_time"]), "trace_write_s": (t3 - t2) - float(out["sampling_time"]),
+                         "accept_rate": float(out["accept_rate"]), "reference_sampling_time_s": ref_t,
+                         "reference_accept_rate": ref_acc, "speedup_vs_reference": (ref_t / (t3 - t0)) if ref_t else None,
+                         "posterior_tau1_mean": float(np.mean(out["posterior"]["tau1"])),
+                         "logp_evals": 3 * 20000, "steps_per_s": 20000 / float(out["sampling_time"])})
+            mc._lp.close()
+    # the three published wells in one call: their 1-well specs stacked into a 3-well plan
+    batched = []
+    for tr, m1, m2, sv in REFERENCE_RUNS:
+        names = [_run_name(w, tr, m1, m2, sv) for w in ("PLM1", "PLM6", "PLM7")]
+        if not all(n in fit for n in names):
+            continue
+        specs = []
+        for w in ("PLM1", "PLM6", "PLM7"):
+            e, (okw, ckw, pkw) = kwargs(w, tr, m1, m2, sv)
+            specs.append(conv_mcmc(w, list(tr), okw, ckw, pkw, "", "0").spec())
+        r = specs[0].rtd
+        rtd = dataclasses.replace(r, obs=np.concatenate([s.rtd.obs for s in specs]),
+                                  sd=np.concatenate([s.rtd.sd for s in specs]))
+        spec3 = ModelSpec(n_wells=3, rtd=rtd)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        x0 = torch.from_numpy(wl.sample_prior(spec3, 3, np.random.default_rng(123423))).cuda(gpu)
+        res = sample_model(spec3, 3, gpu, x0, 10000, 10000, 123423, 1000, space="transformed")
+        from noblegas_rtd_mcmc_amd import trace
+        idd = trace.inference_data(res, dataclasses.replace(spec3, jacobian=True), wells=["PLM1", "PLM6", "PLM7"],
+                                   observed=spec3.rtd.obs)
+        trace.to_netcdf(trace.InferenceData.from_dict(idd), os.path.join(tmp, "batched.netcdf"))
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        ref_t = sum(attrs.get(n, {}).get("sampling_time") or 0.0 for n in names)
+        batched.append({"runs": [n[:-len(".netcdf")] for n in names], "wall_s": wall, "sample_s": float(res["sampling_time"]),
+                        "accept_rate": float(res["accept_rate"]), "reference_sampling_time_s_sum": ref_t,
+                        "speedup_vs_reference": ref_t / wall if ref_t else None})
+    import shutil
+    shutil.rmtree(tmp, ignore_errors=True)
+    return {"config": "conv_mcmc(...).sample_mcmc(): 1 well, N = 25 256, DEMetropolisZ (PyMC3's transformed space), "
+                      "3 chains, tune 10 000, draws 10 000, tune_interval 1000, seed 123423; wall = plan build + "
+                      "sampling + netCDF-4 trace write",
+            "runs": runs, "batched_3_wells": batched,
+            "total_wall_s": sum(r["wall_s"] for r in runs),
+            "reference_total_s": sum(r["reference_sampling_time_s"] or 0.0 for r in runs)}
 
 
 def exact_line(args, spec, theta, Wb, C, N):

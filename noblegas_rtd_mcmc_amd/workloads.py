@@ -241,3 +241,81 @@ def shard_walkers(W_total, rank, world):
     per = (W_total + world - 1) // world
     lo = min(W_total, rank * per)
     return lo, min(W_total, lo + per)
+
+
+def c_in_dict(names=("CFC11", "CFC12", "CFC113", "SF6", "He4_ter", "H3")):
+    """The reference's input-series dict C_in_dict (age_ens_runs_mcmc/C_in_dict.pk, read at
+    run_age_mcmc.py:46) rebuilt from the shipped data: per tracer a one-column DataFrame indexed
+    by age tau = 25255 ... 0 (oldest first), column 'H3_tu' for H3 (prep.py:207-219)."""
+    import pandas as pd
+    out = {}
+    for name in names:
+        s = atmos_series(name)
+        idx = np.flip(s.idx_by_age).astype(np.int64)
+        out[name] = pd.DataFrame({("H3_tu" if name == "H3" else name): np.flip(s.c_by_age)},
+                                 index=pd.Index(idx, name="tau"))
+    return out
+
+
+# run_age_mcmc.py:100-114: the analytical error added to every tracer (PLM6's contaminated SF6:
+# 10.0); the commented dict of :104-108 is what the published exponential-piston run used (the
+# sigma fits of tests/golden/make_pymc3_accept.py show it)
+OBS_PERR = {"CFC12": 0.05, "SF6": 0.05, "H3": 0.05, "He3": 0.05, "He4_ter": 0.05}
+OBS_PERR_ALT = {"CFC12": 0.15, "SF6": 0.15, "H3": 0.10, "He3": 0.15, "He4_ter": 0.10}
+
+
+def reference_run_kwargs(well, tracers, mod_type1="exponential", mod_type2=False, savenum=(0,), mu=None, sd=None,
+                         perr=None, tau1=(1.0, 1000.0), C_in=None):
+    """The keyword dicts run_age_mcmc.py:122-224 hands to conv_mcmc for one well: okw (the
+    observation ensemble and its percent error), pkw (priors and par_names, :143-198), ckw
+    (convolution kwargs per tracer, :203-224).  ens_dict.pk is not shipped, so the ensemble is
+    the two-point [mu - s, mu + s] with s = sd - mu perr: the same mean mu and
+    std(ens) + mu perr = sd that conv_mcmc computes (run_age_mcmc_utils.py:353-356)."""
+    import copy
+    from .spec import LOG10_J_PRIOR_MU
+    alt = perr is OBS_PERR_ALT
+    perr = dict(perr or OBS_PERR)
+    if well == "PLM6" and not alt and perr.get("SF6") == 0.05:
+        perr["SF6"] = 10.0
+    C_in = C_in if C_in is not None else c_in_dict()
+    okw = {}
+    for k, t in enumerate(tracers):
+        s = float(sd[k]) - float(mu[k]) * perr[t]
+        okw[t] = {"obs_df": np.array([float(mu[k]) - s, float(mu[k]) + s]), "obs_perr": perr[t]}
+    pkw = {"tau1_low": float(tau1[0]), "tau1_high": float(tau1[1])}
+    par_names = ["tau1"]
+    if mod_type2:
+        pkw.update(tau2_low=50.0, tau2_high=15000.0, f1_low=0.01, f1_high=0.99)
+        par_names += ["tau2", "f1", "f2"]
+    for c, m in ((1, mod_type1), (2, mod_type2)):
+        if m == "exp_pist_flow":
+            pkw["eta%d_low" % c], pkw["eta%d_high" % c] = 1.0, 5.0
+            par_names += ["eta%d" % c]
+        if m == "dispersion":
+            pkw["D%d_low" % c], pkw["D%d_high" % c] = 0.01, 2.0
+            par_names += ["D%d" % c]
+    if "He4_ter" in tracers and 1 in savenum:
+        pkw["J_mu"], pkw["J_sd"] = LOG10_J_PRIOR_MU, 0.33
+        par_names += ["J"]
+    if "CFC12" in tracers and 2 in savenum:
+        pkw["cfc_thalf_lo"], pkw["cfc_thalf_hi"] = 5.0, 35.0
+        par_names += ["thalf_cfc"]
+    if "SF6" in tracers and 3 in savenum:
+        par_names += ["lamsf6"]
+    pkw["par_names"] = par_names
+    ckw = {"mod_type1": mod_type1, "mod_type2": mod_type2}
+    for t in tracers:
+        ckw[t] = {}
+        if t in ("CFC11", "CFC12", "CFC113", "SF6"):
+            ckw[t]["C_t"] = copy.deepcopy(C_in[t])
+        elif t == "He4_ter":
+            ckw[t]["C_t"] = copy.deepcopy(C_in[t]) * 0.0
+            ckw[t]["rad_accum"] = "4He"
+        elif t == "He3":
+            ckw[t]["C_t"] = copy.deepcopy(C_in["H3"])
+            ckw[t]["t_half"] = 12.34
+            ckw[t]["rad_accum"] = "3He"
+        elif t == "H3":
+            ckw[t]["C_t"] = copy.deepcopy(C_in["H3"])
+            ckw[t]["t_half"] = 12.34
+    return okw, ckw, pkw
