@@ -439,6 +439,13 @@ int ngrtd_surrogate_check(const double* cols, int32_t C, int64_t N, double dtp, 
 int ngrtd_c0_check(double nu_lo, double nu_hi, double* coef, int32_t* e0, int32_t* n_pieces,
                    double* max_abs_err);
 
+/* Host-only (no GPU): the exp_pist_flow channel-table rows a plan with tau1 ~ U(., tau_hi),
+ * eta1 ~ U(., eta_hi) stages in LDS at series length N, age grid tp_k = k + dtp (k >= 1)
+ * (ngrtd.hip epm_window: the head block of every in-support unit's first unmasked age of
+ * convolution_integral_utils.py:189's mask, plus 64 rows); *rows = -1 when the priors bound no
+ * window smaller than the series.  Exposed so that tests check the bound against the mask. */
+int ngrtd_epm_window_check(double tau_hi, double eta_hi, double dtp, int32_t N, int32_t* rows);
+
 #ifdef __cplusplus
 }
 #endif

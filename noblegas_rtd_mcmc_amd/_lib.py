@@ -114,6 +114,7 @@ PROTOTYPES = {
     "ngrtd_fm_log": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]),
     "ngrtd_surrogate_check": (C.c_int, [_dp, C.c_int32, C.c_int64, C.c_double, _dp, _dp]),
     "ngrtd_c0_check": (C.c_int, [C.c_double, C.c_double, _dp, _i32p, _i32p, _dp]),
+    "ngrtd_epm_window_check": (C.c_int, [C.c_double, C.c_double, C.c_double, C.c_int32, _i32p]),
 }
 
 

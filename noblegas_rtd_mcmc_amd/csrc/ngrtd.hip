@@ -2280,6 +2280,12 @@ int ngrtd_surrogate_check(const double* cols, int32_t C, int64_t N, double dtp, 
     return NGRTD_OK;
 }
 
+int ngrtd_epm_window_check(double tau_hi, double eta_hi, double dtp, int32_t N, int32_t* rows) {
+    if (!rows || N < 1) return NGRTD_EINVAL;
+    *rows = epm_window_rows(tau_hi, eta_hi, dtp, N);
+    return NGRTD_OK;
+}
+
 int ngrtd_c0_check(double nu_lo, double nu_hi, double* coef, int32_t* e0, int32_t* n_pieces, double* max_abs_err) {
     if (!e0 || !n_pieces || !max_abs_err) return NGRTD_EINVAL;
     std::vector<double> t;
