@@ -667,7 +667,8 @@ static size_t fused_lds(const RtdArgs& a, const UnitArgs& u, int dz_p = 0) {
     // generic instances with a dispersion component: the same table, and disp_aux [2N]
     const bool disp = a.disp_aux && (a.mod[0] == MOD_DISP || a.mod[1] == MOD_DISP);
     const size_t epm_tab = (a.mod[0] == MOD_EPM || a.mod[1] == MOD_EPM || disp)
-                               ? (size_t)epm_lds_doubles(a.epm_nw, cheb_cp(a.C)) + (disp ? 2 * (size_t)a.N : 0) : 0;
+                               ? (size_t)epm_lds_doubles(a.epm_nw, cheb_cp(a.C)) + (disp ? 2 * (size_t)a.N + kDispExpTab : 0)
+                               : 0;
     const size_t dz = (size_t)dz_p * kFusedUnits;                          // DZ step: the proposals
     // generic instances, dispersion split over the unit's two waves: the theta waves' partial sums
     const size_t xch = (disp && a.disp_split > 0) ? (size_t)(a.C + 1) * kFusedUnits : 0;
@@ -1684,12 +1685,14 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
         }
         a.disp_aux = nullptr;
         if (a.mod[0] == MOD_DISP || a.mod[1] == MOD_DISP) {   // gen_exact's per-age factors
-            std::vector<double> aux(2 * (size_t)p->N);
+            std::vector<double> aux(2 * (size_t)p->N + kDispExpTab);
             for (int k = 0; k < p->N; ++k) {
                 const double tp = k == 0 ? p->tp0 : (double)k + p->dtp;
                 aux[k] = 1.0 / tp;
                 aux[p->N + k] = std::pow(tp, -1.5);
             }
+            // the dispersion loop's exponential table (fexp_tab): 2^(j / T), long double rounded
+            for (int j = 0; j < kDispExpTab; ++j) aux[2 * (size_t)p->N + j] = (double)exp2l((long double)j / kDispExpTab);
             NG_CHECK(upload(ctx, p->table.disp, aux.data(), aux.size()));
             a.disp_aux = p->table.disp.d();
         }

@@ -57,7 +57,9 @@ struct RtdArgs {
     int32_t epm_diag;       // timing diagnostics only (NGRTD_EPM_DIAG, tools/epm_probe.py): bit 0 skips
                             // the head, bit 1 the tail surrogate, bit 2 the exact tails (wrong results)
     // dispersion components of the generic single-launch instances (gen_exact): per age k,
-    // 1 / tp_k at [k] and tp_k^(-3/2) at [N + k]; null when the plan has no dispersion component
+    // 1 / tp_k at [k] and tp_k^(-3/2) at [N + k], then the kDispExpTab values 2^(j / kDispExpTab)
+    // of the dispersion loop's exponential (fexp_tab) at [2N + j]; null when the plan has no
+    // dispersion component
     const double* disp_aux;
     // 1: K = C and tracer t owns exactly channel t (unit_conc's direct path)
     int32_t conc_ident;
@@ -72,6 +74,8 @@ struct RtdArgs {
 // split at the block boundary B = (m / S + 1) S into a head of < S + 1 ages (Horner over the
 // LDS-staged channel table) and q^(B - m) T_{B/S}(1 / beta) from the block-tail surrogates.
 constexpr int kEpmBlock = 16;
+// entries of the dispersion loop's exponential table (RtdArgs::disp_aux; ngrtd_kernels.hpp fexp_tab)
+constexpr int kDispExpTab = 256;
 
 // Chebyshev surrogate of Z_c(tau) = s01(tau) sum_{j>=0} A_{c,1+j} exp(-j / tau) (the
 // exponential RTD channel sums times s01 = exp(-(tp_1 - tp_0) / tau)) for every channel c,

@@ -471,6 +471,16 @@ struct ThetaPre {
     double tau1, nub;
 };
 
+// The per-well data a kernel staged in LDS (UnitArgs::wd_src copied to its LDS block), passed
+// beside the UnitArgs the unit functions read every other field from.  The multi-step
+// DEMetropolisZ instances read UnitArgs through the opaque kernarg pointer: a per-step copy of
+// the whole struct with these pointers redirected parked its scalars in VGPR lanes (round 4:
+// ~660 v_readlane / 212 v_writelane in the step loop); with the view each field is loaded where
+// it is used.  Null: the UnitArgs' own pointers.
+struct WdView {
+    const double *ce_obs, *ce_lam, *ce_hll_sum, *ce_Emin, *rtd_obs, *rtd_lam, *rtd_hll_sum, *c0_tab;
+};
+
 __device__ __forceinline__ void theta_preload(const UnitArgs& a, int64_t u, ThetaPre& t) {
 #pragma unroll
     for (int i = 0; i < 6; ++i) t.ce[i] = a.ce_on ? a.theta[(int64_t)a.row_ce[i] * a.U + u] : 0.0;
@@ -568,7 +578,7 @@ __device__ __forceinline__ double beta_block(const UnitArgs& a, int64_t u, const
 template <int REFB = 0>
 __device__ __forceinline__ double unit_logp_theta(const UnitArgs& a, int64_t u, int l,
                                                   const ThetaPre* pre = nullptr, bool full = false,
-                                                  bool full_jac = false) {
+                                                  bool full_jac = false, const WdView* wv = nullptr) {
     const bool want_like = full || (a.flags & NGRTD_WANT_LIKE);
     const bool want_prior = full || (a.flags & NGRTD_WANT_PRIOR);
     const bool jac = full ? full_jac : (a.flags & NGRTD_WANT_JACOBIAN) != 0;
@@ -581,7 +591,7 @@ __device__ __forceinline__ double unit_logp_theta(const UnitArgs& a, int64_t u, 
         if (want_prior) lp += normal_logp(p[3], a.m_mu, a.m_tau, a.m_log_tau_2pi);
         if (want_like || (!full && a.ce_out)) {
             // noble_gas_mcmc.py:229-250 parameter mapping, then ce_exc_wrapper (:205-213)
-            const double Emin = a.ce_Emin[l];
+            const double Emin = (wv ? wv->ce_Emin : a.ce_Emin)[l];
             const double Ae_log = p[0] * (a.logA_max - a.logA_min) + a.logA_min;
             const double F_log = p[1] * (a.logF_max - a.logF_min) + a.logF_min;
             const double E = p[2] * (a.E_max - Emin) + Emin;
@@ -596,8 +606,9 @@ __device__ __forceinline__ double unit_logp_theta(const UnitArgs& a, int64_t u, 
             if (!full && a.ce_out)
                 for (int j = 0; j < a.G; ++j) a.ce_out[(int64_t)j * a.U + u] = mod[j];
             if (want_like)
-                lp += st_block_inu<kMaxGas>(a.G, a.ce_obs + l * a.G, mod, a.ce_lam + l * a.G, a.ce_hll_sum[l], nu,
-                                             rm[1], C0Tab{a.c0_tab, a.c0_e0, a.c0_np});
+                lp += st_block_inu<kMaxGas>(a.G, (wv ? wv->ce_obs : a.ce_obs) + l * a.G, mod,
+                                             (wv ? wv->ce_lam : a.ce_lam) + l * a.G, (wv ? wv->ce_hll_sum : a.ce_hll_sum)[l],
+                                             nu, rm[1], C0Tab{wv ? wv->c0_tab : a.c0_tab, a.c0_e0, a.c0_np});
         }
     }
     if (full || a.rtd_on) {
@@ -636,12 +647,13 @@ __device__ __forceinline__ double unit_logp_theta(const UnitArgs& a, int64_t u, 
 template <int NMAX = kMaxTracer>
 __device__ __forceinline__ double unit_like_rtd(const UnitArgs& a, int64_t u, int l, const double* conc,
                                                 const ThetaPre* pre = nullptr, bool full = false,
-                                                const double* inu = nullptr) {
+                                                const double* inu = nullptr, const WdView* wv = nullptr) {
     if (!full && (!a.rtd_on || !(a.flags & NGRTD_WANT_LIKE))) return 0.0;
     const double nub = pre ? pre->nub : a.theta[(int64_t)a.row_nu * a.U + u];
     const double nu = nub * (a.rnu_max - a.rnu_min) + a.rnu_min;
-    return st_block_inu<NMAX>(a.K, a.rtd_obs + l * a.K, conc, a.rtd_lam + l * a.K, a.rtd_hll_sum[l], nu,
-                              inu ? *inu : 1.0 / nu, C0Tab{a.c0_tab, a.c0_e0, a.c0_np});
+    return st_block_inu<NMAX>(a.K, (wv ? wv->rtd_obs : a.rtd_obs) + l * a.K, conc, (wv ? wv->rtd_lam : a.rtd_lam) + l * a.K,
+                              (wv ? wv->rtd_hll_sum : a.rtd_hll_sum)[l], nu, inu ? *inu : 1.0 / nu,
+                              C0Tab{wv ? wv->c0_tab : a.c0_tab, a.c0_e0, a.c0_np});
 }
 
 // full log-prob contribution of one unit (same addition order as the reference's sum)
@@ -1841,7 +1853,7 @@ __device__ __forceinline__ void walker_out(double* logp, const DemcAccept& d, co
 template <int C, bool FULL, bool SEQ, int MIX>
 __device__ __forceinline__ void fused_exact(const RtdArgs& a, const UnitArgs& ul, int WB, int64_t w0, int uw,
                                             bool mine, int64_t mu, int ml, double nub, double* conc,
-                                            double& like, LwDecay lw = LwDecay{0.0, 0.0}) {
+                                            double& like, LwDecay lw = LwDecay{0.0, 0.0}, const WdView* wv = nullptr) {
     constexpr bool LW = (MIX & 32) != 0;
     constexpr int NT = mfma_tiles(C);
     const int col = threadIdx.x & 15;
@@ -1909,7 +1921,7 @@ __device__ __forceinline__ void fused_exact(const RtdArgs& a, const UnitArgs& ul
         double num2[C];
         if (MIX & 1) piston_num<C, LW>(a, mu, num2, lw.lam);
         mfma_unit_conc<C, LW>(a, mu, bu, yy, conc, (MIX & 1) ? num2 : nullptr, lw.lam, yw, bw);
-        like = unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL);
+        like = unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL, nullptr, wv);
     }
 }
 
@@ -2277,6 +2289,28 @@ __device__ __forceinline__ void epm_piston_row(const RtdArgs& a, const double* t
 #define NGRTD_GEN_DISP_UNROLL 4
 #endif
 constexpr int kGenDispUnroll = NGRTD_GEN_DISP_UNROLL;
+
+// e^(y ln2 / T), T = kDispExpTab, for an argument already scaled by T / ln 2 (the dispersion
+// loop forms y with the scale folded into its per-unit coefficients, so the reduction needs no
+// product): y = T k' + j + f, |f| <= 1/2, e^(y ln2/T) = 2^k' 2^(j/T) e^r, r = f ln2/T, with
+// 2^(j/T) from the plan's table (tab, LDS: the correctly rounded values) and e^r - 1 by its
+// Taylor series to r^4/24 (|r| <= ln2/512: truncation < 4e-17 relative).  <= ~1.2 ulp.  y <= 0
+// here (no clamp: a very negative y saturates the int conversion and ldexp gives 0; NaN
+// propagates through the polynomial).
+__device__ __forceinline__ double fexp_tab(double y, const double* tab) {
+    constexpr double LN2_T = 6.93147180559945309417e-01 / kDispExpTab;
+    const double kd = rint(y);
+    const double r = (y - kd) * LN2_T;
+    double q = 1.0 / 24.0;
+    q = fma_k(q, r, 1.0 / 6.0);
+    q = fma_k(q, r, 0.5);
+    const double p = fma(r * r, q, r);                   // e^r - 1
+    const int k = (int)kd;
+    const double th = tab[k & (kDispExpTab - 1)];
+    return ldexp(fma(th, p, th), k >> 8);
+}
+static_assert(kDispExpTab == 256, "fexp_tab: k >> 8");
+
 template <int C, bool LW, bool DSP = false>
 __device__ __forceinline__ void gen_exact(const RtdArgs& a, int mod, bool on, double tau, double eta, double D,
                                           double lam, double* num, double& den, const double* tl = nullptr,
@@ -2285,18 +2319,32 @@ __device__ __forceinline__ void gen_exact(const RtdArgs& a, int mod, bool on, do
 #pragma unroll
     for (int c = 0; c <= C; ++c) s[c] = 0.0;
     if (DSP && mod == MOD_DISP && tl && dl) {
+        // The dispersion weight with its exponent expanded (round 5):
+        //   w_k = k1 tp_k^(-3/2) e^(x_k),  x_k = -(1 - tp/tau)^2 (tau/tp) / (4D) = -k2 (tau / tp + tp / tau - 2)
+        // so x_k T/ln2 = ya / tp_k + yb tp_k + yc is two FMAs over the per-age 1/tp_k of disp_aux
+        // (ya, yb, yc per unit: the T/ln2 of the exponential's reduction folded in, fexp_tab on the
+        // plan's 256-entry table: a degree-4 polynomial instead of fexp's degree 6),
+        // and the per-unit factor k1 = sqrt(tau / (4 pi D)) multiplies the sums once at the end
+        // (the normalised weights do not depend on it; its NaN / inf still reach the sums, so
+        // invalid tau and D give the reference's NaN).  tp_k advances by exact additions of 1.
+        // The sums differ from the reference's per-age expression by rounding only: near the
+        // mode the expanded exponent cancels to ~k2 ulp (k2 <= 25 over the D prior): < 2e-14
+        // relative, inside the 1e-12 parity bar.  LW: the per-unit decay e^(-lam tp_k) is
+        // re-anchored by an fexp at the first age of every unrolled group and advanced by
+        // e^(-lam) within it (<= 3 products: a few ulp).
         if (__any(on)) {
             constexpr int CP = cheb_cp(C);
+            constexpr double LTE = kDispExpTab / 6.93147180559945309417e-01;   // T / ln 2
             const double rt = 1.0 / tau;
             const double k1 = sqrt(tau / (4. * kPi * D));
             const double k2 = 1.0 / (4. * D);
+            const double ya = -(k2 * tau) * LTE, yb = -(k2 * rt) * LTE, yc = (2.0 * k2) * LTE;
+            const double rl = LW ? fexp(-lam) : 1.0;         // e^(-lam): one year of decay
             const int N = a.N;
-            // one age: its weight (the generic loop's expressions) into the sums, in age order
-            auto age = [&](int k, double ia, double ip, const double* row) {
-                const double tp = (k == 0) ? a.tp0 : ((double)k + a.dtp);
-                const double d = 1.0 - tp * rt;
-                const double w = (k1 * ip) * fexp(-((d * d) * (tau * ia)) * k2);
-                const double wd = LW ? w * fexp(-lam * tp) : w;
+            const double* etab = dl + 2 * N;                  // 2^(j / kDispExpTab)
+            auto age = [&](double tp, double ia, double ip, const double* row, double dec) {
+                const double w = ip * fexp_tab(fma(ya, ia, fma(yb, tp, yc)), etab);
+                const double wd = LW ? w * dec : w;
 #pragma unroll
                 for (int c = 0; c < C; ++c) s[c] = fma(row[c], (LW && a.chan_lamw[c]) ? wd : w, s[c]);
                 s[C] += w;
@@ -2304,6 +2352,13 @@ __device__ __forceinline__ void gen_exact(const RtdArgs& a, int mod, bool on, do
             constexpr int UA = kGenDispUnroll;
             const int ke = age1 < 0 ? N : age1;             // ages [age0, ke)
             int k = age0;
+            if (k == 0 && k < ke) {                          // age 0: tp_0 = 1e-5 + dtp (not on the unit grid)
+                double row[C];
+                epm_row_load<C>(tl + epm_row(0, CP), row);
+                age(a.tp0, dl[0], dl[N], row, LW ? fexp(-lam * a.tp0) : 1.0);
+                k = 1;
+            }
+            double tp = (double)k + a.dtp;                   // tp_k = k + dtp (k >= 1), exact
             for (; k + UA <= ke; k += UA) {                 // UA ages' LDS operands first, then their sums
                 double ia[UA], ip[UA], row[UA][C];
 #pragma unroll
@@ -2312,14 +2367,22 @@ __device__ __forceinline__ void gen_exact(const RtdArgs& a, int mod, bool on, do
                     ip[j] = dl[N + k + j];
                     epm_row_load<C>(tl + epm_row(k + j, CP), row[j]);
                 }
+                double dec = LW ? fexp(-lam * tp) : 1.0;
 #pragma unroll
-                for (int j = 0; j < UA; ++j) age(k + j, ia[j], ip[j], row[j]);
+                for (int j = 0; j < UA; ++j) {
+                    age(tp, ia[j], ip[j], row[j], dec);
+                    tp += 1.0;
+                    if (LW) dec *= rl;
+                }
             }
             for (; k < ke; ++k) {
                 double row[C];
                 epm_row_load<C>(tl + epm_row(k, CP), row);
-                age(k, dl[k], dl[N + k], row);
+                age(tp, dl[k], dl[N + k], row, LW ? fexp(-lam * tp) : 1.0);
+                tp += 1.0;
             }
+#pragma unroll
+            for (int c = 0; c <= C; ++c) s[c] *= k1;
         }
 #pragma unroll
         for (int c = 0; c < C; ++c) num[c] = s[c];
@@ -2595,7 +2658,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     const bool EPMS = EPM || (GEN && (a.mod[0] == MOD_EPM || a.mod[1] == MOD_EPM)) || DISPS;
     double* tabl = cheb + a.cheb_np * PST;                // EPM: the channel table (epm_row)
     double* daux = tabl + (EPMS ? epm_lds_doubles(a.epm_nw, CP) : 0);   // DISPS: disp_aux [2N]
-    double* wd = daux + (DISPS ? 2 * a.N : 0);
+    double* wd = daux + (DISPS ? 2 * a.N + kDispExpTab : 0);
     constexpr int kWdRegs = (4 * 64 * kFusedWaves + NTH - 1) / NTH;
     double wv[kWdRegs];
 #pragma unroll
@@ -2638,7 +2701,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         }
     }
     if (DISPS)
-        for (int i = tid; i < 2 * a.N; i += NTH) daux[i] = a.disp_aux[i];
+        for (int i = tid; i < 2 * a.N + kDispExpTab; i += NTH) daux[i] = a.disp_aux[i];
 #pragma unroll
     for (int r = 0; r < kWdRegs; ++r) {
         const int i = tid + r * NTH;
@@ -2722,7 +2785,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         const int pi = (DZ && mwl >= WB) ? mi : ml * WB + mwl;
         double* tabl = cheb + a.cheb_np * PST;
         double* daux = tabl + (EPMS ? epm_lds_doubles(a.epm_nw, CP) : 0);
-        double* wd = daux + (DISPS ? 2 * a.N : 0);
+        double* wd = daux + (DISPS ? 2 * a.N + kDispExpTab : 0);
         double* thl = wd + uk.wd_n;
         double* propl = thl + (((MIX & 4) && DZ) ? dk.P * kFusedUnits : 0);   // DZ: [P][512] proposals
         DzLds dl;                                         // DZ: the chains' LDS state (or none)
@@ -2734,23 +2797,30 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             dl.sc = dl.lamb + kFusedUnits;
             dl.nat = (lds_i32*)(dl.sc + kFusedUnits);
         }
+        // the per-well data in LDS: the plain instances redirect a copy of the arguments, the DZ
+        // instances read the kernarg struct itself beside a view of the LDS pointers (WdView: a
+        // redirected copy would live in SGPRs across the step loop -- 238 spilled, ~10% per step)
         UnitArgs ul = uk;
+        WdView wv{};
         {
             const int nce = uk.ce_on ? L * uk.G : 0, nrt = uk.rtd_on ? L * uk.K : 0;
             double* q = wd;
             if (uk.ce_on) {
-                ul.ce_obs = q; q += nce;
-                ul.ce_lam = q; q += nce;
-                ul.ce_hll_sum = q; q += L;
-                ul.ce_Emin = q; q += L;
+                ul.ce_obs = wv.ce_obs = q; q += nce;
+                ul.ce_lam = wv.ce_lam = q; q += nce;
+                ul.ce_hll_sum = wv.ce_hll_sum = q; q += L;
+                ul.ce_Emin = wv.ce_Emin = q; q += L;
             }
             if (uk.rtd_on) {
-                ul.rtd_obs = q; q += nrt;
-                ul.rtd_lam = q; q += nrt;
-                ul.rtd_hll_sum = q;
+                ul.rtd_obs = wv.rtd_obs = q; q += nrt;
+                ul.rtd_lam = wv.rtd_lam = q; q += nrt;
+                ul.rtd_hll_sum = wv.rtd_hll_sum = q;
             }
-            if (uk.c0_tab) ul.c0_tab = wd + (uk.c0_tab - uk.wd_src);
+            wv.c0_tab = uk.c0_tab ? wd + (uk.c0_tab - uk.wd_src) : nullptr;
+            if (uk.c0_tab) ul.c0_tab = wv.c0_tab;
         }
+        const UnitArgs& uu = DZ ? uk : ul;
+        const WdView* wvp = DZ ? &wv : nullptr;
         DzStep sj{};
         if (DZ) sj = dz_step(dk.sch, js);
         const int64_t log_off = (int64_t)js * W;
@@ -2799,7 +2869,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             }
         }
         double th = 0.0, like = 0.0;
-        if (do_theta) th = mvalid ? unit_logp_theta<REFB>(ul, mu, ml, &tp, FULL, (MIX & 4) != 0) : 0.0;
+        if (do_theta) th = mvalid ? unit_logp_theta<REFB>(uu, mu, ml, &tp, FULL, (MIX & 4) != 0, wvp) : 0.0;
         // RTD waves without a unit (blocks of fewer walkers than kFusedUnits / L: fused_wb) skip
         // their body (wave-uniform)
         const bool rtd_w = do_rtd && (DZ || __any(mvalid));
@@ -2815,11 +2885,13 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
                 const double t2 = mvalid ? a.theta[(int64_t)a.row_tau[1] * a.U + mu] : 1.0;
                 gen_component<C, ROLES == 2, LW>(a, uk, cheb, tabl, 1, mvalid, mu, prior_on, t2, thx, n2, r2, nan2);
             }
-            unit_conc<C>(a, mu, n1, r1, conc, two ? n2 : nullptr, r2);
+            // (two calls, not one with a runtime-selected num2 pointer: that put n2 in scratch)
+            if (two) unit_conc<C>(a, mu, n1, r1, conc, n2, r2);
+            else unit_conc<C>(a, mu, n1, r1, conc);
             if (nan1 || nan2)
                 for (int t = 0; t < a.K; ++t) conc[t] = __builtin_nan("");
             const double rnu = 1.0 / (tp.nub * (uk.rnu_max - uk.rnu_min) + uk.rnu_min);
-            like = mvalid ? unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL, &rnu) : 0.0;
+            like = mvalid ? unit_like_rtd<C>(uu, mu, ml, conc, &tp, FULL, &rnu, wvp) : 0.0;
             if (!FULL && a.conc && mvalid)                        // forward(): model concentrations
                 for (int t = 0; t < a.K; ++t) a.conc[(int64_t)t * a.U + mu] = conc[t];
         } else if (DSPI) {
@@ -2875,11 +2947,12 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             }
           if (rtd_w) {
             double conc[kMaxTracer];
-            unit_conc<C>(a, mu, n1, r1, conc, two ? n2 : nullptr, r2);
+            if (two) unit_conc<C>(a, mu, n1, r1, conc, n2, r2);
+            else unit_conc<C>(a, mu, n1, r1, conc);
             if (nan1 || nan2)
                 for (int t = 0; t < a.K; ++t) conc[t] = __builtin_nan("");
             const double rnu = 1.0 / (tp.nub * (uk.rnu_max - uk.rnu_min) + uk.rnu_min);
-            like = mvalid ? unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL, &rnu) : 0.0;
+            like = mvalid ? unit_like_rtd<C>(uu, mu, ml, conc, &tp, FULL, &rnu, wvp) : 0.0;
             if (!FULL && a.conc && mvalid)                        // forward(): model concentrations
                 for (int t = 0; t < a.K; ++t) a.conc[(int64_t)t * a.U + mu] = conc[t];
           }
@@ -2902,7 +2975,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
                 unit_conc<C>(a, mu, num, dd * rr[0], conc, (MIX & 1) ? num2 : nullptr);
                 if (wnan)
                     for (int t = 0; t < a.K; ++t) conc[t] = __builtin_nan("");
-                like = mvalid ? unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL, &rr[1]) : 0.0;
+                like = mvalid ? unit_like_rtd<C>(uu, mu, ml, conc, &tp, FULL, &rr[1], wvp) : 0.0;
             }
             if (!FULL && a.conc && mvalid)                        // forward(): model concentrations
                 for (int t = 0; t < a.K; ++t) a.conc[(int64_t)t * a.U + mu] = conc[t];
@@ -2966,7 +3039,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
                 unit_conc<C>(a, mu, num, rr[0], conc, (MIX & 1) ? num2 : nullptr);
                 if (cnan)
                     for (int t = 0; t < a.K; ++t) conc[t] = __builtin_nan("");
-                like = mvalid ? unit_like_rtd<C>(ul, mu, ml, conc, &tp, FULL, &rr[1]) : 0.0;
+                like = mvalid ? unit_like_rtd<C>(uu, mu, ml, conc, &tp, FULL, &rr[1], wvp) : 0.0;
             }
             NGRTD_PROBE(2);
             if (__any(bad)) {                                     // wave-uniform: exact channel sums
@@ -2978,7 +3051,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
                     __threadfence_block();
                 }
                 // ROLES = 2: one tile per pass keeps the exact path inside the 128-VGPR budget
-                fused_exact<C, FULL, ROLES == 2, MIX>(a, ul, WB, w0, uw, mvalid && bad, mu, ml, tp.nub, conc, like, lw);
+                fused_exact<C, FULL, ROLES == 2, MIX>(a, uu, WB, w0, uw, mvalid && bad, mu, ml, tp.nub, conc, like, lw, wvp);
             }
             if (!FULL && a.conc && mvalid)                        // forward(): model concentrations
                 for (int t = 0; t < a.K; ++t) a.conc[(int64_t)t * a.U + mu] = conc[t];

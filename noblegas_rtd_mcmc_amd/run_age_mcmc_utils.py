@@ -168,13 +168,15 @@ class conv_mcmc:
         return self._lp
 
     def sample_mcmc(self, chains=3, tune=10000, draws=10000, seed=123423, tune_interval=1000, sampler="device",
-                    space="transformed", nwalkers=None):
+                    space="transformed", nwalkers=None, start="test_point"):
         """DEMetropolisZ on the GPU log-prob (replaces mc.sample, :407-429, with its
         arguments as defaults: 3 chains, tune 10 000, draws 10 000, seed 123423,
         tune_interval 1000), one chain per walker of this one well.  sampler: "device"
         (ngrtd_demcz_run, device-resident) or "torch" (sampler.DEMetropolisZ on torch ops;
         same random stream).  space: "transformed" (PyMC3's: logodds / interval / log; the
         log-prob adds the Jacobian) or "natural".  ``nwalkers``: alias of ``chains``.
+        ``start``: "test_point" (PyMC3's default for a non-NUTS step: every chain starts at
+        model.test_point, workloads.test_point) or "prior" (independent prior draws, seeded).
 
         Returns what the reference returns, the InferenceData of the run
         (trace.InferenceData: ``out['posterior'][v]`` is [chain, draw], the indexing of
@@ -182,11 +184,14 @@ class conv_mcmc:
         accepted, lamb, scaling, roles, ...) beside the groups."""
         import torch
         from .sampler import sample_model
-        from .workloads import sample_prior
+        from .workloads import sample_prior, test_point
         if nwalkers is not None:
             chains = nwalkers
+        if start not in ("test_point", "prior"):
+            raise ValueError('start must be "test_point" or "prior"')
         lp = self.build_mcmc_model_joint_sT()
-        x0 = sample_prior(lp.spec, chains, np.random.default_rng(seed))
+        x0 = test_point(lp.spec, chains) if start == "test_point" else sample_prior(lp.spec, chains,
+                                                                                     np.random.default_rng(seed))
         x = torch.from_numpy(x0).to("cuda:%d" % self.device)
         res = sample_model(lp.spec, self.max_walkers, self.device, x, tune, draws, seed, tune_interval, sampler,
                            space, cache=self.__dict__)

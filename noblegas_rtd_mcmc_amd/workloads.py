@@ -115,6 +115,37 @@ def sample_prior(spec, W, rng):
     return th
 
 
+def test_point(spec, W):
+    """PyMC3 3.11's starting point of every chain when mc.sample gets no `start` and the step is
+    not NUTS (run_age_mcmc_utils.py:412-417, noble_gas_mcmc.py:410-415): model.test_point, each
+    free variable's default test value -- the median where the distribution defines one, else the
+    mean (Distribution.get_test_val over defaults ("median", "mean", "mode")): Uniform (a + b)/2,
+    Normal mu, Beta a/(a + b) (mean: no median), HalfNormal sigma sqrt(2/pi) (mean).  theta SoA
+    [P][L][W], every chain at that point."""
+    L = spec.n_wells
+    th = np.zeros((spec.n_params, L, W))
+    c, r = spec.ce, spec.rtd
+    for i, role in enumerate(spec.roles):
+        if role.endswith("_beta"):
+            ab = {"Ae_beta": c.beta_Ae if c else None, "F_beta": c.beta_F if c else None, "E_beta": c.beta_E if c else None,
+                  "b_beta": c.beta_b if c else None, "nu_ce_beta": c.beta_nu if c else None,
+                  "nu_rtd_beta": r.beta_nu if r else None, "thalf_cfc_beta": r.beta_thalf if r else None}[role]
+            v = ab[0] / (ab[0] + ab[1])
+        elif role == "m":
+            v = c.m_mu
+        elif role in ("tau1", "tau2", "f1", "eta1", "eta2", "D1", "D2"):
+            lo, hi = getattr(r, role)
+            v = (lo + hi) / 2.0
+        elif role == "J":
+            v = r.J_mu
+        elif role == "lamsf6":
+            v = r.lamsf6_sd * np.sqrt(2.0 / np.pi)
+        else:
+            raise ValueError(role)
+        th[i] = v
+    return th
+
+
 def prior_sd(spec):
     """Prior standard deviation of every theta row [P][L] -- a per-parameter proposal scale
     (PyMC3 DEMetropolisZ's S) that puts the U(-S, S) * scaling noise of every dimension on
