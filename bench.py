@@ -603,6 +603,8 @@ def model_lines(args, gpu):
     lines = [(m1, m2, sv, args.ages) for m1, m2, sv in PUBLISHED_MODELS + OTHER_MODELS]
     # the published configuration at the reference's own series length (run_age_mcmc.py:46,209)
     lines += [(m1, m2, sv, N_FULL) for m1, m2, sv in PUBLISHED_MODELS if sv and args.ages != N_FULL]
+    # ... and dispersion there (not published; its generic instance stages nothing of the series)
+    lines += [("dispersion", None, "123", N_FULL)] if args.ages != N_FULL else []
     for m1, m2, sv, N in lines:
         a = ap.Namespace(wells=args.wells, ages=N, mod_type1=m1, mod_type2=m2)
         spec = model_spec(a, sv)

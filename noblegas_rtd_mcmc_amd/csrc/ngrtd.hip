@@ -75,6 +75,7 @@ struct TableDev {
     double cheb_err = -1.0; // max relative error measured by the validation (-1: not built)
     DevBuf epm;             // exp_pist_flow block-tail surrogates (epm_prepare)
     DevBuf disp;            // dispersion components: 1 / tp_k, tp_k^(-3/2) (RtdArgs::disp_aux)
+    DevBuf disp_rows;       // ... with the channel rows, one 64-B row per age (RtdArgs::disp_rows)
     bool epm_ok = false;
     double epm_err = -1.0;
     int epm_nb = 0, epm_p0 = 0, epm_np = 0;
@@ -664,11 +665,11 @@ constexpr size_t kFusedMaxLds = 157 * 1024;   // gfx950: 160 KiB per workgroup, 
 static size_t fused_lds(const RtdArgs& a, const UnitArgs& u, int dz_p = 0) {
     // EPM: the channel table, rows of cheb_cp(C) doubles in LDS (the kernel's layout; the global
     // table's rows are a.CP = (C + 1) & ~1, shorter for C = 2, 4)
-    // generic instances with a dispersion component: the same table, and disp_aux [2N]
-    const bool disp = a.disp_aux && (a.mod[0] == MOD_DISP || a.mod[1] == MOD_DISP);
-    const size_t epm_tab = (a.mod[0] == MOD_EPM || a.mod[1] == MOD_EPM || disp)
-                               ? (size_t)epm_lds_doubles(a.epm_nw, cheb_cp(a.C)) + (disp ? 2 * (size_t)a.N + kDispExpTab : 0)
-                               : 0;
+    // generic instances with a dispersion component: fexp_tab's table (the per-age operands are
+    // read from global memory with scalar loads, any N)
+    const bool disp = a.disp_aux && a.disp_rows && (a.mod[0] == MOD_DISP || a.mod[1] == MOD_DISP);
+    const size_t epm_tab = ((a.mod[0] == MOD_EPM || a.mod[1] == MOD_EPM) ? (size_t)epm_lds_doubles(a.epm_nw, cheb_cp(a.C)) : 0) +
+                           (disp ? (size_t)kDispExpTab : 0);
     const size_t dz = (size_t)dz_p * kFusedUnits;                          // DZ step: the proposals
     // generic instances, dispersion split over the unit's two waves: the theta waves' partial sums
     const size_t xch = (disp && a.disp_split > 0) ? (size_t)(a.C + 1) * kFusedUnits : 0;
@@ -844,7 +845,7 @@ static bool gen_path(const RtdArgs& a0, const UnitArgs& u) {
     const bool exp_c = a.mod[0] == MOD_EXP || a.mod[1] == MOD_EXP;
     const bool epm_c = a.mod[0] == MOD_EPM || a.mod[1] == MOD_EPM;
     const bool disp_c = a.mod[0] == MOD_DISP || a.mod[1] == MOD_DISP;
-    if ((exp_c && !a.cheb) || (epm_c && !a.epm) || (disp_c && !a.disp_aux)) return false;
+    if ((exp_c && !a.cheb) || (epm_c && !a.epm) || (disp_c && (!a.disp_aux || !a.disp_rows))) return false;
     return a.C >= 1 && a.C <= 5 && lw_ok(a, u) && u.L >= 1 && u.L <= kFusedUnits &&
            fused_lds(a, u) <= kFusedMaxLds && gen_instance_exists(a.C, full_plan(a, u), gen_mix(a, u));
 }
@@ -1684,6 +1685,7 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
             }
         }
         a.disp_aux = nullptr;
+        a.disp_rows = nullptr;
         if (a.mod[0] == MOD_DISP || a.mod[1] == MOD_DISP) {   // gen_exact's per-age factors
             std::vector<double> aux(2 * (size_t)p->N + kDispExpTab);
             for (int k = 0; k < p->N; ++k) {
@@ -1695,6 +1697,16 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
             for (int j = 0; j < kDispExpTab; ++j) aux[2 * (size_t)p->N + j] = (double)exp2l((long double)j / kDispExpTab);
             NG_CHECK(upload(ctx, p->table.disp, aux.data(), aux.size()));
             a.disp_aux = p->table.disp.d();
+            if (p->table.C <= kDispRow - 2) {   // the single-launch loop's interleaved rows
+                std::vector<double> rows((size_t)p->N * kDispRow, 0.0);
+                for (int k = 0; k < p->N; ++k) {
+                    for (int c = 0; c < p->table.C; ++c) rows[(size_t)k * kDispRow + c] = p->table.cols_host[c][k];
+                    rows[(size_t)k * kDispRow + kDispRow - 2] = aux[k];
+                    rows[(size_t)k * kDispRow + kDispRow - 1] = aux[p->N + k];
+                }
+                NG_CHECK(upload(ctx, p->table.disp_rows, rows.data(), rows.size()));
+                a.disp_rows = p->table.disp_rows.d();
+            }
         }
         u.rtd_on = 1; u.K = K;
         u.rtd_obs = p->rtd_obs.d(); u.rtd_sd = p->rtd_sd.d(); u.conc = p->conc.d();

@@ -61,6 +61,10 @@ struct RtdArgs {
     // of the dispersion loop's exponential (fexp_tab) at [2N + j]; null when the plan has no
     // dispersion component
     const double* disp_aux;
+    // ... and the dispersion loop's per-age operands interleaved, one 64-B row per age k
+    // (read with scalar loads: the rows are wave-uniform): A_{c,k} at [k][c] (c < C <= 5),
+    // 1 / tp_k at [k][6], tp_k^(-3/2) at [k][7]
+    const double* disp_rows;
     // 1: K = C and tracer t owns exactly channel t (unit_conc's direct path)
     int32_t conc_ident;
     // generic instances with a dispersion component (ngrtd.hip gen_disp_split): its ages
@@ -76,6 +80,8 @@ struct RtdArgs {
 constexpr int kEpmBlock = 16;
 // entries of the dispersion loop's exponential table (RtdArgs::disp_aux; ngrtd_kernels.hpp fexp_tab)
 constexpr int kDispExpTab = 256;
+// doubles per age of RtdArgs::disp_rows (one s_load_dwordx16)
+constexpr int kDispRow = 8;
 
 // Chebyshev surrogate of Z_c(tau) = s01(tau) sum_{j>=0} A_{c,1+j} exp(-j / tau) (the
 // exponential RTD channel sums times s01 = exp(-(tp_1 - tp_0) / tau)) for every channel c,

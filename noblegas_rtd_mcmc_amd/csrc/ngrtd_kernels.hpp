@@ -1019,8 +1019,11 @@ __device__ __forceinline__ void mfma_unit_conc(const RtdArgs& a, int64_t u, doub
     if (LW) num[0] = fexp(-lam * a.tp0) * (a.tab0[0] + fexp(-bw * d01) * yw);
     unit_conc<C, ST>(a, u, num, rden, conc, num2);    // (num2: the piston component of a BMM)
     const double tau = a.theta[(int64_t)a.row_tau[0] * a.U + u];
-    if (exp_rtd_nan(a, tau))
-        for (int t = 0; t < a.K; ++t) conc[t] = __builtin_nan("");
+    if (exp_rtd_nan(a, tau)) {
+#pragma unroll
+        for (int t = 0; t < kMaxTracer; ++t)
+            if (t < a.K) conc[t] = __builtin_nan("");
+    }
 }
 
 // lanes with tq = t finish the units of tile t: select that tile's sums
@@ -2311,19 +2314,23 @@ __device__ __forceinline__ double fexp_tab(double y, const double* tab) {
 }
 static_assert(kDispExpTab == 256, "fexp_tab: k >> 8");
 
+// Wave-uniform global data read through the constant address space: the loads are scalar
+// (s_load, the scalar cache) -- no LDS or vector-memory instruction per age.  Read-only.
+typedef __attribute__((address_space(4))) const double k_f64;
+
 template <int C, bool LW, bool DSP = false>
 __device__ __forceinline__ void gen_exact(const RtdArgs& a, int mod, bool on, double tau, double eta, double D,
-                                          double lam, double* num, double& den, const double* tl = nullptr,
-                                          const double* dl = nullptr, int age0 = 0, int age1 = -1) {
+                                          double lam, double* num, double& den, const double* etl = nullptr,
+                                          int age0 = 0, int age1 = -1) {
     double s[C + 1];
 #pragma unroll
     for (int c = 0; c <= C; ++c) s[c] = 0.0;
-    if (DSP && mod == MOD_DISP && tl && dl) {
+    if (DSP && mod == MOD_DISP && etl) {
         // The dispersion weight with its exponent expanded (round 5):
         //   w_k = k1 tp_k^(-3/2) e^(x_k),  x_k = -(1 - tp/tau)^2 (tau/tp) / (4D) = -k2 (tau / tp + tp / tau - 2)
-        // so x_k T/ln2 = ya / tp_k + yb tp_k + yc is two FMAs over the per-age 1/tp_k of disp_aux
+        // so x_k T/ln2 = ya / tp_k + yb tp_k + yc is two FMAs over the per-age 1/tp_k
         // (ya, yb, yc per unit: the T/ln2 of the exponential's reduction folded in, fexp_tab on the
-        // plan's 256-entry table: a degree-4 polynomial instead of fexp's degree 6),
+        // plan's 256-entry table in LDS, etl: a degree-4 polynomial instead of fexp's degree 6),
         // and the per-unit factor k1 = sqrt(tau / (4 pi D)) multiplies the sums once at the end
         // (the normalised weights do not depend on it; its NaN / inf still reach the sums, so
         // invalid tau and D give the reference's NaN).  tp_k advances by exact additions of 1.
@@ -2332,8 +2339,10 @@ __device__ __forceinline__ void gen_exact(const RtdArgs& a, int mod, bool on, do
         // relative, inside the 1e-12 parity bar.  LW: the per-unit decay e^(-lam tp_k) is
         // re-anchored by an fexp at the first age of every unrolled group and advanced by
         // e^(-lam) within it (<= 3 products: a few ulp).
+        // The per-age operands (channel row, 1/tp_k, tp_k^(-3/2): a.disp_rows) are the same for
+        // every lane: scalar loads, one 64-B row per age, so the loop's only LDS read is the
+        // table lookup and nothing of the series is staged (any N).
         if (__any(on)) {
-            constexpr int CP = cheb_cp(C);
             constexpr double LTE = kDispExpTab / 6.93147180559945309417e-01;   // T / ln 2
             const double rt = 1.0 / tau;
             const double k1 = sqrt(tau / (4. * kPi * D));
@@ -2341,44 +2350,44 @@ __device__ __forceinline__ void gen_exact(const RtdArgs& a, int mod, bool on, do
             const double ya = -(k2 * tau) * LTE, yb = -(k2 * rt) * LTE, yc = (2.0 * k2) * LTE;
             const double rl = LW ? fexp(-lam) : 1.0;         // e^(-lam): one year of decay
             const int N = a.N;
-            const double* etab = dl + 2 * N;                  // 2^(j / kDispExpTab)
-            auto age = [&](double tp, double ia, double ip, const double* row, double dec) {
-                const double w = ip * fexp_tab(fma(ya, ia, fma(yb, tp, yc)), etab);
+            const k_f64* rows = (const k_f64*)a.disp_rows;
+            auto age = [&](double tp, const double* r, double dec) {
+                const double w = r[kDispRow - 1] * fexp_tab(fma(ya, r[kDispRow - 2], fma(yb, tp, yc)), etl);
                 const double wd = LW ? w * dec : w;
 #pragma unroll
-                for (int c = 0; c < C; ++c) s[c] = fma(row[c], (LW && a.chan_lamw[c]) ? wd : w, s[c]);
+                for (int c = 0; c < C; ++c) s[c] = fma(r[c], (LW && a.chan_lamw[c]) ? wd : w, s[c]);
                 s[C] += w;
+            };
+            auto load = [&](int k, double* r) {
+#pragma unroll
+                for (int j = 0; j < kDispRow; ++j) r[j] = rows[(int64_t)k * kDispRow + j];
             };
             constexpr int UA = kGenDispUnroll;
             const int ke = age1 < 0 ? N : age1;             // ages [age0, ke)
             int k = age0;
             if (k == 0 && k < ke) {                          // age 0: tp_0 = 1e-5 + dtp (not on the unit grid)
-                double row[C];
-                epm_row_load<C>(tl + epm_row(0, CP), row);
-                age(a.tp0, dl[0], dl[N], row, LW ? fexp(-lam * a.tp0) : 1.0);
+                double r[kDispRow];
+                load(0, r);
+                age(a.tp0, r, LW ? fexp(-lam * a.tp0) : 1.0);
                 k = 1;
             }
             double tp = (double)k + a.dtp;                   // tp_k = k + dtp (k >= 1), exact
-            for (; k + UA <= ke; k += UA) {                 // UA ages' LDS operands first, then their sums
-                double ia[UA], ip[UA], row[UA][C];
+            for (; k + UA <= ke; k += UA) {                 // UA ages' rows first, then their sums
+                double r[UA][kDispRow];
 #pragma unroll
-                for (int j = 0; j < UA; ++j) {
-                    ia[j] = dl[k + j];
-                    ip[j] = dl[N + k + j];
-                    epm_row_load<C>(tl + epm_row(k + j, CP), row[j]);
-                }
+                for (int j = 0; j < UA; ++j) load(k + j, r[j]);
                 double dec = LW ? fexp(-lam * tp) : 1.0;
 #pragma unroll
                 for (int j = 0; j < UA; ++j) {
-                    age(tp, ia[j], ip[j], row[j], dec);
+                    age(tp, r[j], dec);
                     tp += 1.0;
                     if (LW) dec *= rl;
                 }
             }
             for (; k < ke; ++k) {
-                double row[C];
-                epm_row_load<C>(tl + epm_row(k, CP), row);
-                age(tp, dl[k], dl[N + k], row, LW ? fexp(-lam * tp) : 1.0);
+                double r[kDispRow];
+                load(k, r);
+                age(tp, r, LW ? fexp(-lam * tp) : 1.0);
                 tp += 1.0;
             }
 #pragma unroll
@@ -2495,7 +2504,7 @@ __device__ __forceinline__ void gen_component(const RtdArgs& a, const UnitArgs& 
         // split (dispersion, staged tables): this wave's ages [split, N); rden holds the raw
         // normaliser sum until the caller adds the theta wave's [0, split)
         if (DSP) {
-            gen_exact<C, LW, true>(a, mod, ex, tau, eta, D, lw.lam, en, den, daux ? tabl : nullptr, daux, split);
+            gen_exact<C, LW, true>(a, mod, ex, tau, eta, D, lw.lam, en, den, daux, split);
         } else {
             gen_exact<C, LW>(a, mod, ex, tau, eta, D, lw.lam, en, den);
         }
@@ -2654,11 +2663,11 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     // generic instances with MIX bit 7 (a plan with a dispersion component; the others keep
     // the code without it)
     constexpr bool DSPI = GEN && (MIX & 128) != 0;
-    const bool DISPS = DSPI && a.disp_aux && (a.mod[0] == MOD_DISP || a.mod[1] == MOD_DISP);
-    const bool EPMS = EPM || (GEN && (a.mod[0] == MOD_EPM || a.mod[1] == MOD_EPM)) || DISPS;
+    const bool DISPS = DSPI && a.disp_aux && a.disp_rows && (a.mod[0] == MOD_DISP || a.mod[1] == MOD_DISP);
+    const bool EPMS = EPM || (GEN && (a.mod[0] == MOD_EPM || a.mod[1] == MOD_EPM));
     double* tabl = cheb + a.cheb_np * PST;                // EPM: the channel table (epm_row)
-    double* daux = tabl + (EPMS ? epm_lds_doubles(a.epm_nw, CP) : 0);   // DISPS: disp_aux [2N]
-    double* wd = daux + (DISPS ? 2 * a.N + kDispExpTab : 0);
+    double* daux = tabl + (EPMS ? epm_lds_doubles(a.epm_nw, CP) : 0);   // DISPS: fexp_tab's table
+    double* wd = daux + (DISPS ? kDispExpTab : 0);
     constexpr int kWdRegs = (4 * 64 * kFusedWaves + NTH - 1) / NTH;
     double wv[kWdRegs];
 #pragma unroll
@@ -2701,7 +2710,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         }
     }
     if (DISPS)
-        for (int i = tid; i < 2 * a.N + kDispExpTab; i += NTH) daux[i] = a.disp_aux[i];
+        for (int i = tid; i < kDispExpTab; i += NTH) daux[i] = a.disp_aux[2 * a.N + i];
 #pragma unroll
     for (int r = 0; r < kWdRegs; ++r) {
         const int i = tid + r * NTH;
@@ -2785,7 +2794,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
         const int pi = (DZ && mwl >= WB) ? mi : ml * WB + mwl;
         double* tabl = cheb + a.cheb_np * PST;
         double* daux = tabl + (EPMS ? epm_lds_doubles(a.epm_nw, CP) : 0);
-        double* wd = daux + (DISPS ? 2 * a.N + kDispExpTab : 0);
+        double* wd = daux + (DISPS ? kDispExpTab : 0);
         double* thl = wd + uk.wd_n;
         double* propl = thl + (((MIX & 4) && DZ) ? dk.P * kFusedUnits : 0);   // DZ: [P][512] proposals
         DzLds dl;                                         // DZ: the chains' LDS state (or none)
@@ -2888,12 +2897,18 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             // (two calls, not one with a runtime-selected num2 pointer: that put n2 in scratch)
             if (two) unit_conc<C>(a, mu, n1, r1, conc, n2, r2);
             else unit_conc<C>(a, mu, n1, r1, conc);
-            if (nan1 || nan2)
-                for (int t = 0; t < a.K; ++t) conc[t] = __builtin_nan("");
+            if (nan1 || nan2) {
+#pragma unroll
+                for (int t = 0; t < kMaxTracer; ++t)
+                    if (t < a.K) conc[t] = __builtin_nan("");
+            }
             const double rnu = 1.0 / (tp.nub * (uk.rnu_max - uk.rnu_min) + uk.rnu_min);
             like = mvalid ? unit_like_rtd<C>(uu, mu, ml, conc, &tp, FULL, &rnu, wvp) : 0.0;
-            if (!FULL && a.conc && mvalid)                        // forward(): model concentrations
-                for (int t = 0; t < a.K; ++t) a.conc[(int64_t)t * a.U + mu] = conc[t];
+            if (!FULL && a.conc && mvalid) {                      // forward(): model concentrations
+#pragma unroll
+                for (int t = 0; t < kMaxTracer; ++t)   // unrolled: conc stays in registers
+                    if (t < a.K) a.conc[(int64_t)t * a.U + mu] = conc[t];
+            }
         } else if (DSPI) {
             // generic components: the first from tau (prologue), the second (BMM) from tau2.
             // A dispersion component's exact age sum is split over the unit's two waves
@@ -2909,7 +2924,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
                 const double Dc = mvalid ? a.theta[(int64_t)a.row_D[dcomp] * a.U + mu] : 1.0;
                 double lam = 0.0;
                 if (LW) lam = lw_decay(a, tc, mvalid ? a.theta[(int64_t)a.row_thalf * a.U + mu] : 0.5).lam;
-                gen_exact<C, LW, true>(a, MOD_DISP, mvalid, tc, 1.0, Dc, lam, pn, pd, tabl, daux, 0, dsp);
+                gen_exact<C, LW, true>(a, MOD_DISP, mvalid, tc, 1.0, Dc, lam, pn, pd, daux, 0, dsp);
 #pragma unroll
                 for (int c = 0; c < C; ++c) xch[c * kFusedUnits + mi] = pn[c];
                 xch[C * kFusedUnits + mi] = pd;
@@ -2949,12 +2964,18 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             double conc[kMaxTracer];
             if (two) unit_conc<C>(a, mu, n1, r1, conc, n2, r2);
             else unit_conc<C>(a, mu, n1, r1, conc);
-            if (nan1 || nan2)
-                for (int t = 0; t < a.K; ++t) conc[t] = __builtin_nan("");
+            if (nan1 || nan2) {
+#pragma unroll
+                for (int t = 0; t < kMaxTracer; ++t)
+                    if (t < a.K) conc[t] = __builtin_nan("");
+            }
             const double rnu = 1.0 / (tp.nub * (uk.rnu_max - uk.rnu_min) + uk.rnu_min);
             like = mvalid ? unit_like_rtd<C>(uu, mu, ml, conc, &tp, FULL, &rnu, wvp) : 0.0;
-            if (!FULL && a.conc && mvalid)                        // forward(): model concentrations
-                for (int t = 0; t < a.K; ++t) a.conc[(int64_t)t * a.U + mu] = conc[t];
+            if (!FULL && a.conc && mvalid) {                      // forward(): model concentrations
+#pragma unroll
+                for (int t = 0; t < kMaxTracer; ++t)   // unrolled: conc stays in registers
+                    if (t < a.K) a.conc[(int64_t)t * a.U + mu] = conc[t];
+            }
           }
         } else if (EPM && rtd_w) {
             double conc[kMaxTracer];
@@ -2973,12 +2994,18 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
                     if (LW) num2[0] *= fexp(-lam * (ix == 0 ? a.tp0 : (double)ix + a.dtp));
                 }
                 unit_conc<C>(a, mu, num, dd * rr[0], conc, (MIX & 1) ? num2 : nullptr);
-                if (wnan)
-                    for (int t = 0; t < a.K; ++t) conc[t] = __builtin_nan("");
+                if (wnan) {
+#pragma unroll
+                    for (int t = 0; t < kMaxTracer; ++t)
+                        if (t < a.K) conc[t] = __builtin_nan("");
+                }
                 like = mvalid ? unit_like_rtd<C>(uu, mu, ml, conc, &tp, FULL, &rr[1], wvp) : 0.0;
             }
-            if (!FULL && a.conc && mvalid)                        // forward(): model concentrations
-                for (int t = 0; t < a.K; ++t) a.conc[(int64_t)t * a.U + mu] = conc[t];
+            if (!FULL && a.conc && mvalid) {                      // forward(): model concentrations
+#pragma unroll
+                for (int t = 0; t < kMaxTracer; ++t)   // unrolled: conc stays in registers
+                    if (t < a.K) a.conc[(int64_t)t * a.U + mu] = conc[t];
+            }
         } else if (!GEN && rtd_w) {
             // The surrogate channel sums, the concentrations and the RTD likelihood.  Lanes
             // whose tau the surrogate does not cover evaluate piece 0 here and are redone
@@ -3037,8 +3064,11 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
                 double num2[C];
                 if (MIX & 1) piston_num_tau<C, LW>(a, tau2, num2, lw.lam);
                 unit_conc<C>(a, mu, num, rr[0], conc, (MIX & 1) ? num2 : nullptr);
-                if (cnan)
-                    for (int t = 0; t < a.K; ++t) conc[t] = __builtin_nan("");
+                if (cnan) {
+#pragma unroll
+                    for (int t = 0; t < kMaxTracer; ++t)
+                        if (t < a.K) conc[t] = __builtin_nan("");
+                }
                 like = mvalid ? unit_like_rtd<C>(uu, mu, ml, conc, &tp, FULL, &rr[1], wvp) : 0.0;
             }
             NGRTD_PROBE(2);
@@ -3053,8 +3083,11 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
                 // ROLES = 2: one tile per pass keeps the exact path inside the 128-VGPR budget
                 fused_exact<C, FULL, ROLES == 2, MIX>(a, uu, WB, w0, uw, mvalid && bad, mu, ml, tp.nub, conc, like, lw, wvp);
             }
-            if (!FULL && a.conc && mvalid)                        // forward(): model concentrations
-                for (int t = 0; t < a.K; ++t) a.conc[(int64_t)t * a.U + mu] = conc[t];
+            if (!FULL && a.conc && mvalid) {                      // forward(): model concentrations
+#pragma unroll
+                for (int t = 0; t < kMaxTracer; ++t)   // unrolled: conc stays in registers
+                    if (t < a.K) a.conc[(int64_t)t * a.U + mu] = conc[t];
+            }
         }
         NGRTD_PROBE(3);
         if (DZ && kDzPrefetch)   // the next step's partner rows, theta lanes (loads only; zeros elsewhere and

@@ -102,3 +102,28 @@ def test_epm_full_series_window_edges(model):
     assert ok.all(), (np.nonzero(~ok)[0], got[~ok], ref[~ok])
     assert np.isnan(ref).any() and np.isneginf(ref).any() and np.isfinite(ref).sum() > 20
     lp.close()
+
+
+@pytest.mark.parametrize("model", ["dispersion", "dispersion-piston", "exponential-dispersion"])
+@pytest.mark.parametrize("variant", ["rtd_only_123", "joint"])
+def test_dispersion_full_series_single_launch_vs_oracle(model, variant):
+    """The dispersion models at N = 25 256 in ONE launch (the generic instances read the per-age
+    operands with scalar loads: nothing of the series is staged in LDS, any N), 512 walkers x
+    4 wells from the priors, vs the vectorised oracle on 96 walkers; determinism."""
+    import torch
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+    spec = _spec(model, variant, L=4)
+    W = 512
+    th = wl.sample_prior(spec, W, np.random.default_rng(2527))
+    lp = LogProb(spec, max_walkers=W)
+    dev = torch.from_numpy(th).cuda()
+    a = _one_launch(lp, dev)
+    assert np.array_equal(a, lp(dev).cpu().numpy())
+    sel = sorted(set(range(64)) | set(np.random.default_rng(4).choice(W, 32, replace=False).tolist()))
+    from oracle.vectorized import log_prob_vec
+    ref = log_prob_vec(spec, np.ascontiguousarray(th[:, :, sel]))
+    ok = _close(a[sel], ref)
+    assert ok.all(), (np.array(sel)[~ok], a[sel][~ok], ref[~ok])
+    assert np.isfinite(a).mean() > 0.5
+    lp.close()
