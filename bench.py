@@ -482,6 +482,18 @@ def sampler_line(args, spec, lp, theta, gpu):
                                   "ce_only": "CE-only, Ne Ar Kr Xe"}[name]
             pl.close()
             del th
+        # generic model pairs (run_age_mcmc.py:61-70 without a specialised instance) on the joint
+        # c4 shape: one launch per chunk on the generic DZ instances (MIX 64 | 8, + 128)
+        for name, (m1, m2, pn) in (("joint_dispersion", ("dispersion", None, ("tau1", "D1"))),
+                                   ("joint_exponential-exponential", ("exponential", "exponential", ("tau1", "tau2", "f1")))):
+            sp = dataclasses.replace(workloads.c4_spec(L=L, N=spec.rtd.n_ages, mod_type1=m1, mod_type2=m2, par_names=pn),
+                                     jacobian=True)
+            th = torch.from_numpy(workloads.sample_prior(sp, W, np.random.default_rng(34569))).to(theta.device)
+            pl = LogProb(sp, max_walkers=W, device=gpu)
+            out[name] = _dz_time(pl, th, True, True, tune, n)
+            out[name]["model"] = "joint CE + 5 tracers, %s, PyMC3 transformed space" % (m1 + ("-" + m2 if m2 else ""))
+            pl.close()
+            del th
     out["method"] = ("PyMC3 DEMetropolisZ, device-resident (ngrtd_demcz_run: one launch per <= 256 steps, "
                      "each block stepping its own chains); primary = per-well chains (one PyMC3 model per well, "
                      "as the reference runs them) in PyMC3's transformed space")

@@ -907,15 +907,31 @@ static void launch_fused_c(const RtdArgs& a, const UnitArgs& u, int WB, int64_t 
 // FULL instance with C = 5 channels (the c3 / c4 / published-model workloads), the role-split
 // layout, at most kDzMaxP parameter rows, and the proposals fitting in LDS.  -1: not
 // available (ngrtd_demcz_run then runs the proposal kernel + log-prob kernel pair).
+// The generic model pairs (gen_path: dispersion, piston first, exponential / exp_pist_flow
+// seconds) step on the generic DZ instances (MIX 64 | 8, + 128 with a dispersion component)
+// when they carry no sampled half-life.
+static void dz_window(RtdArgs& a, const UnitArgs& u, bool gen) {
+    if (gen) {
+        gen_cheb_window(a, u);
+        gen_disp_split(a, u);
+    } else {
+        cheb_window(a, u);
+    }
+}
 static int dz_mix(const RtdArgs& a0, const UnitArgs& u, int P, bool transformed) {
     RtdArgs a = a0;
-    cheb_window(a, u);
     const bool joint = full_plan(a, u);
     const bool jac = (u.flags & NGRTD_WANT_JACOBIAN) != 0;
     // transformed chains <=> the Jacobian instance (its proposals go through backward())
-    if (!joint || jac != transformed || a.C != 5 || fused_roles() != 2 || P < 1 || P > kDzMaxP || !fused_path(a, u) ||
-        fused_lds(a, u, transformed ? P : 0) > kFusedMaxLds)
-        return -1;
+    if (!joint || jac != transformed || a.C != 5 || fused_roles() != 2 || P < 1 || P > kDzMaxP) return -1;
+    const bool gen = !fused_path(a0, u) && gen_path(a0, u);
+    dz_window(a, u, gen);
+    if (gen) {
+        if (a.row_thalf >= 0 || fused_lds(a, u, transformed ? P : 0) > kFusedMaxLds) return -1;
+        const int r = 8 | (jac ? 4 : 0) | (gen_mix(a, u) & (64 | 128));
+        return fused_dz_instance_exists(r) ? r : -1;
+    }
+    if (!fused_path(a, u) || fused_lds(a, u, transformed ? P : 0) > kFusedMaxLds) return -1;
     const int mix = (a.mod[1] == MOD_PISTON ? 1 : 0) | (a.mod[0] == MOD_EPM ? 2 : 0) | (a.row_thalf >= 0 ? 32 : 0);
     const int r = 8 | (jac ? 4 : 0) | mix;   // 12 (exponential), 13 / 15 (BMMs), 14 (exp_pist_flow) (+ 32: LW)
     return fused_dz_instance_exists(r) ? r : -1;
@@ -957,7 +973,7 @@ static int launch_fused_dz(ngrtd_ctx* ctx, const RtdArgs& a0, const UnitArgs& u,
                            hipStream_t st, const DemcAccept& da, int mix) {
     const int WB = kFusedUnits / L;
     RtdArgs a = a0;
-    cheb_window(a, u);
+    dz_window(a, u, (mix & 64) != 0);
     const int dz_p = (mix & 4) ? da.P : 0;    // transformed chains: the chains'-space proposal rows
     size_t lds = fused_lds(a, u, dz_p);
     // the natural proposal rows in LDS too where they fit (not next to the EPM channel

@@ -28,14 +28,21 @@ static hipError_t launch_dz_mix(const RtdArgs& a, const UnitArgs& u, int WB, int
 
 hipError_t launch_fused_dz_lw_instance(int mix, const RtdArgs& a, const UnitArgs& u, int WB, int64_t W, double* logp,
                                        const DemcAccept& da, size_t lds, size_t max_lds, hipStream_t st);
+hipError_t launch_fused_dz_gen_instance(int mix, const RtdArgs& a, const UnitArgs& u, int WB, int64_t W, double* logp,
+                                        const DemcAccept& da, size_t lds, size_t max_lds, hipStream_t st);
+hipError_t launch_fused_dz_gen_disp_instance(int mix, const RtdArgs& a, const UnitArgs& u, int WB, int64_t W,
+                                             double* logp, const DemcAccept& da, size_t lds, size_t max_lds,
+                                             hipStream_t st);
 
 // The DZ instances: 8 | piston 1 | EPM 2 | Jacobian 4 (13 / 15: the transformed-space BMMs) |
 // per-well chains 16 | the sampled
-// CFC12 half-life 32 (ngrtd_dz_lw.hip; the BMM ones exceed kDzMaxP rows at the c4 shape).
+// CFC12 half-life 32 (ngrtd_dz_lw.hip; the BMM ones exceed kDzMaxP rows at the c4 shape) |
+// generic components 64 (+ 128: a dispersion component; ngrtd_dz_gen*.hip, no half-life).
 bool fused_dz_instance_exists(int mix) {
     switch (mix & ~16) {
     case 8: case 9: case 10: case 11: case 12: case 13: case 14: case 15: return true;
     case 40: case 42: case 44: case 46: return true;
+    case 72: case 76: case 200: case 204: return true;
     default: return false;
     }
 }
@@ -43,6 +50,8 @@ bool fused_dz_instance_exists(int mix) {
 hipError_t launch_fused_dz_instance(int mix, const RtdArgs& a, const UnitArgs& u, int WB, int64_t W, double* logp,
                                     const DemcAccept& da, size_t lds, size_t max_lds, hipStream_t st) {
     if (mix & 32) return launch_fused_dz_lw_instance(mix, a, u, WB, W, logp, da, lds, max_lds, st);
+    if (mix & 128) return launch_fused_dz_gen_disp_instance(mix, a, u, WB, W, logp, da, lds, max_lds, st);
+    if (mix & 64) return launch_fused_dz_gen_instance(mix, a, u, WB, W, logp, da, lds, max_lds, st);
     switch (mix) {
     case 8: return launch_dz_mix<8>(a, u, WB, W, logp, da, lds, max_lds, st);
     case 9: return launch_dz_mix<9>(a, u, WB, W, logp, da, lds, max_lds, st);

@@ -2657,7 +2657,7 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
     // issued before any store, so the prologue pays one memory latency
     constexpr bool EPM = (MIX & 2) != 0;
     constexpr bool GEN = (MIX & 64) != 0;        // generic components (gen_component)
-    static_assert(!GEN || (MIX & (1 | 2 | 8 | 16)) == 0, "generic instances: plain log-prob, runtime models");
+    static_assert(!GEN || (MIX & (1 | 2)) == 0, "generic instances: runtime models (plain log-prob or the DZ step)");
     // the channel table staged in LDS: exp_pist_flow components (epm_sums)
     // ... and dispersion components (gen_exact's LDS loop), with their per-age disp_aux: the
     // generic instances with MIX bit 7 (a plan with a dispersion component; the others keep
@@ -2917,7 +2917,11 @@ __global__ void __launch_bounds__(64 * kFusedWaves * ROLES) logp_fused_kernel(co
             // barrier (block-uniform: every wave reaches it)
             const int dsp = (DISPS && ROLES == 2) ? a.disp_split : 0;
             const int dcomp = a.mod[0] == MOD_DISP ? 0 : 1;
-            double* xch = wd + uk.wd_n;                       // [C + 1][kFusedUnits]
+            // [C + 1][kFusedUnits]: after the per-well data, or (DZ) after the step's proposal
+            // rows and the chains' LDS state (launch_fused_dz sizes the block's LDS as the sum)
+            double* xch = !DZ ? wd + uk.wd_n
+                              : propl + (dk.prop_lds ? dk.P * kFusedUnits : 0) +
+                                    (dk.state_lds ? dk.P * kFusedUnits + 3 * kFusedUnits + kFusedUnits / 2 : 0);
             if (dsp && do_theta) {
                 double pn[C], pd;
                 const double tc = mvalid ? a.theta[(int64_t)a.row_tau[dcomp] * a.U + mu] : 1.0;

@@ -545,3 +545,46 @@ def test_pymc3_backward_matches_torch_backward():
     assert _same(got[3], ut[3])
     with pytest.raises(TypeError):
         tf.backward(ut.float().cuda())
+
+
+GENERIC_PAIRS = [("dispersion", None, ("tau1", "D1")), ("exponential", "exponential", ("tau1", "tau2", "f1")),
+                 ("piston", "exponential", ("tau1", "tau2", "f1")), ("dispersion", "piston", ("tau1", "tau2", "f1", "D1")),
+                 ("exponential", "dispersion", ("tau1", "tau2", "f1", "D2")),
+                 ("exp_pist_flow", "exponential", ("tau1", "tau2", "f1", "eta1"))]
+
+
+@pytest.mark.parametrize("per_well", [True, False])
+@pytest.mark.parametrize("jac", [False, True])
+@pytest.mark.parametrize("pair", GENERIC_PAIRS, ids=lambda p: p[0] + ("-" + p[1] if p[1] else ""))
+def test_single_launch_step_generic_pairs(pair, jac, per_well):
+    """The model pairs of run_age_mcmc.py:61-70 without a specialised instance (dispersion, a
+    piston first component, exponential / dispersion seconds, exp_pist_flow-exponential) step in
+    ONE launch per chunk on the generic DZ instances (MIX 64 | 8, + 128 for dispersion), on the
+    joint c4 shape (5 tracers, 4 wells, 130 walkers: a partial second block): device == torch
+    (sampler.DEMetropolisZ over the parity-tested log-prob) bit for bit through tuning,
+    stop_tuning and the draws."""
+    import dataclasses
+    import torch
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+    from noblegas_rtd_mcmc_amd.sampler import DEMetropolisZ, DeviceDEMetropolisZ, Transform
+    m1, m2, pn = pair
+    spec = dataclasses.replace(wl.c4_spec(L=4, N=1200, mod_type1=m1, mod_type2=m2, par_names=pn), jacobian=jac)
+    W = 130
+    x0 = torch.from_numpy(wl.sample_prior(spec, W, np.random.default_rng(31))).cuda()
+    lp = LogProb(spec, max_walkers=W)
+    kw = dict(tune_interval=4, seed=6170, per_well=per_well)
+    lp.ctx.set_profiling(True)
+    lp.kernel_stats(reset=True)
+    dev = DeviceDEMetropolisZ(lp, **kw).run(x0, tune=12, draws=8)
+    lp.ctx.set_profiling(False)
+    ks = lp.kernel_stats(reset=True)
+    # one launch for the 20 steps (+ the start's log-prob launch of the walker chains, lp(x))
+    assert ks["fused"][1] == (1 if per_well else 2) and ks["rtd"][1] == 0 and ks["unit"][1] == 0, ks
+    tf = Transform.from_spec(spec) if jac else None
+    f = (lambda t: lp.units(t)) if per_well else (lambda t: lp(t))
+    ref = DEMetropolisZ(f, transform=tf, **kw).run(x0, tune=12, draws=8)
+    for k in ("x", "lp", "samples", "logp", "accepted", "accept", "lamb", "scaling"):
+        assert _same(dev[k], ref[k]), k
+    assert 0 < int(dev["accepted"].sum()) < dev["accepted"].numel()
+    lp.close()
