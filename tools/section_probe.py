@@ -18,6 +18,7 @@ joint chains, natural / transformed space), its sections
   13->6 exchange   6->10 decision   10->11 commit barrier   11->12 commit
 
     python tools/section_probe.py [--wells 64] [--walkers 2048] [--variant dz --pw 1 --jac 1]
+                                  [--model exp_pist_flow [--model2 piston] --savenum 123]
 """
 import argparse
 import ctypes as C
@@ -68,6 +69,9 @@ def main():
     ap.add_argument("--jac", type=int, default=1)
     ap.add_argument("--dz-steps", type=int, default=8)
     ap.add_argument("--define", action="append", default=[], help="extra -D for the probe build (A/B)")
+    ap.add_argument("--model", default="exponential", help="first RTD component (mod_type1), e.g. exp_pist_flow")
+    ap.add_argument("--model2", default=None, help="second RTD component (mod_type2), e.g. piston")
+    ap.add_argument("--savenum", default="", help="'123': J, thalf_cfc, lamsf6 sampled")
     args = ap.parse_args()
     build(args.define)
     if args.build_only:
@@ -77,7 +81,8 @@ def main():
     import torch
     from noblegas_rtd_mcmc_amd import _lib, workloads
     from noblegas_rtd_mcmc_amd.engine import LogProb
-    spec = workloads.c4_spec(L=args.wells)
+    spec = workloads.c4_spec(L=args.wells, mod_type1=args.model, mod_type2=args.model2,
+                             par_names=workloads.model_par_names(args.model, args.model2, args.savenum))
     if args.variant == "dz" and args.jac:
         import dataclasses
         spec = dataclasses.replace(spec, jacobian=True)
