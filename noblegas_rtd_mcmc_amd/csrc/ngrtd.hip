@@ -411,8 +411,8 @@ static int epm_prepare(ngrtd_ctx* ctx, TableDev& tab, int N, int p_lo, int p_hi,
             if (!(v >= 0.0) || !std::isfinite(v)) return NGRTD_OK;   // the relative bound needs A >= 0
     const int nb = nb_cap > 0 ? std::min((N - 1) / S, nb_cap) : (N - 1) / S;   // b S < N for b = 1..nb
     const int np = p_hi - p_lo;
-    // the C channel columns only (the kernel sums the normaliser's tail in closed form), rows
-    // packed: a piece is kChebN * C contiguous doubles, read with 16-B loads (kChebN even)
+    // the C channel columns only (the kernel sums the normaliser's tail in closed form),
+    // channel-major: a piece is C runs of kChebN coefficients, read with 16-B loads (kChebN even)
     const size_t per = (size_t)n * C;
     std::vector<double> h((size_t)nb * np * per, 0.0);
     const long double PI = 3.14159265358979323846264338327950288L;
@@ -467,7 +467,7 @@ static int epm_prepare(ngrtd_ctx* ctx, TableDev& tab, int N, int p_lo, int p_hi,
                     for (int k = 0; k < n; ++k) {
                         long double m = 0.0L;
                         for (int j = k; j < n; ++j) m += ch[j] * Tm[j][k];
-                        h[(((size_t)b * np + (p - p_lo)) * n + k) * C + c] = (double)m;
+                        h[((size_t)b * np + (p - p_lo)) * per + (size_t)c * n + k] = (double)m;
                     }
                 }
             const int M = 24;                        // validation: 26 points per piece
@@ -487,7 +487,7 @@ static int epm_prepare(ngrtd_ctx* ctx, TableDev& tab, int N, int p_lo, int p_hi,
                 for (int b = 0; b < nb; ++b)
                     for (int c = 0; c < C; ++c) {
                         double y = 0.0;
-                        cheb_sums<1>(h.data() + ((size_t)b * np + (p - p_lo)) * per + c, C, x, &y);
+                        cheb_sums<1>(h.data() + ((size_t)b * np + (p - p_lo)) * per + (size_t)c * n, 1, x, &y);
                         const long double ex = v[(size_t)b * C + c];
                         const double e = (ex > 0) ? (double)(fabsl((long double)y - ex) / ex) : (y == 0.0 ? 0.0 : HUGE_VAL);
                         if (!(e <= worst)) worst = e;   // NaN -> worst = NaN

@@ -1951,11 +1951,13 @@ __device__ __forceinline__ void epm_row_load(const double* row, double* v) {
     }
 }
 
-// The block-tail surrogate of one piece: kChebN rows of C packed channel coefficients
-// (C kChebN doubles, 16-B aligned), read as 16-B chunks in descending order as Horner
-// consumes the rows (top row first).
-// The first kEpmTailPre chunks Horner reads (the top ones), loaded ahead by the caller --
-// before the head loop, so that their L2 latency passes behind it.
+// The block-tail surrogate of one piece: C channels of kChebN coefficients each, channel-major
+// (C kChebN doubles, 16-B aligned): channel c's monomial coefficients at [c kChebN, (c + 1) kChebN),
+// read as 16-B chunks, each channel's top chunk first as its Horner consumes them.  (Channel-major
+// so that the sampled half-life's channel-0 column at its own piece, LW, is one contiguous run of
+// kChebN doubles instead of kChebN loads at stride C.)
+// The first kEpmTailPre chunks Horner reads, loaded ahead by the caller -- before the head
+// loop, so that their L2 latency passes behind it.
 #ifndef NGRTD_EPM_TAIL_PRE
 #define NGRTD_EPM_TAIL_PRE 14
 #endif
@@ -1975,38 +1977,36 @@ constexpr int kEpmTailPreLw = NGRTD_EPM_TAIL_PRE_LW;
 #define NGRTD_EPM_LW_PRE 1
 #endif
 constexpr bool kEpmLwPre = NGRTD_EPM_LW_PRE != 0;
+static_assert(kChebN % 2 == 0, "pieces of whole 16-B chunks per channel");
 __host__ __device__ constexpr int epm_tail_pre_n(int C, int want) { return want < kChebN * C / 2 ? want : kChebN * C / 2; }
-template <int C, int NPW>
-__device__ __forceinline__ void epm_tail_pre(const double* pt, bool on, double2* pre) {
-    constexpr int NF = kChebN * C, NP = epm_tail_pre_n(C, NPW);
-    const double2* p2 = reinterpret_cast<const double2*>(pt);
-#pragma unroll
-    for (int j = 0; j < NP; ++j) pre[j] = on ? p2[NF / 2 - 1 - j] : double2{0.0, 0.0};
+// chunk of load position q (channel q / (kChebN / 2), its chunks top-down)
+__host__ __device__ constexpr int epm_tail_chunk(int q) {
+    return (q / (kChebN / 2)) * (kChebN / 2) + (kChebN / 2 - 1 - q % (kChebN / 2));
 }
 template <int C, int NPW>
-__device__ __forceinline__ void epm_tail_sums(const double* pt, double x, double* y, const double2* pre) {
-    constexpr int NF = kChebN * C, NP = epm_tail_pre_n(C, NPW);
-    static_assert(NF % 2 == 0, "pieces of whole 16-B chunks");
+__device__ __forceinline__ void epm_tail_pre(const double* pt, bool on, double2* pre) {
+    constexpr int NP = epm_tail_pre_n(C, NPW);
     const double2* p2 = reinterpret_cast<const double2*>(pt);
-    double f[NF];
-    int next = NF / 2 - 1;                              // next chunk to load (descending)
 #pragma unroll
-    for (int k = kChebN - 1; k >= 0; --k) {
+    for (int q = 0; q < NP; ++q) pre[q] = on ? p2[epm_tail_chunk(q)] : double2{0.0, 0.0};
+}
+// y_c = sum_k f_{c,k} x^k by Horner from the top coefficient (the same FMAs in the same order
+// per channel as the row-major layout of round 4: the same bits)
+template <int C, int NPW>
+__device__ __forceinline__ void epm_tail_sums(const double* pt, double x, double* y, const double2* pre) {
+    constexpr int NCH = kChebN / 2, NP = epm_tail_pre_n(C, NPW);
+    const double2* p2 = reinterpret_cast<const double2*>(pt);
 #pragma unroll
-        for (int i = NF / 2 - 1; i >= 0; --i)
-            if (i <= next && 2 * i + 1 >= k * C) {       // compile-time after unrolling
-                const double2 t = (i >= NF / 2 - NP) ? pre[NF / 2 - 1 - i] : p2[i];
-                f[2 * i] = t.x;
-                f[2 * i + 1] = t.y;
-            }
-        next = (k * C) / 2 - 1 < next ? (k * C) / 2 - 1 : next;
-        if (k == kChebN - 1) {
+    for (int c = 0; c < C; ++c) {
+        double acc = 0.0;
 #pragma unroll
-            for (int c = 0; c < C; ++c) y[c] = f[k * C + c];
-        } else {
-#pragma unroll
-            for (int c = 0; c < C; ++c) y[c] = fma(y[c], x, f[k * C + c]);
+        for (int j = NCH - 1; j >= 0; --j) {
+            const int q = c * NCH + (NCH - 1 - j);           // load position of chunk (c, j)
+            const double2 t = (q < NP) ? pre[q] : p2[c * NCH + j];
+            acc = (j == NCH - 1) ? t.y : fma(acc, x, t.y);
+            acc = fma(acc, x, t.x);
         }
+        y[c] = acc;
     }
 }
 
@@ -2097,7 +2097,11 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
     if (LW && kEpmLwPre) {
         const double* pw = a.epm + ((size_t)bt * a.epm_np + (pcw < 0 ? 0 : pcw)) * (size_t)(kChebN * C);
 #pragma unroll
-        for (int k = 0; k < kChebN; ++k) twp[k] = tail_on ? pw[k * C] : 0.0;
+        for (int k = 0; k < kChebN / 2; ++k) {   // channel 0: one contiguous run, 16-B loads
+            const double2 t = tail_on ? reinterpret_cast<const double2*>(pw)[k] : double2{0.0, 0.0};
+            twp[2 * k] = t.x;
+            twp[2 * k + 1] = t.y;
+        }
     }
     double y[C];
 #pragma unroll
@@ -2160,9 +2164,9 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
     if (tail_on) epm_tail_sums<C, NPW>(pt, ex, tl, tpre);
     if (LW && tail_on) {   // channel 0's tail at tau'_w: column 0 of its own piece (L2)
         const double* pw = a.epm + ((size_t)bt * a.epm_np + (pcw < 0 ? 0 : pcw)) * (size_t)(kChebN * C);
-        double v = kEpmLwPre ? twp[kChebN - 1] : pw[(kChebN - 1) * C];
+        double v = kEpmLwPre ? twp[kChebN - 1] : pw[kChebN - 1];
 #pragma unroll
-        for (int k = kChebN - 2; k >= 0; --k) v = fma(v, exw, kEpmLwPre ? twp[k] : pw[k * C]);
+        for (int k = kChebN - 2; k >= 0; --k) v = fma(v, exw, kEpmLwPre ? twp[k] : pw[k]);
         tl[0] = v;
     }
     if (__any(bad) && !(a.epm_diag & 4)) {              // exact tails of the uncovered lanes
