@@ -1713,10 +1713,11 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
             for (int j = 0; j < kDispExpTab; ++j) aux[2 * (size_t)p->N + j] = (double)exp2l((long double)j / kDispExpTab);
             NG_CHECK(upload(ctx, p->table.disp, aux.data(), aux.size()));
             a.disp_aux = p->table.disp.d();
-            if (p->table.C <= kDispRow - 2) {   // the single-launch loop's interleaved rows
+            if (p->table.C <= kDispRow - 3) {   // the single-launch loop's interleaved rows
                 std::vector<double> rows((size_t)p->N * kDispRow, 0.0);
                 for (int k = 0; k < p->N; ++k) {
                     for (int c = 0; c < p->table.C; ++c) rows[(size_t)k * kDispRow + c] = p->table.cols_host[c][k];
+                    rows[(size_t)k * kDispRow + kDispRow - 3] = k == 0 ? p->tp0 : (double)k + p->dtp;
                     rows[(size_t)k * kDispRow + kDispRow - 2] = aux[k];
                     rows[(size_t)k * kDispRow + kDispRow - 1] = aux[p->N + k];
                 }

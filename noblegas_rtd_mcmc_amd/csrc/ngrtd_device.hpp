@@ -63,7 +63,7 @@ struct RtdArgs {
     const double* disp_aux;
     // ... and the dispersion loop's per-age operands interleaved, one 64-B row per age k
     // (read with scalar loads: the rows are wave-uniform): A_{c,k} at [k][c] (c < C <= 5),
-    // 1 / tp_k at [k][6], tp_k^(-3/2) at [k][7]
+    // tp_k at [k][5], 1 / tp_k at [k][6], tp_k^(-3/2) at [k][7]
     const double* disp_rows;
     // 1: K = C and tracer t owns exactly channel t (unit_conc's direct path)
     int32_t conc_ident;

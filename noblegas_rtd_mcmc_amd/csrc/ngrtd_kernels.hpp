@@ -2304,14 +2304,16 @@ constexpr int kGenDispUnroll = NGRTD_GEN_DISP_UNROLL;
 // Taylor series to r^4/24 (|r| <= ln2/512: truncation < 4e-17 relative).  <= ~1.2 ulp.  y <= 0
 // here (no clamp: a very negative y saturates the int conversion and ldexp gives 0; NaN
 // propagates through the polynomial).
+// The polynomial is in f itself, its coefficients (ln2/T)^n / n! (no separate r = f ln2/T).
 __device__ __forceinline__ double fexp_tab(double y, const double* tab) {
-    constexpr double LN2_T = 6.93147180559945309417e-01 / kDispExpTab;
+    constexpr double L1 = 6.93147180559945309417e-01 / kDispExpTab;
+    constexpr double L2 = L1 * L1 / 2.0, L3 = L1 * L1 * L1 / 6.0, L4 = L1 * L1 * L1 * L1 / 24.0;
     const double kd = rint(y);
-    const double r = (y - kd) * LN2_T;
-    double q = 1.0 / 24.0;
-    q = fma_k(q, r, 1.0 / 6.0);
-    q = fma_k(q, r, 0.5);
-    const double p = fma(r * r, q, r);                   // e^r - 1
+    const double f = y - kd;
+    double q = fma_k(L4, f, L3);
+    q = fma_k(q, f, L2);
+    q = fma_k(q, f, L1);
+    const double p = q * f;                              // e^r - 1, r = f ln2/T
     const int k = (int)kd;
     const double th = tab[k & (kDispExpTab - 1)];
     return ldexp(fma(th, p, th), k >> 8);
@@ -2337,7 +2339,7 @@ __device__ __forceinline__ void gen_exact(const RtdArgs& a, int mod, bool on, do
         // plan's 256-entry table in LDS, etl: a degree-4 polynomial instead of fexp's degree 6),
         // and the per-unit factor k1 = sqrt(tau / (4 pi D)) multiplies the sums once at the end
         // (the normalised weights do not depend on it; its NaN / inf still reach the sums, so
-        // invalid tau and D give the reference's NaN).  tp_k advances by exact additions of 1.
+        // invalid tau and D give the reference's NaN).  tp_k comes with the row (no per-lane add).
         // The sums differ from the reference's per-age expression by rounding only: near the
         // mode the expanded exponent cancels to ~k2 ulp (k2 <= 25 over the D prior): < 2e-14
         // relative, inside the 1e-12 parity bar.  LW: the per-unit decay e^(-lam tp_k) is
@@ -2355,8 +2357,9 @@ __device__ __forceinline__ void gen_exact(const RtdArgs& a, int mod, bool on, do
             const double rl = LW ? fexp(-lam) : 1.0;         // e^(-lam): one year of decay
             const int N = a.N;
             const k_f64* rows = (const k_f64*)a.disp_rows;
-            auto age = [&](double tp, const double* r, double dec) {
-                const double w = r[kDispRow - 1] * fexp_tab(fma(ya, r[kDispRow - 2], fma(yb, tp, yc)), etl);
+            // row: A_c at [c], tp_k at [kDispRow - 3], 1/tp_k, tp_k^(-3/2) at the last two
+            auto age = [&](const double* r, double dec) {
+                const double w = r[kDispRow - 1] * fexp_tab(fma(ya, r[kDispRow - 2], fma(yb, r[kDispRow - 3], yc)), etl);
                 const double wd = LW ? w * dec : w;
 #pragma unroll
                 for (int c = 0; c < C; ++c) s[c] = fma(r[c], (LW && a.chan_lamw[c]) ? wd : w, s[c]);
@@ -2369,30 +2372,27 @@ __device__ __forceinline__ void gen_exact(const RtdArgs& a, int mod, bool on, do
             constexpr int UA = kGenDispUnroll;
             const int ke = age1 < 0 ? N : age1;             // ages [age0, ke)
             int k = age0;
-            if (k == 0 && k < ke) {                          // age 0: tp_0 = 1e-5 + dtp (not on the unit grid)
+            if (k == 0 && k < ke) {                          // age 0: tp_0 = 1e-5 + dtp (off the unit grid: its own decay)
                 double r[kDispRow];
                 load(0, r);
-                age(a.tp0, r, LW ? fexp(-lam * a.tp0) : 1.0);
+                age(r, LW ? fexp(-lam * a.tp0) : 1.0);
                 k = 1;
             }
-            double tp = (double)k + a.dtp;                   // tp_k = k + dtp (k >= 1), exact
             for (; k + UA <= ke; k += UA) {                 // UA ages' rows first, then their sums
                 double r[UA][kDispRow];
 #pragma unroll
                 for (int j = 0; j < UA; ++j) load(k + j, r[j]);
-                double dec = LW ? fexp(-lam * tp) : 1.0;
+                double dec = LW ? fexp(-lam * r[0][kDispRow - 3]) : 1.0;
 #pragma unroll
                 for (int j = 0; j < UA; ++j) {
-                    age(tp, r[j], dec);
-                    tp += 1.0;
+                    age(r[j], dec);
                     if (LW) dec *= rl;
                 }
             }
             for (; k < ke; ++k) {
                 double r[kDispRow];
                 load(k, r);
-                age(tp, r, LW ? fexp(-lam * tp) : 1.0);
-                tp += 1.0;
+                age(r, LW ? fexp(-lam * r[kDispRow - 3]) : 1.0);
             }
 #pragma unroll
             for (int c = 0; c <= C; ++c) s[c] *= k1;
