@@ -823,13 +823,20 @@ static void gen_cheb_window(RtdArgs& a, const UnitArgs& u) {
     a.cheb_np = pb - pa + 1;
 }
 // The dispersion component's age split between the unit's theta and RTD waves (the kernel's GEN
-// branch): half the ages each, when the theta waves' partial sums fit the LDS budget (else the
-// RTD wave sums all ages).  NGRTD_NO_DISP_SPLIT=1 disables it (A/B runs).
+// branch): the theta waves sum the first 65 % of the ages (their CE block is shorter than the
+// RTD waves' concentrations + likelihood: A/B over 0.4..0.7, profiles/r05ab_dispersion_split_ab.txt),
+// when the theta waves' partial sums fit the LDS budget (else the RTD wave sums all ages).
+// NGRTD_NO_DISP_SPLIT=1 disables it, NGRTD_DISP_SPLIT_FRAC sets the share (A/B runs).
 static void gen_disp_split(RtdArgs& a, const UnitArgs& u) {
     static const bool off = std::getenv("NGRTD_NO_DISP_SPLIT") != nullptr;
+    static const double frac = [] {   // NGRTD_DISP_SPLIT_FRAC: the theta waves' share of the ages (A/B)
+        const char* e = std::getenv("NGRTD_DISP_SPLIT_FRAC");
+        const double f = e ? std::atof(e) : 0.65;
+        return (f > 0.0 && f < 1.0) ? f : 0.65;
+    }();
     a.disp_split = 0;
     if (off || !a.disp_aux || !(a.mod[0] == MOD_DISP || a.mod[1] == MOD_DISP) || a.N < 2) return;
-    a.disp_split = a.N / 2;
+    a.disp_split = std::max(1, std::min(a.N - 1, (int)(a.N * frac)));
     if (fused_lds(a, u) > kFusedMaxLds) a.disp_split = 0;
 }
 static int gen_mix(const RtdArgs& a, const UnitArgs& u) {
