@@ -823,16 +823,18 @@ static void gen_cheb_window(RtdArgs& a, const UnitArgs& u) {
     a.cheb_np = pb - pa + 1;
 }
 // The dispersion component's age split between the unit's theta and RTD waves (the kernel's GEN
-// branch): the theta waves sum the first 65 % of the ages (their CE block is shorter than the
-// RTD waves' concentrations + likelihood: A/B over 0.4..0.7, profiles/r05ab_dispersion_split_ab.txt),
+// branch): the theta waves sum the first 55 % of the ages (their CE block is shorter than the
+// RTD waves' concentrations + likelihood: the log-prob gains up to 0.65-0.7, but the DEMetropolisZ
+// step, whose theta waves also stage the proposals, loses from 0.6 on and must use the same split
+// for bitwise chains: profiles/r05ab_dispersion_split_ab.txt, r05ad_dispersion_split_dz_ab.txt),
 // when the theta waves' partial sums fit the LDS budget (else the RTD wave sums all ages).
 // NGRTD_NO_DISP_SPLIT=1 disables it, NGRTD_DISP_SPLIT_FRAC sets the share (A/B runs).
 static void gen_disp_split(RtdArgs& a, const UnitArgs& u) {
     static const bool off = std::getenv("NGRTD_NO_DISP_SPLIT") != nullptr;
     static const double frac = [] {   // NGRTD_DISP_SPLIT_FRAC: the theta waves' share of the ages (A/B)
         const char* e = std::getenv("NGRTD_DISP_SPLIT_FRAC");
-        const double f = e ? std::atof(e) : 0.65;
-        return (f > 0.0 && f < 1.0) ? f : 0.65;
+        const double f = e ? std::atof(e) : 0.55;
+        return (f > 0.0 && f < 1.0) ? f : 0.55;
     }();
     a.disp_split = 0;
     if (off || !a.disp_aux || !(a.mod[0] == MOD_DISP || a.mod[1] == MOD_DISP) || a.N < 2) return;

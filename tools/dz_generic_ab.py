@@ -31,14 +31,18 @@ def main():
     from noblegas_rtd_mcmc_amd import workloads as wl
     from noblegas_rtd_mcmc_amd.engine import LogProb
     plans = []
+    sel = [x for x in os.environ.get("DZ_AB_PAIRS", "").split(",") if x]   # (A/B scripts: a subset)
+    modes = ("single",) if os.environ.get("DZ_AB_SINGLE") else ("single", "pair")
     for m1, m2, pn in PAIRS:
+        if sel and (m1 + ("-" + m2 if m2 else "")) not in sel:
+            continue
         sp = dataclasses.replace(wl.c4_spec(L=64, N=1200, mod_type1=m1, mod_type2=m2, par_names=pn), jacobian=True)
         th = torch.from_numpy(wl.sample_prior(sp, 2048, np.random.default_rng(34569))).cuda()
         plans.append((m1 + ("-" + m2 if m2 else ""), LogProb(sp, max_walkers=2048), th))
     for r in range(args.rounds):
         res = {"round": r}
         for name, lp, th in plans:
-            for mode in ("single", "pair"):
+            for mode in modes:
                 if mode == "pair":
                     os.environ["NGRTD_DZ_MODE"] = "pair"
                 try:
