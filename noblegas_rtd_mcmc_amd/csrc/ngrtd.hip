@@ -401,7 +401,7 @@ static int cheb_prepare(ngrtd_ctx* ctx, TableDev& tab, double d01) {
 // epm_piece + cheb_sums, the kernel's own code, at the plan tolerance kChebTol.  Threads split
 // the pieces.  Used only if every table validates (else the plan keeps the multi-kernel path).
 // nb_cap > 0: only blocks 1..nb_cap (the blocks a windowed table's units reach, epm_window).
-static int epm_prepare(ngrtd_ctx* ctx, TableDev& tab, int N, int p_lo, int p_hi, int nb_cap = 0) {
+static int epm_prepare(ngrtd_ctx* ctx, TableDev& tab, int N, int p_lo, int p_hi, int nb_cap = 0, bool mx = false) {
     tab.epm_ok = false;
     const int C = tab.C, S = kEpmBlock, n = kChebN;
     if (C < 1 || C > 5 || tab.cols_host.empty() || N <= S + 1 || p_lo < 0 || p_hi > kEpmPieces || p_hi <= p_lo)
@@ -412,8 +412,10 @@ static int epm_prepare(ngrtd_ctx* ctx, TableDev& tab, int N, int p_lo, int p_hi,
     const int nb = nb_cap > 0 ? std::min((N - 1) / S, nb_cap) : (N - 1) / S;   // b S < N for b = 1..nb
     const int np = p_hi - p_lo;
     // the C channel columns only (the kernel sums the normaliser's tail in closed form),
-    // channel-major: a piece is C runs of kChebN coefficients, read with 16-B loads (kChebN even)
-    const size_t per = (size_t)n * C;
+    // channel-major, read with 16-B loads; mx (plans with the sampled half-life, the LW
+    // instances): mixed precision (ngrtd_kernels.hpp epm_tail_eval1), C runs of kEpmK64
+    // doubles then C runs of kEpmK32 floats
+    const size_t per = (size_t)epm_piece_doubles(C, mx);
     std::vector<double> h((size_t)nb * np * per, 0.0);
     const long double PI = 3.14159265358979323846264338327950288L;
     std::vector<std::vector<long double>> Tm(n, std::vector<long double>(n, 0.0L));
@@ -464,10 +466,13 @@ static int epm_prepare(ngrtd_ctx* ctx, TableDev& tab, int N, int p_lo, int p_hi,
                             acc += f[((size_t)k * nb + b) * C + c] * cs[j][k];
                         ch[j] = acc * (j == 0 ? 1.0L : 2.0L) / n;
                     }
+                    double* pd = h.data() + ((size_t)b * np + (p - p_lo)) * per;
                     for (int k = 0; k < n; ++k) {
                         long double m = 0.0L;
                         for (int j = k; j < n; ++j) m += ch[j] * Tm[j][k];
-                        h[((size_t)b * np + (p - p_lo)) * per + (size_t)c * n + k] = (double)m;
+                        if (!mx) pd[(size_t)c * n + k] = (double)m;
+                        else if (k < kEpmK64) pd[(size_t)c * kEpmK64 + k] = (double)m;
+                        else reinterpret_cast<float*>(pd + (size_t)kEpmK64 * C)[(size_t)c * kEpmK32 + (k - kEpmK64)] = (float)m;
                     }
                 }
             const int M = 24;                        // validation: 26 points per piece
@@ -486,8 +491,7 @@ static int epm_prepare(ngrtd_ctx* ctx, TableDev& tab, int N, int p_lo, int p_hi,
                 tails(1.0L / (long double)taup, v);
                 for (int b = 0; b < nb; ++b)
                     for (int c = 0; c < C; ++c) {
-                        double y = 0.0;
-                        cheb_sums<1>(h.data() + ((size_t)b * np + (p - p_lo)) * per + (size_t)c * n, 1, x, &y);
+                        const double y = epm_tail_eval1(h.data() + ((size_t)b * np + (p - p_lo)) * per, C, c, x, mx);
                         const long double ex = v[(size_t)b * C + c];
                         const double e = (ex > 0) ? (double)(fabsl((long double)y - ex) / ex) : (y == 0.0 ? 0.0 : HUGE_VAL);
                         if (!(e <= worst)) worst = e;   // NaN -> worst = NaN
@@ -1702,7 +1706,7 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
                 nb_cap = rows > 0 ? rows / kEpmBlock : -1;
             }
             if (!disabled && pa >= 0 && pb >= pa && nb_cap >= 0) {
-                NG_CHECK(epm_prepare(ctx, p->table, p->N, pa, pb + 1, nb_cap));
+                NG_CHECK(epm_prepare(ctx, p->table, p->N, pa, pb + 1, nb_cap, a.row_thalf >= 0));   // (LW: mixed pieces)
                 if (p->table.epm_ok) {
                     a.epm = p->table.epm.d();
                     a.epm_nb = p->table.epm_nb; a.epm_p0 = p->table.epm_p0; a.epm_np = p->table.epm_np;

@@ -1977,33 +1977,87 @@ constexpr int kEpmTailPreLw = NGRTD_EPM_TAIL_PRE_LW;
 #define NGRTD_EPM_LW_PRE 1
 #endif
 constexpr bool kEpmLwPre = NGRTD_EPM_LW_PRE != 0;
-static_assert(kChebN % 2 == 0, "pieces of whole 16-B chunks per channel");
-__host__ __device__ constexpr int epm_tail_pre_n(int C, int want) { return want < kChebN * C / 2 ? want : kChebN * C / 2; }
-// chunk of load position q (channel q / (kChebN / 2), its chunks top-down)
-__host__ __device__ constexpr int epm_tail_chunk(int q) {
-    return (q / (kChebN / 2)) * (kChebN / 2) + (kChebN / 2 - 1 - q % (kChebN / 2));
+// Two piece formats, chosen per plan (ngrtd.hip epm_prepare) and per kernel instance (MX):
+//  * MX = false (plans without the sampled half-life): C runs of kChebN doubles, channel-major;
+//  * MX = true (plans with it, the LW instances): mixed precision -- a channel's monomial
+//    coefficients k < kEpmK64 are doubles, the top kEpmK32 = kChebN - kEpmK64 are floats.  Over
+//    the pieces [a, 1.25 a] |m_k| <= 2.3e-9 |f| from k = 8 on (checked over the tracer series
+//    and blocks), so their float rounding adds < 2e-16 relative -- and every plan's table is
+//    validated with this very evaluation (epm_tail_eval1) at kChebTol.  A piece: [C][kEpmK64]
+//    doubles, then [C][kEpmK32] floats (one 16-B chunk per channel): 400 B at C = 5 instead of
+//    480.  The LW instances read two pieces per unit (the shared tail and channel 0's at
+//    tau'_w): 17.6 vs 18.3 us per c4 launch; the plain instances lose with it (their 14 chunks
+//    loaded ahead then hold the converted floats: 18.0 vs 16.9 us), so they keep the doubles
+//    (profiles/r05af_epm_mixed_tail_ab.txt).
+constexpr int kEpmK64 = 8, kEpmK32 = kChebN - kEpmK64;
+static_assert(kEpmK64 % 2 == 0 && kEpmK32 == 4, "per channel: kEpmK64 / 2 double2 chunks + one float4 chunk");
+__host__ __device__ constexpr int epm_piece_doubles(int C, bool mx) { return mx ? C * (kEpmK64 + kEpmK32 / 2) : C * kChebN; }
+// the 16-B chunks of a channel, in the order Horner consumes them: MX, its float4 (the top
+// coefficients) then its double2 chunks top-down; else its double2 chunks top-down
+__host__ __device__ constexpr int epm_chunks_per_chan(bool mx) { return mx ? kEpmK64 / 2 + 1 : kChebN / 2; }
+__host__ __device__ constexpr int epm_tail_pre_n(int C, int want, bool mx) {
+    return want < epm_chunks_per_chan(mx) * C ? want : epm_chunks_per_chan(mx) * C;
 }
-template <int C, int NPW>
+// double2 index of load position q (channel c = q / chunks-per-channel, s = q % it)
+template <int C, bool MX>
+__host__ __device__ constexpr int epm_tail_chunk(int q) {
+    constexpr int NCH = epm_chunks_per_chan(MX);
+    return MX ? ((q % NCH == 0) ? (kEpmK64 / 2) * C + q / NCH : (q / NCH) * (kEpmK64 / 2) + (kEpmK64 / 2 - q % NCH))
+              : (q / NCH) * NCH + (NCH - 1 - q % NCH);
+}
+// channel c's tail at local x, the one evaluation every consumer uses (the device fast path
+// below: the same FMAs in the same order; the host validation of every plan's table)
+__host__ __device__ __forceinline__ double epm_tail_eval1(const double* pt, int C, int c, double x, bool mx) {
+    if (!mx) {
+        const double* d = pt + kChebN * c;
+        double acc = d[kChebN - 1];
+        for (int k = kChebN - 2; k >= 0; --k) acc = fma(acc, x, d[k]);
+        return acc;
+    }
+    const float* f = reinterpret_cast<const float*>(pt + kEpmK64 * C) + kEpmK32 * c;
+    const double* d = pt + kEpmK64 * c;
+    double acc = (double)f[kEpmK32 - 1];
+    for (int k = kEpmK32 - 2; k >= 0; --k) acc = fma(acc, x, (double)f[k]);
+    for (int k = kEpmK64 - 1; k >= 0; --k) acc = fma(acc, x, d[k]);
+    return acc;
+}
+template <int C, int NPW, bool MX>
 __device__ __forceinline__ void epm_tail_pre(const double* pt, bool on, double2* pre) {
-    constexpr int NP = epm_tail_pre_n(C, NPW);
+    constexpr int NP = epm_tail_pre_n(C, NPW, MX);
     const double2* p2 = reinterpret_cast<const double2*>(pt);
 #pragma unroll
-    for (int q = 0; q < NP; ++q) pre[q] = on ? p2[epm_tail_chunk(q)] : double2{0.0, 0.0};
+    for (int q = 0; q < NP; ++q) pre[q] = on ? p2[epm_tail_chunk<C, MX>(q)] : double2{0.0, 0.0};
 }
-// y_c = sum_k f_{c,k} x^k by Horner from the top coefficient (the same FMAs in the same order
-// per channel as the row-major layout of round 4: the same bits)
-template <int C, int NPW>
+// a float4 chunk held in a double2 register pair -> its four floats as doubles
+// (register moves only: a memcpy through a local float[4] put it in scratch)
+__device__ __forceinline__ void epm_f4(const double2& t, double* v) {
+    const unsigned long long a = (unsigned long long)__double_as_longlong(t.x);
+    const unsigned long long b = (unsigned long long)__double_as_longlong(t.y);
+    v[0] = (double)__uint_as_float((unsigned)a);          // little-endian: floats 0, 1 in t.x
+    v[1] = (double)__uint_as_float((unsigned)(a >> 32));
+    v[2] = (double)__uint_as_float((unsigned)b);
+    v[3] = (double)__uint_as_float((unsigned)(b >> 32));
+}
+// y_c = sum_k m_{c,k} x^k by Horner from the top coefficient: epm_tail_eval1's FMAs in its order
+template <int C, int NPW, bool MX>
 __device__ __forceinline__ void epm_tail_sums(const double* pt, double x, double* y, const double2* pre) {
-    constexpr int NCH = kChebN / 2, NP = epm_tail_pre_n(C, NPW);
+    constexpr int NP = epm_tail_pre_n(C, NPW, MX), NCH = epm_chunks_per_chan(MX);
     const double2* p2 = reinterpret_cast<const double2*>(pt);
 #pragma unroll
     for (int c = 0; c < C; ++c) {
         double acc = 0.0;
+        if (MX) {
+            double hi[kEpmK32];
+            epm_f4((c * NCH < NP) ? pre[c * NCH] : p2[epm_tail_chunk<C, MX>(c * NCH)], hi);
+            acc = hi[kEpmK32 - 1];
 #pragma unroll
-        for (int j = NCH - 1; j >= 0; --j) {
-            const int q = c * NCH + (NCH - 1 - j);           // load position of chunk (c, j)
-            const double2 t = (q < NP) ? pre[q] : p2[c * NCH + j];
-            acc = (j == NCH - 1) ? t.y : fma(acc, x, t.y);
+            for (int k = kEpmK32 - 2; k >= 0; --k) acc = fma(acc, x, hi[k]);
+        }
+#pragma unroll
+        for (int s = MX ? 1 : 0; s < NCH; ++s) {            // double2 chunks, top-down
+            const int q = c * NCH + s;
+            const double2 t = (q < NP) ? pre[q] : p2[epm_tail_chunk<C, MX>(q)];
+            acc = (!MX && s == 0) ? t.y : fma(acc, x, t.y);
             acc = fma(acc, x, t.x);
         }
         y[c] = acc;
@@ -2088,20 +2142,21 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
     }
     const bool tail_on = tail && !(a.epm_diag & 2);
     const int bt = (tail_on ? (blk < a.epm_nb ? blk : a.epm_nb) : 1) - 1;   // (a windowed table's blocks: clamped)
-    const double* pt = a.epm + ((size_t)bt * a.epm_np + (pc < 0 ? 0 : pc)) * (size_t)(kChebN * C);
-    double2 tpre[epm_tail_pre_n(C, NPW) > 0 ? epm_tail_pre_n(C, NPW) : 1];
-    epm_tail_pre<C, NPW>(pt, tail_on, tpre);
+    const double* pt = a.epm + ((size_t)bt * a.epm_np + (pc < 0 ? 0 : pc)) * (size_t)epm_piece_doubles(C, LW);
+    double2 tpre[epm_tail_pre_n(C, NPW, LW) > 0 ? epm_tail_pre_n(C, NPW, LW) : 1];
+    epm_tail_pre<C, NPW, LW>(pt, tail_on, tpre);
     // LW: channel 0's tail coefficients at tau'_w (column 0 of its own piece, L2), loaded
     // before the head loop as well (kEpmLwPre)
     double twp[LW ? kChebN : 1];
     if (LW && kEpmLwPre) {
-        const double* pw = a.epm + ((size_t)bt * a.epm_np + (pcw < 0 ? 0 : pcw)) * (size_t)(kChebN * C);
+        const double* pw = a.epm + ((size_t)bt * a.epm_np + (pcw < 0 ? 0 : pcw)) * (size_t)epm_piece_doubles(C, LW);
 #pragma unroll
-        for (int k = 0; k < kChebN / 2; ++k) {   // channel 0: one contiguous run, 16-B loads
+        for (int k = 0; k < kEpmK64 / 2; ++k) {   // channel 0: its double run and its float4
             const double2 t = tail_on ? reinterpret_cast<const double2*>(pw)[k] : double2{0.0, 0.0};
             twp[2 * k] = t.x;
             twp[2 * k + 1] = t.y;
         }
+        epm_f4(tail_on ? reinterpret_cast<const double2*>(pw)[(kEpmK64 / 2) * C] : double2{0.0, 0.0}, twp + kEpmK64);
     }
     double y[C];
 #pragma unroll
@@ -2161,12 +2216,17 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
     double tl[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) tl[c] = 0.0;
-    if (tail_on) epm_tail_sums<C, NPW>(pt, ex, tl, tpre);
+    if (tail_on) epm_tail_sums<C, NPW, LW>(pt, ex, tl, tpre);
     if (LW && tail_on) {   // channel 0's tail at tau'_w: column 0 of its own piece (L2)
-        const double* pw = a.epm + ((size_t)bt * a.epm_np + (pcw < 0 ? 0 : pcw)) * (size_t)(kChebN * C);
-        double v = kEpmLwPre ? twp[kChebN - 1] : pw[kChebN - 1];
+        const double* pw = a.epm + ((size_t)bt * a.epm_np + (pcw < 0 ? 0 : pcw)) * (size_t)epm_piece_doubles(C, LW);
+        double v;
+        if (kEpmLwPre) {   // epm_tail_eval1(pw, C, 0, exw, true) over the prefetched coefficients
+            v = twp[kChebN - 1];
 #pragma unroll
-        for (int k = kChebN - 2; k >= 0; --k) v = fma(v, exw, kEpmLwPre ? twp[k] : pw[k]);
+            for (int k = kChebN - 2; k >= 0; --k) v = fma(v, exw, twp[k]);
+        } else {
+            v = epm_tail_eval1(pw, C, 0, exw, true);
+        }
         tl[0] = v;
     }
     if (__any(bad) && !(a.epm_diag & 4)) {              // exact tails of the uncovered lanes
