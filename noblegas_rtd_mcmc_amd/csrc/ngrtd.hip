@@ -1706,7 +1706,7 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
                 nb_cap = rows > 0 ? rows / kEpmBlock : -1;
             }
             if (!disabled && pa >= 0 && pb >= pa && nb_cap >= 0) {
-                NG_CHECK(epm_prepare(ctx, p->table, p->N, pa, pb + 1, nb_cap, a.row_thalf >= 0));   // (LW: mixed pieces)
+                NG_CHECK(epm_prepare(ctx, p->table, p->N, pa, pb + 1, nb_cap, a.row_thalf >= 0 || kEpmMixedAll));   // (LW: mixed pieces)
                 if (p->table.epm_ok) {
                     a.epm = p->table.epm.d();
                     a.epm_nb = p->table.epm_nb; a.epm_p0 = p->table.epm_p0; a.epm_np = p->table.epm_np;

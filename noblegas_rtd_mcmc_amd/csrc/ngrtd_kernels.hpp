@@ -1959,7 +1959,7 @@ __device__ __forceinline__ void epm_row_load(const double* row, double* v) {
 // The first kEpmTailPre chunks Horner reads, loaded ahead by the caller -- before the head
 // loop, so that their L2 latency passes behind it.
 #ifndef NGRTD_EPM_TAIL_PRE
-#define NGRTD_EPM_TAIL_PRE 14
+#define NGRTD_EPM_TAIL_PRE 5
 #endif
 constexpr int kEpmTailPre = NGRTD_EPM_TAIL_PRE;
 // the DEMetropolisZ instances carry the step's state in registers too: fewer chunks ahead
@@ -1990,6 +1990,14 @@ constexpr bool kEpmLwPre = NGRTD_EPM_LW_PRE != 0;
 //    loaded ahead then hold the converted floats: 18.0 vs 16.9 us), so they keep the doubles
 //    (profiles/r05af_epm_mixed_tail_ab.txt).
 constexpr int kEpmK64 = 8, kEpmK32 = kChebN - kEpmK64;
+// Every plan takes the mixed pieces since the prefetch depth of the plain instances went to
+// one channel's chunks (5): 16.4 vs 17.0 us per c4 exp_pist_flow launch
+// (profiles/r05aj_epm_mixed_all_ab.txt).  NGRTD_EPM_MIXED_ALL=0 builds the all-double pieces
+// for the plans without the sampled half-life (A/B).
+#ifndef NGRTD_EPM_MIXED_ALL
+#define NGRTD_EPM_MIXED_ALL 1
+#endif
+constexpr bool kEpmMixedAll = NGRTD_EPM_MIXED_ALL != 0;
 static_assert(kEpmK64 % 2 == 0 && kEpmK32 == 4, "per channel: kEpmK64 / 2 double2 chunks + one float4 chunk");
 __host__ __device__ constexpr int epm_piece_doubles(int C, bool mx) { return mx ? C * (kEpmK64 + kEpmK32 / 2) : C * kChebN; }
 // the 16-B chunks of a channel, in the order Horner consumes them: MX, its float4 (the top
@@ -2142,14 +2150,15 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
     }
     const bool tail_on = tail && !(a.epm_diag & 2);
     const int bt = (tail_on ? (blk < a.epm_nb ? blk : a.epm_nb) : 1) - 1;   // (a windowed table's blocks: clamped)
-    const double* pt = a.epm + ((size_t)bt * a.epm_np + (pc < 0 ? 0 : pc)) * (size_t)epm_piece_doubles(C, LW);
-    double2 tpre[epm_tail_pre_n(C, NPW, LW) > 0 ? epm_tail_pre_n(C, NPW, LW) : 1];
-    epm_tail_pre<C, NPW, LW>(pt, tail_on, tpre);
+    const double* pt = a.epm + ((size_t)bt * a.epm_np + (pc < 0 ? 0 : pc)) * (size_t)epm_piece_doubles(C, LW || kEpmMixedAll);
+    constexpr bool MX = LW || kEpmMixedAll;             // the plan's piece format (epm_prepare)
+    double2 tpre[epm_tail_pre_n(C, NPW, MX) > 0 ? epm_tail_pre_n(C, NPW, MX) : 1];
+    epm_tail_pre<C, NPW, MX>(pt, tail_on, tpre);
     // LW: channel 0's tail coefficients at tau'_w (column 0 of its own piece, L2), loaded
     // before the head loop as well (kEpmLwPre)
     double twp[LW ? kChebN : 1];
     if (LW && kEpmLwPre) {
-        const double* pw = a.epm + ((size_t)bt * a.epm_np + (pcw < 0 ? 0 : pcw)) * (size_t)epm_piece_doubles(C, LW);
+        const double* pw = a.epm + ((size_t)bt * a.epm_np + (pcw < 0 ? 0 : pcw)) * (size_t)epm_piece_doubles(C, LW || kEpmMixedAll);
 #pragma unroll
         for (int k = 0; k < kEpmK64 / 2; ++k) {   // channel 0: its double run and its float4
             const double2 t = tail_on ? reinterpret_cast<const double2*>(pw)[k] : double2{0.0, 0.0};
@@ -2216,9 +2225,9 @@ __device__ __forceinline__ void epm_sums(const RtdArgs& a, const double* tabl, b
     double tl[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) tl[c] = 0.0;
-    if (tail_on) epm_tail_sums<C, NPW, LW>(pt, ex, tl, tpre);
+    if (tail_on) epm_tail_sums<C, NPW, MX>(pt, ex, tl, tpre);
     if (LW && tail_on) {   // channel 0's tail at tau'_w: column 0 of its own piece (L2)
-        const double* pw = a.epm + ((size_t)bt * a.epm_np + (pcw < 0 ? 0 : pcw)) * (size_t)epm_piece_doubles(C, LW);
+        const double* pw = a.epm + ((size_t)bt * a.epm_np + (pcw < 0 ? 0 : pcw)) * (size_t)epm_piece_doubles(C, LW || kEpmMixedAll);
         double v;
         if (kEpmLwPre) {   // epm_tail_eval1(pw, C, 0, exw, true) over the prefetched coefficients
             v = twp[kChebN - 1];
