@@ -223,7 +223,12 @@ typedef struct {
 /* NGRTD_EXACT_RTD: never use the plan-time surrogate of the exponential channel sums;
  * every unit evaluates them exactly (matrix-core Horner over all N ages).  For A/B and
  * for the exact-path rate bench.py reports beside the headline. */
-enum ngrtd_flags { NGRTD_WANT_LIKE = 1, NGRTD_WANT_PRIOR = 2, NGRTD_WANT_JACOBIAN = 4, NGRTD_EXACT_RTD = 8 };
+/* NGRTD_DISP_WIDE / NGRTD_DISP_LANE: the geometry of a dispersion component's age sum.  By
+ * default a plan of at most 256 units (n_wells x max_walkers) sums each unit's ages across the
+ * lanes of a separate kernel (the reference's own runs: 1 well x 3 chains, N = 25 256) and a
+ * larger plan gives each unit one lane; the flags force either (A/B and tests). */
+enum ngrtd_flags { NGRTD_WANT_LIKE = 1, NGRTD_WANT_PRIOR = 2, NGRTD_WANT_JACOBIAN = 4, NGRTD_EXACT_RTD = 8,
+                   NGRTD_DISP_WIDE = 16, NGRTD_DISP_LANE = 32 };
 
 typedef struct {
     int32_t n_wells;                        /* L */
@@ -291,8 +296,9 @@ int ngrtd_plan_kernel_stats(ngrtd_plan* plan, double* times_ms, int64_t* counts,
  * (VALU) or per segment (MFMA), channels, N, LDS bytes, units, MFMA row tiles (0 = VALU
  * path), age segments, 4-age MFMA steps, Chebyshev surrogate in use (0 none, 1 exponential channel sums, 2 exp_pist_flow block tails), the
  * surrogate's validated max relative error in units of 1e-18 (-1: not built), and
- * info[13] = pieces of the Student-t normaliser table (0: exact c0).  For the roofline
- * accounting in bench.py. */
+ * info[13] = pieces of the Student-t normaliser table (0: exact c0), info[14] = partial
+ * sums per unit of a small-ensemble dispersion plan's wide kernel (0: one lane per unit;
+ * NGRTD_DISP_WIDE), info[15] reserved.  For the roofline accounting in bench.py. */
 int ngrtd_plan_info(ngrtd_plan* plan, int64_t W, int64_t* info, int32_t n);
 
 /* Device-resident DEMetropolisZ: the sampler of the reference, PyMC3 3.11.2

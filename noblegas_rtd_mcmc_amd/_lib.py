@@ -25,6 +25,7 @@ CFC_SPECIES = {11: 0, 12: 1, 113: 2, "SF6": 3}                      # enum ngrtd
 CFC_WHAT = {"equil_air": 0, "equil_aq": 1, "ce_exc": 2, "solubility": 3, "vapor_pressure_atm": 4,
             "lapse_rate_atm": 5}
 WANT_LIKE, WANT_PRIOR, WANT_JACOBIAN, EXACT_RTD = 1, 2, 4, 8
+DISP_WIDE, DISP_LANE = 16, 32
 TUNE_TARGET = {None: 0, "none": 0, "scaling": 1, "lambda": 2}       # enum ngrtd_tune_target
 
 _dp = C.POINTER(C.c_double)

@@ -130,6 +130,7 @@ struct ngrtd_plan {
     DevBuf demc_prop[2], demc_lp, demc_acc;   // ngrtd_demcz_run scratch
     DevBuf demc_xw[2];      // the multi-step launch's walker-major state [P][W][L] (natural, transformed)
     DevBuf demc_pw;         // ... and per-well chains' lp, lamb, scaling [W][L] f64 + n_acc_tune [W][L] i32
+    DevBuf disp_pre;        // disp_wide_kernel's partial sums [G][C + 1][U] (RtdArgs::disp_pre)
 
     RtdArgs rtd{};
     UnitArgs unit{};
@@ -841,7 +842,7 @@ static void gen_disp_split(RtdArgs& a, const UnitArgs& u) {
         return (f > 0.0 && f < 1.0) ? f : 0.55;
     }();
     a.disp_split = 0;
-    if (off || !a.disp_aux || !(a.mod[0] == MOD_DISP || a.mod[1] == MOD_DISP) || a.N < 2) return;
+    if (off || a.disp_pre || !a.disp_aux || !(a.mod[0] == MOD_DISP || a.mod[1] == MOD_DISP) || a.N < 2) return;
     a.disp_split = std::max(1, std::min(a.N - 1, (int)(a.N * frac)));
     if (fused_lds(a, u) > kFusedMaxLds) a.disp_split = 0;
 }
@@ -940,7 +941,9 @@ static int dz_mix(const RtdArgs& a0, const UnitArgs& u, int P, bool transformed)
     const bool gen = !fused_path(a0, u) && gen_path(a0, u);
     dz_window(a, u, gen);
     if (gen) {
-        if (a.row_thalf >= 0 || fused_lds(a, u, transformed ? P : 0) > kFusedMaxLds) return -1;
+        // (a small-ensemble dispersion plan sums its ages in disp_wide_kernel ahead of the log-prob
+        // launch: its steps run the proposal / log-prob / accept kernels)
+        if (a.row_thalf >= 0 || a.disp_pre || fused_lds(a, u, transformed ? P : 0) > kFusedMaxLds) return -1;
         const int r = 8 | (jac ? 4 : 0) | (gen_mix(a, u) & (64 | 128));
         return fused_dz_instance_exists(r) ? r : -1;
     }
@@ -1021,6 +1024,49 @@ static int fused_wb(int64_t W, int L) {
     if (fixed) return wb;
     while (wb > 1 && cdiv(W, wb) < kCUs) wb /= 2;
     return wb;
+}
+// Small ensembles with a dispersion component (the reference's own runs: one well, 3 chains,
+// N = 25 256): the component's ages go across the lanes of disp_wide_kernel (G blocks of
+// kDispWideThreads per unit) instead of along one lane per unit, and the generic log-prob
+// launch reads the sums (RtdArgs::disp_pre).  A plan-time choice -- the sums' order then does
+// not depend on the launch's walker count: plans of at most kDispWideUnits units (L x
+// max_walkers) with exactly one dispersion component and the interleaved rows; the flags
+// NGRTD_DISP_WIDE / NGRTD_DISP_LANE force either geometry.  G: enough blocks to cover the CUs
+// (kCUs / units), each lane summing at least kDispWideMinAges ages.  Returns G (0: lane loop).
+constexpr int64_t kDispWideUnits = 256;
+constexpr int kDispWideMinAges = 8;
+static int disp_wide_plan(const RtdArgs& a, int32_t flags, int64_t Umax) {
+    const int nd = (a.mod[0] == MOD_DISP ? 1 : 0) + (a.mod[1] == MOD_DISP ? 1 : 0);
+    if (nd != 1 || !a.disp_aux || !a.disp_rows || a.C < 1 || a.C > 5 || a.N < 1 || (flags & NGRTD_DISP_LANE)) return 0;
+    if (!(flags & NGRTD_DISP_WIDE) && Umax > kDispWideUnits) return 0;
+    const int64_t gmax = std::max<int64_t>(1, a.N / ((int64_t)kDispWideThreads * kDispWideMinAges));
+    const int64_t want = std::max<int64_t>(1, cdiv(kCUs, std::max<int64_t>(Umax, 1)));
+    return (int)std::min<int64_t>({want, gmax, 64});
+}
+template <int C>
+static void launch_disp_wide_c(const RtdArgs& a, int comp, hipStream_t st) {
+    const dim3 grid((unsigned)a.disp_pre_g, (unsigned)a.U);
+    if (a.row_thalf >= 0)
+        hipLaunchKernelGGL((disp_wide_kernel<C, true>), grid, dim3(kDispWideThreads), 0, st, a, comp, a.disp_pre_g,
+                           const_cast<double*>(a.disp_pre));
+    else
+        hipLaunchKernelGGL((disp_wide_kernel<C, false>), grid, dim3(kDispWideThreads), 0, st, a, comp, a.disp_pre_g,
+                           const_cast<double*>(a.disp_pre));
+}
+// the dispersion sums ahead of a generic log-prob / forward launch of a wide plan (no-op otherwise)
+static int launch_disp_wide(ngrtd_ctx* ctx, const RtdArgs& a, const UnitArgs& u, hipStream_t st) {
+    if (!a.disp_pre || a.U <= 0 || fused_path(a, u)) return NGRTD_OK;
+    if (a.U > 65535) return set_err(ctx, NGRTD_EINVAL, "disp_wide_kernel: %lld units", (long long)a.U);
+    const int comp = a.mod[0] == MOD_DISP ? 0 : 1;
+    switch (a.C) {
+    case 1: launch_disp_wide_c<1>(a, comp, st); break;
+    case 2: launch_disp_wide_c<2>(a, comp, st); break;
+    case 3: launch_disp_wide_c<3>(a, comp, st); break;
+    case 4: launch_disp_wide_c<4>(a, comp, st); break;
+    default: launch_disp_wide_c<5>(a, comp, st); break;
+    }
+    HIP_TRY(ctx, hipGetLastError());
+    return NGRTD_OK;
 }
 static int launch_fused(ngrtd_ctx* ctx, const RtdArgs& a0, const UnitArgs& u, int64_t W, int L, double* logp,
                         hipStream_t st, const DemcAccept* dap = nullptr) {
@@ -1738,6 +1784,14 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
                 a.disp_rows = p->table.disp_rows.d();
             }
         }
+        a.disp_pre = nullptr;
+        a.disp_pre_g = 0;
+        const int dg = disp_wide_plan(a, d->flags, Umax);
+        if (dg > 0) {
+            HIP_TRY(ctx, p->disp_pre.ensure((size_t)dg * (a.C + 1) * Umax * sizeof(double)));
+            a.disp_pre = p->disp_pre.d();
+            a.disp_pre_g = dg;
+        }
         u.rtd_on = 1; u.K = K;
         u.rtd_obs = p->rtd_obs.d(); u.rtd_sd = p->rtd_sd.d(); u.conc = p->conc.d();
         u.row_tau1 = ri[NGRTD_ROLE_TAU1]; u.row_nu = ri[NGRTD_ROLE_NU_RTD_BETA]; u.row_tau2 = ri[NGRTD_ROLE_TAU2];
@@ -1895,6 +1949,11 @@ static int plan_run(ngrtd_plan* p, const double* theta, int64_t W, double* logp,
         RtdArgs a = p->rtd;
         a.theta = theta; a.U = U; a.conc = logp ? nullptr : rtd_out;
         if (single_path(a, u)) {
+            if (a.disp_pre) {   // a small-ensemble dispersion plan's sums (counted as an RTD launch)
+                NG_CHECK(timed_begin(p, prof, st, &ev));
+                NG_CHECK(launch_disp_wide(ctx, a, u, st));
+                NG_CHECK(timed_end(p, prof, st, 0, ev));
+            }
             NG_CHECK(timed_begin(p, prof, st, &ev));
             NG_CHECK(launch_fused(ctx, a, u, W, p->desc.n_wells, logp, st, dap));
             NG_CHECK(timed_end(p, prof, st, 3, ev));
@@ -2021,6 +2080,7 @@ static int plan_run_units(ngrtd_plan* p, const double* theta, int64_t W, double*
         a.theta = theta; a.U = U; a.conc = nullptr;
         if (single_path(a, u)) {
             u.unit_out = out;
+            NG_CHECK(launch_disp_wide(ctx, a, u, st));
             return launch_fused(ctx, a, u, W, L, out, st);
         }
         a.conc = p->conc.d();
@@ -2345,8 +2405,9 @@ int ngrtd_c0_check(double nu_lo, double nu_hi, double* coef, int32_t* e0, int32_
 int ngrtd_plan_info(ngrtd_plan* p, int64_t W, int64_t* info, int32_t n) {
     if (!p) return NGRTD_ESTATE;
     const int64_t U = (int64_t)p->desc.n_wells * W;
-    int64_t v[14] = {0};
+    int64_t v[16] = {0};
     v[13] = p->unit.c0_np;
+    v[14] = p->rtd.disp_pre_g;   // disp_wide_kernel partials per unit (0: the lane loop)
     if (p->desc.rtd_enabled) {
         RtdArgs a = p->rtd;
         v[11] = a.cheb != nullptr ? 1 : (a.epm != nullptr ? 2 : 0);
@@ -2365,7 +2426,7 @@ int ngrtd_plan_info(ngrtd_plan* p, int64_t W, int64_t* info, int32_t n) {
         v[4] = p->table.C; v[5] = p->N;
     }
     v[7] = U;
-    for (int i = 0; i < n && i < 14; ++i) info[i] = v[i];
+    for (int i = 0; i < n && i < 16; ++i) info[i] = v[i];
     return NGRTD_OK;
 }
 

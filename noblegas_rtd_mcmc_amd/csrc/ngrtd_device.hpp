@@ -72,6 +72,11 @@ struct RtdArgs {
     // generic instances with a dispersion component (ngrtd.hip gen_disp_split): its ages
     // [0, disp_split) are summed by the unit's theta wave, [disp_split, N) by its RTD wave; 0: not split
     int32_t disp_split;
+    // small ensembles (ngrtd.hip disp_wide_plan): the dispersion component's channel sums come
+    // from disp_wide_kernel, disp_pre_g partials per unit at disp_pre[(g (C + 1) + c) U + u]
+    // (c = C: the normaliser), added in order by gen_component; null: gen_exact's loop
+    const double* disp_pre;
+    int32_t disp_pre_g;
 };
 
 // exp_pist_flow (convolution_integral_utils.py:186-190) on the yearly grid: the unmasked

@@ -2371,9 +2371,17 @@ constexpr int kGenDispUnroll = NGRTD_GEN_DISP_UNROLL;
 // product): y = T k' + j + f, |f| <= 1/2, e^(y ln2/T) = 2^k' 2^(j/T) e^r, r = f ln2/T, with
 // 2^(j/T) from the plan's table (tab, LDS: the correctly rounded values) and e^r - 1 by its
 // Taylor series to r^4/24 (|r| <= ln2/512: truncation < 4e-17 relative).  <= ~1.2 ulp.  y <= 0
-// here (no clamp: a very negative y saturates the int conversion and ldexp gives 0; NaN
-// propagates through the polynomial).
+// here.  The conversion of k = rint(y) to int is the hardware's v_cvt_i32_f64, written as
+// one instruction (fcvt_i32): it saturates out-of-range values and maps NaN to 0, a defined
+// result for every input (a C++ cast of an out-of-range double is undefined, and LLVM may
+// fold it to poison).  A very negative y then gives k = INT_MIN, k >> 8 far below -1075, and
+// ldexp returns 0; NaN propagates through f and the polynomial.
 // The polynomial is in f itself, its coefficients (ln2/T)^n / n! (no separate r = f ln2/T).
+__device__ __forceinline__ int fcvt_i32(double x) {
+    int k;
+    asm("v_cvt_i32_f64 %0, %1" : "=v"(k) : "v"(x));
+    return k;
+}
 __device__ __forceinline__ double fexp_tab(double y, const double* tab) {
     constexpr double L1 = 6.93147180559945309417e-01 / kDispExpTab;
     constexpr double L2 = L1 * L1 / 2.0, L3 = L1 * L1 * L1 / 6.0, L4 = L1 * L1 * L1 * L1 / 24.0;
@@ -2383,7 +2391,7 @@ __device__ __forceinline__ double fexp_tab(double y, const double* tab) {
     q = fma_k(q, f, L2);
     q = fma_k(q, f, L1);
     const double p = q * f;                              // e^r - 1, r = f ln2/T
-    const int k = (int)kd;
+    const int k = fcvt_i32(kd);
     const double th = tab[k & (kDispExpTab - 1)];
     return ldexp(fma(th, p, th), k >> 8);
 }
@@ -2508,6 +2516,75 @@ __device__ __forceinline__ void gen_exact(const RtdArgs& a, int mod, bool on, do
     den = s[C];
 }
 
+// ------------------------------------------------------ dispersion, small ensembles
+// The lane-per-unit loop above gives each unit ONE lane that walks all N ages: at the
+// reference's own shape (one well, 3 chains, N = 25 256: run_age_mcmc.py:209,
+// run_age_mcmc_utils.py:412-417) three lanes of the whole chip run 25 256 dependent
+// iterations each, ~1 ms per log-prob.  For plans with few units (ngrtd.hip disp_wide_plan)
+// the channel sums of the dispersion component come from this kernel instead, with the ages
+// across the lanes: block (g, u) sums unit u's ages [g S, (g + 1) S), S = ceil(N / G), lane t
+// every kDispWideThreads-th age of it, each lane reading its own 64-B row of a.disp_rows
+// (a wave reads 4 KiB contiguous per iteration).  The per-lane partial sums meet in a fixed
+// order -- a butterfly within the wave (__shfl_xor, the same tree every launch), then the
+// waves in index order -- so the result is deterministic; it is scaled by
+// k1 = sqrt(tau / (4 pi D)) and stored as partial g of unit u, out[(g (C + 1) + c) U + u]
+// (c = C: the normaliser).  gen_component adds the G partials in order g = 0..G-1.
+// Per age: the weight of gen_exact's loop (same expansion of the exponent, fexp_tab on the
+// plan's 2^(j/256) table staged in LDS), LW: its own decay fexp(-lam tp_k) (no re-anchoring).
+// The sums differ from the lane-per-unit loop's by summation order only (<= a few ulp of the
+// sums; parity vs the oracle at rtol 1e-12 either way).
+constexpr int kDispWideThreads = 256;
+template <int C, bool LW>
+NGRTD_KLINK __global__ void __launch_bounds__(kDispWideThreads) disp_wide_kernel(const RtdArgs a, int32_t comp,
+                                                                               int32_t G, double* __restrict__ out) {
+    constexpr int NW = kDispWideThreads / 64;
+    __shared__ double etl[kDispExpTab];
+    __shared__ double red[NW][C + 1];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int g = blockIdx.x;
+    const int64_t u = blockIdx.y;
+    for (int i = tid; i < kDispExpTab; i += kDispWideThreads) etl[i] = a.disp_aux[2 * a.N + i];
+    if (LW) fm_lds_init();
+    const double tau = a.theta[(int64_t)a.row_tau[comp] * a.U + u];
+    const double D = a.theta[(int64_t)a.row_D[comp] * a.U + u];
+    const double lam = LW ? lw_decay(a, tau, a.theta[(int64_t)a.row_thalf * a.U + u]).lam : 0.0;
+    constexpr double LTE = kDispExpTab / 6.93147180559945309417e-01;   // T / ln 2
+    const double rt = 1.0 / tau;
+    const double k1 = sqrt(tau / (4. * kPi * D));
+    const double k2 = 1.0 / (4. * D);
+    const double ya = -(k2 * tau) * LTE, yb = -(k2 * rt) * LTE, yc = (2.0 * k2) * LTE;
+    const int S = (a.N + G - 1) / G;
+    const int k0 = g * S, ke = min(a.N, k0 + S);
+    __syncthreads();
+    double s[C + 1];
+#pragma unroll
+    for (int c = 0; c <= C; ++c) s[c] = 0.0;
+    const double4* rows = reinterpret_cast<const double4*>(a.disp_rows);
+    for (int k = k0 + tid; k < ke; k += kDispWideThreads) {
+        const double4 r0 = rows[2 * (int64_t)k], r1 = rows[2 * (int64_t)k + 1];
+        const double r[kDispRow] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+        const double w = r[kDispRow - 1] * fexp_tab(fma(ya, r[kDispRow - 2], fma(yb, r[kDispRow - 3], yc)), etl);
+        const double wd = LW ? w * fexp(-lam * r[kDispRow - 3]) : w;
+#pragma unroll
+        for (int c = 0; c < C; ++c) s[c] = fma(r[c], (LW && a.chan_lamw[c]) ? wd : w, s[c]);
+        s[C] += w;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+        for (int c = 0; c <= C; ++c) s[c] += __shfl_xor(s[c], o);
+    if (lane == 0)
+#pragma unroll
+        for (int c = 0; c <= C; ++c) red[wave][c] = s[c];
+    __syncthreads();
+    if (tid <= C) {
+        double t = red[0][tid];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) t += red[w][tid];
+        out[((int64_t)g * (C + 1) + tid) * a.U + u] = t * k1;
+    }
+}
+
 // One component (comp 0: tau1 / eta1 / D1, comp 1: tau2 / eta2 / D2) of a unit: its numerators
 // num[c] and reciprocal normaliser rden (conc = (A + J B) rden, unit_conc), and *nanc when the
 // concentrations are NaN without being summed (the skip lanes above).  tau: the component's tau
@@ -2569,6 +2646,17 @@ __device__ __forceinline__ void gen_component(const RtdArgs& a, const UnitArgs& 
         double dn, dd, lam;
         epm_sums<C, kEpmTailPreDz, LW>(a, tabl, mvalid, tau, eta, num, dn, dd, thx, &lam, &nanc);
         rden = dd / dn;
+    } else if (DSP && a.disp_pre) {
+        // dispersion sums of disp_wide_kernel (small ensembles): its G partials in order
+        double s[C + 1];
+#pragma unroll
+        for (int c = 0; c <= C; ++c) s[c] = a.disp_pre[(int64_t)c * a.U + mu];
+        for (int g = 1; g < a.disp_pre_g; ++g)
+#pragma unroll
+            for (int c = 0; c <= C; ++c) s[c] += a.disp_pre[((int64_t)g * (C + 1) + c) * a.U + mu];
+#pragma unroll
+        for (int c = 0; c < C; ++c) num[c] = s[c];
+        rden = 1.0 / s[C];
     } else {
         ex = mvalid;
     }

@@ -46,7 +46,8 @@ class LogProb:
         for i in range(_lib.ROLE_COUNT):
             d.role_index[i] = ri[i]
         d.flags = ((_lib.WANT_LIKE if spec.include_like else 0) | (_lib.WANT_PRIOR if spec.include_prior else 0)
-                   | (_lib.WANT_JACOBIAN if spec.jacobian else 0) | (_lib.EXACT_RTD if spec.exact_rtd else 0))
+                   | (_lib.WANT_JACOBIAN if spec.jacobian else 0) | (_lib.EXACT_RTD if spec.exact_rtd else 0)
+                   | {"auto": 0, "wide": _lib.DISP_WIDE, "lane": _lib.DISP_LANE}[spec.disp_geometry])
         if spec.ce is not None:
             c = spec.ce
             d.ce_enabled = 1
@@ -277,10 +278,10 @@ class LogProb:
         return {"rtd": (ms[0], n[0]), "unit": (ms[1], n[1]), "reduce": (ms[2], n[2]), "fused": (ms[3], n[3])}
 
     def info(self, W):
-        v = (C.c_int64 * 14)()
-        self.ctx.check(self.lib.ngrtd_plan_info(self.plan, int(W), v, 14), "plan_info")
+        v = (C.c_int64 * 16)()
+        self.ctx.check(self.lib.ngrtd_plan_info(self.plan, int(W), v, 16), "plan_info")
         keys = ("R", "NW", "blocks", "slice_ages", "channels", "N", "lds_bytes", "units", "mfma_rows", "S_seg",
-                "nsteps", "surrogate", "surrogate_err_e18", "c0_pieces")
+                "nsteps", "surrogate", "surrogate_err_e18", "c0_pieces", "disp_wide_g")
         d = dict(zip(keys, list(v)))
         d["surrogate_max_rel_err"] = d.pop("surrogate_err_e18") * 1e-18 if v[12] >= 0 else None
         return d

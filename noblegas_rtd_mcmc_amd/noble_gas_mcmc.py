@@ -93,17 +93,21 @@ class CEModel:
         return {"Ae": Ae, "F": F, "E": E, "b": b, "m": t[3], "T": T, "nu": nu}
 
     def sample(self, nwalkers=100, tune=500, draws=500, seed=12345, tune_interval=100, sampler="device",
-               space="transformed", prior_samples=10000):
+               space="transformed", prior_samples=10000, start="test_point"):
         """DEMetropolisZ on the GPU log-prob (replaces mc.sample, :408-415): one chain per
         (walker, well), each well its own model as the reference runs them (logp / accepted
         [draws][L][W]).  sampler: "device" (ngrtd_demcz_run, device-resident) or "torch"
         (sampler.DEMetropolisZ on torch ops; same random stream).  space: "transformed"
         (PyMC3's: logodds for the Beta variables; the log-prob adds the Jacobian) or
-        "natural"."""
+        "natural".  start: "test_point" (PyMC3's default start for a non-NUTS step: every chain
+        at model.test_point) or "prior" (independent prior draws, seeded)."""
         import torch
         from .sampler import sample_model
-        from .workloads import sample_prior
-        x0 = sample_prior(self.spec, nwalkers, np.random.default_rng(seed))
+        from .workloads import sample_prior, test_point
+        if start not in ("test_point", "prior"):
+            raise ValueError('start must be "test_point" or "prior"')
+        x0 = (test_point(self.spec, nwalkers) if start == "test_point"
+              else sample_prior(self.spec, nwalkers, np.random.default_rng(seed)))
         x = torch.from_numpy(x0).to("cuda:%d" % self.device)
         res = sample_model(self.spec, self.max_walkers, self.device, x, tune, draws, seed, tune_interval, sampler,
                            space, cache=self.__dict__)

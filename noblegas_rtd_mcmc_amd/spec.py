@@ -200,6 +200,9 @@ class ModelSpec:
     include_like: bool = True
     jacobian: bool = False             # add PyMC3 transform log|J| (parity unpinned)
     exact_rtd: bool = False            # no channel-sum surrogate: exact sums on the matrix cores
+    # a dispersion component's age sum: "auto" (plans of <= 256 units across the lanes of the
+    # wide kernel, larger ones one lane per unit), "wide" or "lane" (ngrtd.h NGRTD_DISP_*)
+    disp_geometry: str = "auto"
     roles: List[str] = field(default_factory=list)
 
     def __post_init__(self):

@@ -78,18 +78,22 @@ def test_ranks_on_gpu_equal_one_process(tmp_path, W, L, per_well, nproc):
 
 
 @pytest.mark.parametrize("nproc", [2, 8])
-def test_bench_ranks_one_gpu(nproc):
+def test_bench_ranks_one_gpu(nproc, tmp_path):
     """bench.py's N > 1 branch (LogpStepLoop + all-gather, max-over-ranks timing, the
     sampler leg on every rank) end to end on the one GPU: a valid JSON line; nproc = 8 is
     c5's strong partition (8 x 256 walkers of the 2048-walker ensemble)."""
     r = _torchrun(["bench.py", "--gpus", str(nproc), "--steps", "10", "--warmup", "2", "--scaling", "strong",
-                   "--backend", "gloo", "--one-device", "--sampler-steps", "16", "--no-cpu-baseline"], nproc=nproc)
+                   "--backend", "gloo", "--one-device", "--sampler-steps", "16", "--no-cpu-baseline",
+                   "--side-out", str(tmp_path / "side.json")], nproc=nproc)
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:] + r.stderr[-2000:]
     d = json.loads(lines[0])
     assert d["n_gpus"] == nproc and d["value"] > 0 and d["config"]["walkers_per_gpu"] == 2048 // nproc
     assert d["config"]["one_device"] is True and d["ensemble_finite_frac"] > 0.5
-    assert "error" not in d["sampler"] and d["sampler"]["transformed"]["us_per_step"] > 0
+    assert len(lines[0]) < 8000 and "sampler_error" not in d["side"] and d["side"]["sampler"]["transformed"][0] > 0
+    full = json.load(open(tmp_path / "side.json"))     # the full record beside the headline
+    assert "error" not in full["sampler"] and full["sampler"]["transformed"]["us_per_step"] > 0
+    assert full["value"] == d["value"]
 
 
 def test_rccl_pipeline_world_one(tmp_path):
