@@ -2401,6 +2401,9 @@ static_assert(kDispExpTab == 256, "fexp_tab: k >> 8");
 // (s_load, the scalar cache) -- no LDS or vector-memory instruction per age.  Read-only.
 typedef __attribute__((address_space(4))) const double k_f64;
 
+// LW: the sampled half-life decays channel 0 and only it (ngrtd.hip lw_ok admits no other plan to
+// the single-launch instances), a compile-time channel: a runtime a.chan_lamw[c] select cost two
+// v_cndmask_b32 per channel per age in the dispersion loop (10 of its ~40 VALU per age).
 template <int C, bool LW, bool DSP = false>
 __device__ __forceinline__ void gen_exact(const RtdArgs& a, int mod, bool on, double tau, double eta, double D,
                                           double lam, double* num, double& den, const double* etl = nullptr,
@@ -2439,7 +2442,7 @@ __device__ __forceinline__ void gen_exact(const RtdArgs& a, int mod, bool on, do
                 const double w = r[kDispRow - 1] * fexp_tab(fma(ya, r[kDispRow - 2], fma(yb, r[kDispRow - 3], yc)), etl);
                 const double wd = LW ? w * dec : w;
 #pragma unroll
-                for (int c = 0; c < C; ++c) s[c] = fma(r[c], (LW && a.chan_lamw[c]) ? wd : w, s[c]);
+                for (int c = 0; c < C; ++c) s[c] = fma(r[c], (LW && c == 0) ? wd : w, s[c]);
                 s[C] += w;
             };
             auto load = [&](int k, double* r) {
@@ -2507,7 +2510,7 @@ __device__ __forceinline__ void gen_exact(const RtdArgs& a, int mod, bool on, do
             const double wd = LW ? w * fexp(-lam * tp) : w;
             const double* row = a.tab + (int64_t)k * a.CP;
 #pragma unroll
-            for (int c = 0; c < C; ++c) s[c] = fma(row[c], (LW && a.chan_lamw[c]) ? wd : w, s[c]);
+            for (int c = 0; c < C; ++c) s[c] = fma(row[c], (LW && c == 0) ? wd : w, s[c]);
             s[C] += w;
         }
     }
@@ -2566,7 +2569,7 @@ NGRTD_KLINK __global__ void __launch_bounds__(kDispWideThreads) disp_wide_kernel
         const double w = r[kDispRow - 1] * fexp_tab(fma(ya, r[kDispRow - 2], fma(yb, r[kDispRow - 3], yc)), etl);
         const double wd = LW ? w * fexp(-lam * r[kDispRow - 3]) : w;
 #pragma unroll
-        for (int c = 0; c < C; ++c) s[c] = fma(r[c], (LW && a.chan_lamw[c]) ? wd : w, s[c]);
+        for (int c = 0; c < C; ++c) s[c] = fma(r[c], (LW && c == 0) ? wd : w, s[c]);
         s[C] += w;
     }
 #pragma unroll

@@ -41,6 +41,10 @@ def c_in():
     return wl.c_in_dict()
 
 
+# every run's comparison, kept for the pooled tuning test at the end of the module
+_DONE = {}
+
+
 @pytest.mark.parametrize("name", sorted(RUNS), ids=lambda n: n[:-7])
 def test_posterior_matches_reference(name, c_in):
     import torch
@@ -48,6 +52,7 @@ def test_posterior_matches_reference(name, c_in):
         pytest.skip("no GPU")
     e, r = RUNS[name]
     res = pc.compare_run(e, r, chains=48, C_in=c_in)
+    _DONE[name] = res
     bad = []
     for v, s in res["vars"].items():
         if not abs(s["z_between"]) <= 5.0:
@@ -57,3 +62,43 @@ def test_posterior_matches_reference(name, c_in):
     if r["accept_rate"] is not None and not abs(res["accept_rate"] - r["accept_rate"]) <= 0.12:
         bad.append(("accept", res["accept_rate"], r["accept_rate"]))
     assert not bad, json.dumps(bad)
+
+
+def _frac_rank(x, sample):
+    """Mid-rank of x among the sample, in [0, 1] (ties count half)."""
+    import numpy as np
+    a = np.asarray(sample)
+    return (float((a < x).sum()) + 0.5 * float((a == x).sum())) / a.size
+
+
+def test_tuning_matches_reference_chains(c_in):
+    """The tuning rule against the reference's own chains (tests/golden/ref_tuning.json, made by
+    tests/golden/make_tuning_fixture.py from the 22 traces' sample_stats): PyMC3's 'lambda'
+    tuning (run_age_mcmc_utils.py:412-417: tune_interval 1000 over 10 000 tune steps) leaves
+    every chain with lambda_0 = 2.38 / sqrt(2 ndim) times a product of PyMC3's tune() factors,
+    and each reference chain is one draw of that final lambda (and of its draw-phase
+    acceptance).  Pooled over the 66 reference chains, their mid-ranks among our 48 chains of
+    the same run are uniform if the tuning matches: their mean lies in [0.3, 0.7], and at most
+    8 of them (12 %; 2/49 = 4 % expected) fall outside our chains' [min, max] -- a wrong rule
+    (no tuning, scaling tuned instead of lambda, other factors) moves whole runs out."""
+    import json
+    import numpy as np
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    tun = json.load(open(os.path.join(REPO, "tests", "golden", "ref_tuning.json")))
+    ranks = {"lambda": [], "accept": []}
+    out = {"lambda": 0, "accept": 0}
+    for name in sorted(RUNS):
+        res = _DONE.get(name)
+        if res is None:
+            e, r = RUNS[name]
+            res = _DONE[name] = pc.compare_run(e, r, chains=48, C_in=c_in)
+        t = tun[name[:-len(".netcdf")]]
+        for key, ref, dev in (("lambda", t["lambda"], res["lambda"]), ("accept", t["accept_rate"], res["chain_accept"])):
+            for x in ref:
+                ranks[key].append(_frac_rank(x, dev))
+                out[key] += int(x < min(dev) or x > max(dev))
+    summary = {k: {"mean_rank": float(np.mean(v)), "outside": out[k], "n": len(v)} for k, v in ranks.items()}
+    for k, v in summary.items():
+        assert v["n"] == 66 and 0.3 <= v["mean_rank"] <= 0.7 and v["outside"] <= 8, summary

@@ -46,6 +46,10 @@ def compare_run(e, r, chains=48, tune=10000, draws=10000, start="test_point", se
         mc._lp.close()
     res = {"run": e["name"][:-7], "chains": chains, "start": start, "accept_rate": float(out["accept_rate"]),
            "ref_accept_rate": r["accept_rate"], "sample_s": float(out["sampling_time"]), "vars": {}}
+    # the tuning state each chain ends with (lambda frozen after tune steps) and its draw-phase
+    # acceptance: compared with the reference's chains (tests/golden/ref_tuning.json)
+    res["lambda"] = [float(x) for x in np.asarray(out["lamb"], dtype=np.float64).reshape(-1)]
+    res["chain_accept"] = [float(x) for x in np.asarray(out["accepted"], dtype=np.float64).reshape(draws, -1).mean(axis=0)]
     for v, rv in r["vars"].items():
         a = np.asarray(out["posterior"][v], dtype=np.float64)       # [chain][draw]
         cm = a.mean(axis=1)
