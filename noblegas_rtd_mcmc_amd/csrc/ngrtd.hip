@@ -510,7 +510,14 @@ static int epm_prepare(ngrtd_ctx* ctx, TableDev& tab, int N, int p_lo, int p_hi,
     for (int t = 0; t < nt; ++t)
         if (!(worst_t[t] <= worst)) worst = worst_t[t];
     tab.epm_err = worst;
-    if (!(worst <= kChebTol)) return NGRTD_OK;
+    if (!(worst <= kChebTol)) {
+        // no table: the plan runs the multi-kernel path (ngrtd_plan_info info[11] = 0); the
+        // instances compile one piece format, so there is no all-double retry (kEpmMixedAll)
+        if (std::getenv("NGRTD_VERBOSE"))
+            std::fprintf(stderr, "ngrtd: exp_pist_flow block-tail table (%s pieces) fails validation: max rel err %.3g > %.3g\n",
+                         mx ? "mixed" : "double", worst, kChebTol);
+        return NGRTD_OK;
+    }
     HIP_TRY(ctx, tab.epm.ensure(h.size() * sizeof(double)));
     HIP_TRY(ctx, hipMemcpy(tab.epm.p, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
     tab.epm_ok = true;
@@ -705,7 +712,10 @@ static double lw_tau_lo(const RtdArgs& a, double tau_lo) {
 // support needs: the block-tail table covers its tau'); units outside the support box have
 // log-prob -inf by their priors and epm_sums gives them finite zero sums (or NaN where the
 // reference's weights are NaN).  NGRTD_EPM_WINDOW: 1 (default) only when the whole table does not
-// fit, 2 whenever the window is smaller (A/B runs), 0 never.
+// fit with room for a DEMetropolisZ step's rows beside it (kEpmDzMargin: the single-launch and the
+// lane-chain steps add up to kDzMaxP proposal rows per unit slot; windowing the plain log-prob of
+// such a plan too keeps one table for every launch of the plan -- in-support units get the same
+// sums from either table), 2 whenever the window is smaller (A/B runs), 0 never.
 static int epm_window_rows(double tau_hi, double eta_hi, double dtp, int N) {
     if (!(tau_hi >= 0.0 && eta_hi >= 1.0) || !std::isfinite(tau_hi) || !std::isfinite(eta_hi)) return -1;
     const double mm = std::ceil(tau_hi * (1 - 1 / eta_hi) - dtp) + 1.0;
@@ -726,7 +736,8 @@ static void epm_window(RtdArgs& a, const UnitArgs& u) {
     if (!(u.tau1_lo <= u.tau1_hi && u.eta1_lo <= u.eta1_hi && u.eta1_lo > 0.0)) return;
     const int rows = epm_window_rows(u.tau1_hi, u.eta1_hi, a.dtp, a.N);
     if (rows < 0 || rows >= a.epm_nw || rows / kEpmBlock > a.epm_nb) return;
-    if (mode == 1 && fused_lds(a, u, 0) <= kFusedMaxLds) return;
+    constexpr size_t kEpmDzMargin = (size_t)kDzMaxP * kFusedUnits * sizeof(double);
+    if (mode == 1 && fused_lds(a, u, 0) + kEpmDzMargin <= kFusedMaxLds) return;
     a.epm_nw = rows;
     a.ew_on = 1;
     a.ew_tau_lo = u.tau1_lo; a.ew_tau_hi = u.tau1_hi;
@@ -1752,7 +1763,8 @@ int ngrtd_plan_create(ngrtd_ctx* ctx, const ngrtd_model_desc* d, int64_t max_wal
                 nb_cap = rows > 0 ? rows / kEpmBlock : -1;
             }
             if (!disabled && pa >= 0 && pb >= pa && nb_cap >= 0) {
-                NG_CHECK(epm_prepare(ctx, p->table, p->N, pa, pb + 1, nb_cap, a.row_thalf >= 0 || kEpmMixedAll));   // (LW: mixed pieces)
+                // mixed-precision pieces for every plan (kEpmMixedAll; LW plans always)
+                NG_CHECK(epm_prepare(ctx, p->table, p->N, pa, pb + 1, nb_cap, a.row_thalf >= 0 || kEpmMixedAll));
                 if (p->table.epm_ok) {
                     a.epm = p->table.epm.d();
                     a.epm_nb = p->table.epm_nb; a.epm_p0 = p->table.epm_p0; a.epm_np = p->table.epm_np;

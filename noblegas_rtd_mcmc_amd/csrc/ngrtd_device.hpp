@@ -43,9 +43,10 @@ struct RtdArgs {
     // exp_pist_flow block tails (logp_fused_kernel EPM mode, ngrtd.hip epm_prepare): table
     // b = 1..epm_nb holds pieces [epm_p0, epm_p0 + epm_np) of the surrogate of
     //   T_b(tau') = sum_{k >= b S} A_{c,k} exp(-(k - b S) / tau'),  S = kEpmBlock,
-    // laid out [b - 1][piece - epm_p0] x [C][kChebN] doubles (channel-major), or with the sampled
-    // half-life (C kEpmK64 doubles, C kEpmK32 floats) (ngrtd_kernels.hpp epm_tail_eval1); null
-    // when the plan has none
+    // laid out [b - 1][piece - epm_p0] x (C kEpmK64 doubles, then C kEpmK32 floats: the mixed
+    // pieces every plan takes, ngrtd_kernels.hpp kEpmMixedAll / epm_tail_eval1; [C][kChebN]
+    // doubles, channel-major, in a build with NGRTD_EPM_MIXED_ALL=0 for the plans without the
+    // sampled half-life); null when the plan has none
     const double* epm;
     int32_t epm_nb, epm_p0, epm_np;
     // rows [0, epm_nw) of the channel table staged in LDS for the exp_pist_flow sums (a multiple

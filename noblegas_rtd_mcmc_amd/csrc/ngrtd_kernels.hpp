@@ -1986,14 +1986,16 @@ constexpr bool kEpmLwPre = NGRTD_EPM_LW_PRE != 0;
 //    validated with this very evaluation (epm_tail_eval1) at kChebTol.  A piece: [C][kEpmK64]
 //    doubles, then [C][kEpmK32] floats (one 16-B chunk per channel): 400 B at C = 5 instead of
 //    480.  The LW instances read two pieces per unit (the shared tail and channel 0's at
-//    tau'_w): 17.6 vs 18.3 us per c4 launch; the plain instances lose with it (their 14 chunks
-//    loaded ahead then hold the converted floats: 18.0 vs 16.9 us), so they keep the doubles
-//    (profiles/r05af_epm_mixed_tail_ab.txt).
+//    tau'_w): 17.6 vs 18.3 us per c4 launch (profiles/r05af_epm_mixed_tail_ab.txt).
 constexpr int kEpmK64 = 8, kEpmK32 = kChebN - kEpmK64;
-// Every plan takes the mixed pieces since the prefetch depth of the plain instances went to
-// one channel's chunks (5): 16.4 vs 17.0 us per c4 exp_pist_flow launch
-// (profiles/r05aj_epm_mixed_all_ab.txt).  NGRTD_EPM_MIXED_ALL=0 builds the all-double pieces
-// for the plans without the sampled half-life (A/B).
+// Every plan -- with or without the sampled half-life -- takes the mixed pieces since the
+// prefetch depth of the plain instances went to one channel's chunks (5): 16.4 vs 17.0 us per
+// c4 exp_pist_flow launch (profiles/r05aj_epm_mixed_all_ab.txt).  The format is compiled into
+// the instances, so a plan whose mixed table fails the kChebTol validation has no all-double
+// table to fall back to: it runs without block-tail surrogates (the multi-kernel path), and
+// ngrtd_plan_info reports it (info[11] = 0 for an exp_pist_flow plan; epm_prepare logs it with
+// NGRTD_VERBOSE=1).  NGRTD_EPM_MIXED_ALL=0 builds the all-double pieces for the plans without
+// the sampled half-life (A/B).
 #ifndef NGRTD_EPM_MIXED_ALL
 #define NGRTD_EPM_MIXED_ALL 1
 #endif
@@ -2365,6 +2367,11 @@ __device__ __forceinline__ void epm_piston_row(const RtdArgs& a, const double* t
 #define NGRTD_GEN_DISP_UNROLL 4
 #endif
 constexpr int kGenDispUnroll = NGRTD_GEN_DISP_UNROLL;
+// LW: age groups between two exact decay anchors in the dispersion loop (8 x 4 = 32 ages)
+#ifndef NGRTD_DISP_DECAY_GROUPS
+#define NGRTD_DISP_DECAY_GROUPS 8
+#endif
+constexpr int kDispDecayGroups = NGRTD_DISP_DECAY_GROUPS;
 
 // e^(y ln2 / T), T = kDispExpTab, for an argument already scaled by T / ln 2 (the dispersion
 // loop forms y with the scale folded into its per-unit coefficients, so the reduction needs no
@@ -2458,11 +2465,15 @@ __device__ __forceinline__ void gen_exact(const RtdArgs& a, int mod, bool on, do
                 age(r, LW ? fexp(-lam * a.tp0) : 1.0);
                 k = 1;
             }
-            for (; k + UA <= ke; k += UA) {                 // UA ages' rows first, then their sums
+            // LW: the decay e^(-lam tp_k) re-anchored by an fexp at the first age of every
+            // kDispDecayGroups-th group (a wave-uniform branch: k is the same in every lane) and
+            // advanced by e^(-lam) in between (< kDispDecayGroups UA products: a few ulp)
+            double dec = 1.0;
+            for (int g = 0; k + UA <= ke; k += UA, ++g) {   // UA ages' rows first, then their sums
                 double r[UA][kDispRow];
 #pragma unroll
                 for (int j = 0; j < UA; ++j) load(k + j, r[j]);
-                double dec = LW ? fexp(-lam * r[0][kDispRow - 3]) : 1.0;
+                if (LW && g % kDispDecayGroups == 0) dec = fexp(-lam * r[0][kDispRow - 3]);
 #pragma unroll
                 for (int j = 0; j < UA; ++j) {
                     age(r[j], dec);
