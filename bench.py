@@ -644,7 +644,7 @@ OTHER_MODELS = (("piston", None, ""), ("piston", None, "123"), ("dispersion", No
 
 N_FULL = 25256            # the reference's series length: the whole C_in_dict (run_age_mcmc.py:46,209)
 TAU2_HI_EPM2 = 1000.0     # tau2 range of a second exp_pist_flow component's lines at N = 1200
-MODEL_PMC_SUMMARIES = ("r05_model_pmc.json",)   # tools/gpu_model_pmc.sh + tools/model_pmc_summary.py, newest first
+MODEL_PMC_SUMMARIES = ("r06_model_pmc.json", "r05_model_pmc.json")   # tools/gpu_model_pmc.sh + tools/model_pmc_summary.py, newest first
 
 
 def model_pmc_summary(key):

@@ -100,5 +100,8 @@ def test_tuning_matches_reference_chains(c_in):
                 ranks[key].append(_frac_rank(x, dev))
                 out[key] += int(x < min(dev) or x > max(dev))
     summary = {k: {"mean_rank": float(np.mean(v)), "outside": out[k], "n": len(v)} for k, v in ranks.items()}
+    if os.path.isdir(os.path.join(REPO, "gpurun_out")):      # the measured ranks, for DESIGN.md §5.1
+        with open(os.path.join(REPO, "gpurun_out", "tuning_ranks.json"), "w") as f:
+            json.dump({"summary": summary, "ranks": ranks}, f)
     for k, v in summary.items():
         assert v["n"] == 66 and 0.3 <= v["mean_rank"] <= 0.7 and v["outside"] <= 8, summary
