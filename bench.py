@@ -75,6 +75,8 @@ def parse():
     ap.add_argument("--pipeline", action="store_true",
                     help="gather every step through LogpStepLoop's two-deep async pipeline even at N = 1 (RCCL at "
                          "world size 1: the device-tensor branch of the N > 1 step on a one-GPU box)")
+    ap.add_argument("--no-native", action="store_true",
+                    help="N > 1: step through torch.distributed's all-gather loop instead of the native one")
     ap.add_argument("--side-out", default=os.path.join(REPO, "gpurun_out", "bench_side.json"),
                     help="file the full record (every side leg) is written to; stdout's last line is the headline")
     return ap.parse_args()
@@ -306,6 +308,14 @@ def main():
     fast_n = lp.bind_n(theta, loop.out)
     loop.evaluate = lambda out: fasts[out.data_ptr()]()
     loop.evaluate_n = lambda out, k: fast_n(k)     # N = 1: the K steps in one native call
+    # N > 1 over RCCL (device buffers): the K steps -- launch + all-gather, two in flight -- in one
+    # native call too (ngrtd_logp_gather_n on libngrtd's own communicator); gloo rehearsals and
+    # --no-native keep torch.distributed's loop
+    native = None
+    if loop.collective and args.backend == "nccl" and not args.no_native:
+        from noblegas_rtd_mcmc_amd.distributed import NativeComm
+        native = NativeComm(lp.ctx)
+        loop.gather_n = lambda k: native.gather_n(lp, theta, Wb, loop.bufs2, loop.gathers2, k)
 
     # which kernels does one step launch? (one profiled step)
     lp.ctx.set_profiling(True)
@@ -374,7 +384,7 @@ def main():
     #  * otherwise the kernels of every k-th step get their own event pairs (read back
     #    after the region, no host syncs inside it).
     lp.kernel_stats(reset=True)
-    per_step_events = loop.collective or not single_kernel
+    per_step_events = (loop.collective and native is None) or not single_kernel
     t0 = time.perf_counter()
     if per_step_events:
         def hook(i, before):
@@ -389,7 +399,7 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     ks = dict(lp.kernel_stats(reset=True))
-    if not per_step_events:
+    if not per_step_events and native is None:
         ks["fused"] = (lp.region_ms(), args.steps)
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
@@ -402,6 +412,18 @@ def main():
     finite_frac = float(torch.isfinite(loop.ensemble()).double().mean())
     if not finite_frac > 0.5:
         raise SystemExit("bench: only %.3f of the ensemble log-probs are finite" % finite_frac)
+    if native is not None:
+        # the native loop's region holds launches and gathers: the kernel's own duration for the
+        # roofline from a burst of event-bracketed launches right after it (outside the timed region)
+        ks["gather_region_ms_per_step"] = (lp.region_ms(), args.steps)
+        lp.ctx.set_profiling(True)
+        lp.kernel_stats(reset=True)
+        loop.run(max(10, args.steps // 4))
+        torch.cuda.synchronize()
+        lp.ctx.set_profiling(False)
+        ks["fused"] = lp.kernel_stats(reset=True)["fused"]
+        if world > 1:
+            dist.barrier()
 
     if rank == 0:
         line = report(args, spec, lp, ks, dt, world, W_total, Wb, plan_build_ms, theta, theta_h, side)
@@ -412,10 +434,14 @@ def main():
             line["config"]["backend"] = args.backend + (" (host-staged all-gather)" if args.backend == "gloo" else "")
             line["config"]["one_device"] = bool(args.one_device)
             line["config"]["pipeline"] = bool(args.pipeline or world > 1)
+            line["config"]["step_loop"] = ("native (ngrtd_logp_gather_n: libngrtd's RCCL communicator)" if native is not None
+                                           else "torch.distributed")
         # the full record (every side leg) goes to a file; stdout's LAST line is the compact
         # headline object the driver parses (<= HEADLINE_MAX_BYTES, tests/test_bench_line_cpu.py)
         side_path = write_side(line, args.side_out)
         print(json.dumps(headline(line, side_path)), flush=True)
+    if native is not None:
+        native.close()
     if dist.is_initialized():
         dist.destroy_process_group()
 

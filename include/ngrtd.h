@@ -278,6 +278,28 @@ int ngrtd_logp_n(ngrtd_plan* plan, const double* theta, int64_t W, double* logp,
  * kernel time for the roofline: the n launches back to back, as rocprofv3 sees them. */
 int ngrtd_plan_region_ms(ngrtd_plan* plan, float* ms);
 
+/* Multi-GPU walker blocks (BASELINE c5; the reference itself runs one process per PyMC3 chain,
+ * run_age_mcmc_utils.py:416, and has no multi-GPU counterpart): an RCCL communicator over the
+ * job's ranks (one process per GPU) and the bench step loop with its all-gather in native code.
+ * rccl_path: the RCCL library to dlopen (the one torch loaded, so that both share it; NULL:
+ * "librccl.so.1").  ngrtd_comm_unique_id runs on rank 0; the caller broadcasts the 128 bytes. */
+typedef struct ngrtd_comm ngrtd_comm;
+int ngrtd_comm_unique_id(const char* rccl_path, uint8_t* id128);
+int ngrtd_comm_create(ngrtd_ctx* ctx, const char* rccl_path, const uint8_t* id128, int32_t nranks, int32_t rank,
+                      ngrtd_comm** out);
+int ngrtd_comm_destroy(ngrtd_comm* comm);
+
+/* n steps of distributed.LogpStepLoop on device buffers: step i writes this rank's block log-probs
+ * (W walkers) into bufs + (i % 2) per and all-gathers the per-entry blocks of every rank into
+ * gathered + (i % 2) per nranks (ncclAllGather on the communicator's own stream), two steps in
+ * flight: step i's gather overlaps step i + 1's launch, step i + 2's launch waits for it (it
+ * reuses the buffer) -- stream events, no host synchronisation, no per-step host round trip.
+ * bufs: [2][per] (entries W..per-1 untouched: the caller pads them), gathered: [2][nranks per].
+ * The plan's stream waits for the last gathers before returning, so a sync on it covers them;
+ * ngrtd_plan_region_ms then gives the n steps' device time (launches + gathers). */
+int ngrtd_logp_gather_n(ngrtd_plan* plan, ngrtd_comm* comm, const double* theta, int64_t W, int64_t per,
+                        double* bufs, double* gathered, int64_t n);
+
 /* Forward model outputs of the plan (posterior predictive, run_age_mcmc.py:251-319,
  * noble_gas_mcmc.py:645-653): ce_out [G][L][W] (may be NULL), rtd_out [K][L][W]
  * (may be NULL).                                                                     */

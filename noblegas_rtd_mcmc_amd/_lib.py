@@ -116,6 +116,11 @@ PROTOTYPES = {
     "ngrtd_surrogate_check": (C.c_int, [_dp, C.c_int32, C.c_int64, C.c_double, _dp, _dp]),
     "ngrtd_c0_check": (C.c_int, [C.c_double, C.c_double, _dp, _i32p, _i32p, _dp]),
     "ngrtd_epm_window_check": (C.c_int, [C.c_double, C.c_double, C.c_double, C.c_int32, _i32p]),
+    "ngrtd_comm_unique_id": (C.c_int, [C.c_char_p, C.c_void_p]),
+    "ngrtd_comm_create": (C.c_int, [C.c_void_p, C.c_char_p, C.c_void_p, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
+    "ngrtd_comm_destroy": (C.c_int, [C.c_void_p]),
+    "ngrtd_logp_gather_n": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p,
+                                      C.c_int64]),
 }
 
 

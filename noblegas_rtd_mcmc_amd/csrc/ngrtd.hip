@@ -5,6 +5,8 @@
 // convolution_integral_utils.py:305-333 applies them), chooses the launch geometry and
 // enqueues the kernels of ngrtd_kernels.hpp on the context stream.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <dlfcn.h>
 
 #include <algorithm>
 #include <cmath>
@@ -2066,6 +2068,119 @@ int ngrtd_logp_n(ngrtd_plan* p, const double* theta, int64_t W, double* logp, in
     HIP_TRY(ctx, hipEventRecord(p->region[0], S(ctx)));
     for (int64_t i = 0; i < n; ++i) NG_CHECK(plan_run(p, theta, W, logp, nullptr, nullptr));
     HIP_TRY(ctx, hipEventRecord(p->region[1], S(ctx)));
+    p->region_set = true;
+    return NGRTD_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------ RCCL (multi-GPU walker blocks)
+// The RCCL entry points are resolved with dlsym from the library the caller names (the one torch
+// already loaded, so one RCCL instance serves both) -- libngrtd has no link-time RCCL dependency.
+struct RcclApi {
+    void* lib = nullptr;
+    decltype(&ncclGetUniqueId) get_id = nullptr;
+    decltype(&ncclCommInitRank) init = nullptr;
+    decltype(&ncclAllGather) all_gather = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclGetErrorString) err = nullptr;
+    bool load(const char* path) {
+        lib = dlopen(path && *path ? path : "librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!lib) return false;
+        get_id = reinterpret_cast<decltype(get_id)>(dlsym(lib, "ncclGetUniqueId"));
+        init = reinterpret_cast<decltype(init)>(dlsym(lib, "ncclCommInitRank"));
+        all_gather = reinterpret_cast<decltype(all_gather)>(dlsym(lib, "ncclAllGather"));
+        destroy = reinterpret_cast<decltype(destroy)>(dlsym(lib, "ncclCommDestroy"));
+        err = reinterpret_cast<decltype(err)>(dlsym(lib, "ncclGetErrorString"));
+        return get_id && init && all_gather && destroy && err;
+    }
+};
+
+struct ngrtd_comm {
+    ngrtd_ctx* ctx = nullptr;
+    RcclApi api;
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+    hipStream_t gs = nullptr;               // the gathers' stream
+    hipEvent_t eval[2] = {nullptr, nullptr}, gath[2] = {nullptr, nullptr};
+    bool pending[2] = {false, false};       // a gather of buffer s may still run
+};
+
+extern "C" {
+
+int ngrtd_comm_unique_id(const char* rccl_path, uint8_t* id128) {
+    if (!id128) return NGRTD_EINVAL;
+    RcclApi api;
+    if (!api.load(rccl_path)) return NGRTD_EDEVICE;
+    ncclUniqueId id;
+    if (api.get_id(&id) != ncclSuccess) return NGRTD_EDEVICE;
+    std::memcpy(id128, id.internal, NCCL_UNIQUE_ID_BYTES);
+    return NGRTD_OK;
+}
+
+int ngrtd_comm_create(ngrtd_ctx* ctx, const char* rccl_path, const uint8_t* id128, int32_t nranks, int32_t rank,
+                      ngrtd_comm** out) {
+    if (!ctx || !id128 || !out || nranks < 1 || rank < 0 || rank >= nranks) return NGRTD_EINVAL;
+    *out = nullptr;
+    std::unique_ptr<ngrtd_comm> c(new ngrtd_comm);
+    c->ctx = ctx;
+    c->nranks = nranks;
+    c->rank = rank;
+    if (!c->api.load(rccl_path)) return set_err(ctx, NGRTD_EDEVICE, "cannot load RCCL (%s): %s", rccl_path ? rccl_path : "librccl.so.1", dlerror());
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    ncclUniqueId id;
+    std::memcpy(id.internal, id128, NCCL_UNIQUE_ID_BYTES);
+    const ncclResult_t r = c->api.init(&c->comm, nranks, id, rank);
+    if (r != ncclSuccess) return set_err(ctx, NGRTD_EDEVICE, "ncclCommInitRank: %s", c->api.err(r));
+    HIP_TRY(ctx, hipStreamCreateWithFlags(&c->gs, hipStreamNonBlocking));
+    for (int s = 0; s < 2; ++s) {
+        HIP_TRY(ctx, hipEventCreateWithFlags(&c->eval[s], hipEventDisableTiming));
+        HIP_TRY(ctx, hipEventCreateWithFlags(&c->gath[s], hipEventDisableTiming));
+    }
+    *out = c.release();
+    return NGRTD_OK;
+}
+
+int ngrtd_comm_destroy(ngrtd_comm* c) {
+    if (!c) return NGRTD_ESTATE;
+    if (c->gs) (void)hipStreamSynchronize(c->gs);
+    if (c->comm) (void)c->api.destroy(c->comm);
+    for (int s = 0; s < 2; ++s) {
+        if (c->eval[s]) (void)hipEventDestroy(c->eval[s]);
+        if (c->gath[s]) (void)hipEventDestroy(c->gath[s]);
+    }
+    if (c->gs) (void)hipStreamDestroy(c->gs);
+    delete c;
+    return NGRTD_OK;
+}
+
+int ngrtd_logp_gather_n(ngrtd_plan* p, ngrtd_comm* c, const double* theta, int64_t W, int64_t per, double* bufs,
+                        double* gathered, int64_t n) {
+    if (!p || !c) return NGRTD_ESTATE;
+    ngrtd_ctx* ctx = p->ctx;
+    if (c->ctx != ctx) return set_err(ctx, NGRTD_EINVAL, "communicator of another context");
+    if (!theta || !bufs || !gathered || W < 1 || W > p->max_w || per < W || n < 0)
+        return set_err(ctx, NGRTD_EINVAL, "bad theta/bufs/gathered/W (max %lld)/per/n", (long long)p->max_w);
+    for (hipEvent_t& e : p->region)
+        if (!e) e = ctx->take_event();
+    hipStream_t st = S(ctx);
+    HIP_TRY(ctx, hipEventRecord(p->region[0], st));
+    for (int64_t i = 0; i < n; ++i) {
+        const int s = (int)(i & 1);
+        double* b = bufs + (int64_t)s * per;
+        double* g = gathered + (int64_t)s * per * c->nranks;
+        if (c->pending[s]) HIP_TRY(ctx, hipStreamWaitEvent(st, c->gath[s], 0));   // buffer s is free again
+        NG_CHECK(plan_run(p, theta, W, b, nullptr, nullptr));
+        HIP_TRY(ctx, hipEventRecord(c->eval[s], st));
+        HIP_TRY(ctx, hipStreamWaitEvent(c->gs, c->eval[s], 0));
+        const ncclResult_t r = c->api.all_gather(b, g, (size_t)per, ncclDouble, c->comm, c->gs);
+        if (r != ncclSuccess) return set_err(ctx, NGRTD_EDEVICE, "ncclAllGather: %s", c->api.err(r));
+        HIP_TRY(ctx, hipEventRecord(c->gath[s], c->gs));
+        c->pending[s] = true;
+    }
+    for (int s = 0; s < 2; ++s)      // the plan's stream waits for the gathers in flight
+        if (c->pending[s]) HIP_TRY(ctx, hipStreamWaitEvent(st, c->gath[s], 0));
+    HIP_TRY(ctx, hipEventRecord(p->region[1], st));
     p->region_set = true;
     return NGRTD_OK;
 }

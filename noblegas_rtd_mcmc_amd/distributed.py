@@ -12,6 +12,9 @@ a single collective per step, never bucketed.
 or per walker) over the shards: its chains propose from their own histories, so sampling
 itself exchanges nothing; the trace's log-probs are gathered once at the end.
 """
+import ctypes as C
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -37,6 +40,58 @@ def all_gather_into(out, buf, group=None):
     dist.all_gather_into_tensor(ho, buf.cpu(), group=group)
     out.copy_(ho)
     return out
+
+
+def rccl_library_path():
+    """The RCCL library torch itself loaded (its bundled librccl.so when present), so that the
+    native communicator (ngrtd_comm) shares one RCCL instance with torch.distributed; None:
+    the system's librccl.so.1."""
+    d = os.path.join(os.path.dirname(torch.__file__), "lib")
+    for name in ("librccl.so", "librccl.so.1"):
+        path = os.path.join(d, name)
+        if os.path.exists(path):
+            return path
+    return None
+
+
+class NativeComm:
+    """libngrtd's own RCCL communicator (ngrtd_comm) over the ranks of ``group``: rank 0 draws the
+    unique id, torch.distributed broadcasts it, every rank joins.  ``gather_n(plan, theta, W,
+    bufs, gathers, k)`` runs k steps of LogpStepLoop in native code (ngrtd_logp_gather_n: the
+    block's log-prob launch, then ncclAllGather on the communicator's stream, two steps in flight)
+    -- no Python, ctypes or torch.distributed call per step."""
+
+    def __init__(self, ctx, group=None):
+        from . import _lib
+        self.ctx, self.lib = ctx, ctx.lib
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        path = rccl_library_path()
+        self.path = path.encode() if path else None
+        obj = [None]
+        if self.rank == 0:
+            buf = (C.c_uint8 * 128)()
+            st = self.lib.ngrtd_comm_unique_id(self.path, buf)
+            if st != _lib.NGRTD_OK:
+                raise _lib.NgrtdError("ngrtd_comm_unique_id failed (%d)" % st)
+            obj = [bytes(buf)]
+        dist.broadcast_object_list(obj, src=0, group=group)
+        idb = (C.c_uint8 * 128).from_buffer_copy(obj[0])
+        h = C.c_void_p()
+        ctx.check(self.lib.ngrtd_comm_create(ctx.h, self.path, idb, self.world, self.rank, C.byref(h)), "ngrtd_comm_create")
+        self.h = h
+
+    def gather_n(self, plan, theta, W, bufs, gathers, k):
+        """bufs: CUDA float64 [2][per], gathers: [2][world per] (contiguous)."""
+        per = bufs.shape[1]
+        self.ctx.set_stream(torch.cuda.current_stream(theta.device).cuda_stream)
+        self.ctx.check(self.lib.ngrtd_logp_gather_n(plan.plan, self.h, C.c_void_p(theta.data_ptr()), int(W), int(per),
+                                                    C.c_void_p(bufs.data_ptr()), C.c_void_p(gathers.data_ptr()), int(k)),
+                       "ngrtd_logp_gather_n")
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.ngrtd_comm_destroy(self.h)
+            self.h = None
 
 
 class LogpStepLoop:
@@ -76,11 +131,16 @@ class LogpStepLoop:
         # gather every step: several ranks, or a forced pipeline (world 1 included)
         self.collective = self.world > 1 or bool(pipeline)
         nb = 2 if self.collective else 1
-        self.bufs = [torch.full((self.per,), float("nan"), dtype=dtype, device=device) for _ in range(nb)]
+        # the two block buffers and the two gathered vectors as rows of one tensor each (the
+        # native loop, gather_n, takes them as [2][per] / [2][world per])
+        self.bufs2 = torch.full((nb, self.per), float("nan"), dtype=dtype, device=device)
+        self.bufs = [self.bufs2[i] for i in range(nb)]
         self.outs = [b[: self.hi - self.lo] for b in self.bufs]
-        self.gathers = ([torch.empty(self.per * self.world, dtype=dtype, device=device) for _ in range(nb)]
-                        if self.collective else self.bufs)
+        self.gathers2 = torch.empty((nb, self.per * self.world), dtype=dtype, device=device) if self.collective else None
+        self.gathers = [self.gathers2[i] for i in range(nb)] if self.collective else self.bufs
         self.buf, self.out, self.gathered = self.bufs[0], self.outs[0], self.gathers[0]
+        # optional: gather_n(k) = k steps of the two-deep pipeline in native code (NativeComm)
+        self.gather_n = None
 
     def step(self):
         self.evaluate(self.outs[0])
@@ -101,6 +161,11 @@ class LogpStepLoop:
         k = int(k)
         if not self.collective and self.evaluate_n is not None and hook is None:
             self.evaluate_n(self.out, k)
+            return self.gathered
+        if self.collective and self.gather_n is not None and hook is None and self.pipeline is not False:
+            self.gather_n(k)
+            if k:
+                self.gathered = self.gathers[(k - 1) & 1]
             return self.gathered
         if not self.collective or self.pipeline is False or host_staged(self.group, self.bufs[0]):
             for i in range(k):

@@ -56,8 +56,20 @@ def main():
         step["i"] = K - 1
         seq = loop.step().clone()
         torch.cuda.synchronize()
+        # the native loop (ngrtd_logp_gather_n on libngrtd's own RCCL communicator): 3 steps per
+        # call (buffers 0, 1, 0), a different ensemble per call -- both gathered rows must be the
+        # call's own ensemble (each call's launches wait for the previous call's gathers)
+        from noblegas_rtd_mcmc_amd.distributed import NativeComm
+        native = NativeComm(lp.ctx)
+        nat = []
+        for i in range(K):
+            native.gather_n(lp, thetas[i], W, loop.bufs2, loop.gathers2, 3)
+            nat.append(loop.gathers2[:, :W].clone())
+        torch.cuda.synchronize()
+        native.close()
         np.savez(os.path.join(outdir, "pipeline.npz"), direct=direct.cpu().numpy(), snaps=snaps.cpu().numpy(),
-                 ens=ens.cpu().numpy(), seq=seq.cpu().numpy(), backend=dist.get_backend())
+                 ens=ens.cpu().numpy(), seq=seq.cpu().numpy(), backend=dist.get_backend(),
+                 native=torch.stack(nat).cpu().numpy())
         lp.close()
     finally:
         dist.destroy_process_group()

@@ -100,7 +100,9 @@ def test_rccl_pipeline_world_one(tmp_path):
     """LogpStepLoop's RCCL branch on device tensors, at world size 1 on the one GPU
     (LogpStepLoop(pipeline=True)): 12 steps over 12 different ensembles with two steps in
     flight; every step's gathered vector equals the direct log-prob of its own ensemble bit
-    for bit (snapshots taken behind the wait on each gather), as does the sequential step()."""
+    for bit (snapshots taken behind the wait on each gather), as does the sequential step().
+    Then the native loop (NativeComm: libngrtd's own RCCL communicator, ngrtd_logp_gather_n)
+    over the same buffers, 3 steps per call on each ensemble: both gathered rows equal it."""
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()), RANK="0", WORLD_SIZE="1",
                LOCAL_RANK="0")
     subprocess.run([sys.executable, os.path.join(REPO, "tests", "dist_gpu_pipeline.py"), str(tmp_path), "1000", "8",
@@ -113,3 +115,7 @@ def test_rccl_pipeline_world_one(tmp_path):
         assert np.array_equal(snaps[i], direct[i], equal_nan=True), i
     assert np.array_equal(z["ens"], direct[-1], equal_nan=True)
     assert np.array_equal(z["seq"], direct[-1], equal_nan=True)
+    nat = z["native"]                  # [K][2][W]: the native loop's two gathered rows per call
+    for i in range(direct.shape[0]):
+        assert np.array_equal(nat[i][0], direct[i], equal_nan=True), i
+        assert np.array_equal(nat[i][1], direct[i], equal_nan=True), i
