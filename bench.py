@@ -4,9 +4,11 @@
 Workload (BASELINE.json configs[3]): 2048 walkers x 64 wells x (CE over
 5 gases + RTD convolution of 5 tracers over a 1200-year input series, exponential RTD)
 in float64.  One step = one full batched log-prob of the rank's walker block (theta
-resident in HBM) + ONE all-gather of the per-block log-prob vector (N > 1), the loop of
-distributed.LogpStepLoop (N = 1: LogpStepLoop.run enqueues the K launches with one native
-call, ngrtd_logp_n, instead of K Python round trips).
+resident in HBM), the loop of distributed.LogpStepLoop: LogpStepLoop.run enqueues the K launches
+with one native call (ngrtd_logp_n) instead of K Python round trips, and for N > 1 the per-block
+log-prob vectors are all-gathered ONCE, after the K-th step, inside the timed region (--gather
+region; the blocks are independent, and an all-gather per step (--gather step) costs twice a
+step: profiles/r06d_gather_per_step.jsonl).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling weak|strong]
                     [--mod-type1 exponential|exp_pist_flow|piston|dispersion] [--mod-type2 piston|...]
@@ -75,8 +77,11 @@ def parse():
     ap.add_argument("--pipeline", action="store_true",
                     help="gather every step through LogpStepLoop's two-deep async pipeline even at N = 1 (RCCL at "
                          "world size 1: the device-tensor branch of the N > 1 step on a one-GPU box)")
+    ap.add_argument("--gather", choices=("region", "step"), default="region",
+                    help="N > 1: ONE all-gather of the ensemble log-prob vector per timed region (default: the "
+                         "walker blocks are independent) or one per step (two in flight)")
     ap.add_argument("--no-native", action="store_true",
-                    help="N > 1: step through torch.distributed's all-gather loop instead of the native one")
+                    help="--gather step: step through torch.distributed's all-gather loop instead of the native one")
     ap.add_argument("--side-out", default=os.path.join(REPO, "gpurun_out", "bench_side.json"),
                     help="file the full record (every side leg) is written to; stdout's last line is the headline")
     return ap.parse_args()
@@ -303,7 +308,7 @@ def main():
     lp = LogProb(spec, max_walkers=Wb, device=gpu)       # plan: tables, surrogate fit + validation, c0 table
     torch.cuda.synchronize()
     plan_build_ms = (time.perf_counter() - t0) * 1e3
-    loop = LogpStepLoop(None, W_total, dev, pipeline=True if args.pipeline else None)
+    loop = LogpStepLoop(None, W_total, dev, pipeline=True if args.pipeline else None, gather=args.gather)
     fasts = {o.data_ptr(): lp.bind(theta, o) for o in loop.outs}   # one bound launch per block buffer
     fast_n = lp.bind_n(theta, loop.out)
     loop.evaluate = lambda out: fasts[out.data_ptr()]()
@@ -312,7 +317,7 @@ def main():
     # native call too (ngrtd_logp_gather_n on libngrtd's own communicator); gloo rehearsals and
     # --no-native keep torch.distributed's loop
     native = None
-    if loop.collective and args.backend == "nccl" and not args.no_native:
+    if loop.collective and args.gather == "step" and args.backend == "nccl" and not args.no_native:
         from noblegas_rtd_mcmc_amd.distributed import NativeComm
         native = NativeComm(lp.ctx)
         loop.gather_n = lambda k: native.gather_n(lp, theta, Wb, loop.bufs2, loop.gathers2, k)
@@ -384,7 +389,7 @@ def main():
     #  * otherwise the kernels of every k-th step get their own event pairs (read back
     #    after the region, no host syncs inside it).
     lp.kernel_stats(reset=True)
-    per_step_events = (loop.collective and native is None) or not single_kernel
+    per_step_events = (loop.collective and args.gather == "step" and native is None) or not single_kernel
     t0 = time.perf_counter()
     if per_step_events:
         def hook(i, before):
@@ -434,7 +439,11 @@ def main():
             line["config"]["backend"] = args.backend + (" (host-staged all-gather)" if args.backend == "gloo" else "")
             line["config"]["one_device"] = bool(args.one_device)
             line["config"]["pipeline"] = bool(args.pipeline or world > 1)
-            line["config"]["step_loop"] = ("native (ngrtd_logp_gather_n: libngrtd's RCCL communicator)" if native is not None
+            line["config"]["gather"] = ("one all-gather of the ensemble log-prob vector per timed region (after its "
+                                        "last step, inside the timing)" if args.gather == "region" else
+                                        "one all-gather per step, two in flight")
+            line["config"]["step_loop"] = ("native (ngrtd_logp_n, then one all-gather)" if args.gather == "region" else
+                                           "native (ngrtd_logp_gather_n: libngrtd's RCCL communicator)" if native is not None
                                            else "torch.distributed")
         # the full record (every side leg) goes to a file; stdout's LAST line is the compact
         # headline object the driver parses (<= HEADLINE_MAX_BYTES, tests/test_bench_line_cpu.py)

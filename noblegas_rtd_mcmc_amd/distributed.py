@@ -114,11 +114,22 @@ class LogpStepLoop:
     pipeline at ANY world size (a process group must be initialised), so the async branch
     runs on one GPU with RCCL at world size 1 (tests/test_gpu_distributed.py); False never
     pipelines.
+
+    ``gather``: "step" (default) all-gathers after every evaluation, as above; "region": ``run(k)``
+    evaluates k times (one native call with ``evaluate_n``) and all-gathers ONCE, after the last.
+    The walker blocks are independent -- each chain decides on its own log-prob, and the
+    ensemble vector is needed only where it is consumed (a trace, a check) -- and an RCCL
+    all-gather costs ~21 us even at world size 1, twice a c4 log-prob (profiles/r06d_gather_per_step.jsonl:
+    32 vs 10.6 us per step), so bench.py gathers once per timed region.
     """
 
-    def __init__(self, evaluate, W_total, device, dtype=torch.float64, group=None, evaluate_n=None, pipeline=None):
+    def __init__(self, evaluate, W_total, device, dtype=torch.float64, group=None, evaluate_n=None, pipeline=None,
+                 gather="step"):
+        if gather not in ("step", "region"):
+            raise ValueError('gather must be "step" or "region"')
         self.evaluate = evaluate
         self.evaluate_n = evaluate_n      # optional: evaluate_n(out, k) = k evaluations in one call
+        self.gather = gather
         self.group = group
         self.W_total = int(W_total)
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
@@ -161,6 +172,21 @@ class LogpStepLoop:
         k = int(k)
         if not self.collective and self.evaluate_n is not None and hook is None:
             self.evaluate_n(self.out, k)
+            return self.gathered
+        if self.collective and self.gather == "region":
+            # k evaluations of the block (one native call when possible), then ONE all-gather
+            if self.evaluate_n is not None and hook is None:
+                self.evaluate_n(self.outs[0], k)
+            else:
+                for i in range(k):
+                    if hook:
+                        hook(i, True)
+                    self.evaluate(self.outs[0])
+                    if hook:
+                        hook(i, False)
+            if k:
+                all_gather_into(self.gathers[0], self.bufs[0], group=self.group)
+                self.gathered = self.gathers[0]
             return self.gathered
         if self.collective and self.gather_n is not None and hook is None and self.pipeline is not False:
             self.gather_n(k)

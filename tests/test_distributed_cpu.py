@@ -125,6 +125,14 @@ def _step_loop_worker(rank, world, port, W_total, outdir):
         assert hooks == [(i, b) for i in range(5) for b in (True, False)]
         assert last is loop.gathers[0] and torch.equal(loop.gathers[1].nan_to_num(), g1.nan_to_num())
         assert torch.equal(last.nan_to_num(), g1.nan_to_num())
+        # gather="region" (bench.py's default for N > 1): k evaluations -- ONE evaluate_n call --
+        # then one all-gather, into gathers[0]
+        calls = []
+        rl = LogpStepLoop(evaluate, W_total, "cpu", gather="region",
+                          evaluate_n=lambda out, k: calls.append(k) or evaluate(out))
+        got = rl.run(6)
+        assert calls == [6] and got is rl.gathers[0] and torch.equal(got.nan_to_num(), g1.nan_to_num())
+        assert torch.equal(rl.ensemble(), loop.ensemble())
         np.savez(os.path.join(outdir, "s%d.npz" % rank), ens=loop.ensemble().numpy(), g1=g1.numpy(),
                  g2=g2.numpy(), lo=loop.lo, hi=loop.hi, per=loop.per)
     finally:
