@@ -2079,6 +2079,12 @@ int ngrtd_logp_n(ngrtd_plan* p, const double* theta, int64_t W, double* logp, in
 // already loaded, so one RCCL instance serves both) -- libngrtd has no link-time RCCL dependency.
 struct RcclApi {
     void* lib = nullptr;
+    RcclApi() = default;
+    RcclApi(const RcclApi&) = delete;
+    RcclApi& operator=(const RcclApi&) = delete;
+    ~RcclApi() {
+        if (lib) dlclose(lib);   // (a library torch loaded stays loaded: dlclose drops our reference)
+    }
     decltype(&ncclGetUniqueId) get_id = nullptr;
     decltype(&ncclCommInitRank) init = nullptr;
     decltype(&ncclAllGather) all_gather = nullptr;
@@ -2104,6 +2110,15 @@ struct ngrtd_comm {
     hipStream_t gs = nullptr;               // the gathers' stream
     hipEvent_t eval[2] = {nullptr, nullptr}, gath[2] = {nullptr, nullptr};
     bool pending[2] = {false, false};       // a gather of buffer s may still run
+    ~ngrtd_comm() {                         // (also the cleanup of a half-built communicator)
+        if (gs) (void)hipStreamSynchronize(gs);
+        if (comm) (void)api.destroy(comm);
+        for (int s = 0; s < 2; ++s) {
+            if (eval[s]) (void)hipEventDestroy(eval[s]);
+            if (gath[s]) (void)hipEventDestroy(gath[s]);
+        }
+        if (gs) (void)hipStreamDestroy(gs);
+    }
 };
 
 extern "C" {
@@ -2143,13 +2158,6 @@ int ngrtd_comm_create(ngrtd_ctx* ctx, const char* rccl_path, const uint8_t* id12
 
 int ngrtd_comm_destroy(ngrtd_comm* c) {
     if (!c) return NGRTD_ESTATE;
-    if (c->gs) (void)hipStreamSynchronize(c->gs);
-    if (c->comm) (void)c->api.destroy(c->comm);
-    for (int s = 0; s < 2; ++s) {
-        if (c->eval[s]) (void)hipEventDestroy(c->eval[s]);
-        if (c->gath[s]) (void)hipEventDestroy(c->gath[s]);
-    }
-    if (c->gs) (void)hipStreamDestroy(c->gs);
     delete c;
     return NGRTD_OK;
 }
