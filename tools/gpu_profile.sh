@@ -9,6 +9,10 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${1:-run}
 # BENCH_ARGS: extra bench.py flags (e.g. "--mod-type1 exp_pist_flow"); SKIP_TESTS=1 skips pytest
 BA=${BENCH_ARGS:-}
+# PMC_ARGS: extra flags of the PMC passes only (default: no side legs -- the headline kernel's
+# counters; every counter pass serialises each dispatch, and the side legs' sampling runs
+# dispatch hundreds of thousands of kernels)
+PA=${PMC_ARGS:---no-models --no-reference-runs --no-sampler}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
@@ -28,7 +32,7 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" \
            "GRBM_GUI_ACTIVE SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT"; do
   i=$((i+1))
   step "pmc$i $grp"
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d $OUT/pmc$i -o pmc$i -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-exact $BA > $OUT/pmc_bench.json 2> $OUT/pmc$i.err || { echo "pmc$i failed rc=$?" >> $OUT/steps.log; exit 1; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d $OUT/pmc$i -o pmc$i -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-exact $PA $BA > $OUT/pmc_bench.json 2> $OUT/pmc$i.err || { echo "pmc$i failed rc=$?" >> $OUT/steps.log; exit 1; }
 done
 step summary
 python tools/profile_summary.py $OUT $OUT/summ > /dev/null || { echo "summary failed" >> $OUT/steps.log; exit 1; }

@@ -47,13 +47,15 @@ def build(defines=()):
     import __graft_entry__ as g
     lib = probe_lib(defines)
     if not os.path.exists(lib) or os.path.getmtime(lib) < max(os.path.getmtime(p) for p in g._deps()):
-        objs = []
-        for src in g._sources():
+        objs, procs = [], []
+        for src in g._sources():          # in parallel, as __graft_entry__.build
             obj = src + ".probe%d.o" % os.getpid()
-            subprocess.run(["hipcc"] + g.HIPCC_FLAGS + g.EXTRA_FLAGS.get(os.path.basename(src), []) +
-                           ["-DNGRTD_SECTION_PROBE"] + ["-D" + d for d in defines] + ["-c", "-o", obj, src],
-                           check=True)
+            procs.append(subprocess.Popen(["hipcc"] + g.HIPCC_FLAGS + g.EXTRA_FLAGS.get(os.path.basename(src), []) +
+                                          ["-DNGRTD_SECTION_PROBE"] + ["-D" + d for d in defines] + ["-c", "-o", obj, src]))
             objs.append(obj)
+        for pr in procs:
+            if pr.wait() != 0:
+                raise subprocess.CalledProcessError(pr.returncode, pr.args)
         subprocess.run(["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", lib] + objs, check=True)
         for o in objs:
             os.remove(o)
