@@ -24,6 +24,7 @@ groups, variables, the dimension scales with their REFERENCE_LIST back-reference
 variable's DIMENSION_LIST and netCDF's _Netcdf4Dimid / _Netcdf4Coordinates / _NCProperties.
 """
 import struct
+import os
 import zlib
 
 import numpy as np
@@ -835,6 +836,34 @@ class H5Writer:
         sh = np.frombuffer(np.ascontiguousarray(blk).tobytes(), np.uint8).reshape(-1, es).T.tobytes()   # shuffle
         return zlib.compress(sh, self.level)
 
+    def _payloads(self, work):
+        """(h, off, payload) for the (dataset, chunk offset) pairs of ``work``, in order, deflated
+        on a few threads (zlib releases the GIL: the compression is ~60 % of a trace write) with
+        at most ``2 * threads`` payloads held at a time.  Same bytes as one by one."""
+        import concurrent.futures as cf
+        try:
+            nt = len(os.sched_getaffinity(0))
+        except (AttributeError, OSError):
+            nt = os.cpu_count() or 1
+        nt = max(1, min(8, nt, len(work)))
+        if nt == 1:
+            for h, off in work:
+                yield h, off, self._chunk_payload(h, off)
+            return
+        with cf.ThreadPoolExecutor(max_workers=nt) as ex:
+            pending = []
+            it = iter(work)
+            for h, off in it:
+                pending.append((h, off, ex.submit(self._chunk_payload, h, off)))
+                if len(pending) >= 2 * nt:
+                    break
+            for h, off in it:
+                hh, oo, fu = pending.pop(0)
+                yield hh, oo, fu.result()
+                pending.append((h, off, ex.submit(self._chunk_payload, h, off)))
+            for hh, oo, fu in pending:
+                yield hh, oo, fu.result()
+
     def _messages(self, h, ctx):
         o = self.objs[h]
         msgs = []
@@ -947,8 +976,9 @@ class H5Writer:
     def save(self, path_or_file):
         """Write the file (a path or a seekable binary file object).  Datasets are streamed
         after the metadata: a contiguous one as its bytes, a chunked one as its B-tree nodes
-        (their count follows from the chunk count) then each chunk, compressed and written
-        one at a time (only one chunk's payload is held); the superblock and object headers,
+        (their count follows from the chunk count) then each chunk, compressed on a few
+        threads ahead of the writes (a bounded window of payloads held, _payloads) and written
+        in order; the superblock and object headers,
         whose sizes pass 1 fixed, are written last, when every address is known."""
         import io
         lay = self._layout()
@@ -965,6 +995,9 @@ class H5Writer:
                 f.write(blob)
             p = lay["end"]
             data, btree = {}, {}
+            # every chunk of every compressed dataset, in the order they are written below
+            stream = self._payloads([(h, off) for h in self.order
+                                     if self.compress and self.objs[h]["kind"] == "dataset" for off in self._chunk_list(h)])
             for h in self.order:
                 if self.objs[h]["kind"] != "dataset":
                     continue
@@ -984,7 +1017,8 @@ class H5Writer:
                     p += self._node_size(h)
                 ch = []
                 for off in offs:
-                    pl = self._chunk_payload(h, off)
+                    hh, oo, pl = next(stream)
+                    assert hh == h and oo == off
                     p = (p + 7) // 8 * 8
                     put(p, pl)
                     ch.append((off, p, len(pl)))
