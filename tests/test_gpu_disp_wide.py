@@ -148,14 +148,16 @@ def test_wide_independent_of_ensemble_size():
     lp.close()
 
 
+@pytest.mark.parametrize("per_well", [True, False])
 @pytest.mark.parametrize("jac", [True, False])
 @pytest.mark.parametrize("model", ["dispersion", "dispersion-piston"])
-def test_reference_shape_demcz_bitwise(model, jac):
+def test_reference_shape_demcz_bitwise(model, jac, per_well):
     """The reference's own dispersion run shape -- RTD-only, 4 tracers, savenum 123, 1 well,
     3 chains, N = 25 256 -- through the device DEMetropolisZ (per-well chains: the proposal
     kernel, the wide sums + generic log-prob, the accept kernel per step) against the torch
     sampler over the same plan's ngrtd_logp_units, bit for bit through tuning, stop_tuning and
-    the draws."""
+    the draws.  per_well False: one chain per walker, the decision in the log-prob launch's
+    per-walker reduction (plan_run with the DemcAccept), on the wide plan."""
     import torch
     from noblegas_rtd_mcmc_amd import workloads as wl
     from noblegas_rtd_mcmc_amd.engine import LogProb
@@ -165,10 +167,11 @@ def test_reference_shape_demcz_bitwise(model, jac):
     x0 = torch.from_numpy(wl.test_point(spec, W)).cuda()
     lp = LogProb(spec, max_walkers=W)
     assert lp.info(W)["disp_wide_g"] > 0
-    kw = dict(tune_interval=4, seed=1234, per_well=True)
+    kw = dict(tune_interval=4, seed=1234, per_well=per_well)
     dev = DeviceDEMetropolisZ(lp, **kw).run(x0, tune=16, draws=12)
     tf = Transform.from_spec(spec) if jac else None
-    ref = DEMetropolisZ(lambda t: lp.units(t), transform=tf, **kw).run(x0, tune=16, draws=12)
+    f = (lambda t: lp.units(t)) if per_well else (lambda t: lp(t))
+    ref = DEMetropolisZ(f, transform=tf, **kw).run(x0, tune=16, draws=12)
     for k in ("x", "lp", "samples", "logp", "accepted", "accept", "lamb", "scaling"):
         assert _same(dev[k], ref[k]), k
     assert 0 < int(dev["accepted"].sum()) < dev["accepted"].numel()
