@@ -92,7 +92,8 @@ HEADLINE_MAX_BYTES = 7000     # the driver keeps a bounded stdout tail: the last
 # the headline keys kept verbatim (the contract's fields + the measured companions of `value`)
 HEADLINE_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
                  "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "plan_build_ms",
-                 "value_amortized_20k", "exact_value", "host_staged_value", "ensemble_finite_frac", "kernels_ms",
+                 "value_amortized_20k", "conv_evals_per_s", "exact_value", "host_staged_value", "ensemble_finite_frac",
+                 "kernels_ms",
                  "geometry")
 
 
@@ -552,6 +553,8 @@ def report(args, spec, lp, ks, dt, world, W_total, Wb, plan_build_ms, theta, the
         "kernels_ms": {k: v[0] / max(v[1], 1) for k, v in ks.items()},
         "geometry": info,
     }
+    # also (walker, well, tracer) convolution evaluations per second
+    line["conv_evals_per_s"] = line["value"] * spec.n_wells * len(spec.rtd.tracers)
     line.update({k: v for k, v in side.items() if k != "models"})
     # the reference's run length (run_age_mcmc_utils.py:412-417: tune 10 000 + draws 10 000)
     # with the plan build paid once: W S / (S t_step + plan_build)
