@@ -156,8 +156,10 @@ def headline(full, side_path=None):
         rr = full.get(leg)
         if isinstance(rr, dict) and "error" not in rr:
             s = {"runs": {r["run"]: [_r(r.get("wall_s")), _r(r.get("speedup_vs_reference")), _r(r.get("accept_rate"), 3)]
+                          + ([_r(r["speedup_vs_oracle_projection"])] if r.get("speedup_vs_oracle_projection") else [])
                           for r in rr.get("runs", []) if isinstance(r, dict) and "run" in r},
-                 "fields": "[wall_s, speedup_vs_reference, accept_rate]"}
+                 "fields": "[wall_s, speedup_vs_reference, accept_rate(, speedup_vs_oracle_projection: runs with no "
+                           "shipped reference time)]"}
             for k in ("total_wall_s", "reference_total_s", "reference_total_s_projected"):
                 if k in rr:
                     s[k] = _r(rr[k])
