@@ -265,10 +265,13 @@ __global__ void __launch_bounds__(dzc_threads(MIX), 2)
         const UnitArgs& uk = kernarg_opaque<UnitArgs>(kDzcArgU);
         const DemcAccept& d = kernarg_opaque<DemcAccept>(kDzcArgD);
         const DzStep sj = dz_step(d.sch, js);
-        const bool de = e1 >= 0;
+        // timing diagnostics (NGRTD_DZ_DIAG, tools/dzc_probe.py; wrong results): bit 6 no RTD
+        // likelihood, 7 no theta part, 8 no logs, 9 no history append, 10 no partner rows
+        const int dg = d.dz_diag;
+        const bool de = e1 >= 0 && !(dg & 1024);
         const int64_t R = (int64_t)P * L;
         // the state becomes history entry sj.at (chains' space)
-        if (valid && sj.at >= 0) {
+        if (valid && sj.at >= 0 && !(dg & 512)) {
             double* hrow = d.hist + ((size_t)sj.at * W + w) * R + l;
 #pragma unroll
             for (int p = 0; p < kDzcMaxP; ++p)
@@ -324,14 +327,16 @@ __global__ void __launch_bounds__(dzc_threads(MIX), 2)
             tp.tau1 = props[uk.row_tau1 * NT + tid];
             tp.nub = props[uk.row_nu * NT + tid];
         }
-        const double th = unit_logp_theta(ul, tid, l, &tp, false, false);
+        const double th = (dg & 128) ? 0.0 : unit_logp_theta(ul, tid, l, &tp, false, false);
         double like = 0.0;
         if constexpr (!CEO) {
-            const double tau = props[a.row_tau[0] * NT + tid];
-            const double eta = EPM ? props[a.row_eta[0] * NT + tid] : 1.0;
-            const double tau2 = (MIX & 1) ? props[a.row_tau[1] * NT + tid] : 1.0;
-            const double thx = LW ? props[a.row_thalf * NT + tid] : 0.5;
-            like = dzc_rtd_like<C, MIX>(ar, ul, cheb, tabl, valid, tid, slot0, l, tau, eta, tau2, thx, tp.nub);
+            if (!(dg & 64)) {
+                const double tau = props[a.row_tau[0] * NT + tid];
+                const double eta = EPM ? props[a.row_eta[0] * NT + tid] : 1.0;
+                const double tau2 = (MIX & 1) ? props[a.row_tau[1] * NT + tid] : 1.0;
+                const double thx = LW ? props[a.row_thalf * NT + tid] : 0.5;
+                like = dzc_rtd_like<C, MIX>(ar, ul, cheb, tabl, valid, tid, slot0, l, tau, eta, tau2, thx, tp.nub);
+            }
         }
         const double lpp = th + like;
         // metrop_select + tune (demc_decide_at_u's arithmetic, on the registers)
@@ -349,7 +354,7 @@ __global__ void __launch_bounds__(dzc_threads(MIX), 2)
             }
             nat = na;
         }
-        if (valid) {
+        if (valid && !(dg & 256)) {
             const int64_t li = (int64_t)js * U + (int64_t)l * W + w;
             if (d.acc_log) d.acc_log[li] = (uint8_t)acc;
             if (d.lp_log) d.lp_log[li] = cur;
