@@ -82,6 +82,9 @@ def parse():
                          "walker blocks are independent) or one per step (two in flight)")
     ap.add_argument("--no-native", action="store_true",
                     help="--gather step: step through torch.distributed's all-gather loop instead of the native one")
+    ap.add_argument("--full-line", action="store_true",
+                    help="print the full record (every side leg) as the last line instead of the headline "
+                         "(the A/B scripts under tools/ parse it)")
     ap.add_argument("--side-out", default=os.path.join(REPO, "gpurun_out", "bench_side.json"),
                     help="file the full record (every side leg) is written to; stdout's last line is the headline")
     return ap.parse_args()
@@ -452,7 +455,7 @@ def main():
         # the full record (every side leg) goes to a file; stdout's LAST line is the compact
         # headline object the driver parses (<= HEADLINE_MAX_BYTES, tests/test_bench_line_cpu.py)
         side_path = write_side(line, args.side_out)
-        print(json.dumps(headline(line, side_path)), flush=True)
+        print(json.dumps(line if args.full_line else headline(line, side_path)), flush=True)
     if native is not None:
         native.close()
     if dist.is_initialized():

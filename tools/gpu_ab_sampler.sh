@@ -13,7 +13,7 @@ for i in 1 2 3; do
   line="round $i:"
   for cfg in "$@"; do
     n=${cfg%%:*}; ev=${cfg#*:}
-    timeout -k 10 240 env ${ev//,/ } python bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-models --no-exact \
+    timeout -k 10 240 env ${ev//,/ } python bench.py --full-line --steps 200 --warmup 20 --no-cpu-baseline --no-models --no-exact \
       --no-reference-runs \
       > $OUT/$n.$i.json 2> $OUT/$n.$i.err || { echo "$n failed"; exit 1; }
     line="$line | $n $(python -c "import json;d=json.load(open('$OUT/$n.$i.json'));s=d['sampler'];print('%.2f/%.2f/%.2f lane %.2f/%.2f/%.2f/%.2f' % (s['transformed']['us_per_step'], s['natural']['us_per_step'], s['transformed_joint']['us_per_step'], *[s[k]['us_per_step'] for k in ('rtd_4tracer_123', 'rtd_4tracer_123_exp_pist_flow', 'rtd_1tracer', 'ce_only')]))")"
