@@ -266,7 +266,9 @@ __global__ void __launch_bounds__(dzc_threads(MIX), 2)
         const DemcAccept& d = kernarg_opaque<DemcAccept>(kDzcArgD);
         const DzStep sj = dz_step(d.sch, js);
         // timing diagnostics (NGRTD_DZ_DIAG, tools/dzc_probe.py; wrong results): bit 6 no RTD
-        // likelihood, 7 no theta part, 8 no logs, 9 no history append, 10 no partner rows
+        // likelihood, 7 no theta part, 8 no logs, 9 no history append, 10 no partner rows, 11 no
+        // backward transform of the proposal, 12 no proposal (the state), 13 no tuning, 14 no
+        // Metropolis draw (logu = 0)
         const int dg = d.dz_diag;
         const bool de = e1 >= 0 && !(dg & 1024);
         const int64_t R = (int64_t)P * L;
@@ -284,9 +286,10 @@ __global__ void __launch_bounds__(dzc_threads(MIX), 2)
         for (int p = 0; p < kDzcMaxP; ++p) {
             if (p < P) {
                 const double sr = d.S ? d.S[(int64_t)p * L + l] : 1.0;
-                v[p] = dz_value_core(de, x[p], c1 ? x[p] : a1[p], c2 ? x[p] : a2[p], lamb, sc, ke, dz_pw_elem(cid, p),
-                                     d.S != nullptr, sr);
-                props[p * NT + tid] = TR ? pymc3_backward(d.tr_kind[p], d.tr_a[p], d.tr_b[p], v[p]) : v[p];
+                v[p] = (dg & 4096) ? x[p]
+                                   : dz_value_core(de, x[p], c1 ? x[p] : a1[p], c2 ? x[p] : a2[p], lamb, sc, ke,
+                                                   dz_pw_elem(cid, p), d.S != nullptr, sr);
+                props[p * NT + tid] = (TR && !(dg & 2048)) ? pymc3_backward(d.tr_kind[p], d.tr_a[p], d.tr_b[p], v[p]) : v[p];
             } else {
                 v[p] = 0.0;
             }
@@ -340,11 +343,11 @@ __global__ void __launch_bounds__(dzc_threads(MIX), 2)
         }
         const double lpp = th + like;
         // metrop_select + tune (demc_decide_at_u's arithmetic, on the registers)
-        const double logu = demc_logu(sj.key, cid);
+        const double logu = (dg & 16384) ? 0.0 : demc_logu(sj.key, cid);
         const double mr = lpp - lp;
         const bool acc = __builtin_isfinite(mr) && logu < mr;
         const double cur = acc ? lpp : lp;
-        if (d.n_acc_tune) {
+        if (d.n_acc_tune && !(dg & 8192)) {
             int32_t na = nat + (acc ? 1 : 0);
             if (sj.tune_now) {
                 const double rate = (double)na / (double)d.tune_interval;
