@@ -25,7 +25,7 @@ def main():
         objs.append(obj)
     if any(p.wait() for p in procs):
         sys.exit("compile failed")
-    subprocess.run(["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out] + objs, check=True)
+    subprocess.run(["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out] + objs + ["-ldl"], check=True)
     for o in objs:
         os.remove(o)
     print(out)

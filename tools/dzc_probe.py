@@ -4,7 +4,8 @@ run shape -- RTD-only, 1 well, 3 chains, N = 25 256, PyMC3's transformed space -
 the drop-in's sampler keeps (accepted, lp, accept stat), after 1000 tune steps; NGRTD_DZ_DIAG
 selects timing-only variants of the step (wrong results; bits in ngrtd_dzc.hpp).  JSON lines.
 
-    [NGRTD_DZ_DIAG=k] python tools/dzc_probe.py [--tracers 4|1] [--model exponential|exp_pist_flow]"""
+    [NGRTD_DZ_DIAG=k] python tools/dzc_probe.py [--tracers 4|1] [--model exponential|exp_pist_flow]
+        [--phase draw|tune]"""
 import argparse
 import dataclasses
 import json
@@ -23,6 +24,8 @@ def main():
     ap.add_argument("--model", default="exponential")
     ap.add_argument("--chains", type=int, default=3)
     ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--phase", choices=("draw", "tune"), default="draw",
+                    help="time draw-phase steps (after 1000 tune steps) or steps inside the tuning phase")
     args = ap.parse_args()
     import torch
     from noblegas_rtd_mcmc_amd import workloads as wl
@@ -36,7 +39,8 @@ def main():
     lp = LogProb(spec, max_walkers=W)
     n = args.steps
     s = DeviceDEMetropolisZ(lp, tune_interval=1000, seed=7, transformed=True, per_well=True)
-    x, l, z = s.start(th, 1000, 1000 + 2 * n + 1)
+    n_tune = 1000 if args.phase == "draw" else 1000 + 2 * n
+    x, l, z = s.start(th, n_tune, 1000 + 2 * n + 1)
     lp.demcz(x, l, 1000, z)
     acc = torch.empty((n, W), dtype=torch.uint8, device="cuda")
     lpl = torch.empty((n, W), dtype=torch.float64, device="cuda")
@@ -47,7 +51,7 @@ def main():
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / n
     print(json.dumps({"diag": int(os.environ.get("NGRTD_DZ_DIAG", "0")), "tracers": args.tracers, "model": args.model,
-                      "chains": W, "us_per_step": dt * 1e6}))
+                      "phase": args.phase, "chains": W, "us_per_step": dt * 1e6}))
     lp.close()
 
 
