@@ -4,6 +4,9 @@
 // model, natural or transformed space.  Compiled like ngrtd_dz.hip, without machine LICM.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include "../../include/ngrtd.h"
 #define NGRTD_FUSED_ONLY
 #include "ngrtd_dzc.hpp"
@@ -16,8 +19,19 @@ static hipError_t launch_dzc(const RtdArgs& a, const UnitArgs& u, const DemcAcce
     static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&dz_chain_kernel<C, MIX>),
                                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)max_lds);
     (void)attr;
+    // threads per block: NT, or the waves the chains need when they are fewer -- the
+    // reference's own runs are 3 chains (1 well) or 4 (CE): one wave alone on its SIMD instead
+    // of 8 waves of shadow lanes, two per SIMD, issuing the same step (NGRTD_DZC_MIN_THREADS:
+    // a floor, for A/B runs)
     constexpr int NT = dzc_threads(MIX);
-    hipLaunchKernelGGL((dz_chain_kernel<C, MIX>), dim3((unsigned)((U + NT - 1) / NT)), dim3(NT), lds, st, a, u, da);
+    static const int min_t = [] {
+        const char* e = getenv("NGRTD_DZC_MIN_THREADS");
+        const int v = e ? atoi(e) : 64;
+        return v < 64 ? 64 : v > NT ? NT : v / 64 * 64;
+    }();
+    int tb = (int)std::min<int64_t>(NT, (U + 63) / 64 * 64);
+    tb = std::max(tb, min_t);
+    hipLaunchKernelGGL((dz_chain_kernel<C, MIX>), dim3((unsigned)((U + tb - 1) / tb)), dim3(tb), lds, st, a, u, da);
     return hipGetLastError();
 }
 
@@ -65,3 +79,12 @@ hipError_t launch_dz_chain(int C, int mix, const RtdArgs& a, const UnitArgs& u, 
 }
 
 }  // namespace ngrtd
+
+#ifdef NGRTD_SECTION_PROBE
+// this translation unit's probe buffer (the lane-chain step's sections; tools/dzc_probe.py)
+extern "C" int ngrtd_probe_read_dzc(unsigned long long* dst, int64_t n) {
+    using ngrtd::g_probe;
+    if (n > (int64_t)(sizeof(g_probe) / sizeof(g_probe[0]))) n = sizeof(g_probe) / sizeof(g_probe[0]);
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_probe), (size_t)n * sizeof(unsigned long long)) == hipSuccess ? 0 : -2;
+}
+#endif

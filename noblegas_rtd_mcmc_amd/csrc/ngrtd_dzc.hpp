@@ -177,10 +177,22 @@ __device__ __forceinline__ double dzc_rtd_like(const RtdArgs& a, const UnitArgs&
 // the step loop through the opaque kernarg pointer (kernarg_opaque: otherwise every field is
 // hoisted out of the loop into registers)
 constexpr size_t kDzcArgU = ka_align(sizeof(RtdArgs), alignof(UnitArgs));
+// Probe build (tools/dzc_probe.py --sections): shader-clock cycles per section of the step,
+// summed over the launch's steps, lane 0 of each wave -> g_probe[wave][0..5], steps at [6]
+#ifdef NGRTD_SECTION_PROBE
+#define DZC_MARK(k)                                                                           \
+    do {                                                                                     \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                          \
+        pacc[k] += t_ - pt_;                                                                 \
+        pt_ = t_;                                                                            \
+    } while (0)
+#else
+#define DZC_MARK(k) do {} while (0)
+#endif
 constexpr size_t kDzcArgD = ka_align(kDzcArgU + sizeof(UnitArgs), alignof(DemcAccept));
 
 // One lane = one per-well chain (unit (w, l), walker-major: slot i of block b is unit
-// b NT + i = w L + l).  C: RTD channels (0 for the CE-only model); MIX: 1 piston second
+// b nth + i = w L + l, nth = blockDim.x <= NT threads).  C: RTD channels (0 for the CE-only model); MIX: 1 piston second
 // component, 2 exp_pist_flow first component, 4 PyMC3's transformed space (the plan carries
 // the Jacobians), 32 the sampled CFC12 half-life, 64 the CE-only model (no RTD block).
 // State arrays as logp_fused_kernel's DZ instances: dacc.zx the chains'-space rows and
@@ -196,6 +208,7 @@ __global__ void __launch_bounds__(dzc_threads(MIX), 2)
     static_assert(CEO || (C >= 1 && C <= 5), "RTD channels");
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int tid = threadIdx.x;
+    const int nth = blockDim.x;                           // <= NT: small ensembles launch fewer waves
     const RtdArgs& a0 = ak;
     // ---- prologue: tables -> LDS, once per launch
     double* cheb = lds;
@@ -207,23 +220,26 @@ __global__ void __launch_bounds__(dzc_threads(MIX), 2)
         const int n = a0.cheb_np * (kChebN * CP / 2);
         const double2* src = reinterpret_cast<const double2*>(a0.cheb + (size_t)a0.cheb_p0 * kChebN * CP);
         double2* dst = reinterpret_cast<double2*>(cheb);
-        for (int i = tid; i < n; i += NT) dst[(i / (kChebN * CP / 2)) * (PST / 2) + i % (kChebN * CP / 2)] = src[i];
+#pragma unroll 8
+        for (int i = tid; i < n; i += nth) dst[(i / (kChebN * CP / 2)) * (PST / 2) + i % (kChebN * CP / 2)] = src[i];
         }
     }
     if constexpr (!CEO && EPM) {
         const int nrow = a0.epm_nw;                      // (a windowed table: its rows only)
-        for (int i = tid; i < nrow * CP; i += NT) {
+#pragma unroll 8   // (loads batched ahead of the stores: one wave stages alone for small ensembles)
+        for (int i = tid; i < nrow * CP; i += nth) {
             const int k = i / CP, c = i % CP;
             tabl[epm_row(k, CP) + c] = (k < a0.N && c < C) ? a0.tab[(int64_t)k * a0.CP + c] : 0.0;
         }
     }
-    for (int i = tid; i < ua.wd_n; i += NT) wd[i] = ua.wd_src[i];
+#pragma unroll 8
+    for (int i = tid; i < ua.wd_n; i += nth) wd[i] = ua.wd_src[i];
     fm_lds_init();
     __syncthreads();
     // ---- the lane's chain
     const int L = ua.L;
     const int64_t W = ua.W, U = (int64_t)L * W;
-    const int64_t g = (int64_t)blockIdx.x * NT + tid;
+    const int64_t g = (int64_t)blockIdx.x * nth + tid;
     const bool valid = g < U;
     const int64_t gv = valid ? g : U - 1;                 // a lane past the end shadows the last unit, stores nothing
     const int64_t w = gv / L;
@@ -260,6 +276,9 @@ __global__ void __launch_bounds__(dzc_threads(MIX), 2)
         }
     };
     partner_rows(dacc, 0);
+#ifdef NGRTD_SECTION_PROBE
+    unsigned long long pacc[6] = {0, 0, 0, 0, 0, 0}, pt_ = __builtin_amdgcn_s_memtime();
+#endif
     for (int js = 0; js < nst; ++js) {
         const RtdArgs& a = kernarg_opaque<RtdArgs>(0);
         const UnitArgs& uk = kernarg_opaque<UnitArgs>(kDzcArgU);
@@ -279,6 +298,7 @@ __global__ void __launch_bounds__(dzc_threads(MIX), 2)
             for (int p = 0; p < kDzcMaxP; ++p)
                 if (p < P) hrow[(int64_t)p * L] = x[p];
         }
+        DZC_MARK(0);                                      // schedule + history append
         const bool c1 = e1 == sj.at, c2 = e2 == sj.at;    // an entry appended in this launch is the state
         const uint64_t ke = rng_mix(sj.key + 2);
         double v[kDzcMaxP];
@@ -294,7 +314,9 @@ __global__ void __launch_bounds__(dzc_threads(MIX), 2)
                 v[p] = 0.0;
             }
         }
+        DZC_MARK(1);                                      // proposal values, natural rows -> LDS
         partner_rows(d, js + 1);                          // the next step's partners (in flight from here)
+        DZC_MARK(2);
         // the proposal's log-prob: the log-prob kernels' functions over the LDS rows
         RtdArgs ar = a;
         ar.theta = props;
@@ -331,6 +353,7 @@ __global__ void __launch_bounds__(dzc_threads(MIX), 2)
             tp.nub = props[uk.row_nu * NT + tid];
         }
         const double th = (dg & 128) ? 0.0 : unit_logp_theta(ul, tid, l, &tp, false, false);
+        DZC_MARK(3);                                      // argument views, theta part
         double like = 0.0;
         if constexpr (!CEO) {
             if (!(dg & 64)) {
@@ -342,6 +365,7 @@ __global__ void __launch_bounds__(dzc_threads(MIX), 2)
             }
         }
         const double lpp = th + like;
+        DZC_MARK(4);                                      // RTD likelihood
         // metrop_select + tune (demc_decide_at_u's arithmetic, on the registers)
         const double logu = (dg & 16384) ? 0.0 : demc_logu(sj.key, cid);
         const double mr = lpp - lp;
@@ -367,7 +391,15 @@ __global__ void __launch_bounds__(dzc_threads(MIX), 2)
         lp = cur;
 #pragma unroll
         for (int p = 0; p < kDzcMaxP; ++p) x[p] = acc ? v[p] : x[p];
+        DZC_MARK(5);                                      // decision, tuning, logs
     }
+#ifdef NGRTD_SECTION_PROBE
+    if ((tid & 63) == 0) {
+        unsigned long long* o = g_probe + ((size_t)blockIdx.x * (nth >> 6) + (tid >> 6)) * kProbeSlots;
+        for (int k = 0; k < 6; ++k) o[k] = pacc[k];
+        o[6] = (unsigned long long)nst;
+    }
+#endif
     // ---- the chain back: state (natural, and transformed), per-chain scalars, accept count
     if (valid) {
 #pragma unroll

@@ -26,7 +26,14 @@ def main():
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--phase", choices=("draw", "tune"), default="draw",
                     help="time draw-phase steps (after 1000 tune steps) or steps inside the tuning phase")
+    ap.add_argument("--sections", action="store_true",
+                    help="probe build (tools/section_probe.py): shader-clock cycles per section of a step")
     args = ap.parse_args()
+    if args.sections:
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__))))
+        import section_probe
+        section_probe.build()
+        os.environ["NGRTD_LIB"] = section_probe.probe_lib(())
     import torch
     from noblegas_rtd_mcmc_amd import workloads as wl
     from noblegas_rtd_mcmc_amd.engine import LogProb
@@ -50,8 +57,21 @@ def main():
     lp.demcz(x, l, n, z, accepted_log=acc, logp_log=lpl, accept_log=arl)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / n
-    print(json.dumps({"diag": int(os.environ.get("NGRTD_DZ_DIAG", "0")), "tracers": args.tracers, "model": args.model,
-                      "phase": args.phase, "chains": W, "us_per_step": dt * 1e6}))
+    res = {"diag": int(os.environ.get("NGRTD_DZ_DIAG", "0")), "tracers": args.tracers, "model": args.model,
+           "phase": args.phase, "chains": W, "us_per_step": dt * 1e6}
+    if args.sections:   # the last launch's sums, wave 0 (the chains' wave)
+        import ctypes as C
+        from noblegas_rtd_mcmc_amd import _lib
+        rd = _lib.load().ngrtd_probe_read_dzc
+        rd.argtypes = [C.c_void_p, C.c_int64]
+        buf = np.zeros(16, dtype=np.uint64)
+        assert rd(buf.ctypes.data, buf.size) == 0
+        ns = max(int(buf[6]), 1)
+        names = ("schedule_append", "proposal", "partner_rows", "args_theta", "rtd_like", "decision_logs")
+        res["cycles_per_step"] = {k: float(buf[i]) / ns for i, k in enumerate(names)}
+        res["cycles_per_step"]["total"] = float(buf[:6].sum()) / ns
+        res["launch_steps"] = ns
+    print(json.dumps(res))
     lp.close()
 
 

@@ -56,7 +56,7 @@ def build(defines=()):
         for pr in procs:
             if pr.wait() != 0:
                 raise subprocess.CalledProcessError(pr.returncode, pr.args)
-        subprocess.run(["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", lib] + objs, check=True)
+        subprocess.run(["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", lib] + objs + ["-ldl"], check=True)
         for o in objs:
             os.remove(o)
 
