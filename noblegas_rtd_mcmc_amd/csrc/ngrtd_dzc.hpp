@@ -318,11 +318,20 @@ __global__ void __launch_bounds__(dzc_threads(MIX), 2)
         partner_rows(d, js + 1);                          // the next step's partners (in flight from here)
         DZC_MARK(2);
         // the proposal's log-prob: the log-prob kernels' functions over the LDS rows
-        RtdArgs ar = a;
+        RtdArgs ar = a;   // (from the by-value parameter: no gain, profiles/r06w_dzc_rtdargs_ab.txt)
         ar.theta = props;
         ar.U = NT;
         ar.conc = nullptr;
+        // the unit view from the by-value parameter, not the opaque kernarg reference: the fields
+        // the theta part and the likelihood read stay in registers (SGPRs, spilled to VGPR lanes)
+        // across the loop instead of a scalar load and wait per field and step -- 12.1 -> 11.0 us
+        // per 4-tracer c4 step, 9.3 -> 8.3 us at the reference's 3 chains
+        // (profiles/r06v_dzc_unitargs_ab.txt)
+#ifdef NGRTD_DZC_UA_OPAQUE   // (A/B: the opaque reference)
         UnitArgs ul = uk;
+#else
+        UnitArgs ul = ua;
+#endif
         ul.theta = props;
         ul.U = NT;
         ul.W = W;
