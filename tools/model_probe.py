@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--walkers", type=int, default=2048)
     ap.add_argument("--wells", type=int, default=64)
+    ap.add_argument("--ages", type=int, default=1200, help="N (25256: the reference's full series)")
     args = ap.parse_args()
     import torch
     import bench
@@ -34,7 +35,7 @@ def main():
     for m in args.models.split(","):
         mod, _, sv = m.partition(":")
         m1, _, m2 = mod.partition("-")
-        ns = argparse.Namespace(wells=args.wells, ages=1200, mod_type1=m1, mod_type2=m2 or None)
+        ns = argparse.Namespace(wells=args.wells, ages=args.ages, mod_type1=m1, mod_type2=m2 or None)
         spec = bench.model_spec(ns, sv if sv != "0" else "")
         th = torch.from_numpy(wl.sample_prior(spec, args.walkers, np.random.default_rng(34568))).cuda()
         lp = LogProb(spec, max_walkers=args.walkers)
