@@ -142,6 +142,9 @@ def main():
         tt = t[sel]
         r = {"prologue": tt[:, 1] - tt[:, 0], "work": tt[:, 3] - tt[:, 1], "exchange": tt[:, 6] - tt[:, 3],
              "reduce": tt[:, 7] - tt[:, 6], "total": tt[:, 7] - tt[:, 0]}
+        if args.variant != "dz":   # the prologue's loads + LDS stores (0 -> 9), its barrier (9 -> 1)
+            r["prologue_loads_stores"] = tt[:, 9] - tt[:, 0]
+            r["prologue_barrier"] = tt[:, 1] - tt[:, 9]
         if grp == "theta_role" and args.variant == "dz":
             r["dz_stage"] = tt[:, 4] - tt[:, 0]
         if grp == "rtd_role":
@@ -159,6 +162,12 @@ def main():
     res["xcd0_theta_end_p10_p50_max"] = np.percentile(t[sel & (w < 8), 3] - t0, [10, 50, 100]).tolist()
     res["xcd0_rtd_end_p10_p50_max"] = np.percentile(t[sel & (w >= 8), 3] - t0, [10, 50, 100]).tolist()
     res["xcd0_wave_end_p10_p50_max"] = np.percentile(t[sel, 7] - t0, [10, 50, 100]).tolist()
+    # wave start times within each XCD, relative to the XCD's median start (dispatch ramp)
+    ramp = []
+    for x in range(8):
+        sx = t[(blk % 8) == x, 0].astype(np.float64)
+        ramp.append((np.percentile(sx, [1, 50, 99]) - np.median(sx)).tolist())
+    res["wave_start_p1_p50_p99_vs_median_per_xcd"] = ramp
     print(json.dumps(res, indent=1))
 
 
