@@ -153,6 +153,34 @@ def test_single_launch_step_reference_shapes(shape, jac):
     lp.close()
 
 
+@pytest.mark.parametrize("model", ["exponential", "exp_pist_flow"])
+def test_lane_chain_launch_geometry_independent(model):
+    """The lane-chain step launches only the waves its chains need (ngrtd_dzc.hip: 3 chains in one
+    64-lane block, 70 in one 128-lane block, 600 in 512-lane blocks): a chain's draws do not
+    depend on that geometry -- the first 3 chains of the 70- and 600-chain runs equal the 3-chain
+    run bit for bit (1 well: a chain's random streams and history are keyed by its index alone)."""
+    import dataclasses
+    import torch
+    from noblegas_rtd_mcmc_amd import workloads as wl
+    from noblegas_rtd_mcmc_amd.engine import LogProb
+    from noblegas_rtd_mcmc_amd.sampler import DeviceDEMetropolisZ
+    spec = dataclasses.replace(wl.rtd_only_spec(L=1, N=1200, mod_type1=model), jacobian=True)
+    x0 = torch.from_numpy(wl.sample_prior(spec, 600, np.random.default_rng(5))).cuda()
+    kw = dict(tune_interval=4, seed=99, per_well=True)
+    outs = {}
+    for W in (3, 70, 600):
+        lp = LogProb(spec, max_walkers=W)
+        lp.ctx.set_profiling(True)
+        lp.kernel_stats(reset=True)
+        outs[W] = DeviceDEMetropolisZ(lp, **kw).run(x0[..., :W].contiguous(), tune=12, draws=8)
+        assert lp.kernel_stats(reset=True)["fused"][1] == 1   # the lane-chain launch: one for the 20 steps
+        lp.close()
+    for W in (70, 600):
+        for k in ("samples", "logp", "accepted", "lamb", "scaling"):
+            assert _same(outs[W][k][..., :3], outs[3][k]), (W, k)
+    assert 0 < int(outs[600]["accepted"].sum()) < outs[600]["accepted"].numel()
+
+
 @pytest.mark.parametrize("jac", [True, False])
 @pytest.mark.parametrize("shape", ["rtd4_exp_pist_flow_123", "rtd4_exp_pist_flow-piston_123", "rtd4_exp_pist_flow",
                                    "rtd1_exp_pist_flow", "joint_epm_bmm"])
