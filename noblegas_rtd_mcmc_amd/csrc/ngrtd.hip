@@ -2415,6 +2415,13 @@ int ngrtd_demcz_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64
             RtdArgs dwin = dr;
             if (!(dzc & 64)) cheb_window(dwin, du);
             da.state_lds = 0; da.prop_lds = 0; da.prop_skip = 0;
+            // up to 64 chains (the reference's own runs: 3 or 4): a theta wave beside the chain
+            // wave (NGRTD_DZC_THETA_WAVE=0: off, A/B runs)
+            static const bool tw_off = [] {
+                const char* e = std::getenv("NGRTD_DZC_THETA_WAVE");
+                return e && std::atoi(e) == 0;
+            }();
+            da.theta_wave = (!tw_off && du.U <= 64 && !(dzc & 64)) ? 1 : 0;   // (the CE-only model: no RTD half)
             HIP_TRY(ctx, launch_dz_chain(dwin.C, dzc, dwin, du, da, du.U, dzc_lds, kFusedMaxLds, st));
         } else {
             NG_CHECK(launch_fused_dz(ctx, dr, du, W, p->desc.n_wells, p->demc_lp.d(), st, da, dzm));

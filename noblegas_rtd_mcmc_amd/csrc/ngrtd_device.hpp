@@ -271,6 +271,9 @@ struct DemcAccept {
     int32_t per_well;
     int64_t well0;
     double* ar_log;         // [chains] this step's PyMC3 `accept` stat exp(mr) (null: not logged)
+    // lane-chain step (ngrtd_dzc.hpp dz_chain_kernel) of <= 64 chains: 1 = the block's second
+    // wave evaluates the chains' theta parts while the first evaluates their RTD likelihoods
+    int32_t theta_wave;
 };
 
 // One DEMetropolisZ step's schedule (ngrtd_demcz_run's host loop, restated so that a

@@ -13,12 +13,21 @@
 
 namespace ngrtd {
 
+template <int C, int MIX, bool TW>
+static hipError_t launch_dzc_tw(const RtdArgs& a, const UnitArgs& u, const DemcAccept& da, unsigned blocks,
+                                unsigned threads, size_t lds, size_t max_lds, hipStream_t st) {
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&dz_chain_kernel<C, MIX, TW>),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)max_lds);
+    (void)attr;
+    hipLaunchKernelGGL((dz_chain_kernel<C, MIX, TW>), dim3(blocks), dim3(threads), lds, st, a, u, da);
+    return hipGetLastError();
+}
+
 template <int C, int MIX>
 static hipError_t launch_dzc(const RtdArgs& a, const UnitArgs& u, const DemcAccept& da, int64_t U, size_t lds,
                              size_t max_lds, hipStream_t st) {
-    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&dz_chain_kernel<C, MIX>),
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)max_lds);
-    (void)attr;
+    // one chain wave + its theta wave per block (da.theta_wave: <= 64 chains)
+    if (da.theta_wave) return launch_dzc_tw<C, MIX, true>(a, u, da, (unsigned)((U + 63) / 64), 128, lds, max_lds, st);
     // threads per block: NT, or the waves the chains need when they are fewer -- the
     // reference's own runs are 3 chains (1 well) or 4 (CE): one wave alone on its SIMD instead
     // of 8 waves of shadow lanes, two per SIMD, issuing the same step (NGRTD_DZC_MIN_THREADS:
@@ -31,8 +40,7 @@ static hipError_t launch_dzc(const RtdArgs& a, const UnitArgs& u, const DemcAcce
     }();
     int tb = (int)std::min<int64_t>(NT, (U + 63) / 64 * 64);
     tb = std::max(tb, min_t);
-    hipLaunchKernelGGL((dz_chain_kernel<C, MIX>), dim3((unsigned)((U + tb - 1) / tb)), dim3(tb), lds, st, a, u, da);
-    return hipGetLastError();
+    return launch_dzc_tw<C, MIX, false>(a, u, da, (unsigned)((U + tb - 1) / tb), (unsigned)tb, lds, max_lds, st);
 }
 
 #define NGRTD_DZC_RTD(CC)                                                                          \

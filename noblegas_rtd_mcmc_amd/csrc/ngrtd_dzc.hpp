@@ -37,7 +37,7 @@ __host__ __device__ constexpr int dzc_threads(int) { return 512; }
 // (epm_nw: the EPM table rows staged, RtdArgs::epm_nw)
 __host__ __device__ constexpr size_t dzc_lds_doubles(int C, int mix, int cheb_np, int epm_nw, int wd_n, int P) {
     return (size_t)cheb_np * cheb_lds_stride(C) + ((mix & 2) ? (size_t)epm_lds_doubles(epm_nw, cheb_cp(C)) : 0) +
-           (size_t)((wd_n + 1) & ~1) + (size_t)P * dzc_threads(mix);
+           (size_t)((wd_n + 1) & ~1) + (size_t)P * dzc_threads(mix) + 64;   // (+ the theta parts [64])
 }
 
 // Exact (matrix-core) channel sums of the wave's 64 lanes (slots slot0 + 0..63) as 4 tiles
@@ -198,7 +198,7 @@ constexpr size_t kDzcArgD = ka_align(kDzcArgU + sizeof(UnitArgs), alignof(DemcAc
 // State arrays as logp_fused_kernel's DZ instances: dacc.zx the chains'-space rows and
 // dacc.x / dacc.xu the natural / transformed rows ([P][W][L], walker-major), the per-chain
 // lp / lamb / scaling / tuning counters [W][L]; logs [n_steps][L][W].
-template <int C, int MIX>
+template <int C, int MIX, bool TW = false>
 __global__ void __launch_bounds__(dzc_threads(MIX), 2)
     dz_chain_kernel(const RtdArgs ak, const UnitArgs ua, const DemcAccept dacc) {
     constexpr int NT = dzc_threads(MIX);
@@ -215,6 +215,7 @@ __global__ void __launch_bounds__(dzc_threads(MIX), 2)
     double* tabl = cheb + (CEO ? 0 : a0.cheb_np * PST);
     double* wd = tabl + ((!CEO && EPM) ? epm_lds_doubles(a0.epm_nw, CP) : 0);
     double* props = wd + ((ua.wd_n + 1) & ~1);            // [P][NT] the lanes' proposals (natural)
+    double* thl = props + (size_t)dacc.P * NT;            // [64] theta parts (dacc.theta_wave)
     if constexpr (!CEO) {
         if (a0.cheb) {
         const int n = a0.cheb_np * (kChebN * CP / 2);
@@ -236,16 +237,24 @@ __global__ void __launch_bounds__(dzc_threads(MIX), 2)
     for (int i = tid; i < ua.wd_n; i += nth) wd[i] = ua.wd_src[i];
     fm_lds_init();
     __syncthreads();
-    // ---- the lane's chain
+    // ---- the lane's chain.  TW (dacc.theta_wave: <= 64 chains, 128 threads): wave 0 runs the
+    // chains, wave 1 lane i evaluates the theta part of lane i's proposal each step (between two
+    // block barriers) while wave 0 evaluates the RTD likelihood -- the two halves of a step's
+    // log-prob depend only on the proposal, and one lane ran them one after the other.  Its own
+    // instances: the extra paths cost the plain ones registers (spills, 2-5 % per c4 step)
+    constexpr bool thw = TW;
+    const bool helper = thw && tid >= 64;                 // (wave-uniform)
+    const int cl = helper ? tid - 64 : tid;               // the chain lane this lane serves
+    const int cpb = thw ? 64 : nth;                       // chains per block
     const int L = ua.L;
     const int64_t W = ua.W, U = (int64_t)L * W;
-    const int64_t g = (int64_t)blockIdx.x * nth + tid;
+    const int64_t g = (int64_t)blockIdx.x * cpb + cl;
     const bool valid = g < U;
     const int64_t gv = valid ? g : U - 1;                 // a lane past the end shadows the last unit, stores nothing
     const int64_t w = gv / L;
     const int l = (int)(gv % L);
     const int P = dacc.P;
-    const int slot0 = tid & ~63;
+    const int slot0 = cl & ~63;
     const uint64_t cid = dz_cid(dacc.well0, l, dacc.Wg, dacc.chain0, w);
     double x[kDzcMaxP];                                   // the chain's state (its own space)
 #pragma unroll
@@ -292,7 +301,7 @@ __global__ void __launch_bounds__(dzc_threads(MIX), 2)
         const bool de = e1 >= 0 && !(dg & 1024);
         const int64_t R = (int64_t)P * L;
         // the state becomes history entry sj.at (chains' space)
-        if (valid && sj.at >= 0 && !(dg & 512)) {
+        if (!helper && valid && sj.at >= 0 && !(dg & 512)) {
             double* hrow = d.hist + ((size_t)sj.at * W + w) * R + l;
 #pragma unroll
             for (int p = 0; p < kDzcMaxP; ++p)
@@ -304,7 +313,7 @@ __global__ void __launch_bounds__(dzc_threads(MIX), 2)
         double v[kDzcMaxP];
 #pragma unroll
         for (int p = 0; p < kDzcMaxP; ++p) {
-            if (p < P) {
+            if (p < P && !helper) {
                 const double sr = d.S ? d.S[(int64_t)p * L + l] : 1.0;
                 v[p] = (dg & 4096) ? x[p]
                                    : dz_value_core(de, x[p], c1 ? x[p] : a1[p], c2 ? x[p] : a2[p], lamb, sc, ke,
@@ -315,7 +324,8 @@ __global__ void __launch_bounds__(dzc_threads(MIX), 2)
             }
         }
         DZC_MARK(1);                                      // proposal values, natural rows -> LDS
-        partner_rows(d, js + 1);                          // the next step's partners (in flight from here)
+        if (!helper) partner_rows(d, js + 1);             // the next step's partners (in flight from here)
+        if (thw) __syncthreads();                         // the proposal rows -> the theta wave
         DZC_MARK(2);
         // the proposal's log-prob: the log-prob kernels' functions over the LDS rows
         RtdArgs ar = a;   // (from the by-value parameter: no gain, profiles/r06w_dzc_rtdargs_ab.txt)
@@ -356,22 +366,28 @@ __global__ void __launch_bounds__(dzc_threads(MIX), 2)
         ThetaPre tp{};
         if constexpr (CEO) {
 #pragma unroll
-            for (int i = 0; i < 6; ++i) tp.ce[i] = props[uk.row_ce[i] * NT + tid];
+            for (int i = 0; i < 6; ++i) tp.ce[i] = props[uk.row_ce[i] * NT + cl];
         } else {
-            tp.tau1 = props[uk.row_tau1 * NT + tid];
-            tp.nub = props[uk.row_nu * NT + tid];
+            tp.tau1 = props[uk.row_tau1 * NT + cl];
+            tp.nub = props[uk.row_nu * NT + cl];
         }
-        const double th = (dg & 128) ? 0.0 : unit_logp_theta(ul, tid, l, &tp, false, false);
+        double th = 0.0;
+        if (!(dg & 128) && (!thw || helper)) th = unit_logp_theta(ul, cl, l, &tp, false, false);
         DZC_MARK(3);                                      // argument views, theta part
         double like = 0.0;
         if constexpr (!CEO) {
-            if (!(dg & 64)) {
+            if (!(dg & 64) && !helper) {
                 const double tau = props[a.row_tau[0] * NT + tid];
                 const double eta = EPM ? props[a.row_eta[0] * NT + tid] : 1.0;
                 const double tau2 = (MIX & 1) ? props[a.row_tau[1] * NT + tid] : 1.0;
                 const double thx = LW ? props[a.row_thalf * NT + tid] : 0.5;
                 like = dzc_rtd_like<C, MIX>(ar, ul, cheb, tabl, valid, tid, slot0, l, tau, eta, tau2, thx, tp.nub);
             }
+        }
+        if (thw) {                                        // the theta parts -> the chain lanes
+            if (helper) thl[cl] = th;
+            __syncthreads();
+            if (!helper) th = thl[cl];
         }
         const double lpp = th + like;
         DZC_MARK(4);                                      // RTD likelihood
@@ -390,13 +406,13 @@ __global__ void __launch_bounds__(dzc_threads(MIX), 2)
             }
             nat = na;
         }
-        if (valid && !(dg & 256)) {
+        if (valid && !helper && !(dg & 256)) {
             const int64_t li = (int64_t)js * U + (int64_t)l * W + w;
             if (d.acc_log) d.acc_log[li] = (uint8_t)acc;
             if (d.lp_log) d.lp_log[li] = cur;
             if (d.ar_log) d.ar_log[li] = exp(mr);
         }
-        nacc += (valid && acc) ? 1 : 0;
+        nacc += (valid && !helper && acc) ? 1 : 0;
         lp = cur;
 #pragma unroll
         for (int p = 0; p < kDzcMaxP; ++p) x[p] = acc ? v[p] : x[p];
@@ -410,7 +426,7 @@ __global__ void __launch_bounds__(dzc_threads(MIX), 2)
     }
 #endif
     // ---- the chain back: state (natural, and transformed), per-chain scalars, accept count
-    if (valid) {
+    if (valid && !helper) {
 #pragma unroll
         for (int p = 0; p < kDzcMaxP; ++p) {
             if (p < P) {
