@@ -38,7 +38,7 @@ FP64_PEAK = 78.6e12          # MI355X FP64 peak (vector and matrix, AMD spec: 25
 FP64_VALU_MEASURED = 38.3e12 # v_fma_f64 throughput measured by tools/ubench_fp64.hip (profiles/r01_ubench_fp64.txt)
 FP64_MFMA_MEASURED = 78.3e12 # v_mfma_f64_16x16x4f64, same microbenchmark
 HBM_PEAK = 8.0e12            # MI355X_MICROARCH.md chip table
-PMC_SUMMARIES = ("r06fin_pmc.json", "r06_pmc.json", "r05_pmc.json", "r04_pmc.json", "r03s2f_pmc.json", "r03s2_pmc.json", "r03_pmc.json", "r02_pmc.json", "r01_pmc.json")   # newest first (tools/gpu_profile.sh)
+PMC_SUMMARIES = ("r06fin2_pmc.json", "r06fin_pmc.json", "r06_pmc.json", "r05_pmc.json", "r04_pmc.json", "r03s2f_pmc.json", "r03s2_pmc.json", "r03_pmc.json", "r02_pmc.json", "r01_pmc.json")   # newest first (tools/gpu_profile.sh)
 
 # the RTD parameters each model adds (run_age_mcmc.py:145-178)
 MODEL_PARS = {"exponential": (), "piston": (), "exp_pist_flow": ("eta",), "dispersion": ("D",)}
