@@ -2446,20 +2446,40 @@ int ngrtd_demcz_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64
         }
         HIP_TRY(ctx, hipGetLastError());
     }
-    for (int64_t j = 0; !multi && j < n_steps; ++j) {
+    // step j's bookkeeping (the host restatement dz_step mirrors): the previous step's state
+    // becomes history entry s - 1 (the previous call appended its own last state), then
+    // proposals draw from [hist_lo, hist_len)
+    auto step_args = [&](int64_t j) {
         const int64_t s = z->steps_done;
-        const uint64_t key = demc_key(z->seed, (uint64_t)s);
-        // the previous step's state becomes history entry s - 1 (the previous call appended
-        // its own last state), then proposals draw from [hist_lo, hist_len)
         const int64_t append_at = j > 0 ? z->hist_len : -1;
         if (j > 0) z->hist_len += 1;
         if (s == z->n_tune && z->n_tune > 0)   // stop_tuning before the first draw: drop the
             z->hist_lo += (int64_t)(z->drop_fraction * (double)(z->hist_len - z->hist_lo));   // oldest
         DemczArgs d = base;
-        d.propose = 1; d.append_at = append_at; d.lo = z->hist_lo; d.it = z->hist_len - z->hist_lo; d.key = key;
-        if (pw) hipLaunchKernelGGL(demcz_propose_pw_kernel, gpw, dim3(256), 0, st, d);
-        else hipLaunchKernelGGL(demcz_propose_kernel, grid, dim3(kZThreads), 0, st, d);
-        HIP_TRY(ctx, hipGetLastError());
+        d.propose = 1; d.append_at = append_at; d.lo = z->hist_lo; d.it = z->hist_len - z->hist_lo;
+        d.key = demc_key(z->seed, (uint64_t)s);
+        return d;
+    };
+    // per-well chains: step j's accept and step j + 1's append + proposal (after the last step:
+    // the final append) in one launch (demc_accept_propose_pw_kernel; NGRTD_DZ_NO_FUSE=1: the
+    // separate kernels, A/B runs)
+    static const bool no_fuse = [] {
+        const char* e = std::getenv("NGRTD_DZ_NO_FUSE");
+        return e && std::atoi(e) != 0;
+    }();
+    const bool fuse = pw && !no_fuse;
+    bool staged = false;                   // this step's proposal ran in the previous launch
+    DemczArgs d = base;
+    for (int64_t j = 0; !multi && j < n_steps; ++j) {
+        if (!staged) {
+            d = step_args(j);
+            if (pw) hipLaunchKernelGGL(demcz_propose_pw_kernel, gpw, dim3(256), 0, st, d);
+            else hipLaunchKernelGGL(demcz_propose_kernel, grid, dim3(kZThreads), 0, st, d);
+            HIP_TRY(ctx, hipGetLastError());
+        }
+        staged = false;
+        const int64_t s = z->steps_done;
+        const uint64_t key = d.key;
         const int64_t next = s + 1;
         const int32_t tune_now = (z->tune_target != NGRTD_TUNE_NONE && next < z->n_tune &&
                                   next % z->tune_interval == 0) ? 1 : 0;
@@ -2471,19 +2491,33 @@ int ngrtd_demcz_run(ngrtd_plan* p, double* theta, double* logp, int64_t W, int64
         if (pw) {   // per-unit log-probs of the proposal, then one decision per unit
             da.L = p->desc.n_wells; da.Wg = Wg; da.per_well = 1; da.well0 = z->well0;
             NG_CHECK(plan_run_units(p, prop_x, W, p->demc_lp.d()));
-            hipLaunchKernelGGL(demc_accept_pw_kernel, gpw, dim3(256), 0, st, da, (const double*)p->demc_lp.d(), W);
+            z->steps_done = next;
+            if (fuse) {
+                if (j + 1 < n_steps) {
+                    d = step_args(j + 1);
+                } else {                       // the last step's state: history entry steps_done - 1
+                    d = base;
+                    d.propose = 0; d.append_at = z->hist_len;
+                }
+                hipLaunchKernelGGL(demc_accept_propose_pw_kernel, gpw, dim3(256), 0, st, da,
+                                   (const double*)p->demc_lp.d(), W, d);
+                staged = true;
+            } else {
+                hipLaunchKernelGGL(demc_accept_pw_kernel, gpw, dim3(256), 0, st, da, (const double*)p->demc_lp.d(), W);
+            }
             HIP_TRY(ctx, hipGetLastError());
         } else {
             NG_CHECK(plan_run(p, prop_x, W, p->demc_lp.d(), nullptr, nullptr, &da));
+            z->steps_done = next;
         }
-        z->steps_done = next;
     }
-    // the last step's state: history entry steps_done - 1
-    DemczArgs d = base;
-    d.propose = 0; d.append_at = z->hist_len;
-    if (pw) hipLaunchKernelGGL(demcz_propose_pw_kernel, gpw, dim3(256), 0, st, d);
-    else hipLaunchKernelGGL(demcz_propose_kernel, grid, dim3(kZThreads), 0, st, d);
-    HIP_TRY(ctx, hipGetLastError());
+    if (!staged) {   // the last step's state: history entry steps_done - 1
+        d = base;
+        d.propose = 0; d.append_at = z->hist_len;
+        if (pw) hipLaunchKernelGGL(demcz_propose_pw_kernel, gpw, dim3(256), 0, st, d);
+        else hipLaunchKernelGGL(demcz_propose_kernel, grid, dim3(kZThreads), 0, st, d);
+        HIP_TRY(ctx, hipGetLastError());
+    }
     z->hist_len += 1;
     return NGRTD_OK;
 }

@@ -1521,12 +1521,10 @@ __device__ __forceinline__ double dz_value(const DemcAccept& d, bool de, double 
 // rows [P][L][W] are read and written coalesced), noise and accept draws of the unit's
 // own stream (dz_cid), partner indices of the walker, the joint chains' history layout.  The
 // arithmetic of dz_stage's per-well branch (bitwise).
-NGRTD_KLINK __global__ void __launch_bounds__(256) demcz_propose_pw_kernel(const DemczArgs d) {
-    fm_lds_init();                           // fexp (pymc3_backward)
-    __syncthreads();
+// Per-well chains: unit c's history append (append_at) and proposal (demcz_propose_pw_kernel's
+// body; also run right after the accept step by demc_accept_propose_pw_kernel)
+__device__ __forceinline__ void demcz_propose_pw_unit(const DemczArgs& d, int64_t c) {
     const int64_t W = d.W, U = d.W * d.L;
-    const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (c >= U) return;
     const int64_t l = c / W, w = c % W;
     const int P = d.P;
     const uint64_t cid = dz_cid(d.well0, l, d.Wg, d.chain0, w);
@@ -1557,22 +1555,44 @@ NGRTD_KLINK __global__ void __launch_bounds__(256) demcz_propose_pw_kernel(const
         if (d.prop_x) d.prop_x[(int64_t)p * U + c] = pymc3_backward(d.tr_kind[p], d.tr_a[p], d.tr_b[p], v);
     }
 }
+NGRTD_KLINK __global__ void __launch_bounds__(256) demcz_propose_pw_kernel(const DemczArgs d) {
+    fm_lds_init();                           // fexp (pymc3_backward)
+    __syncthreads();
+    const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (c < d.W * d.L) demcz_propose_pw_unit(d, c);
+}
 
 // Per-well chains, the accept step after the per-unit log-prob (ngrtd_logp_units): one
 // thread per unit c = l W + w decides its own chain and copies its P proposal rows.
-NGRTD_KLINK __global__ void __launch_bounds__(256) demc_accept_pw_kernel(const DemcAccept d,
-                                                                          const double* __restrict__ ulp, int64_t W) {
-    fm_lds_init();                           // flog (demc_logu)
-    __syncthreads();
+__device__ __forceinline__ void demc_accept_pw_unit(const DemcAccept& d, const double* __restrict__ ulp, int64_t W,
+                                                    int64_t c) {
     const int64_t U = W * d.L;
-    const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (c >= U) return;
     const int64_t l = c / W, w = c % W;
     if (demc_decide(d, c, dz_cid(d.well0, l, d.Wg, d.chain0, w), ulp[c], d.key, d.tune_now, 0)) {
         for (int p = 0; p < d.P; ++p) d.x[(int64_t)p * U + c] = d.prop[(int64_t)p * U + c];
         if (d.xu)
             for (int p = 0; p < d.P; ++p) d.xu[(int64_t)p * U + c] = d.prop_u[(int64_t)p * U + c];
     }
+}
+NGRTD_KLINK __global__ void __launch_bounds__(256) demc_accept_pw_kernel(const DemcAccept d,
+                                                                          const double* __restrict__ ulp, int64_t W) {
+    fm_lds_init();                           // flog (demc_logu)
+    __syncthreads();
+    const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (c < W * d.L) demc_accept_pw_unit(d, ulp, W, c);
+}
+// Step j's accept and step j + 1's append + proposal in one launch (per-well chains): each
+// thread decides its unit, then appends and proposes from the state it just wrote -- a chain
+// reads only its own history rows -- so the kernel pair's bits with one launch fewer per step
+NGRTD_KLINK __global__ void __launch_bounds__(256) demc_accept_propose_pw_kernel(const DemcAccept da,
+                                                                                 const double* __restrict__ ulp,
+                                                                                 int64_t W, const DemczArgs d) {
+    fm_lds_init();                           // flog (demc_logu), fexp (pymc3_backward)
+    __syncthreads();
+    const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (c >= W * da.L) return;
+    demc_accept_pw_unit(da, ulp, W, c);
+    demcz_propose_pw_unit(d, c);
 }
 
 // The multi-step launch's LDS copies of its block's chain state (DemcAccept::state_lds):
